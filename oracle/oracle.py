@@ -1,0 +1,347 @@
+"""CPU oracle for splink's comparison + EM hot path.
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() (as the
+checker) and bench.py's cpu_baseline leg.  The product never imports it.
+
+Two layers, both restating the reference's semantics independently of the
+product code:
+
+* `liboracle.so` (splink_oracle.c): Jaro-Winkler (commons-text 1.4, UTF-16
+  units), Levenshtein (Spark, code points), the standard comparison templates,
+  the E-step and the M-step sufficient statistics, OpenMP-parallel.
+* this module: the reference's SQL semantics for blocking and arbitrary CASE
+  expressions, executed by sqlite with the C functions registered as UDFs
+  (blocking.py:95-160,219-268; gammas.py:65-89), and the EM driver loop
+  (iterate.py:37-63, maximisation_step.py:16-117, params.py:248-336).
+
+Pinned by the reference-generated fixtures in tests/golden/ (see
+tests/test_oracle_golden.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sqlite3
+import subprocess
+
+import numpy as np
+import pandas as pd
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return _LIB_PATH
+
+
+def _lib():
+    global _LIB
+    try:
+        return _LIB
+    except NameError:
+        pass
+    if not os.path.exists(_LIB_PATH):
+        build()
+    lib = ctypes.CDLL(_LIB_PATH)
+    lib.orc_jaro_winkler_u16.restype = ctypes.c_double
+    lib.orc_jaro_winkler_u16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+    lib.orc_levenshtein_u32.restype = ctypes.c_int64
+    lib.orc_levenshtein_u32.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+    lib.orc_gammas.restype = ctypes.c_int
+    lib.orc_em_stats.restype = ctypes.c_int
+    lib.orc_score.restype = None
+    _LIB = lib
+    return lib
+
+
+def _u16(s: str) -> np.ndarray:
+    return np.frombuffer(s.encode("utf-16-le", "surrogatepass"), dtype=np.uint16)
+
+
+def _u32(s: str) -> np.ndarray:
+    return np.array([ord(c) for c in s], dtype=np.uint32)
+
+
+def jaro_winkler(a, b):
+    if a is None or b is None:
+        return None
+    x, y = _u16(a), _u16(b)
+    return _lib().orc_jaro_winkler_u16(x.ctypes.data, len(x), y.ctypes.data, len(y))
+
+
+def levenshtein(a, b):
+    if a is None or b is None:
+        return None
+    x, y = _u32(a), _u32(b)
+    return int(_lib().orc_levenshtein_u32(x.ctypes.data, len(x), y.ctypes.data, len(y)))
+
+
+# ------------------------------------------------------------------------------------
+# string columns for the bulk template path
+# ------------------------------------------------------------------------------------
+class _StrColC(ctypes.Structure):
+    _fields_ = [("u16", ctypes.c_void_p), ("off16", ctypes.c_void_p), ("u32", ctypes.c_void_p),
+                ("off32", ctypes.c_void_p), ("valid", ctypes.c_void_p)]
+
+
+class StrCol:
+    """A string column encoded as UTF-16 units and code points (the JW / Levenshtein alphabets)."""
+
+    def __init__(self, values):
+        vals = [None if (v is None or (isinstance(v, float) and np.isnan(v))) else str(v) for v in values]
+        self.valid = np.array([v is not None for v in vals], dtype=np.uint8)
+        u16 = [_u16(v) if v is not None else np.zeros(0, np.uint16) for v in vals]
+        u32 = [_u32(v) if v is not None else np.zeros(0, np.uint32) for v in vals]
+        self.off16 = np.zeros(len(vals) + 1, dtype=np.int64)
+        self.off32 = np.zeros(len(vals) + 1, dtype=np.int64)
+        self.off16[1:] = np.cumsum([len(a) for a in u16])
+        self.off32[1:] = np.cumsum([len(a) for a in u32])
+        self.u16 = np.concatenate(u16 + [np.zeros(1, np.uint16)])
+        self.u32 = np.concatenate(u32 + [np.zeros(1, np.uint32)])
+        self.c = _StrColC(self.u16.ctypes.data, self.off16.ctypes.data, self.u32.ctypes.data,
+                          self.off32.ctypes.data, self.valid.ctypes.data)
+
+
+KIND = {"eq": 0, "jw": 1, "lev": 2}
+
+
+def template_gammas(specs, cols_l, cols_r, pl, pr):
+    """gammas (int8 [P, K]) for standard templates.  specs: [(kind, num_levels, thresholds)]."""
+    K = len(specs)
+    kinds = np.array([KIND[s[0]] for s in specs], dtype=np.int32)
+    nlev = np.array([s[1] for s in specs], dtype=np.int32)
+    thr = np.zeros((K, 3), dtype=np.float64)
+    for k, s in enumerate(specs):
+        thr[k, :len(s[2])] = s[2]
+    arr_l = (_StrColC * K)(*[c.c for c in cols_l])
+    arr_r = arr_l if cols_r is cols_l else (_StrColC * K)(*[c.c for c in cols_r])
+    pl = np.ascontiguousarray(pl, dtype=np.int32)
+    pr = np.ascontiguousarray(pr, dtype=np.int32)
+    out = np.empty((len(pl), K), dtype=np.int8)
+    _lib().orc_gammas(ctypes.c_int(K), kinds.ctypes.data_as(ctypes.c_void_p), nlev.ctypes.data_as(ctypes.c_void_p),
+                      thr.ctypes.data_as(ctypes.c_void_p), ctypes.cast(arr_l, ctypes.c_void_p),
+                      ctypes.cast(arr_r, ctypes.c_void_p), ctypes.c_int64(len(pl)),
+                      pl.ctypes.data_as(ctypes.c_void_p), pr.ctypes.data_as(ctypes.c_void_p),
+                      out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+# ------------------------------------------------------------------------------------
+# E / M with Spark numeric semantics
+# ------------------------------------------------------------------------------------
+def quantise(p):
+    """`cast({p:.35f} as double)` (expectation_step.py:212)."""
+    return float(f"{p:.35f}")
+
+
+def f32(x):
+    """`cast(... as float)` (maximisation_step.py:19, 68-69)."""
+    return None if x is None else float(np.float32(x))
+
+
+def em_stats(gam, nlev, lam, m, u):
+    """Sufficient statistics of one E+M pass (layout documented in splink_oracle.c)."""
+    gam = np.ascontiguousarray(gam, dtype=np.int8)
+    nlev = np.ascontiguousarray(nlev, dtype=np.int32)
+    K = len(nlev)
+    mq = np.array([quantise(x) for row in m for x in row], dtype=np.float64)
+    uq = np.array([quantise(x) for row in u for x in row], dtype=np.float64)
+    n_stats = 3 + 4 * int(np.sum(nlev + 1))
+    out = np.zeros(n_stats, dtype=np.float64)
+    lamd = float(repr(lam))
+    one_minus = float(repr(1 - lam))
+    _lib().orc_em_stats(ctypes.c_int(K), nlev.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(gam.shape[0]),
+                        gam.ctypes.data_as(ctypes.c_void_p), ctypes.c_double(lamd), ctypes.c_double(one_minus),
+                        mq.ctypes.data_as(ctypes.c_void_p), uq.ctypes.data_as(ctypes.c_void_p),
+                        out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(0))
+    return out
+
+
+def score(gam, nlev, lam, m, u):
+    """Final E-step: match_probability per pair, NaN where the reference yields NULL."""
+    gam = np.ascontiguousarray(gam, dtype=np.int8)
+    nlev = np.ascontiguousarray(nlev, dtype=np.int32)
+    mq = np.array([quantise(x) for row in m for x in row], dtype=np.float64)
+    uq = np.array([quantise(x) for row in u for x in row], dtype=np.float64)
+    out = np.empty(gam.shape[0], dtype=np.float64)
+    _lib().orc_score(ctypes.c_int(len(nlev)), nlev.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(gam.shape[0]),
+                     gam.ctypes.data_as(ctypes.c_void_p), ctypes.c_double(float(repr(lam))),
+                     ctypes.c_double(float(repr(1 - lam))), mq.ctypes.data_as(ctypes.c_void_p),
+                     uq.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def m_step(stats, nlev):
+    """New λ and π from the statistics, with Spark's NULL / float32 semantics
+    (maximisation_step.py:16-90; params.py:248-274 drops level -1, absent levels -> 0)."""
+    S, rows, nn = stats[0], stats[1], stats[2]
+    lam = f32(S / rows) if (nn > 0 and rows > 0) else None
+    m_new, u_new = [], []
+    off = 0
+    for L in nlev:
+        slots = stats[3 + 4 * off: 3 + 4 * (off + L + 1)].reshape(L + 1, 4)
+        off += L + 1
+        valid = slots[1:]
+        den_ok = valid[:, 1].sum() > 0
+        den_m, den_u = valid[:, 2].sum(), valid[:, 3].sum()
+        mk, uk = [], []
+        for v in range(L):
+            r, nnv, sm, su = slots[v + 1]
+            if r == 0:
+                mk.append(0)
+                uk.append(0)
+                continue
+            if nnv == 0 or not den_ok:
+                mk.append(None)
+                uk.append(None)
+                continue
+            mk.append(f32(sm / den_m) if den_m != 0 else None)
+            uk.append(f32(su / den_u) if den_u != 0 else None)
+        m_new.append(mk)
+        u_new.append(uk)
+    return lam, m_new, u_new
+
+
+def em_iterate(gam, nlev, lam, m, u, max_iterations, em_convergence):
+    """iterate.py:37-63 on a gamma matrix; returns (history of (λ, m, u) after each M-step, final mp)."""
+    history = []
+    for _ in range(max_iterations):
+        stats = em_stats(gam, nlev, lam, m, u)
+        new_lam, new_m, new_u = m_step(stats, nlev)
+        old = [x for row in m for x in row] + [x for row in u for x in row]
+        new = [x for row in new_m for x in row] + [x for row in new_u for x in row]
+        lam, m, u = new_lam, new_m, new_u
+        history.append((lam, [list(r) for r in m], [list(r) for r in u]))
+        if all(abs(a - b) < em_convergence for a, b in zip(new, old)):  # params.py:316-336
+            break
+    return history, score(gam, nlev, lam, m, u)
+
+
+# ------------------------------------------------------------------------------------
+# Reference SQL semantics through sqlite (small inputs)
+# ------------------------------------------------------------------------------------
+def _length(s):
+    return None if s is None else float(len(s))
+
+
+def _lev(a, b):
+    v = levenshtein(a, b)
+    return None if v is None else float(v)
+
+
+def connect():
+    con = sqlite3.connect(":memory:")
+    con.create_function("jaro_winkler_sim", 2, jaro_winkler, deterministic=True)
+    con.create_function("levenshtein", 2, _lev, deterministic=True)
+    con.create_function("length", 1, _length, deterministic=True)
+    return con
+
+
+def block(settings, df=None, df_l=None, df_r=None):
+    """Candidate pairs as (row_l, row_r) indices into the (possibly concatenated) tables.
+
+    Restates blocking.py:95-160 / 219-268: one inner join per rule, each excluding pairs an
+    earlier rule already produced (`AND NOT (ifnull((rule_j), false) ...)`), plus the link-type
+    predicate.  Returns (pairs DataFrame, left table, right table)."""
+    con = connect()
+    lt = settings["link_type"]
+    uid = settings.get("unique_id_column_name", "unique_id")
+    if lt == "dedupe_only":
+        left = right = df.reset_index(drop=True)
+    elif lt == "link_only":
+        left, right = df_l.reset_index(drop=True), df_r.reset_index(drop=True)
+    else:
+        left = pd.concat([df_l.assign(_source_table="left"), df_r.assign(_source_table="right")],
+                         ignore_index=True)
+        right = left
+    left.assign(_row=np.arange(len(left))).to_sql("tl", con, index=False)
+    right.assign(_row=np.arange(len(right))).to_sql("tr", con, index=False)
+    if lt == "dedupe_only":
+        where = f"where l.{uid} < r.{uid}"
+    elif lt == "link_only":
+        where = ""
+    else:
+        where = (f"where (l._source_table < r._source_table) or "
+                 f"(l.{uid} < r.{uid} and l._source_table = r._source_table)")
+    rules = settings.get("blocking_rules") or []
+    parts = []
+    if not rules:
+        parts.append(f"select l._row as row_l, r._row as row_r from tl l cross join tr r {where}")
+    for k, rule in enumerate(rules):
+        prev = " or ".join(f"ifnull(({p}), 0)" for p in rules[:k])
+        notprev = f"and not ({prev})" if prev else ""
+        parts.append(f"select l._row as row_l, r._row as row_r from tl l inner join tr r on {rule} {notprev} {where}")
+    pairs = pd.read_sql(" union all ".join(parts), con)
+    return pairs, left, right
+
+
+def comparison_frame(pairs, left, right):
+    l = left.iloc[pairs["row_l"].to_numpy()].reset_index(drop=True).add_suffix("_l")
+    r = right.iloc[pairs["row_r"].to_numpy()].reset_index(drop=True).add_suffix("_r")
+    return pd.concat([l, r], axis=1)
+
+
+def sql_gammas(cmp_df, case_expressions):
+    """Evaluate each CASE expression over the comparison frame with sqlite (gammas.py:65-89)."""
+    con = connect()
+    cmp_df = cmp_df.copy()
+    for c in cmp_df.columns:
+        if cmp_df[c].dtype == object:
+            cmp_df[c] = cmp_df[c].where(cmp_df[c].notna(), None)
+    cmp_df.to_sql("cmp", con, index=False)
+    out = np.empty((len(cmp_df), len(case_expressions)), dtype=np.int8)
+    for k, expr in enumerate(case_expressions):
+        e = _strip_alias(expr)
+        vals = [r[0] for r in con.execute(f"select {e} from cmp").fetchall()]
+        out[:, k] = np.array([-99 if v is None else v for v in vals], dtype=np.int64)
+    return out
+
+
+def _strip_alias(expr):
+    s = " ".join(expr.split())
+    low = s.lower()
+    i = low.rfind(" end")
+    return s[: i + 4] if i >= 0 else s
+
+
+def _bayes(ps):
+    """term_frequencies.py:21-46: Πp / (Πp + Π(1-p)), products left-associative; x/0 -> NULL."""
+    a = ps[0]
+    for p in ps[1:]:
+        a = a * p
+    b = 1.0 - ps[0]
+    for p in ps[1:]:
+        b = b * (1.0 - p)
+    d = a + b
+    return float("nan") if d == 0 else a / d
+
+
+def tf_adjust(cols_l, cols_r, mp, lam):
+    """make_adjustment_for_term_frequencies (term_frequencies.py:122-168).
+
+    cols_l / cols_r: list (one per tf column) of per-pair values; mp: per-pair match probability
+    (NaN = NULL).  Returns (tf_adjusted_match_prob, [per-column *_adj])."""
+    one_minus = float(repr(1 - lam))
+    adjs = []
+    for vl, vr in zip(cols_l, cols_r):
+        acc = {}
+        for a, b, p in zip(vl, vr, mp):
+            if a is None or b is None or a != b:
+                continue
+            s = acc.setdefault(a, [0.0, 0])
+            if not np.isnan(p):
+                s[0] += p
+                s[1] += 1
+        lookup = {}
+        for v, (s, n) in acc.items():
+            lookup[v] = float("nan") if n == 0 else _bayes([s / n, one_minus])
+        col = []
+        for a, b in zip(vl, vr):
+            x = lookup.get(a) if (a is not None and b is not None and a == b) else None
+            col.append(0.5 if x is None or np.isnan(x) else x)
+        adjs.append(np.array(col, dtype=np.float64))
+    out = np.array([float("nan") if np.isnan(p) else _bayes([p] + [c[i] for c in adjs])
+                    for i, p in enumerate(mp)], dtype=np.float64)
+    return out, adjs
