@@ -1,0 +1,200 @@
+/*
+ * splink_hip.h -- C ABI of libsplink_hip.so, the MI355X (gfx950) execution engine for
+ * splink's pairwise-comparison + EM hot path.
+ *
+ * The reference (splink 0.1.7) has no native boundary: every stage is a Python
+ * function that emits Spark SQL.  These entry points replace the
+ * Spark execution (L0) of those stages; the Python layer in splink_amd/ keeps the
+ * reference's stage-function API and calls them through ctypes.  Each entry point
+ * names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Every function returns SPK_OK (0) or a negative SPK_E_* code; spk_last_error()
+ *     gives a thread-local message.
+ *   - Host buffers passed in are BORROWED for the duration of the call; outputs are
+ *     caller-allocated.  Device state is owned by the context.
+ *   - A context is bound to one HIP device and one stream and is not re-entrant;
+ *     callers serialise.  Multi-GPU = one process (one context) per GPU; the only
+ *     cross-GPU exchange is the EM pattern histogram (spk_em_histogram writes it to a
+ *     caller-provided device buffer, the caller all-reduces it, spk_em_finalize reads it).
+ */
+#ifndef SPLINK_HIP_H
+#define SPLINK_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPK_OK 0
+#define SPK_E_INVALID (-1) /* bad argument / shape (Python: ValueError) */
+#define SPK_E_HIP (-2)     /* HIP runtime failure */
+#define SPK_E_OOM (-3)     /* device allocation failed */
+#define SPK_E_STATE (-4)   /* call out of order (e.g. gammas before pairs) */
+#define SPK_E_LIMIT (-5)   /* input beyond a supported limit (e.g. string length) */
+
+#define SPK_LINK_DEDUPE 0        /* "dedupe_only"     */
+#define SPK_LINK_ONLY 1          /* "link_only"       */
+#define SPK_LINK_AND_DEDUPE 2    /* "link_and_dedupe" */
+
+typedef struct spk_ctx spk_ctx;
+
+const char *spk_last_error(void);
+int spk_version(void);
+int spk_device_count(int *out);
+
+/* ---- context ------------------------------------------------------------------ */
+int spk_ctx_create(int device, spk_ctx **out);
+void spk_ctx_destroy(spk_ctx *ctx);
+/* Run all work on `hip_stream` (a hipStream_t; NULL = the context's own stream). */
+int spk_ctx_set_stream(spk_ctx *ctx, void *hip_stream);
+int spk_ctx_sync(spk_ctx *ctx);
+/* Link type of the loaded tables (needed before spk_pairs_load / spk_gammas when spk_block is not used). */
+int spk_ctx_set_link_type(spk_ctx *ctx, int link_type);
+/* Elapsed milliseconds of the last launch of each kernel family, measured with HIP events
+ * on the context stream: [0] block, [1] gamma, [2] em_hist, [3] em_final, [4] score. */
+int spk_ctx_kernel_ms(spk_ctx *ctx, double *out5);
+int spk_ctx_enable_timing(spk_ctx *ctx, int on);
+
+/* ---- record tables (replaces createOrReplaceTempView of df / df_l / df_r,
+ *      blocking.py:209-222, and the vertical concatenation of :70-93) ------------ */
+/* side 0 = df (dedupe_only, link_and_dedupe after concatenation) or df_l; side 1 = df_r. */
+int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols);
+/* String column from Arrow-style UTF-8: offsets[n_rows+1] into data; valid[n_rows] (1 = non-null).
+ * Decoded on the device to UTF-16 code units (Jaro-Winkler alphabet) + code-point lengths. */
+int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, const uint8_t *data,
+                       const uint8_t *valid);
+int spk_table_add_float64(spk_ctx *ctx, int side, int col, const double *values, const uint8_t *valid);
+/* Order rank per row for the link-type predicate: dedupe `l.uid < r.uid` (blocking.py:136),
+ * link_and_dedupe `(l.src < r.src) or (l.uid < r.uid and same src)` (:139).  Equal rank = equal key. */
+int spk_table_set_rank(spk_ctx *ctx, int side, const int64_t *rank);
+/* Blocking key ids of rule `rule` for each row (-1 = NULL: the row never matches the rule).
+ * which = 0: key of the row as the join's l-side; which = 1: as the r-side. */
+int spk_table_set_key(spk_ctx *ctx, int side, int rule, int which, const int64_t *keys);
+
+/* ---- blocking (replaces block_using_rules / cartesian_block, blocking.py:162-318) -- */
+/* Generates candidate pairs for rules 0..n_rules-1 in order, each excluding pairs an earlier
+ * rule matched (`AND NOT ifnull(rule_j, false)`, :59-68), with the link-type predicate.
+ * rule_symmetric[r] = 1 when the rule's l- and r-side keys are the same function of a row.
+ * Pairs are generated for the shard [shard/n_shards] of the global candidate-ordinal space
+ * and stay on the device (int32 row indices). */
+int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t *rule_symmetric, int shard,
+              int n_shards, int64_t *out_n_pairs, int64_t *out_n_candidates_total);
+int spk_pairs_count(spk_ctx *ctx, int64_t *out);
+int spk_pairs_copy(spk_ctx *ctx, int64_t start, int64_t count, int32_t *out_l, int32_t *out_r);
+/* Use caller-provided pairs (e.g. add_gammas on an externally built comparison frame). */
+int spk_pairs_load(spk_ctx *ctx, int64_t n, const int32_t *rows_l, const int32_t *rows_r);
+
+/* ---- comparison programs (replaces add_gammas / the CASE templates,
+ *      gammas.py:65-124, case_statements.py:62-277) ----------------------------- */
+/* Operand of a predicate: a column of the pair's l- or r-record, or a literal, with an
+ * optional ifnull() default and an optional substr(start, len) (code points, Spark rules). */
+typedef struct {
+    int32_t kind;        /* 0 column, 1 string literal, 2 number literal */
+    int32_t side;        /* 0 = `_l` record, 1 = `_r` record */
+    int32_t col;         /* column index in the side's table */
+    int32_t lit;         /* string literal index (kind 1) or ifnull default string (-1 none) */
+    double num;          /* number literal (kind 2) or ifnull default number */
+    int32_t has_num_default;
+    int32_t substr_start; /* 1-based Spark substr position; 0 = no substr */
+    int32_t substr_len;
+    int32_t pad;
+} spk_operand;
+
+/* Predicate instruction (RPN over Kleene booleans). */
+#define SPK_OP_ISNULL 1     /* a IS NULL */
+#define SPK_OP_NOTNULL 2    /* a IS NOT NULL */
+#define SPK_OP_STR_CMP 3    /* a cmp b (strings; = / != / < / <= / > / >=, UTF-8 byte order) */
+#define SPK_OP_NUM_CMP 4    /* a cmp b (numbers) */
+#define SPK_OP_JW 5         /* jaro_winkler_sim(a, b) cmp t */
+#define SPK_OP_LEV 6        /* levenshtein(a, b) cmp t */
+#define SPK_OP_LEVRATIO 7   /* levenshtein(a,b)/((length(a)+length(b))/2) cmp t */
+#define SPK_OP_ABSDIFF 8    /* abs(a - b) cmp t */
+#define SPK_OP_PERCDIFF 9   /* abs(a - b)/abs(case when a > b then a else b end) cmp t */
+#define SPK_OP_CONST 10     /* constant: i0 = 0 false, 1 true, 2 null */
+#define SPK_OP_AND 20
+#define SPK_OP_OR 21
+#define SPK_OP_NOT 22
+#define SPK_OP_LEN 11       /* length(a) cmp t */
+
+#define SPK_CMP_EQ 0
+#define SPK_CMP_NE 1
+#define SPK_CMP_LT 2
+#define SPK_CMP_LE 3
+#define SPK_CMP_GT 4
+#define SPK_CMP_GE 5
+
+typedef struct {
+    int32_t op;
+    int32_t a, b;   /* operand indices */
+    int32_t cmp;    /* SPK_CMP_* */
+    int32_t i0;
+    int32_t pad;
+    double t;       /* threshold */
+} spk_instr;
+
+typedef struct {
+    int32_t n_levels;    /* L_k; gamma values are -1..L_k-1 */
+    int32_t else_level;
+    int32_t n_when;
+    int32_t first_when;  /* index into the when arrays */
+} spk_column_program;
+
+/* Install the comparison programs and evaluate them over the current pairs, producing one
+ * packed comparison-vector code per pair: code = Σ_k (γ_k + 1) · Π_{j<k} (L_j + 1). */
+int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *cols, int n_when,
+               const int32_t *when_first_instr, const int32_t *when_n_instr, const int32_t *when_level,
+               int n_instr, const spk_instr *instr, int n_operands, const spk_operand *operands,
+               int n_lits, const int64_t *lit_offsets, const uint8_t *lit_utf8);
+/* Decode codes to int8 gamma columns, [count x K] row-major. */
+int spk_gammas_copy(spk_ctx *ctx, int64_t start, int64_t count, int8_t *out);
+/* Use a caller-provided gamma matrix (int8 [n x K], values -1..L_k-1). */
+int spk_gammas_load(spk_ctx *ctx, int n_cols, const int32_t *n_levels, int64_t n, const int8_t *gammas);
+int spk_n_patterns(spk_ctx *ctx, int64_t *out);
+/* Pairs the last spk_gammas evaluated in the global-memory pass (strings beyond LDS staging). */
+int spk_gammas_deferred(spk_ctx *ctx, int64_t *out);
+
+/* ---- the jar's similarity UDFs as bulk device functions ---------------------------------
+ * spk_jaro_winkler_sim replaces uk.gov.moj.dash.linkage.JaroWinklerSimilarity.call(String, String)
+ * (commons-text 1.4 JaroWinklerDistance.apply, registered as `jaro_winkler_sim`, tests/test_spark.py:45);
+ * spk_levenshtein replaces Spark's levenshtein(l, r) (case_statements.py:121).  n pairs of UTF-8 strings
+ * (Arrow offsets, no NULLs), results in out[n] (host).  Same device code as the comparison kernel. */
+int spk_jaro_winkler_sim(spk_ctx *ctx, int64_t n, const int64_t *l_offsets, const uint8_t *l_utf8,
+                         const int64_t *r_offsets, const uint8_t *r_utf8, double *out);
+int spk_levenshtein(spk_ctx *ctx, int64_t n, const int64_t *l_offsets, const uint8_t *l_utf8,
+                    const int64_t *r_offsets, const uint8_t *r_utf8, double *out);
+
+/* ---- EM (replaces run_expectation_step + run_maximisation_step's aggregate,
+ *      expectation_step.py:25-221, maximisation_step.py:41-90) ------------------ */
+/* Streams every pair's code once and writes the pattern histogram (uint64 [n_patterns]) to
+ * d_hist, a DEVICE buffer (NULL = context-owned).  The histogram is the sufficient statistic of
+ * the E+M step; callers sharding pairs over GPUs all-reduce it (exact integer sum). */
+int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist);
+/* E-step per pattern with the reference's literal arithmetic, then the M-step sums:
+ * out_stats (host) = [Σmp, rows, non-null rows, Σ ln(λΠm + (1-λ)Πu), non-null ln rows] + per column k,
+ * per level v in -1..L_k-1:
+ * [rows, non-null rows, Σmp, Σ(1-mp)].  m/u are flattened [Σ L_k], already quantised as
+ * `cast({p:.35f} as double)`; lambda/one_minus are `cast({λ} as double)`/`cast({1-λ} as double)`. */
+int spk_em_finalize(spk_ctx *ctx, const uint64_t *d_hist, double lambda, double one_minus, const double *m,
+                    const double *u, double *out_stats, int n_stats);
+/* Final E-step: match_probability per pair (NaN = NULL).  out_mp = host buffer for
+ * [start, start+count), or NULL to keep the result on the device only. */
+int spk_score(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u, int64_t start,
+              int64_t count, double *out_mp);
+
+/* ---- term-frequency adjustment (term_frequencies.py:122-168) ------------------- */
+/* For value ids of one column (per row, -1 NULL; both sides in one id space) accumulate, over
+ * pairs with equal non-null values, Σ mp and count(mp) per value id (n_values slots). */
+int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
+                      double *out_sum, int64_t *out_count);
+/* tf_adjusted_match_prob = bayes(mp, adj_1, ..., adj_n) (:98-117) with adj_c = table_c[id] for pairs
+ * with equal non-null values and 0.5 otherwise.  out (host) [start, start+count). */
+int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0, const int64_t *const *ids_side1,
+                 const double *const *adj_tables, const int64_t *table_sizes, int64_t start, int64_t count,
+                 double *out_tf_mp, double *out_adj /* [count x n_tf_cols] or NULL */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPLINK_HIP_H */

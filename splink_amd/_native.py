@@ -1,0 +1,290 @@
+"""ctypes binding to libsplink_hip.so (the C ABI declared in include/splink_hip.h).
+
+There is no CPU fallback: if the library or a gfx950 device is missing, every product
+entry point raises `NativeUnavailable`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SPLINK_AMD_LIB", os.path.join(_HERE, "libsplink_hip.so"))
+
+SPK_OK = 0
+SPK_E_INVALID = -1
+SPK_E_HIP = -2
+SPK_E_OOM = -3
+SPK_E_STATE = -4
+SPK_E_LIMIT = -5
+
+LINK_TYPES = {"dedupe_only": 0, "link_only": 1, "link_and_dedupe": 2}
+
+# ---- C structs mirrored as numpy structured dtypes (same layout as splink_hip.h) ----------
+OPERAND_DTYPE = np.dtype([("kind", "<i4"), ("side", "<i4"), ("col", "<i4"), ("lit", "<i4"), ("num", "<f8"),
+                          ("has_num_default", "<i4"), ("substr_start", "<i4"), ("substr_len", "<i4"),
+                          ("pad", "<i4")], align=True)
+INSTR_DTYPE = np.dtype([("op", "<i4"), ("a", "<i4"), ("b", "<i4"), ("cmp", "<i4"), ("i0", "<i4"), ("pad", "<i4"),
+                        ("t", "<f8")], align=True)
+PROGRAM_DTYPE = np.dtype([("n_levels", "<i4"), ("else_level", "<i4"), ("n_when", "<i4"), ("first_when", "<i4")],
+                         align=True)
+assert OPERAND_DTYPE.itemsize == 40 and INSTR_DTYPE.itemsize == 32 and PROGRAM_DTYPE.itemsize == 16
+
+OP = {"ISNULL": 1, "NOTNULL": 2, "STR_CMP": 3, "NUM_CMP": 4, "JW": 5, "LEV": 6, "LEVRATIO": 7, "ABSDIFF": 8,
+      "PERCDIFF": 9, "CONST": 10, "LEN": 11, "AND": 20, "OR": 21, "NOT": 22}
+CMP = {"=": 0, "==": 0, "!=": 1, "<>": 1, "<": 2, "<=": 3, ">": 4, ">=": 5}
+
+EXPORTS = [
+    "spk_last_error", "spk_version", "spk_device_count", "spk_ctx_create", "spk_ctx_destroy", "spk_ctx_set_stream",
+    "spk_ctx_sync", "spk_ctx_set_link_type", "spk_ctx_kernel_ms", "spk_ctx_enable_timing", "spk_table_create",
+    "spk_table_add_utf8", "spk_table_add_float64", "spk_table_set_rank", "spk_table_set_key", "spk_block",
+    "spk_pairs_count", "spk_pairs_copy", "spk_pairs_load", "spk_gammas", "spk_gammas_copy", "spk_gammas_load",
+    "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
+    "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein",
+]
+
+
+class NativeUnavailable(RuntimeError):
+    """libsplink_hip.so or a gfx950 HIP device is unavailable (there is no CPU fallback)."""
+
+
+_lib = None
+
+
+def load_library():
+    """Load libsplink_hip.so (no device needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeUnavailable(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.spk_last_error.restype = ctypes.c_char_p
+    lib.spk_ctx_destroy.restype = None
+    for name in EXPORTS:
+        getattr(lib, name)  # raises AttributeError when a declared symbol is missing
+    _lib = lib
+    return lib
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int(0)
+    lib.spk_device_count(ctypes.byref(n))
+    return n.value
+
+
+def _ptr(a):
+    return ctypes.c_void_p(0) if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def check(rc: int, what: str):
+    if rc == SPK_OK:
+        return
+    msg = load_library().spk_last_error().decode("utf-8", "replace")
+    if rc in (SPK_E_INVALID, SPK_E_LIMIT):
+        raise ValueError(f"{what}: {msg}")
+    raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+class Context:
+    """One spk_ctx: one device, one stream, one set of tables / pairs / codes."""
+
+    def __init__(self, device: int = 0):
+        lib = load_library()
+        if device_count() <= device:
+            raise NativeUnavailable(f"no HIP device {device} visible (splink_amd needs an MI355X / gfx950)")
+        h = ctypes.c_void_p()
+        check(lib.spk_ctx_create(ctypes.c_int(device), ctypes.byref(h)), "spk_ctx_create")
+        self._h = h
+        self._lib = lib
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.spk_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- calls ------------------------------------------------------------------------
+    def set_stream(self, stream_ptr: int):
+        check(self._lib.spk_ctx_set_stream(self._h, ctypes.c_void_p(stream_ptr)), "spk_ctx_set_stream")
+
+    def sync(self):
+        check(self._lib.spk_ctx_sync(self._h), "spk_ctx_sync")
+
+    def set_link_type(self, link_type: int):
+        check(self._lib.spk_ctx_set_link_type(self._h, ctypes.c_int(link_type)), "spk_ctx_set_link_type")
+
+    def enable_timing(self, on: bool = True):
+        check(self._lib.spk_ctx_enable_timing(self._h, ctypes.c_int(1 if on else 0)), "spk_ctx_enable_timing")
+
+    def kernel_ms(self):
+        out = np.zeros(5, dtype=np.float64)
+        check(self._lib.spk_ctx_kernel_ms(self._h, _ptr(out)), "spk_ctx_kernel_ms")
+        return dict(zip(["block", "gamma", "em_hist", "em_final", "score"], out.tolist()))
+
+    def table_create(self, side: int, n_rows: int, n_cols: int):
+        check(self._lib.spk_table_create(self._h, ctypes.c_int(side), ctypes.c_int64(n_rows), ctypes.c_int(n_cols)),
+              "spk_table_create")
+
+    def table_add_utf8(self, side, col, offsets, data, valid):
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, dtype=np.uint8)
+        valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        check(self._lib.spk_table_add_utf8(self._h, ctypes.c_int(side), ctypes.c_int(col), _ptr(offsets), _ptr(data),
+                                           _ptr(valid)), "spk_table_add_utf8")
+
+    def table_add_float64(self, side, col, values, valid):
+        values = np.ascontiguousarray(values, dtype=np.float64)
+        valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        check(self._lib.spk_table_add_float64(self._h, ctypes.c_int(side), ctypes.c_int(col), _ptr(values),
+                                              _ptr(valid)), "spk_table_add_float64")
+
+    def table_set_rank(self, side, rank):
+        rank = np.ascontiguousarray(rank, dtype=np.int64)
+        check(self._lib.spk_table_set_rank(self._h, ctypes.c_int(side), _ptr(rank)), "spk_table_set_rank")
+
+    def table_set_key(self, side, rule, which, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        check(self._lib.spk_table_set_key(self._h, ctypes.c_int(side), ctypes.c_int(rule), ctypes.c_int(which),
+                                          _ptr(keys)), "spk_table_set_key")
+
+    def block(self, link_type: int, symmetric, shard: int = 0, n_shards: int = 1):
+        sym = np.ascontiguousarray(symmetric, dtype=np.int32)
+        n_pairs = ctypes.c_int64(0)
+        n_total = ctypes.c_int64(0)
+        check(self._lib.spk_block(self._h, ctypes.c_int(link_type), ctypes.c_int(len(sym)), _ptr(sym),
+                                  ctypes.c_int(shard), ctypes.c_int(n_shards), ctypes.byref(n_pairs),
+                                  ctypes.byref(n_total)), "spk_block")
+        return n_pairs.value, n_total.value
+
+    def pairs_count(self) -> int:
+        n = ctypes.c_int64(0)
+        check(self._lib.spk_pairs_count(self._h, ctypes.byref(n)), "spk_pairs_count")
+        return n.value
+
+    def pairs_copy(self, start: int = 0, count: int | None = None):
+        if count is None:
+            count = self.pairs_count() - start
+        l = np.empty(count, dtype=np.int32)
+        r = np.empty(count, dtype=np.int32)
+        check(self._lib.spk_pairs_copy(self._h, ctypes.c_int64(start), ctypes.c_int64(count), _ptr(l), _ptr(r)),
+              "spk_pairs_copy")
+        return l, r
+
+    def pairs_load(self, rows_l, rows_r):
+        rows_l = np.ascontiguousarray(rows_l, dtype=np.int32)
+        rows_r = np.ascontiguousarray(rows_r, dtype=np.int32)
+        check(self._lib.spk_pairs_load(self._h, ctypes.c_int64(len(rows_l)), _ptr(rows_l), _ptr(rows_r)),
+              "spk_pairs_load")
+
+    def gammas(self, programs, when_first, when_n, when_level, instrs, operands, lit_offsets, lit_bytes):
+        programs = np.ascontiguousarray(programs, dtype=PROGRAM_DTYPE)
+        wf = np.ascontiguousarray(when_first, dtype=np.int32)
+        wn = np.ascontiguousarray(when_n, dtype=np.int32)
+        wl = np.ascontiguousarray(when_level, dtype=np.int32)
+        instrs = np.ascontiguousarray(instrs, dtype=INSTR_DTYPE)
+        operands = np.ascontiguousarray(operands, dtype=OPERAND_DTYPE)
+        lo = np.ascontiguousarray(lit_offsets, dtype=np.int64)
+        lb = np.ascontiguousarray(lit_bytes, dtype=np.uint8)
+        if lb.size == 0:
+            lb = np.zeros(1, dtype=np.uint8)
+        check(self._lib.spk_gammas(self._h, ctypes.c_int(len(programs)), _ptr(programs), ctypes.c_int(len(wf)),
+                                   _ptr(wf), _ptr(wn), _ptr(wl), ctypes.c_int(len(instrs)), _ptr(instrs),
+                                   ctypes.c_int(len(operands)), _ptr(operands), ctypes.c_int(len(lo) - 1), _ptr(lo),
+                                   _ptr(lb)), "spk_gammas")
+
+    def gammas_load(self, n_levels, gammas):
+        nl = np.ascontiguousarray(n_levels, dtype=np.int32)
+        g = np.ascontiguousarray(gammas, dtype=np.int8)
+        check(self._lib.spk_gammas_load(self._h, ctypes.c_int(len(nl)), _ptr(nl), ctypes.c_int64(g.shape[0]), _ptr(g)),
+              "spk_gammas_load")
+
+    def gammas_copy(self, K: int, start: int, count: int):
+        out = np.empty((count, K), dtype=np.int8)
+        check(self._lib.spk_gammas_copy(self._h, ctypes.c_int64(start), ctypes.c_int64(count), _ptr(out)),
+              "spk_gammas_copy")
+        return out
+
+    def n_patterns(self) -> int:
+        n = ctypes.c_int64(0)
+        check(self._lib.spk_n_patterns(self._h, ctypes.byref(n)), "spk_n_patterns")
+        return n.value
+
+    def gammas_deferred(self) -> int:
+        n = ctypes.c_int64(0)
+        check(self._lib.spk_gammas_deferred(self._h, ctypes.byref(n)), "spk_gammas_deferred")
+        return n.value
+
+    def em_histogram(self, d_hist_ptr: int = 0):
+        check(self._lib.spk_em_histogram(self._h, ctypes.c_void_p(d_hist_ptr)), "spk_em_histogram")
+
+    def em_finalize(self, d_hist_ptr, lam, one_minus, m, u, n_stats):
+        m = np.ascontiguousarray(m, dtype=np.float64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        out = np.zeros(n_stats, dtype=np.float64)
+        check(self._lib.spk_em_finalize(self._h, ctypes.c_void_p(d_hist_ptr), ctypes.c_double(lam),
+                                        ctypes.c_double(one_minus), _ptr(m), _ptr(u), _ptr(out),
+                                        ctypes.c_int(n_stats)), "spk_em_finalize")
+        return out
+
+    def score(self, lam, one_minus, m, u, start=0, count=0, want_host=True):
+        m = np.ascontiguousarray(m, dtype=np.float64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        out = np.empty(count, dtype=np.float64) if want_host else None
+        check(self._lib.spk_score(self._h, ctypes.c_double(lam), ctypes.c_double(one_minus), _ptr(m), _ptr(u),
+                                  ctypes.c_int64(start), ctypes.c_int64(count), _ptr(out)), "spk_score")
+        return out
+
+    def _udf(self, fn, left, right):
+        from .table import encode_utf8
+        import pandas as pd
+        lo, ld, _ = encode_utf8(pd.Series(list(left), dtype=object))
+        ro, rd, _ = encode_utf8(pd.Series(list(right), dtype=object))
+        ld = ld if ld.size else np.zeros(1, np.uint8)
+        rd = rd if rd.size else np.zeros(1, np.uint8)
+        out = np.empty(len(lo) - 1, dtype=np.float64)
+        check(getattr(self._lib, fn)(self._h, ctypes.c_int64(len(out)), _ptr(lo), _ptr(ld), _ptr(ro), _ptr(rd),
+                                     _ptr(out)), fn)
+        return out
+
+    def jaro_winkler_sim(self, left, right):
+        return self._udf("spk_jaro_winkler_sim", left, right)
+
+    def levenshtein(self, left, right):
+        return self._udf("spk_levenshtein", left, right)
+
+    def tf_accumulate(self, n_values, ids0, ids1):
+        ids0 = np.ascontiguousarray(ids0, dtype=np.int64)
+        ids1 = np.ascontiguousarray(ids1, dtype=np.int64)
+        s = np.zeros(max(n_values, 1), dtype=np.float64)
+        c = np.zeros(max(n_values, 1), dtype=np.int64)
+        check(self._lib.spk_tf_accumulate(self._h, ctypes.c_int64(n_values), _ptr(ids0), _ptr(ids1), _ptr(s), _ptr(c)),
+              "spk_tf_accumulate")
+        return s[:n_values], c[:n_values]
+
+    def tf_apply(self, ids0_list, ids1_list, tables, start, count, want_adj=True):
+        n = len(tables)
+        keep = [np.ascontiguousarray(a, dtype=np.int64) for a in ids0_list] + \
+               [np.ascontiguousarray(a, dtype=np.int64) for a in ids1_list] + \
+               [np.ascontiguousarray(t, dtype=np.float64) if len(t) else np.zeros(1) for t in tables]
+        P = ctypes.c_void_p * n
+        ids0 = P(*[a.ctypes.data for a in keep[:n]])
+        ids1 = P(*[a.ctypes.data for a in keep[n:2 * n]])
+        tabs = P(*[a.ctypes.data for a in keep[2 * n:]])
+        sizes = np.array([len(t) for t in tables], dtype=np.int64)
+        out = np.empty(count, dtype=np.float64)
+        adj = np.empty((count, n), dtype=np.float64) if want_adj else None
+        check(self._lib.spk_tf_apply(self._h, ctypes.c_int(n), ids0, ids1, tabs, _ptr(sizes), ctypes.c_int64(start),
+                                     ctypes.c_int64(count), _ptr(out), _ptr(adj)), "spk_tf_apply")
+        return out, adj

@@ -1,0 +1,342 @@
+// Context, record-table upload (UTF-8 -> UTF-16 on the device) and pair buffers.
+#include <cstring>
+
+#include "spk_internal.h"
+
+namespace spk {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+Table::~Table() {
+    for (Column *c : cols) delete c;
+    for (int w = 0; w < 2; ++w)
+        for (DevBuf<int64_t> *k : key[w]) delete k;
+}
+
+int ensure_desc(spk_ctx *ctx, Table &t) {
+    if (!t.desc_dirty && t.d_desc.p) return SPK_OK;
+    std::vector<ColDesc> h(t.cols.size());
+    for (size_t i = 0; i < t.cols.size(); ++i) {
+        Column *c = t.cols[i];
+        ColDesc d{};
+        d.kind = c ? c->kind : COL_NONE;
+        if (c && c->kind == COL_STR) {
+            d.units = c->units.p;
+            d.off = c->off.p;
+            d.len16 = c->len16.p;
+            d.cplen = c->cplen.p;
+            d.hash = c->hash.p;
+        } else if (c && c->kind == COL_NUM) {
+            d.val = c->val.p;
+            d.valid = c->valid.p;
+        }
+        h[i] = d;
+    }
+    SPK_TRY(t.d_desc.alloc(h.size() ? h.size() : 1));
+    if (!h.empty())
+        SPK_HIP(hipMemcpyAsync(t.d_desc.p, h.data(), h.size() * sizeof(ColDesc), hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    t.desc_dirty = false;
+    return SPK_OK;
+}
+
+// One thread per row: decode the row's UTF-8 into UTF-16 units at its byte offset, count code
+// points, hash the units.  Surrogate-encoded (CESU / "surrogatepass") 3-byte sequences decode to
+// lone surrogate units, exactly as a Java String would hold them.
+__global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const uint8_t *__restrict__ bytes,
+                              const uint8_t *__restrict__ valid, uint16_t *__restrict__ units,
+                              int32_t *__restrict__ len16, int32_t *__restrict__ cplen, uint64_t *__restrict__ hash) {
+    int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= n) return;
+    if (!valid[row]) {
+        len16[row] = -1;
+        cplen[row] = -1;
+        hash[row] = 0;
+        return;
+    }
+    int64_t b = off8[row], e = off8[row + 1];
+    uint16_t *dst = units + b;
+    int32_t nu = 0, nc = 0;
+    uint64_t h = 1469598103934665603ull;
+    while (b < e) {
+        uint32_t c0 = bytes[b];
+        uint32_t cp;
+        int len;
+        if (c0 < 0x80) { cp = c0; len = 1; }
+        else if (c0 < 0xE0) { cp = c0 & 0x1F; len = 2; }
+        else if (c0 < 0xF0) { cp = c0 & 0x0F; len = 3; }
+        else { cp = c0 & 0x07; len = 4; }
+        for (int i = 1; i < len && b + i < e; ++i) cp = (cp << 6) | (bytes[b + i] & 0x3F);
+        b += len;
+        if (cp >= 0x10000) {
+            uint32_t v = cp - 0x10000;
+            uint16_t hi = (uint16_t)(0xD800 + (v >> 10)), lo = (uint16_t)(0xDC00 + (v & 0x3FF));
+            dst[nu++] = hi;
+            dst[nu++] = lo;
+            h = (h ^ hi) * 1099511628211ull;
+            h = (h ^ lo) * 1099511628211ull;
+        } else {
+            dst[nu++] = (uint16_t)cp;
+            h = (h ^ cp) * 1099511628211ull;
+        }
+        ++nc;
+    }
+    len16[row] = nu;
+    cplen[row] = nc;
+    hash[row] = h ^ (uint64_t)nu;
+}
+
+}  // namespace spk
+
+using namespace spk;
+
+int spk_ctx::begin(Kern k) {
+    if (!timing) return SPK_OK;
+    SPK_HIP(hipEventRecord(ev0[k], stream));
+    return SPK_OK;
+}
+int spk_ctx::end(Kern k) {
+    if (!timing) return SPK_OK;
+    SPK_HIP(hipEventRecord(ev1[k], stream));
+    ev_used[k] = true;
+    return SPK_OK;
+}
+
+extern "C" {
+
+const char *spk_last_error(void) { return g_last_error.c_str(); }
+int spk_version(void) { return 1; }
+
+int spk_device_count(int *out) {
+    SPK_REQUIRE(out, SPK_E_INVALID, "spk_device_count: null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return SPK_OK;
+}
+
+int spk_ctx_create(int device, spk_ctx **out) {
+    SPK_REQUIRE(out, SPK_E_INVALID, "spk_ctx_create: null out");
+    int n = 0;
+    SPK_HIP(hipGetDeviceCount(&n));
+    SPK_REQUIRE(device >= 0 && device < n, SPK_E_INVALID, "spk_ctx_create: no such HIP device");
+    SPK_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    SPK_HIP(hipGetDeviceProperties(&prop, device));
+    SPK_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, SPK_E_INVALID,
+                std::string("libsplink_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
+    spk_ctx *c = new spk_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        set_error(std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        return SPK_E_HIP;
+    }
+    c->stream = c->own_stream;
+    for (int k = 0; k < K_COUNT; ++k) {
+        (void)hipEventCreate(&c->ev0[k]);
+        (void)hipEventCreate(&c->ev1[k]);
+    }
+    *out = c;
+    return SPK_OK;
+}
+
+void spk_ctx_destroy(spk_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (int k = 0; k < K_COUNT; ++k) {
+        (void)hipEventDestroy(ctx->ev0[k]);
+        (void)hipEventDestroy(ctx->ev1[k]);
+    }
+    hipStream_t own = ctx->own_stream;
+    delete ctx;
+    if (own) (void)hipStreamDestroy(own);
+}
+
+int spk_ctx_set_stream(spk_ctx *ctx, void *hip_stream) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return SPK_OK;
+}
+
+int spk_ctx_sync(spk_ctx *ctx) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+int spk_ctx_enable_timing(spk_ctx *ctx, int on) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->timing = on != 0;
+    return SPK_OK;
+}
+
+int spk_ctx_kernel_ms(spk_ctx *ctx, double *out5) {
+    SPK_REQUIRE(ctx && out5, SPK_E_INVALID, "null arg");
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    for (int k = 0; k < K_COUNT; ++k) {
+        float ms = 0.f;
+        if (ctx->ev_used[k]) SPK_HIP(hipEventElapsedTime(&ms, ctx->ev0[k], ctx->ev1[k]));
+        out5[k] = ctx->ev_used[k] ? (double)ms : -1.0;
+    }
+    return SPK_OK;
+}
+
+int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols) {
+    SPK_REQUIRE(ctx && (side == 0 || side == 1), SPK_E_INVALID, "spk_table_create: bad side");
+    SPK_REQUIRE(n_rows >= 0 && n_rows < (int64_t)INT32_MAX && n_cols >= 0, SPK_E_LIMIT,
+                "spk_table_create: row count must be < 2^31");
+    SPK_HIP(hipSetDevice(ctx->device));
+    Table &t = ctx->table[side];
+    for (Column *c : t.cols) delete c;
+    t.cols.assign((size_t)n_cols, nullptr);
+    for (int w = 0; w < 2; ++w) {
+        for (DevBuf<int64_t> *k : t.key[w]) delete k;
+        t.key[w].clear();
+    }
+    t.rank.release();
+    t.n = n_rows;
+    t.desc_dirty = true;
+    ctx->pairs_valid = false;
+    ctx->codes_valid = false;
+    return SPK_OK;
+}
+
+static int get_col(spk_ctx *ctx, int side, int col, Column **out) {
+    SPK_REQUIRE(ctx && (side == 0 || side == 1), SPK_E_INVALID, "bad side");
+    Table &t = ctx->table[side];
+    SPK_REQUIRE(t.n >= 0, SPK_E_STATE, "table not created");
+    SPK_REQUIRE(col >= 0 && col < 4096, SPK_E_INVALID, "column index out of range");
+    if (col >= (int)t.cols.size()) t.cols.resize((size_t)col + 1, nullptr);
+    delete t.cols[col];
+    t.cols[col] = new Column();
+    t.desc_dirty = true;
+    *out = t.cols[col];
+    return SPK_OK;
+}
+
+int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, const uint8_t *data,
+                       const uint8_t *valid) {
+    SPK_REQUIRE(offsets && valid, SPK_E_INVALID, "spk_table_add_utf8: null buffer");
+    Column *c = nullptr;
+    SPK_TRY(get_col(ctx, side, col, &c));
+    SPK_HIP(hipSetDevice(ctx->device));
+    int64_t n = ctx->table[side].n;
+    int64_t nbytes = offsets[n];
+    SPK_REQUIRE(offsets[0] == 0 && nbytes >= 0, SPK_E_INVALID, "spk_table_add_utf8: offsets must start at 0");
+    c->kind = COL_STR;
+    DevBuf<uint8_t> d_bytes, d_valid;
+    SPK_TRY(d_bytes.alloc((size_t)nbytes + 1));
+    SPK_TRY(d_valid.alloc((size_t)n + 1));
+    SPK_TRY(c->units.alloc((size_t)nbytes + 1));
+    SPK_TRY(c->off.alloc((size_t)n + 1));
+    SPK_TRY(c->len16.alloc((size_t)n + 1));
+    SPK_TRY(c->cplen.alloc((size_t)n + 1));
+    SPK_TRY(c->hash.alloc((size_t)n + 1));
+    if (nbytes) SPK_HIP(hipMemcpyAsync(d_bytes.p, data, (size_t)nbytes, hipMemcpyHostToDevice, ctx->stream));
+    if (n) SPK_HIP(hipMemcpyAsync(d_valid.p, valid, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(c->off.p, offsets, (size_t)(n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+    if (n) {
+        int bs = 256;
+        k_utf8_decode<<<(unsigned)((n + bs - 1) / bs), bs, 0, ctx->stream>>>(n, c->off.p, d_bytes.p, d_valid.p,
+                                                                          c->units.p, c->len16.p, c->cplen.p,
+                                                                          c->hash.p);
+        SPK_HIP(hipGetLastError());
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->codes_valid = false;
+    return SPK_OK;
+}
+
+int spk_table_add_float64(spk_ctx *ctx, int side, int col, const double *values, const uint8_t *valid) {
+    SPK_REQUIRE(values && valid, SPK_E_INVALID, "spk_table_add_float64: null buffer");
+    Column *c = nullptr;
+    SPK_TRY(get_col(ctx, side, col, &c));
+    SPK_HIP(hipSetDevice(ctx->device));
+    int64_t n = ctx->table[side].n;
+    c->kind = COL_NUM;
+    SPK_TRY(c->val.alloc((size_t)n + 1));
+    SPK_TRY(c->valid.alloc((size_t)n + 1));
+    if (n) {
+        SPK_HIP(hipMemcpyAsync(c->val.p, values, (size_t)n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(c->valid.p, valid, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->codes_valid = false;
+    return SPK_OK;
+}
+
+int spk_table_set_rank(spk_ctx *ctx, int side, const int64_t *rank) {
+    SPK_REQUIRE(ctx && (side == 0 || side == 1) && rank, SPK_E_INVALID, "spk_table_set_rank: bad args");
+    Table &t = ctx->table[side];
+    SPK_REQUIRE(t.n >= 0, SPK_E_STATE, "table not created");
+    SPK_HIP(hipSetDevice(ctx->device));
+    for (int64_t i = 0; i < t.n; ++i)
+        SPK_REQUIRE(rank[i] >= 0 && rank[i] < (int64_t)UINT32_MAX, SPK_E_LIMIT, "rank must be in [0, 2^32)");
+    SPK_TRY(t.rank.alloc((size_t)t.n + 1));
+    if (t.n) SPK_HIP(hipMemcpyAsync(t.rank.p, rank, (size_t)t.n * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+int spk_table_set_key(spk_ctx *ctx, int side, int rule, int which, const int64_t *keys) {
+    SPK_REQUIRE(ctx && (side == 0 || side == 1) && keys && rule >= 0 && (which == 0 || which == 1), SPK_E_INVALID,
+                "spk_table_set_key: bad args");
+    Table &t = ctx->table[side];
+    SPK_REQUIRE(t.n >= 0, SPK_E_STATE, "table not created");
+    SPK_HIP(hipSetDevice(ctx->device));
+    for (int64_t i = 0; i < t.n; ++i)
+        SPK_REQUIRE(keys[i] >= -1 && keys[i] < (int64_t)INT32_MAX, SPK_E_LIMIT, "key ids must be in [-1, 2^31)");
+    while ((int)t.key[which].size() <= rule) t.key[which].push_back(new DevBuf<int64_t>());
+    SPK_TRY(t.key[which][rule]->alloc((size_t)t.n + 1));
+    if (t.n)
+        SPK_HIP(hipMemcpyAsync(t.key[which][rule]->p, keys, (size_t)t.n * sizeof(int64_t), hipMemcpyHostToDevice,
+                               ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+int spk_pairs_count(spk_ctx *ctx, int64_t *out) {
+    SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
+    SPK_REQUIRE(ctx->pairs_valid, SPK_E_STATE, "no pairs (run spk_block or spk_pairs_load)");
+    *out = ctx->n_pairs;
+    return SPK_OK;
+}
+
+int spk_pairs_copy(spk_ctx *ctx, int64_t start, int64_t count, int32_t *out_l, int32_t *out_r) {
+    SPK_REQUIRE(ctx && ctx->pairs_valid, SPK_E_STATE, "no pairs");
+    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "pair range out of bounds");
+    SPK_HIP(hipSetDevice(ctx->device));
+    if (count && out_l)
+        SPK_HIP(hipMemcpyAsync(out_l, ctx->pl.p + start, (size_t)count * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (count && out_r)
+        SPK_HIP(hipMemcpyAsync(out_r, ctx->pr.p + start, (size_t)count * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+int spk_pairs_load(spk_ctx *ctx, int64_t n, const int32_t *rows_l, const int32_t *rows_r) {
+    SPK_REQUIRE(ctx && n >= 0 && (n == 0 || (rows_l && rows_r)), SPK_E_INVALID, "spk_pairs_load: bad args");
+    SPK_HIP(hipSetDevice(ctx->device));
+    int64_t nl = ctx->table[0].n, nr = ctx->side_table(1).n;
+    for (int64_t i = 0; i < n; ++i)
+        SPK_REQUIRE(rows_l[i] >= 0 && rows_l[i] < nl && rows_r[i] >= 0 && rows_r[i] < nr, SPK_E_INVALID,
+                    "spk_pairs_load: row index out of range");
+    SPK_TRY(ctx->pl.alloc((size_t)n + 1));
+    SPK_TRY(ctx->pr.alloc((size_t)n + 1));
+    if (n) {
+        SPK_HIP(hipMemcpyAsync(ctx->pl.p, rows_l, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(ctx->pr.p, rows_r, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->n_pairs = n;
+    ctx->pairs_valid = true;
+    ctx->codes_valid = false;
+    return SPK_OK;
+}
+
+}  // extern "C"

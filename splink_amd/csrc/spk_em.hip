@@ -1,0 +1,455 @@
+// EM over packed comparison-vector codes (replaces expectation_step.py:25-221 and the GROUP BY
+// aggregate of maximisation_step.py:41-90), final scoring and term-frequency adjustment.
+//
+// The E-step's match_probability is a function of the comparison vector only, so the M-step's
+// sufficient statistic is the histogram of codes.  Each EM iteration streams every pair's code
+// once (HBM-bound: 2 or 4 bytes per pair) into an LDS-privatised histogram with wave-level
+// aggregation of equal codes, then evaluates mp per pattern with the reference's literal
+// arithmetic and reduces the per-(column, level) sums in a fixed order (deterministic, and
+// identical for any sharding of pairs over GPUs since the histogram is an exact integer sum).
+#include <cmath>
+
+#include "spk_internal.h"
+
+namespace spk {
+
+constexpr int H_THREADS = 512;
+constexpr int H_LDS_BINS = 16384;  // LDS-privatised up to this many patterns (64 KiB)
+
+template <typename CodeT, bool LDS>
+__global__ __launch_bounds__(H_THREADS) void k_hist(const CodeT *__restrict__ codes, int64_t P, int n_pat,
+                                                    unsigned long long *__restrict__ ghist) {
+    extern __shared__ uint32_t sh[];
+    if (LDS) {
+        for (int b = threadIdx.x; b < n_pat; b += H_THREADS) sh[b] = 0;
+        __syncthreads();
+    }
+    constexpr int VEC = 16 / sizeof(CodeT);  // codes per 16-byte load
+    const int64_t n_vec = P / VEC;
+    const int lane = threadIdx.x & 63;
+    using V4 = uint4;
+    const V4 *cv = reinterpret_cast<const V4 *>(codes);
+    for (int64_t v = (int64_t)blockIdx.x * H_THREADS + threadIdx.x;; v += (int64_t)gridDim.x * H_THREADS) {
+        // wave-uniform loop exit keeps every lane inside the ballots below
+        const bool in = v < n_vec;
+        if (!__any(in)) break;
+        CodeT c[VEC];
+        if (in) {
+            V4 w = cv[v];
+            const CodeT *e = reinterpret_cast<const CodeT *>(&w);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) c[j] = e[j];
+        }
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            uint32_t mine = in ? (uint32_t)c[j] : 0xFFFFFFFFu;
+            unsigned long long todo = __ballot(in);
+            // aggregate up to 4 distinct codes per wave with ballots, the rest with plain atomics
+            for (int it = 0; it < 4 && todo; ++it) {
+                const int leader = __ffsll(todo) - 1;
+                const uint32_t lc = __shfl(mine, leader);
+                const unsigned long long same = __ballot(mine == lc) & todo;
+                if (lane == leader) {
+                    if (LDS) atomicAdd(&sh[lc], (uint32_t)__popcll(same));
+                    else atomicAdd(&ghist[lc], (unsigned long long)__popcll(same));
+                }
+                todo &= ~same;
+            }
+            if ((todo >> lane) & 1ull) {
+                if (LDS) atomicAdd(&sh[mine], 1u);
+                else atomicAdd(&ghist[mine], 1ull);
+            }
+        }
+    }
+    // tail (P not a multiple of VEC): block 0 handles it
+    if (blockIdx.x == 0) {
+        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += H_THREADS) {
+            if (LDS) atomicAdd(&sh[codes[p]], 1u);
+            else atomicAdd(&ghist[codes[p]], 1ull);
+        }
+    }
+    if (LDS) {
+        __syncthreads();
+        for (int b = threadIdx.x; b < n_pat; b += H_THREADS) {
+            uint32_t v = sh[b];
+            if (v) atomicAdd(&ghist[b], (unsigned long long)v);
+        }
+    }
+}
+
+struct PatArgs {
+    int K;
+    int64_t n_pat;
+    const int64_t *stride;
+    const int32_t *nlev;
+    const int32_t *moff;  // offset of column k in the flattened m/u arrays
+    const double *m, *u;
+    double lambda, one_minus;
+};
+
+// mp per pattern: (λ·m1·…·mK) / ((λ·m1·…·mK) + ((1-λ)·u1·…·uK)), left-associative products,
+// γ = -1 contributes 1.0; a zero denominator is NULL (NaN) as in Spark (expectation_step.py:167-185).
+__global__ void k_pattern_mp(PatArgs A, double *__restrict__ mpat, double *__restrict__ llpat) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.n_pat) return;
+    double num = A.lambda;
+    for (int k = 0; k < A.K; ++k) {
+        int g = (int)((p / A.stride[k]) % (A.nlev[k] + 1)) - 1;
+        num = num * (g < 0 ? 1.0 : A.m[A.moff[k] + g]);
+    }
+    double den = A.one_minus;
+    for (int k = 0; k < A.K; ++k) {
+        int g = (int)((p / A.stride[k]) % (A.nlev[k] + 1)) - 1;
+        den = den * (g < 0 ? 1.0 : A.u[A.moff[k] + g]);
+    }
+    double d = num + den;
+    mpat[p] = d == 0.0 ? NAN : num / d;
+    llpat[p] = d > 0.0 ? log(d) : NAN;  // ln(λΠm + (1-λ)Πu), NULL for ln(<= 0) (expectation_step.py:224-256)
+}
+
+constexpr int S_THREADS = 256;
+constexpr int N_HEAD = 5;  // [Σmp, rows, non-null rows, Σ ln(...), non-null ln rows]
+
+// One block per statistics slot: slot 0 = totals, slot 1 + s = (column k, level v) in order.
+// Each thread sums a fixed strided subset of patterns; a fixed LDS tree finishes: deterministic.
+__global__ __launch_bounds__(S_THREADS) void k_stats(PatArgs A, const unsigned long long *__restrict__ hist,
+                                                     const double *__restrict__ mpat,
+                                                     const double *__restrict__ llpat,
+                                                     const int32_t *__restrict__ slot_k,
+                                                     const int32_t *__restrict__ slot_v, double *__restrict__ out) {
+    __shared__ double s[6][S_THREADS];
+    const int slot = blockIdx.x;
+    int kk = -1, vv = 0;
+    if (slot > 0) {
+        kk = slot_k[slot - 1];
+        vv = slot_v[slot - 1];
+    }
+    double rows = 0, nn = 0, sm = 0, s1 = 0, sll = 0, nll = 0;
+    for (int64_t p = threadIdx.x; p < A.n_pat; p += S_THREADS) {
+        unsigned long long c = hist[p];
+        if (!c) continue;
+        if (kk >= 0) {
+            int g = (int)((p / A.stride[kk]) % (A.nlev[kk] + 1)) - 1;
+            if (g != vv) continue;
+        }
+        double cd = (double)c;
+        double mp = mpat[p];
+        rows += cd;
+        if (!isnan(mp)) {
+            nn += cd;
+            sm += cd * mp;
+            s1 += cd * (1.0 - mp);
+        }
+        double ll = llpat[p];
+        if (!isnan(ll)) {
+            nll += cd;
+            sll += cd * ll;
+        }
+    }
+    s[0][threadIdx.x] = rows;
+    s[1][threadIdx.x] = nn;
+    s[2][threadIdx.x] = sm;
+    s[3][threadIdx.x] = s1;
+    s[4][threadIdx.x] = sll;
+    s[5][threadIdx.x] = nll;
+    __syncthreads();
+    for (int off = S_THREADS / 2; off > 0; off >>= 1) {
+        if (threadIdx.x < off)
+            for (int q = 0; q < 6; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (slot == 0) {
+            out[0] = s[2][0];
+            out[1] = s[0][0];
+            out[2] = s[1][0];
+            out[3] = s[4][0];
+            out[4] = s[5][0];
+        } else {
+            double *o = out + N_HEAD + 4 * (slot - 1);
+            o[0] = s[0][0];
+            o[1] = s[1][0];
+            o[2] = s[2][0];
+            o[3] = s[3][0];
+        }
+    }
+}
+
+template <typename CodeT>
+__global__ void k_score(const CodeT *__restrict__ codes, int64_t start, int64_t n, const double *__restrict__ mpat,
+                        double *__restrict__ mp) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    mp[i] = mpat[codes[start + i]];
+}
+
+__global__ void k_tf_accumulate(int64_t P, const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
+                                const int64_t *__restrict__ ids0, const int64_t *__restrict__ ids1,
+                                const double *__restrict__ mp, int64_t n_values, double *__restrict__ sum,
+                                unsigned long long *__restrict__ cnt) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    int64_t a = ids0[pl[p]], b = ids1[pr[p]];
+    if (a < 0 || a != b || a >= n_values) return;
+    double v = mp[p];
+    if (isnan(v)) return;
+    atomicAdd(&sum[a], v);
+    atomicAdd(&cnt[a], 1ull);
+}
+
+struct TfApply {
+    int n;
+    const int64_t *ids0[8];
+    const int64_t *ids1[8];
+    const double *tab[8];
+    int64_t tab_n[8];
+};
+
+// bayes(mp, adj...) = Πp / (Πp + Π(1-p)) (term_frequencies.py:21-46, :98-117)
+__global__ void k_tf_apply(TfApply T, int64_t start, int64_t n, const int32_t *__restrict__ pl,
+                           const int32_t *__restrict__ pr, const double *__restrict__ mp, double *__restrict__ out,
+                           double *__restrict__ out_adj) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t p = start + i;
+    double m = mp[p];
+    double adj[8];
+    for (int c = 0; c < T.n; ++c) {
+        int64_t a = T.ids0[c][pl[p]], b = T.ids1[c][pr[p]];
+        double v = 0.5;
+        if (a >= 0 && a == b && a < T.tab_n[c]) {
+            double x = T.tab[c][a];
+            if (!isnan(x)) v = x;
+        }
+        adj[c] = v;
+        if (out_adj) out_adj[i * T.n + c] = v;
+    }
+    if (isnan(m)) {
+        out[i] = NAN;
+        return;
+    }
+    double a = m, b = 1.0 - m;
+    for (int c = 0; c < T.n; ++c) a = a * adj[c];
+    for (int c = 0; c < T.n; ++c) b = b * (1.0 - adj[c]);
+    double d = a + b;
+    out[i] = d == 0.0 ? NAN : a / d;
+}
+
+static int upload_tables(spk_ctx *ctx, const double *m, const double *u, DevBuf<int64_t> &d_stride,
+                         DevBuf<int32_t> &d_nlev, DevBuf<int32_t> &d_moff, PatArgs &A) {
+    int K = ctx->K;
+    std::vector<int32_t> moff(K);
+    int tot = 0;
+    for (int k = 0; k < K; ++k) {
+        moff[k] = tot;
+        tot += ctx->n_levels[k];
+    }
+    SPK_TRY(ctx->mu.alloc((size_t)2 * tot + 2));
+    SPK_TRY(d_stride.alloc((size_t)K));
+    SPK_TRY(d_nlev.alloc((size_t)K));
+    SPK_TRY(d_moff.alloc((size_t)K));
+    SPK_HIP(hipMemcpyAsync(ctx->mu.p, m, (size_t)tot * 8, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(ctx->mu.p + tot, u, (size_t)tot * 8, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(d_stride.p, ctx->stride.data(), (size_t)K * 8, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(d_nlev.p, ctx->n_levels.data(), (size_t)K * 4, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(d_moff.p, moff.data(), (size_t)K * 4, hipMemcpyHostToDevice, ctx->stream));
+    A.K = K;
+    A.n_pat = ctx->n_patterns;
+    A.stride = d_stride.p;
+    A.nlev = d_nlev.p;
+    A.moff = d_moff.p;
+    A.m = ctx->mu.p;
+    A.u = ctx->mu.p + tot;
+    return SPK_OK;
+}
+
+static int compute_mpat(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u, PatArgs &A,
+                        DevBuf<int64_t> &d_stride, DevBuf<int32_t> &d_nlev, DevBuf<int32_t> &d_moff) {
+    SPK_TRY(upload_tables(ctx, m, u, d_stride, d_nlev, d_moff, A));
+    A.lambda = lambda;
+    A.one_minus = one_minus;
+    SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
+    SPK_TRY(ctx->llpat.alloc((size_t)ctx->n_patterns));
+    k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat.p, ctx->llpat.p);
+    SPK_HIP(hipGetLastError());
+    ctx->mpat_valid = true;
+    return SPK_OK;
+}
+
+}  // namespace spk
+
+using namespace spk;
+
+extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_histogram: no gammas");
+    SPK_HIP(hipSetDevice(ctx->device));
+    const int64_t n_pat = ctx->n_patterns;
+    unsigned long long *h = reinterpret_cast<unsigned long long *>(d_hist);
+    if (!h) {
+        SPK_TRY(ctx->hist.alloc((size_t)n_pat));
+        h = reinterpret_cast<unsigned long long *>(ctx->hist.p);
+    }
+    SPK_TRY(ctx->begin(K_EMHIST));
+    SPK_HIP(hipMemsetAsync(h, 0, (size_t)n_pat * 8, ctx->stream));
+    const int64_t P = ctx->n_pairs;
+    const int vec = 16 / ctx->code_bytes;
+    int64_t blocks = (P / vec + H_THREADS - 1) / H_THREADS;
+    if (blocks > 256 * 4) blocks = 256 * 4;
+    if (blocks < 1) blocks = 1;
+    const bool lds = n_pat <= H_LDS_BINS;
+    size_t shm = lds ? (size_t)n_pat * 4 : 0;
+    if (ctx->code_bytes == 2) {
+        if (lds) k_hist<uint16_t, true><<<(unsigned)blocks, H_THREADS, shm, ctx->stream>>>(
+            reinterpret_cast<const uint16_t *>(ctx->codes.p), P, (int)n_pat, h);
+        else k_hist<uint16_t, false><<<(unsigned)blocks, H_THREADS, 0, ctx->stream>>>(
+            reinterpret_cast<const uint16_t *>(ctx->codes.p), P, (int)n_pat, h);
+    } else {
+        if (lds) k_hist<uint32_t, true><<<(unsigned)blocks, H_THREADS, shm, ctx->stream>>>(
+            reinterpret_cast<const uint32_t *>(ctx->codes.p), P, (int)n_pat, h);
+        else k_hist<uint32_t, false><<<(unsigned)blocks, H_THREADS, 0, ctx->stream>>>(
+            reinterpret_cast<const uint32_t *>(ctx->codes.p), P, (int)n_pat, h);
+    }
+    SPK_HIP(hipGetLastError());
+    SPK_TRY(ctx->end(K_EMHIST));
+    if (d_hist) SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+extern "C" int spk_em_finalize(spk_ctx *ctx, const uint64_t *d_hist, double lambda, double one_minus, const double *m,
+                               const double *u, double *out_stats, int n_stats) {
+    SPK_REQUIRE(ctx && m && u && out_stats, SPK_E_INVALID, "spk_em_finalize: null arg");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_finalize: no gammas");
+    SPK_HIP(hipSetDevice(ctx->device));
+    int n_slots = 0;
+    std::vector<int32_t> sk, sv;
+    for (int k = 0; k < ctx->K; ++k)
+        for (int v = -1; v < ctx->n_levels[k]; ++v) {
+            sk.push_back(k);
+            sv.push_back(v);
+            ++n_slots;
+        }
+    SPK_REQUIRE(n_stats == N_HEAD + 4 * n_slots, SPK_E_INVALID, "spk_em_finalize: n_stats mismatch");
+    const unsigned long long *h = reinterpret_cast<const unsigned long long *>(d_hist ? d_hist : ctx->hist.p);
+    SPK_REQUIRE(h, SPK_E_STATE, "spk_em_finalize: no histogram");
+    SPK_TRY(ctx->begin(K_EMFIN));
+    PatArgs A{};
+    DevBuf<int64_t> d_stride;
+    DevBuf<int32_t> d_nlev, d_moff, d_sk, d_sv;
+    SPK_TRY(compute_mpat(ctx, lambda, one_minus, m, u, A, d_stride, d_nlev, d_moff));
+    SPK_TRY(d_sk.alloc((size_t)n_slots));
+    SPK_TRY(d_sv.alloc((size_t)n_slots));
+    SPK_TRY(ctx->stats.alloc((size_t)n_stats));
+    SPK_HIP(hipMemcpyAsync(d_sk.p, sk.data(), (size_t)n_slots * 4, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(d_sv.p, sv.data(), (size_t)n_slots * 4, hipMemcpyHostToDevice, ctx->stream));
+    k_stats<<<(unsigned)(n_slots + 1), S_THREADS, 0, ctx->stream>>>(A, h, ctx->mpat.p, ctx->llpat.p, d_sk.p, d_sv.p,
+                                                                     ctx->stats.p);
+    SPK_HIP(hipGetLastError());
+    SPK_TRY(ctx->end(K_EMFIN));
+    SPK_HIP(hipMemcpyAsync(out_stats, ctx->stats.p, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
+                         int64_t start, int64_t count, double *out_mp) {
+    SPK_REQUIRE(ctx && m && u, SPK_E_INVALID, "spk_score: null arg");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_score: no gammas");
+    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_score: range");
+    SPK_HIP(hipSetDevice(ctx->device));
+    PatArgs A{};
+    DevBuf<int64_t> d_stride;
+    DevBuf<int32_t> d_nlev, d_moff;
+    SPK_TRY(compute_mpat(ctx, lambda, one_minus, m, u, A, d_stride, d_nlev, d_moff));
+    SPK_TRY(ctx->mp.alloc((size_t)ctx->n_pairs + 1));
+    SPK_TRY(ctx->begin(K_SCORE));
+    if (count) {
+        unsigned g = (unsigned)((count + 255) / 256);
+        if (ctx->code_bytes == 2)
+            k_score<uint16_t><<<g, 256, 0, ctx->stream>>>(reinterpret_cast<const uint16_t *>(ctx->codes.p), start,
+                                                          count, ctx->mpat.p, ctx->mp.p + start);
+        else
+            k_score<uint32_t><<<g, 256, 0, ctx->stream>>>(reinterpret_cast<const uint32_t *>(ctx->codes.p), start,
+                                                          count, ctx->mpat.p, ctx->mp.p + start);
+        SPK_HIP(hipGetLastError());
+    }
+    SPK_TRY(ctx->end(K_SCORE));
+    if (out_mp && count)
+        SPK_HIP(hipMemcpyAsync(out_mp, ctx->mp.p + start, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
+                                 double *out_sum, int64_t *out_count) {
+    SPK_REQUIRE(ctx && ids_side0 && ids_side1 && out_sum && out_count && n_values >= 0, SPK_E_INVALID,
+                "spk_tf_accumulate: bad args");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_accumulate: run spk_score over all pairs first");
+    SPK_HIP(hipSetDevice(ctx->device));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0, d1;
+    DevBuf<double> ds;
+    DevBuf<unsigned long long> dc;
+    SPK_TRY(d0.alloc((size_t)t0.n + 1));
+    SPK_TRY(d1.alloc((size_t)t1.n + 1));
+    SPK_TRY(ds.alloc((size_t)n_values + 1));
+    SPK_TRY(dc.alloc((size_t)n_values + 1));
+    SPK_HIP(hipMemcpyAsync(d0.p, ids_side0, (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(d1.p, ids_side1, (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemsetAsync(ds.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
+    SPK_HIP(hipMemsetAsync(dc.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
+    int64_t P = ctx->n_pairs;
+    if (P)
+        k_tf_accumulate<<<(unsigned)((P + 255) / 256), 256, 0, ctx->stream>>>(P, ctx->pl.p, ctx->pr.p, d0.p, d1.p,
+                                                                          ctx->mp.p, n_values, ds.p, dc.p);
+    SPK_HIP(hipGetLastError());
+    if (n_values) {
+        SPK_HIP(hipMemcpyAsync(out_sum, ds.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(out_count, dc.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0,
+                            const int64_t *const *ids_side1, const double *const *adj_tables,
+                            const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
+                            double *out_adj) {
+    SPK_REQUIRE(ctx && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID, "spk_tf_apply: 1..8 columns");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply: run spk_score first");
+    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply: range");
+    SPK_HIP(hipSetDevice(ctx->device));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0[8], d1[8];
+    DevBuf<double> dt[8], dout, dadj;
+    TfApply T{};
+    T.n = n_tf_cols;
+    for (int c = 0; c < n_tf_cols; ++c) {
+        SPK_TRY(d0[c].alloc((size_t)t0.n + 1));
+        SPK_TRY(d1[c].alloc((size_t)t1.n + 1));
+        SPK_TRY(dt[c].alloc((size_t)table_sizes[c] + 1));
+        SPK_HIP(hipMemcpyAsync(d0[c].p, ids_side0[c], (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(d1[c].p, ids_side1[c], (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (table_sizes[c])
+            SPK_HIP(hipMemcpyAsync(dt[c].p, adj_tables[c], (size_t)table_sizes[c] * 8, hipMemcpyHostToDevice,
+                                   ctx->stream));
+        T.ids0[c] = d0[c].p;
+        T.ids1[c] = d1[c].p;
+        T.tab[c] = dt[c].p;
+        T.tab_n[c] = table_sizes[c];
+    }
+    SPK_TRY(dout.alloc((size_t)count + 1));
+    if (out_adj) SPK_TRY(dadj.alloc((size_t)count * n_tf_cols + 1));
+    if (count)
+        k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
+                                                                         ctx->mp.p, dout.p,
+                                                                         out_adj ? dadj.p : nullptr);
+    SPK_HIP(hipGetLastError());
+    if (count) {
+        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (out_adj)
+            SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * n_tf_cols * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}

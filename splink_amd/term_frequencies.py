@@ -1,0 +1,88 @@
+"""Term-frequency adjustment (reference: splink/term_frequencies.py:122-168).
+
+Per tf column c: over pairs whose c_l and c_r are equal and non-NULL, the mean match
+probability per value (adj_lambda, :49-65) is Bayes-combined with 1-λ; pairs without a
+lookup value get 0.5 (:68-95); tf_adjusted_match_prob = bayes(mp, adj_c1, ...) (:98-117).
+The per-value sums and the per-pair Bayes combination run on the GPU
+(spk_tf_accumulate / spk_tf_apply); the per-value lookup arithmetic is a handful of
+operations per distinct value.
+"""
+import warnings
+from collections import OrderedDict
+
+import numpy as np
+import pandas as pd
+
+from . import table as T
+from .check_types import check_types
+from .frames import ExpectationFrame, SplinkDataFrame, _HostColumns, df_e_column_order
+from .params import Params
+
+
+def _bayes_pair(a, b):
+    """sql_gen_bayes_string([a, b]) (:21-46) for vectors a and a scalar b."""
+    num = a * b
+    den = num + (1.0 - a) * (1.0 - b)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        out = num / den
+    out[den == 0] = np.nan
+    return out
+
+
+class TermFrequencyFrame(SplinkDataFrame):
+    def __init__(self, df_e: ExpectationFrame, settings, tf_cols, tf_mp, adj, retain_adjustment_columns):
+        self.df_e = df_e
+        self.job = df_e.job
+        self.settings = settings
+        self.tf_cols = tf_cols
+        self.tf_mp = tf_mp
+        self.adj = adj
+        self.retain = retain_adjustment_columns
+
+    def _column_order(self):
+        cols = ["tf_adjusted_match_prob", "match_probability"] + df_e_column_order(self.settings, tf_adj_cols=True)
+        if not self.retain:
+            cols = [c for c in cols if not (c.endswith("_adj") and c[:-4] in self.tf_cols)]
+        return cols
+
+    def toPandas(self):
+        base = self.df_e.toPandas()
+        data = OrderedDict()
+        for c in self._column_order():
+            if c == "tf_adjusted_match_prob":
+                data[c] = self.tf_mp
+            elif c.endswith("_adj") and c[:-4] in self.tf_cols:
+                data[c] = self.adj[:, self.tf_cols.index(c[:-4])]
+            else:
+                data[c] = base[c].to_numpy()
+        return pd.DataFrame(data)
+
+
+@check_types
+def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings: dict, spark: object,
+                                         retain_adjustment_columns: bool = False):
+    tf_cols = [c["col_name"] for c in settings["comparison_columns"] if c["term_frequency_adjustments"] is True]
+    if not tf_cols:
+        warnings.warn("No term frequency adjustment columns are specified in your settings object.  "
+                      "Returning original df")
+        return df_e
+    job = df_e.job
+    df_e.gammas.ensure_codes()
+    job.score(df_e.lam, df_e.level_probs, want_host=False)  # device mp for exactly this df_e
+    one_minus = float(1 - params.params["λ"])
+    ids0_list, ids1_list, tables = [], [], []
+    for c in tf_cols:
+        t0, tr = job.tables[0], job.r_table()
+        vals = [pd.Series([None if T.is_null_scalar(v) else v for v in t[c].tolist()], dtype=object)
+                for t in ((t0, tr) if job.link_type == "link_only" else (t0,))]
+        codes, n_values = T.factorize_joint(vals)
+        ids0 = codes[0]
+        ids1 = codes[1] if len(codes) > 1 else codes[0]
+        sums, counts = job.ctx.tf_accumulate(n_values, ids0, ids1)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
+        tables.append(_bayes_pair(adj_lambda, one_minus))
+        ids0_list.append(ids0)
+        ids1_list.append(ids1)
+    tf_mp, adj = job.ctx.tf_apply(ids0_list, ids1_list, tables, 0, job.n_pairs, want_adj=True)
+    return TermFrequencyFrame(df_e, settings, tf_cols, tf_mp, adj, retain_adjustment_columns)

@@ -1,0 +1,265 @@
+"""Parity of the HIP path (through the C ABI) with the reference goldens and the CPU oracle."""
+import copy
+import math
+import warnings
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import oracle as orc
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+warnings.filterwarnings("ignore")
+
+PIPELINES = ["test1", "main_api_nojaro", "main_api_jaro", "test2_nulls", "synthetic_cfg1", "custom_exprs", "link_tf"]
+LINK_CASES = ["link_only_plain_rules", "link_only_plain_cartesian", "link_and_dedupe_plain_rules",
+              "link_and_dedupe_plain_cartesian", "link_only_repeat_rules", "link_only_repeat_cartesian",
+              "link_and_dedupe_repeat_rules", "link_and_dedupe_repeat_cartesian", "dedupe_only_plain_rules",
+              "dedupe_only_repeat_rules", "blocks_dedupe"]
+
+
+@pytest.fixture(scope="module")
+def amd():
+    from splink_amd import AmdSession, _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the -m gpu tests need an MI355X")
+    return AmdSession(0)
+
+
+def spark_for(jaro, amd):
+    return amd if jaro else "supress_warnings"
+
+
+def frame(d):
+    return pd.DataFrame(d) if d else None
+
+
+def rel_close(a, b, tol=1e-9):
+    if a is None or b is None:
+        return a is None and b is None
+    if isinstance(a, float) and math.isnan(a):
+        return b is None or (isinstance(b, float) and math.isnan(b))
+    return abs(a - b) <= tol * max(abs(a), abs(b), 1e-300)
+
+
+def sort_like_golden(df):
+    keys = [k for k in ("_source_table_l", "unique_id_l", "_source_table_r", "unique_id_r") if k in df.columns]
+    rest = [c for c in df.columns if c.startswith("gamma_")]
+    return df.sort_values(keys + rest, kind="mergesort").reset_index(drop=True)
+
+
+def compare_frames(got: pd.DataFrame, exp: dict, columns):
+    assert list(got.columns) == list(columns)
+    got = sort_like_golden(got)
+    for c in columns:
+        gv, ev = got[c].tolist(), exp[c]
+        assert len(gv) == len(ev), c
+        for a, b in zip(gv, ev):
+            if isinstance(b, float) or (isinstance(a, float) and not isinstance(b, str)):
+                a = None if a is None else float(a)
+                assert rel_close(a, b), (c, a, b)
+            else:
+                if isinstance(a, float) and math.isnan(a):
+                    a = None
+                assert a == b, (c, a, b)
+
+
+def check_history(params, g):
+    hist = params.param_history[1:] + [params.params]
+    assert len(hist) == len(g["iterations"])
+    for p, it in zip(hist, g["iterations"]):
+        assert rel_close(p["λ"], it["lambda"])
+        for gname, d in it["pi"].items():
+            for i, (m, u) in enumerate(zip(d["m"], d["u"])):
+                assert rel_close(p["π"][gname]["prob_dist_match"][f"level_{i}"]["probability"], m), (gname, i)
+                assert rel_close(p["π"][gname]["prob_dist_non_match"][f"level_{i}"]["probability"], u), (gname, i)
+
+
+def run_linker(g, amd):
+    from splink_amd import Splink
+    settings = copy.deepcopy(g["settings_in"])
+    linker = Splink(settings, spark_for(g["jaro"], amd), df=frame(g.get("df")), df_l=frame(g.get("df_l")),
+                    df_r=frame(g.get("df_r")))
+    return linker
+
+
+@pytest.mark.parametrize("name", PIPELINES)
+def test_pipeline_matches_reference(name, amd):
+    g = load_golden(name)
+    linker = run_linker(g, amd)
+    if "error" in g:
+        with pytest.raises(Exception):
+            linker.get_scored_comparisons().toPandas()
+        return
+    df_e = linker.get_scored_comparisons()
+    compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])
+    check_history(linker.params, g)
+    if "df_tf" in g:
+        tf = linker.make_term_frequency_adjustments(df_e).toPandas()
+        compare_frames(tf, g["df_tf"], g["df_tf_columns"])
+
+
+@pytest.mark.parametrize("case", LINK_CASES)
+def test_link_options_match_reference(case, amd):
+    g = load_golden("link_options")[case]
+    linker = run_linker(g, amd)
+    if "error" in g:
+        with pytest.raises(Exception):
+            linker.get_scored_comparisons().toPandas()
+        return
+    df_e = linker.get_scored_comparisons()
+    compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])
+    check_history(linker.params, g)
+
+
+def test_em_from_gamma_table(amd):
+    from splink_amd.iterate import iterate
+    from splink_amd.params import Params
+    g = load_golden("dgp")
+    settings = copy.deepcopy(g["settings_in"])
+    params = Params(settings, "supress_warnings")
+    df_e = iterate(frame(g["df_gammas"]), params, params.settings, "supress_warnings")
+    check_history(params, g)
+    compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])
+
+
+def test_case_levels(amd):
+    from splink_amd.gammas import add_gammas
+    g = load_golden("case_levels")
+    tables = {"str_comp": frame(g["str_comp"]), "float_comp": frame(g["float_comp"]), "df_names": frame(g["names"])}
+    for case in g["cases"]:
+        t = tables[case["table"]]
+        st = {"link_type": "dedupe_only", "comparison_columns": [
+            {"custom_name": "x", "custom_columns_used": ["a"], "num_levels": 4,
+             "case_expression": case["case_expression"]}]}
+        gf = add_gammas(t, st, amd)
+        got = gf.gamma_matrix()[:, 0].tolist()
+        assert got == case["levels"], case["name"]
+
+
+def test_udf_exact_values(amd):
+    from splink_amd import _native as N
+    g = load_golden("string_values")
+    ctx = N.Context(0)
+    left = [a for a, b in g["pairs"]]
+    right = [b for a, b in g["pairs"]]
+    jw = ctx.jaro_winkler_sim(left, right)
+    lev = ctx.levenshtein(left, right)
+    for i, (a, b) in enumerate(g["pairs"]):
+        assert jw[i] == g["jw"][i], (a, b, jw[i], g["jw"][i])  # bit-exact fp64
+        assert lev[i] == g["lev"][i], (a, b)
+
+
+def test_udf_long_and_surrogate_strings(amd):
+    from splink_amd import _native as N
+    rng = np.random.Generator(np.random.PCG64(7))
+    alpha = list("abcdefgh") + ["é", "\U0001F600", "\U0001D400"]
+    left, right = [], []
+    for n in (0, 1, 39, 40, 41, 63, 64, 65, 100, 300, 1000):
+        for _ in range(8):
+            a = "".join(rng.choice(alpha, size=n))
+            b = "".join(rng.choice(alpha, size=max(0, n + int(rng.integers(-5, 6)))))
+            left.append(a)
+            right.append(b)
+    ctx = N.Context(0)
+    jw, lev = ctx.jaro_winkler_sim(left, right), ctx.levenshtein(left, right)
+    for i in range(len(left)):
+        assert jw[i] == orc.jaro_winkler(left[i], right[i])
+        assert lev[i] == orc.levenshtein(left[i], right[i])
+
+
+def _synthetic(n, seed, **kw):
+    from splink_amd.synthetic import make_records
+    return make_records(n, seed=seed, **kw)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
+
+
+def _pandas_block(df, rules, uid="unique_id"):
+    """Independent equi-join restatement with pandas merges (hash joins)."""
+    seen = None
+    out = []
+    for cols in rules:
+        l = df.dropna(subset=cols).reset_index().rename(columns={"index": "row"})
+        m = l.merge(l, on=cols, suffixes=("_l", "_r"))
+        m = m[m[f"{uid}_l"] < m[f"{uid}_r"]]
+        pairs = set(zip(m["row_l"].to_numpy(), m["row_r"].to_numpy()))
+        if seen is not None:
+            pairs -= seen
+        out.append(pairs)
+        seen = pairs if seen is None else seen | pairs
+    allp = set().union(*out)
+    return np.array(sorted(allp), dtype=np.int64).reshape(-1, 2)
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_blocking_and_gammas_at_scale(amd, shards):
+    from splink_amd.engine import Job
+    from splink_amd.synthetic import cfg_settings
+    from splink_amd.settings import complete_settings_dict
+    df = _synthetic(30000, seed=11, surname_vocab=800, first_vocab=400, city_vocab=100)
+    st = complete_settings_dict(cfg_settings(2), amd)
+    exp = _pandas_block(df, [["surname"], ["dob"]])
+    rows = []
+    codes = []
+    for s in range(shards):
+        job = Job("dedupe_only", [df], "unique_id", 0, shard=(s, shards))
+        job.block(st["blocking_rules"])
+        l, r = job.pair_rows()
+        rows.append(np.stack([l, r], axis=1))
+        job.gammas(st)
+        codes.append(job.gammas_host())
+    got_pairs = np.concatenate(rows)
+    order = np.lexsort((got_pairs[:, 1], got_pairs[:, 0]))
+    assert len(got_pairs) == len(exp)
+    assert (got_pairs[order] == exp).all()
+    gam = np.concatenate(codes)
+    cols = [orc.StrCol(df[c].tolist()) for c in ["first_name", "surname", "dob", "city", "email"]]
+    specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
+    ref = orc.template_gammas(specs, cols, cols, got_pairs[:, 0], got_pairs[:, 1])
+    assert (gam == ref).all()
+
+
+def test_em_at_scale_matches_oracle(amd):
+    from splink_amd.engine import Job, m_step_rows
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings
+    df = _synthetic(30000, seed=12, surname_vocab=600, first_vocab=400, city_vocab=100)
+    settings = cfg_settings(2, max_iterations=10)
+    params = Params(settings, amd)
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    gam = job.gammas_host()
+    names, nlev = job.code_meta
+    lam = params.params["λ"]
+    lp = params._level_probabilities()
+    hist_o, mp_o = orc.em_iterate(gam, nlev, lam, [m for m, _ in lp], [u for _, u in lp], 10, 1e-12)
+    for lam_o, m_o, u_o in hist_o:
+        stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        new_lambda, rows = m_step_rows(stats, names, nlev)
+        params._update_params(new_lambda, rows)
+        assert rel_close(params.params["λ"], lam_o)
+        for k, (m, u) in enumerate(params._level_probabilities()):
+            assert all(rel_close(a, b) for a, b in zip(m, m_o[k]))
+            assert all(rel_close(a, b) for a, b in zip(u, u_o[k]))
+    mp = job.score(params.params["λ"], params._level_probabilities())
+    assert np.allclose(mp, mp_o, rtol=1e-9, atol=0)
+
+
+def test_edge_cases(amd):
+    from splink_amd import Splink
+    # empty input: no pairs
+    empty = pd.DataFrame({"unique_id": pd.Series([], dtype=np.int64), "name": pd.Series([], dtype=object)})
+    st = {"link_type": "dedupe_only", "comparison_columns": [{"col_name": "name"}],
+          "blocking_rules": ["l.name = r.name"], "max_iterations": 0}
+    df_e = Splink(st, amd, df=empty).get_scored_comparisons()
+    assert df_e.count() == 0 and len(df_e.toPandas()) == 0
+    # every key NULL: no pairs; single record: no pairs
+    df = pd.DataFrame({"unique_id": [1, 2, 3], "name": [None, None, None]})
+    assert Splink(copy.deepcopy(st), amd, df=df).get_scored_comparisons().count() == 0
+    # duplicate unique ids are never paired with each other
+    df = pd.DataFrame({"unique_id": [1, 1, 2], "name": ["a", "a", "a"]})
+    out = Splink(copy.deepcopy(st), amd, df=df).get_scored_comparisons().toPandas()
+    assert sorted(zip(out.unique_id_l, out.unique_id_r)) == [(1, 2), (1, 2)]

@@ -1,0 +1,159 @@
+"""Host-side logic that needs no GPU: settings completion, the SQL compiler, Params, M-step algebra."""
+import copy
+import json
+import math
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from conftest import load_golden
+
+from splink_amd import case_statements as cs
+from splink_amd.compiler import Schema, compile_comparisons, compile_rule
+from splink_amd.engine import N_HEAD, m_step_rows
+from splink_amd.params import Params, load_params_from_json
+from splink_amd.session import AmdSession
+from splink_amd.settings import complete_settings_dict
+from splink_amd.sqlexpr import Bin, Case, Col, Func, Lit, parse
+from splink_amd.validate import ValidationError, validate_settings
+
+warnings.filterwarnings("ignore")
+GOLDENS = ["test1", "main_api_nojaro", "main_api_jaro", "test2_nulls", "synthetic_cfg1", "custom_exprs", "link_tf"]
+
+
+def spark_for(jaro):
+    return AmdSession(0) if jaro else "supress_warnings"
+
+
+@pytest.mark.parametrize("name", GOLDENS)
+def test_settings_completion_matches_reference(name):
+    g = load_golden(name)
+    ours = complete_settings_dict(copy.deepcopy(g["settings_in"]), spark_for(g["jaro"]))
+    ref = g["settings_completed"]
+    for k in ("em_convergence", "unique_id_column_name", "additional_columns_to_retain", "retain_matching_columns",
+              "retain_intermediate_calculation_columns", "max_iterations", "proportion_of_matches", "link_type"):
+        assert ours[k] == ref[k], k
+    forms = {}
+    for key in ("df", "df_l"):
+        if key in g:
+            for c, vals in g[key].items():
+                forms[c] = "num" if all(v is None or isinstance(v, (int, float)) for v in vals) else "str"
+    schema = Schema(forms)
+    for a, b in zip(ours["comparison_columns"], ref["comparison_columns"]):
+        for k in ("gamma_index", "num_levels", "data_type", "term_frequency_adjustments"):
+            assert a[k] == b[k]
+        assert a["m_probabilities"] == pytest.approx(b["m_probabilities"], rel=1e-15)
+        assert a["u_probabilities"] == pytest.approx(b["u_probabilities"], rel=1e-15)
+    # our template text and the reference's compile to the same device program
+    pa = compile_comparisons(ours, schema)
+    pb = compile_comparisons(ref, schema)
+    assert (pa.programs == pb.programs).all()
+    assert (pa.instrs == pb.instrs).all()
+    assert pa.operands == pb.operands and pa.literals == pb.literals
+
+
+def test_params_layout_and_json_roundtrip(tmp_path):
+    g = load_golden("test1")
+    p = Params(copy.deepcopy(g["settings_in"]), "supress_warnings")
+    assert list(p.params["π"]["gamma_mob"].keys()) == ["gamma_index", "desc", "column_name", "custom_comparison",
+                                                        "num_levels", "prob_dist_match", "prob_dist_non_match"]
+    rows = g["iterations"][0]["pi_rows"]
+    p._update_params(g["iterations"][0]["lambda"], rows)
+    assert p.params["π"]["gamma_mob"]["prob_dist_match"]["level_0"]["probability"] == \
+        g["iterations"][0]["pi"]["gamma_mob"]["m"][0]
+    assert len(p.param_history) == 1 and p.iteration == 2
+    path = tmp_path / "m.json"
+    p.save_params_to_json_file(str(path))
+    with pytest.raises(ValueError):
+        p.save_params_to_json_file(str(path))
+    q = load_params_from_json(str(path))
+    assert q.params == json.loads(json.dumps(p.params))
+    assert q.iteration == 1  # the reference does not restore the iteration counter (params.py:569-573)
+    d = json.load(open(path))
+    assert set(d) == {"current_params", "historical_params", "settings"}
+
+
+def _stats_from_histogram(gam, nlev, lam, m, u):
+    """Product statistics layout from the oracle's per-pair statistics (test helper)."""
+    s = orc.em_stats(gam, nlev, lam, m, u)
+    out = [s[0], s[1], s[2], 0.0, 0.0]
+    return np.array(out + list(s[3:]))
+
+
+@pytest.mark.parametrize("name", ["test1", "test2_nulls", "synthetic_cfg1"])
+def test_m_step_rows_match_reference_rows(name):
+    g = load_golden(name)
+    st = g["settings_completed"]
+    names = [f"gamma_{c.get('custom_name', c.get('col_name'))}" for c in st["comparison_columns"]]
+    nlev = [c["num_levels"] for c in st["comparison_columns"]]
+    gam = np.array([g["gammas"][n] for n in names], dtype=np.int8).T
+    m = [g["initial"]["pi"][n]["m"] for n in names]
+    u = [g["initial"]["pi"][n]["u"] for n in names]
+    stats = _stats_from_histogram(gam, nlev, g["initial"]["lambda"], m, u)
+    lam, rows = m_step_rows(stats, names, nlev)
+    it = g["iterations"][0]
+    assert lam == pytest.approx(it["lambda"], rel=1e-9)
+    key = lambda r: (r["gamma_col"], r["gamma_value"])
+    exp = sorted(it["pi_rows"], key=key)
+    got = sorted(rows, key=key)
+    assert [key(r) for r in got] == [key(r) for r in exp]
+    for a, b in zip(got, exp):
+        for k in ("new_probability_match", "new_probability_non_match"):
+            assert (a[k] is None) == (b[k] is None)
+            if a[k] is not None:
+                assert a[k] == pytest.approx(b[k], rel=1e-9)
+
+
+def test_parser_basics():
+    e = parse("case when a_l is null or a_r is null then -1 when a_l = a_r then 1 else 0 end as gamma_a")
+    assert isinstance(e, Case) and len(e.whens) == 2 and e.else_ == Lit(0)
+    assert parse("substr(x_l, 1, 3)") == Func("substr", (Col("x_l"), Lit(1), Lit(3)))
+    assert parse("l.first_name = r.first_name") == Bin("=", Col("first_name", "l"), Col("first_name", "r"))
+    assert parse("'it''s'") == Lit("it's")
+    with pytest.raises(ValueError):
+        parse("case when a = then 1 end")
+
+
+def test_compiler_rejects_unsupported_sql():
+    schema = Schema({"a": "str", "b": "num"})
+    bad = [
+        "case when a_l is null then -1 when soundex(a_l) = soundex(a_r) then 1 else 0 end",
+        "case when a_l = a_r then 1 end",  # no ELSE
+        "case when a_l = a_r then 5 else 0 end",  # level out of range for 2 levels
+        "case when a_l like 'x%' then 1 else 0 end",
+    ]
+    for expr in bad:
+        st = {"comparison_columns": [{"col_name": "a", "num_levels": 2, "case_expression": expr}]}
+        with pytest.raises(ValueError):
+            compile_comparisons(st, schema)
+    with pytest.raises(ValueError):
+        compile_rule("l.a < r.a", schema)
+    with pytest.raises(ValueError):
+        compile_rule("l.a = l.a", schema)
+
+
+def test_blocking_rule_compile():
+    schema = Schema({"surname": "str", "dob": "str", "first_name": "str"})
+    r = compile_rule("l.surname = r.surname AND substr(l.dob,1,4) = substr(r.dob,1,4)", schema)
+    assert r.symmetric and len(r.terms) == 2
+    r = compile_rule("l.first_name = r.surname", schema)
+    assert not r.symmetric
+
+
+def test_validation_errors():
+    with pytest.raises(ValidationError):
+        validate_settings({"link_type": "dedupe", "comparison_columns": [{"col_name": "a"}]})
+    with pytest.raises(ValidationError):
+        validate_settings({"link_type": "dedupe_only", "comparison_columns": []})
+    with pytest.raises(ValidationError):
+        validate_settings({"link_type": "dedupe_only", "comparison_columns": [{"col_name": "a", "bogus": 1}]})
+    validate_settings({"link_type": "dedupe_only", "comparison_columns": [{"col_name": "a"}]})
+
+
+def test_jaro_detection():
+    assert cs._check_jaro_registered(None) is False
+    assert cs._check_jaro_registered("supress_warnings") is False
+    assert cs._check_jaro_registered(AmdSession(0)) is True
