@@ -230,14 +230,6 @@ class ExpectationFrame(SplinkDataFrame):
         return self._mp
 
     def _column_order(self):
-        if getattr(self.job, "passthrough", None) is not None:
-            base = [c for c in self.job.passthrough.columns]
-            extra = []
-            if self.settings["retain_intermediate_calculation_columns"]:
-                for n in self.gammas.gamma_names:
-                    g = n[len("gamma_"):]
-                    extra += [f"prob_gamma_{g}_non_match", f"prob_gamma_{g}_match"]
-            return ["match_probability"] + base + extra
         return ["match_probability"] + df_e_column_order(self.settings)
 
     def _prob_columns(self, gam):
