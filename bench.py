@@ -181,6 +181,7 @@ def main():
         "breakdown_ms": {"gamma": g_ms, "em_hist": h_ms, "em_final": float(np.mean(fin_ms)), "score": score_ms,
                          "block_device": block_kernel_ms, "block_wall_incl_host_prep": block_s * 1e3},
         "deferred_pairs": job.ctx.gammas_deferred(),
+        "exact_cells_per_column": dict(zip(names, job.ctx.gammas_exact_counts(len(names)))),
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)
@@ -197,7 +198,8 @@ def cpu_baseline(job, df, st, seconds):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     l, r = job.pair_rows()
-    cols = [orc.StrCol(df[c].tolist()) for c in COLS]
+    t = job.tables[0]  # pair rows index the job's (blocking-key clustered) table
+    cols = [orc.StrCol(t[c].tolist()) for c in COLS]
     specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
     lp = [(c["m_probabilities"], c["u_probabilities"]) for c in st["comparison_columns"]]
     nlev = [c["num_levels"] for c in st["comparison_columns"]]

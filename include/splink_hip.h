@@ -62,9 +62,13 @@ int spk_ctx_enable_timing(spk_ctx *ctx, int on);
 /* side 0 = df (dedupe_only, link_and_dedupe after concatenation) or df_l; side 1 = df_r. */
 int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols);
 /* String column from Arrow-style UTF-8: offsets[n_rows+1] into data; valid[n_rows] (1 = non-null).
- * Decoded on the device to UTF-16 code units (Jaro-Winkler alphabet) + code-point lengths. */
+ * Decoded on the device to UTF-16 code units (Jaro-Winkler alphabet) + code-point lengths.
+ * value_ids (optional, may be NULL): a dictionary id per row, equal iff the strings are equal, in
+ * one id space for side 0 and side 1 (Arrow dictionary encoding), in [0, 2^32) for non-NULL rows.
+ * With ids, string equality in comparison programs is one integer compare; without, a hash then
+ * a unit compare.  A column holds at most 2^34 UTF-16 units. */
 int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, const uint8_t *data,
-                       const uint8_t *valid);
+                       const uint8_t *valid, const int64_t *value_ids);
 int spk_table_add_float64(spk_ctx *ctx, int side, int col, const double *values, const uint8_t *valid);
 /* Order rank per row for the link-type predicate: dedupe `l.uid < r.uid` (blocking.py:136),
  * link_and_dedupe `(l.src < r.src) or (l.uid < r.uid and same src)` (:139).  Equal rank = equal key. */
@@ -154,6 +158,15 @@ int spk_gammas_load(spk_ctx *ctx, int n_cols, const int32_t *n_levels, int64_t n
 int spk_n_patterns(spk_ctx *ctx, int64_t *out);
 /* Pairs the last spk_gammas evaluated in the global-memory pass (strings beyond LDS staging). */
 int spk_gammas_deferred(spk_ctx *ctx, int64_t *out);
+/* Per comparison column: pairs the last spk_gammas could not decide from bounds in the filter pass
+ * and evaluated with the exact similarity (out[n], n >= number of columns). */
+int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
+/* Columns in the shape of the case_statements.py templates (NULL branch, then single-leaf tests
+ * on the same two plain operands) are filtered straight from the row records; every other column
+ * by the general interpreter.  on = 0 sends every column through the interpreter (same results;
+ * for testing).  spk_gammas_simple_count: how many columns the last spk_gammas took as simple. */
+int spk_gammas_set_simple(spk_ctx *ctx, int on);
+int spk_gammas_simple_count(spk_ctx *ctx, int *out);
 
 /* ---- the jar's similarity UDFs as bulk device functions ---------------------------------
  * spk_jaro_winkler_sim replaces uk.gov.moj.dash.linkage.JaroWinklerSimilarity.call(String, String)

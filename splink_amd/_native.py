@@ -42,7 +42,8 @@ EXPORTS = [
     "spk_table_add_utf8", "spk_table_add_float64", "spk_table_set_rank", "spk_table_set_key", "spk_block",
     "spk_pairs_count", "spk_pairs_copy", "spk_pairs_load", "spk_gammas", "spk_gammas_copy", "spk_gammas_load",
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
-    "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein",
+    "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
+    "spk_gammas_set_simple", "spk_gammas_simple_count",
 ]
 
 
@@ -135,14 +136,15 @@ class Context:
         check(self._lib.spk_table_create(self._h, ctypes.c_int(side), ctypes.c_int64(n_rows), ctypes.c_int(n_cols)),
               "spk_table_create")
 
-    def table_add_utf8(self, side, col, offsets, data, valid):
+    def table_add_utf8(self, side, col, offsets, data, valid, value_ids=None):
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         data = np.ascontiguousarray(data, dtype=np.uint8)
         if data.size == 0:
             data = np.zeros(1, dtype=np.uint8)
         valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        ids = None if value_ids is None else np.ascontiguousarray(value_ids, dtype=np.int64)
         check(self._lib.spk_table_add_utf8(self._h, ctypes.c_int(side), ctypes.c_int(col), _ptr(offsets), _ptr(data),
-                                           _ptr(valid)), "spk_table_add_utf8")
+                                           _ptr(valid), _ptr(ids)), "spk_table_add_utf8")
 
     def table_add_float64(self, side, col, values, valid):
         values = np.ascontiguousarray(values, dtype=np.float64)
@@ -224,6 +226,19 @@ class Context:
     def gammas_deferred(self) -> int:
         n = ctypes.c_int64(0)
         check(self._lib.spk_gammas_deferred(self._h, ctypes.byref(n)), "spk_gammas_deferred")
+        return n.value
+
+    def gammas_exact_counts(self, K: int):
+        out = np.zeros(max(K, 1), dtype=np.int64)
+        check(self._lib.spk_gammas_exact_counts(self._h, _ptr(out), ctypes.c_int(len(out))), "spk_gammas_exact_counts")
+        return out[:K].tolist()
+
+    def gammas_set_simple(self, on: bool):
+        check(self._lib.spk_gammas_set_simple(self._h, ctypes.c_int(1 if on else 0)), "spk_gammas_set_simple")
+
+    def gammas_simple_count(self) -> int:
+        n = ctypes.c_int(0)
+        check(self._lib.spk_gammas_simple_count(self._h, ctypes.byref(n)), "spk_gammas_simple_count")
         return n.value
 
     def em_histogram(self, d_hist_ptr: int = 0):

@@ -8,6 +8,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["spk_ctx.hip", "spk_block.hip", "spk_gamma.hip", "spk_em.hip"]
+HEADERS = ["spk_internal.h", "spk_strsim.h"]
 OUT = os.path.join(HERE, "libsplink_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # the Jaro-Winkler / E-step arithmetic must round exactly like the JVM: no FMA contraction
@@ -18,7 +19,7 @@ def _stale():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    srcs = [os.path.join(HERE, "csrc", s) for s in SOURCES + ["spk_internal.h"]]
+    srcs = [os.path.join(HERE, "csrc", s) for s in SOURCES + HEADERS]
     srcs.append(os.path.join(HERE, "..", "include", "splink_hip.h"))
     return any(os.path.getmtime(s) > t for s in srcs)
 

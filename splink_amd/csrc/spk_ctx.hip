@@ -23,10 +23,8 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
         d.kind = c ? c->kind : COL_NONE;
         if (c && c->kind == COL_STR) {
             d.units = c->units.p;
-            d.off = c->off.p;
-            d.len16 = c->len16.p;
-            d.cplen = c->cplen.p;
-            d.hash = c->hash.p;
+            d.meta = c->meta.p;
+            d.planes = c->planes.p;
         } else if (c && c->kind == COL_NUM) {
             d.val = c->val.p;
             d.valid = c->valid.p;
@@ -41,24 +39,39 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
     return SPK_OK;
 }
 
-// One thread per row: decode the row's UTF-8 into UTF-16 units at its byte offset, count code
-// points, hash the units.  Surrogate-encoded (CESU / "surrogatepass") 3-byte sequences decode to
-// lone surrogate units, exactly as a Java String would hold them.
+// One thread per row: decode the row's UTF-8 into UTF-16 units at its aligned start, count code
+// points, hash the units and build the bucket sketch used by the comparison filters.
+// Surrogate-encoded (CESU / "surrogatepass") 3-byte sequences decode to lone surrogate units,
+// exactly as a Java String would hold them.
+__device__ inline void sketch_add(uint64_t &sk, uint32_t unit) {
+    const uint32_t b = sketch_bucket(unit);
+    if (((sk >> (4 * b)) & 15ull) == 15ull) sk |= 1ull << 60;  // saturated: flag nibble 15
+    else sk += 1ull << (4 * b);
+}
+
 __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const uint8_t *__restrict__ bytes,
                               const uint8_t *__restrict__ valid, uint16_t *__restrict__ units,
-                              int32_t *__restrict__ len16, int32_t *__restrict__ cplen, uint64_t *__restrict__ hash) {
+                              RecMeta *__restrict__ meta, uint64_t *__restrict__ planes,
+                              const int64_t *__restrict__ ids) {
     int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= n) return;
+    RecMeta m;
+    const int64_t start = (off8[row] + 3 * row + 3) & ~(int64_t)3;
+    m.off4 = (uint32_t)(start >> 2);
+    m.head = 0;
     if (!valid[row]) {
-        len16[row] = -1;
-        cplen[row] = -1;
-        hash[row] = 0;
+        m.len16 = -1;
+        m.cpf = 0;
+        m.key = 0;
+        m.sketch = 0;
+        meta[row] = m;
+        for (int b = 0; b < N_PLANES; ++b) planes[row * N_PLANES + b] = 0;
         return;
     }
     int64_t b = off8[row], e = off8[row + 1];
-    uint16_t *dst = units + b;
+    uint16_t *dst = units + start;
     int32_t nu = 0, nc = 0;
-    uint64_t h = 1469598103934665603ull;
+    uint64_t h = 1469598103934665603ull, sk = 0;
     while (b < e) {
         uint32_t c0 = bytes[b];
         uint32_t cp;
@@ -76,15 +89,33 @@ __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const
             dst[nu++] = lo;
             h = (h ^ hi) * 1099511628211ull;
             h = (h ^ lo) * 1099511628211ull;
+            sketch_add(sk, hi);
+            sketch_add(sk, lo);
         } else {
             dst[nu++] = (uint16_t)cp;
             h = (h ^ cp) * 1099511628211ull;
+            sketch_add(sk, cp);
         }
         ++nc;
     }
-    len16[row] = nu;
-    cplen[row] = nc;
-    hash[row] = h ^ (uint64_t)nu;
+    // bit-planes for short Latin-1 rows
+    uint64_t pl[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool ok = nu <= 64;
+    for (int i = 0; ok && i < nu; ++i) {
+        const uint32_t c = dst[i];
+        if (c >= 256) { ok = false; break; }
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) pl[b] |= (uint64_t)((c >> b) & 1u) << i;
+    }
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) planes[row * N_PLANES + b] = ok ? pl[b] : 0;
+    for (int i = 0; i < 4 && i < nu; ++i) m.head |= (uint64_t)dst[i] << (16 * i);
+    m.len16 = nu;
+    m.cpf = (uint32_t)nc | (ok ? CPF_PLANES : 0u) | (ids ? CPF_ID : 0u);
+    h ^= (uint64_t)nu;
+    m.key = ids ? (uint32_t)ids[row] : (uint32_t)(h ^ (h >> 32));
+    m.sketch = sk;
+    meta[row] = m;
 }
 
 }  // namespace spk
@@ -220,7 +251,7 @@ static int get_col(spk_ctx *ctx, int side, int col, Column **out) {
 }
 
 int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, const uint8_t *data,
-                       const uint8_t *valid) {
+                       const uint8_t *valid, const int64_t *value_ids) {
     SPK_REQUIRE(offsets && valid, SPK_E_INVALID, "spk_table_add_utf8: null buffer");
     Column *c = nullptr;
     SPK_TRY(get_col(ctx, side, col, &c));
@@ -228,23 +259,35 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
     int64_t n = ctx->table[side].n;
     int64_t nbytes = offsets[n];
     SPK_REQUIRE(offsets[0] == 0 && nbytes >= 0, SPK_E_INVALID, "spk_table_add_utf8: offsets must start at 0");
+    SPK_REQUIRE(nbytes + 3 * n + 16 < ((int64_t)1 << 34), SPK_E_LIMIT,
+                "spk_table_add_utf8: a string column is limited to 2^34 UTF-16 units (16 GiB of text)");
+    if (value_ids) {
+        for (int64_t i = 0; i < n; ++i)
+            SPK_REQUIRE(!valid[i] || (value_ids[i] >= 0 && value_ids[i] <= (int64_t)UINT32_MAX), SPK_E_INVALID,
+                        "spk_table_add_utf8: value ids must lie in [0, 2^32) for non-NULL rows");
+    }
     c->kind = COL_STR;
     DevBuf<uint8_t> d_bytes, d_valid;
     SPK_TRY(d_bytes.alloc((size_t)nbytes + 1));
     SPK_TRY(d_valid.alloc((size_t)n + 1));
-    SPK_TRY(c->units.alloc((size_t)nbytes + 1));
-    SPK_TRY(c->off.alloc((size_t)n + 1));
-    SPK_TRY(c->len16.alloc((size_t)n + 1));
-    SPK_TRY(c->cplen.alloc((size_t)n + 1));
-    SPK_TRY(c->hash.alloc((size_t)n + 1));
+    SPK_TRY(c->units.alloc((size_t)(nbytes + 3 * n + 16)));
+    SPK_TRY(c->meta.alloc((size_t)n + 1));
+    SPK_TRY(c->planes.alloc((size_t)(n + 1) * N_PLANES));
+    DevBuf<int64_t> d_off8, d_ids;
+    SPK_TRY(d_off8.alloc((size_t)n + 1));
+    if (value_ids) {
+        SPK_TRY(d_ids.alloc((size_t)n + 1));
+        if (n) SPK_HIP(hipMemcpyAsync(d_ids.p, value_ids, (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
     if (nbytes) SPK_HIP(hipMemcpyAsync(d_bytes.p, data, (size_t)nbytes, hipMemcpyHostToDevice, ctx->stream));
     if (n) SPK_HIP(hipMemcpyAsync(d_valid.p, valid, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemcpyAsync(c->off.p, offsets, (size_t)(n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+    SPK_HIP(hipMemsetAsync(c->units.p, 0, (size_t)(nbytes + 3 * n + 16) * 2, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(d_off8.p, offsets, (size_t)(n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
     if (n) {
         int bs = 256;
-        k_utf8_decode<<<(unsigned)((n + bs - 1) / bs), bs, 0, ctx->stream>>>(n, c->off.p, d_bytes.p, d_valid.p,
-                                                                          c->units.p, c->len16.p, c->cplen.p,
-                                                                          c->hash.p);
+        k_utf8_decode<<<(unsigned)((n + bs - 1) / bs), bs, 0, ctx->stream>>>(n, d_off8.p, d_bytes.p, d_valid.p,
+                                                                          c->units.p, c->meta.p, c->planes.p,
+                                                                          value_ids ? d_ids.p : nullptr);
         SPK_HIP(hipGetLastError());
     }
     SPK_HIP(hipStreamSynchronize(ctx->stream));

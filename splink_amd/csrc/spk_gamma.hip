@@ -1,28 +1,61 @@
 // Comparison vectors (replaces gammas.py:65-124 evaluating the CASE templates of
 // case_statements.py:62-277 with the jar's jaro_winkler_sim and Spark's levenshtein).
 //
-// One pair per lane.  Every comparison column is a small program of WHEN branches; each branch
-// is an RPN predicate over Kleene booleans (SQL three-valued logic, NULL = not taken).  The
-// program is uniform across the wave, so instruction fetch and dispatch are scalar; only the
-// string work diverges.  Strings of a JW / Levenshtein operand are staged in LDS in a
-// [position][lane] layout (lane-indexed banks, conflict-free for any per-lane position).
-// Pairs whose strings exceed the LDS staging capacity (or carry surrogates for Levenshtein) are
-// deferred to a second, global-memory pass with no length restriction up to SLOW_LIMIT.
+// Every comparison column is a small program of WHEN branches; each branch is an RPN predicate
+// over SQL three-valued logic (NULL = branch not taken).  The program is uniform across a wave,
+// so instruction fetch and dispatch are scalar; only the string work diverges.
 //
-// Output: one packed code per pair, code = Σ_k (γ_k + 1) · Π_{j<k}(L_j + 1), uint16 when the
-// pattern space fits, else uint32.
-//
-// Jaro-Winkler arithmetic follows commons-text 1.4 exactly; the library is built
-// with -ffp-contract=off so no FMA contraction changes the rounding.
+// One lane per pair diverges badly if a wave must wait for its slowest lane's Jaro-Winkler or
+// Levenshtein, so the evaluation is split:
+//   1. filter pass (one lane per pair): NULL tests, equality (hash first), numeric tests and
+//      *bounds* for the string similarities -- a Jaro-Winkler upper bound and a Levenshtein
+//      lower / upper bound from 32-byte per-row metadata (lengths, hash, bucket sketch).  A
+//      fourth truth value, UNDECIDED, propagates through AND / OR / NOT; a column whose WHEN
+//      sequence is decided gets its level here, the others are appended (wave-aggregated) to
+//      that column's work list.
+//   2. exact pass (one lane per listed (pair, column)): the full interpreter with the exact
+//      similarities computed from registers: match masks from per-row bit-planes (8 planes of
+//      Latin-1 units, <= 64 units), Levenshtein after stripping the common prefix / suffix,
+//      32-bit masks when the (trimmed) pattern fits.  Strings beyond 64 units, and surrogate
+//      strings under Levenshtein, go to
+//   3. the global-memory pass (two-row DP / flag words in scratch, any length up to SLOW_LIMIT).
+// Passes 2 and 3 add their level into a 32-bit code per pair; a pack pass writes the final
+// code = Σ_k (γ_k + 1) · Π_{j<k}(L_j + 1) as uint16 when the pattern space fits, else uint32.
+// Bounds are exact decisions (never approximations), so the result is the exact evaluation.
+#include <algorithm>
 #include <cmath>
 
-#include "spk_internal.h"
+#include "spk_strsim.h"
 
 namespace spk {
 
-constexpr int G_THREADS = 256;
-constexpr int MAXU = 40;          // LDS staging capacity per string (UTF-16 units)
-constexpr int SLOW_LIMIT = 1024;  // deferred-pass capacity per string
+constexpr int F_THREADS = 256;  // filter pass
+constexpr int X_THREADS = 256;  // exact pass
+constexpr int U_THREADS = 128;  // UDF kernel: 2 x 64 x 128 x 2 B = 32 KiB of LDS per block
+
+enum Mode { M_FILTER = 0, M_EXACT = 1, M_SLOW = 2 };
+enum Status { ST_DONE = 0, ST_UNDECIDED = 1, ST_NEEDS_SLOW = 2 };
+
+// A "simple" comparison column: the shape every case_statements.py template has --
+//   WHEN x_l IS NULL OR x_r IS NULL THEN null_level
+//   WHEN test_1(x_l, x_r) THEN level_1 ... WHEN test_n(x_l, x_r) THEN level_n ELSE else_level
+// with each test one leaf (=, <>, jaro_winkler_sim cmp t, levenshtein [ratio] cmp t, numeric
+// compare / abs diff / percent diff) over the same two plain operands.  The filter pass evaluates
+// these straight from the two rows' metadata records, loaded for several columns at once; every
+// other program runs through the general interpreter.  Both give identical levels.
+constexpr int MAX_TESTS = 6;
+constexpr int SIMPLE_GROUP = 4;  // simple columns whose row records are in flight together
+constexpr int MAX_SIMPLE = 64;   // = the column limit of set_pattern_space
+enum SimpleKind : int32_t { SK_STR = 1, SK_NUM = 2 };
+struct SimpleCol {
+    int32_t k;  // comparison column (position in the code)
+    int32_t kind;
+    int32_t col;  // table column, the same index on both sides
+    int32_t null_level, else_level, n_tests;
+    int32_t op[MAX_TESTS], cmp[MAX_TESTS], level[MAX_TESTS];
+    double t[MAX_TESTS];
+    int64_t stride;
+};
 
 struct GammaArgs {
     const ColDesc *cols0, *cols1;  // tables for operand side 0 (`_l`) and 1 (`_r`)
@@ -37,29 +70,34 @@ struct GammaArgs {
     const int64_t *lit_off;
     const int32_t *lit_len, *lit_cplen;
     const int64_t *stride;
-    uint8_t *codes;
-    int code_bytes;
-    int32_t *defer_list;
-    unsigned int *defer_count;
-    const int32_t *work;  // slow pass: pair indices
-    int64_t n_work;
+    uint32_t *code32;
+    int32_t *work;                // [K][P] pair indices per column needing the exact pass, by region
+    unsigned int *region_count;   // [K][n_regions] list length of each region
+    int64_t region_len;           // pair ordinals per region (one filter workgroup each)
+    int n_regions;
+    int32_t *slow;             // slow-pass lists, column k at slow_off[k]
+    const int64_t *slow_off;
+    unsigned int *slow_count;  // [K]
     int *err;
+    const SimpleCol *simple;   // filter pass: simple columns ...
+    int n_simple;
+    const int32_t *complex_k;  // ... and the columns the interpreter evaluates
+    int n_complex;
 };
 
-struct StrView {
-    const uint16_t *p;
-    int32_t n;    // UTF-16 units
-    int32_t ncp;  // code points
-    int32_t null;
-    uint64_t hash;
-    int32_t has_hash;
-};
+enum : int { KF = 0, KT = 1, KN = 2, KU = 3 };  // false, true, NULL, undecided (filter pass)
 
-enum : int { KF = 0, KT = 1, KN = 2 };
-
-__device__ inline int k_and(int a, int b) { return (a == KF || b == KF) ? KF : ((a == KN || b == KN) ? KN : KT); }
-__device__ inline int k_or(int a, int b) { return (a == KT || b == KT) ? KT : ((a == KN || b == KN) ? KN : KF); }
-__device__ inline int k_not(int a) { return a == KN ? KN : (a == KT ? KF : KT); }
+__device__ inline int k_and(int a, int b) {
+    if (a == KF || b == KF) return KF;
+    if (a == KU || b == KU) return KU;
+    return (a == KN || b == KN) ? KN : KT;
+}
+__device__ inline int k_or(int a, int b) {
+    if (a == KT || b == KT) return KT;
+    if (a == KU || b == KU) return KU;
+    return (a == KN || b == KN) ? KN : KF;
+}
+__device__ inline int k_not(int a) { return (a == KN || a == KU) ? a : (a == KT ? KF : KT); }
 
 __device__ inline int cmpd(double a, double b, int cmp) {
     bool r;
@@ -74,6 +112,19 @@ __device__ inline int cmpd(double a, double b, int cmp) {
     return r ? KT : KF;
 }
 
+// `v cmp t` for an unknown v in [lo, hi]: decided only if every v in the interval agrees.
+__device__ inline int decide(double lo, double hi, int cmp, double t) {
+    if (lo == hi) return cmpd(lo, t, cmp);
+    switch (cmp) {
+        case SPK_CMP_GT: return lo > t ? KT : (hi <= t ? KF : KU);
+        case SPK_CMP_GE: return lo >= t ? KT : (hi < t ? KF : KU);
+        case SPK_CMP_LT: return hi < t ? KT : (lo >= t ? KF : KU);
+        case SPK_CMP_LE: return hi <= t ? KT : (lo > t ? KF : KU);
+        case SPK_CMP_EQ: return (t < lo || t > hi) ? KF : KU;
+        default: return (t < lo || t > hi) ? KT : KU;
+    }
+}
+
 // Spark UTF8String.substringSQL(pos, len) on a code-point range, mapped to UTF-16 units.
 __device__ inline void apply_substr(StrView &s, int pos, int len) {
     int nc = s.ncp;
@@ -81,7 +132,8 @@ __device__ inline void apply_substr(StrView &s, int pos, int len) {
     long end = (long)start + len;
     if (start < 0) start = 0;
     if (end > nc) end = nc;
-    s.has_hash = 0;
+    s.has_meta = 0;
+    s.planes = nullptr;
     if (start >= end) {
         s.n = 0;
         s.ncp = 0;
@@ -106,29 +158,28 @@ __device__ inline void apply_substr(StrView &s, int pos, int len) {
 }
 
 __device__ inline StrView lit_view(const GammaArgs &A, int lit) {
-    StrView s;
-    s.p = A.lit_units + A.lit_off[lit];
-    s.n = A.lit_len[lit];
-    s.ncp = A.lit_cplen[lit];
-    s.null = 0;
-    s.has_hash = 0;
-    s.hash = 0;
+    return plain_view(A.lit_units + A.lit_off[lit], A.lit_len[lit], A.lit_cplen[lit]);
+}
+
+// A row's string view from its metadata record.
+__device__ inline StrView row_view(const ColDesc &c, const RecMeta &m, int64_t row, int col) {
+    StrView s = plain_view(c.units + meta_off(m), m.len16, meta_cplen(m));
+    s.planes = (m.cpf & CPF_PLANES) ? c.planes + row * N_PLANES : nullptr;
+    s.has_meta = 1;
+    s.exact_key = (m.cpf & CPF_ID) ? col + 1 : 0;  // ids are per column (both sides share)
+    s.key = m.key;
+    s.sketch = m.sketch;
     return s;
 }
 
 __device__ inline StrView get_str(const GammaArgs &A, const spk_operand &op, int32_t x, int32_t y) {
-    StrView s{nullptr, 0, 0, 1, 0, 0};
+    StrView s;
     if (op.kind == 0) {
-        int32_t row = op.side ? y : x;
         const ColDesc &c = (op.side ? A.cols1 : A.cols0)[op.col];
-        int32_t n = c.len16[row];
-        if (n >= 0) {
-            s.p = c.units + c.off[row];
-            s.n = n;
-            s.ncp = c.cplen[row];
-            s.null = 0;
-            s.hash = c.hash[row];
-            s.has_hash = 1;
+        const int32_t row = op.side ? y : x;
+        const RecMeta m = c.meta[row];
+        if (m.len16 >= 0) {
+            s = row_view(c, m, row, op.col);
         } else if (op.lit >= 0) {
             s = lit_view(A, op.lit);
         }
@@ -144,8 +195,8 @@ __device__ inline bool get_num(const GammaArgs &A, const spk_operand &op, int32_
         v = op.num;
         return true;
     }
-    int32_t row = op.side ? y : x;
     const ColDesc &c = (op.side ? A.cols1 : A.cols0)[op.col];
+    const int32_t row = op.side ? y : x;
     if (c.valid[row]) {
         v = c.val[row];
         return true;
@@ -155,14 +206,6 @@ __device__ inline bool get_num(const GammaArgs &A, const spk_operand &op, int32_
         return true;
     }
     return false;
-}
-
-__device__ inline bool units_equal(const StrView &a, const StrView &b) {
-    if (a.n != b.n) return false;
-    if (a.has_hash && b.has_hash && a.hash != b.hash) return false;
-    for (int i = 0; i < a.n; ++i)
-        if (a.p[i] != b.p[i]) return false;
-    return true;
 }
 
 // code-point order (= Spark's UTF-8 byte order) for <, <=, >, >=
@@ -182,184 +225,18 @@ __device__ inline int str_order(const StrView &a, const StrView &b) {
     return 0;
 }
 
-// ---- accessors -------------------------------------------------------------------------
-struct LdsAcc {
-    const uint16_t *b;
-    __device__ uint16_t operator[](int i) const { return b[i * G_THREADS]; }
-};
-struct GlbAcc {
-    const uint16_t *p;
-    __device__ uint16_t operator[](int i) const { return p[i]; }
-};
-
-__device__ inline double jw_finish(int m, int t, int prefix, int lf, int ls, int lmx) {
-    if (m == 0) return 0.0;
-    double md = (double)m;
-    double j = ((md / (double)lf + md / (double)ls) + (md - (double)(t / 2)) / md) / 3.0;
-    if (j < 0.7) return j;
-    double w = 1.0 / (double)lmx;
-    if (w > 0.1) w = 0.1;
-    return j + (w * (double)prefix) * (1.0 - j);
-}
-
-// commons-text 1.4 JaroWinklerDistance for strings of <= 64 units (bit-mask flags).
-template <class Acc>
-__device__ double jw_small(Acc first, int lf, Acc second, int ls) {
-    const bool fmax = lf > ls;
-    const Acc mx = fmax ? first : second;
-    const Acc mn = fmax ? second : first;
-    const int lmx = fmax ? lf : ls, lmn = fmax ? ls : lf;
-    const int range = lmx / 2 - 1 > 0 ? lmx / 2 - 1 : 0;
-    uint64_t flags = 0, matched = 0;
-    int m = 0;
-    for (int mi = 0; mi < lmn; ++mi) {
-        const uint16_t c = mn[mi];
-        const int lo = mi - range > 0 ? mi - range : 0;
-        const int hi = mi + range + 1 < lmx ? mi + range + 1 : lmx;
-        for (int xi = lo; xi < hi; ++xi) {
-            if (!((flags >> xi) & 1ull) && mx[xi] == c) {
-                flags |= 1ull << xi;
-                matched |= 1ull << mi;
-                ++m;
-                break;
-            }
-        }
-    }
-    if (m == 0) return 0.0;
-    int t = 0;
-    uint64_t fm = flags, mm = matched;
-    while (mm) {
-        int i = __ffsll((unsigned long long)mm) - 1;
-        int x = __ffsll((unsigned long long)fm) - 1;
-        t += mn[i] != mx[x];
-        mm &= mm - 1;
-        fm &= fm - 1;
-    }
-    int prefix = 0;
-    for (int mi = 0; mi < lmn; ++mi) {
-        if (first[mi] == second[mi]) ++prefix;
-        else break;
-    }
-    return jw_finish(m, t, prefix, lf, ls, lmx);
-}
-
-// Same algorithm, any length up to SLOW_LIMIT (flag words in scratch).
-__device__ double jw_long(GlbAcc first, int lf, GlbAcc second, int ls) {
-    const bool fmax = lf > ls;
-    const GlbAcc mx = fmax ? first : second;
-    const GlbAcc mn = fmax ? second : first;
-    const int lmx = fmax ? lf : ls, lmn = fmax ? ls : lf;
-    const int range = lmx / 2 - 1 > 0 ? lmx / 2 - 1 : 0;
-    uint64_t flags[SLOW_LIMIT / 64], matched[SLOW_LIMIT / 64];
-    for (int i = 0; i < SLOW_LIMIT / 64; ++i) flags[i] = matched[i] = 0;
-    int m = 0;
-    for (int mi = 0; mi < lmn; ++mi) {
-        const uint16_t c = mn[mi];
-        const int lo = mi - range > 0 ? mi - range : 0;
-        const int hi = mi + range + 1 < lmx ? mi + range + 1 : lmx;
-        for (int xi = lo; xi < hi; ++xi) {
-            if (!((flags[xi >> 6] >> (xi & 63)) & 1ull) && mx[xi] == c) {
-                flags[xi >> 6] |= 1ull << (xi & 63);
-                matched[mi >> 6] |= 1ull << (mi & 63);
-                ++m;
-                break;
-            }
-        }
-    }
-    if (m == 0) return 0.0;
-    int t = 0, xi = 0;
-    for (int mi = 0; mi < lmn; ++mi) {
-        if (!((matched[mi >> 6] >> (mi & 63)) & 1ull)) continue;
-        while (!((flags[xi >> 6] >> (xi & 63)) & 1ull)) ++xi;
-        t += mn[mi] != mx[xi];
-        ++xi;
-    }
-    int prefix = 0;
-    for (int mi = 0; mi < lmn; ++mi) {
-        if (first[mi] == second[mi]) ++prefix;
-        else break;
-    }
-    return jw_finish(m, t, prefix, lf, ls, lmx);
-}
-
-// Levenshtein (Myers 1999 bit-parallel), pattern <= 64 symbols.
-template <class Acc>
-__device__ int lev_myers(Acc pat, int m, Acc txt, int n) {
-    if (m == 0) return n;
-    if (n == 0) return m;
-    uint64_t vp = ~0ull, vn = 0;
-    const uint64_t hib = 1ull << (m - 1);
-    int dist = m;
-    for (int j = 0; j < n; ++j) {
-        const uint16_t c = txt[j];
-        uint64_t eq = 0;
-        for (int i = 0; i < m; ++i) eq |= (uint64_t)(pat[i] == c) << i;
-        const uint64_t x = eq | vn;
-        const uint64_t d0 = (((x & vp) + vp) ^ vp) | x;
-        uint64_t hp = vn | ~(d0 | vp);
-        uint64_t hn = d0 & vp;
-        dist += (hp & hib) ? 1 : 0;
-        dist -= (hn & hib) ? 1 : 0;
-        hp = (hp << 1) | 1ull;
-        hn = hn << 1;
-        vp = hn | ~(d0 | hp);
-        vn = hp & d0;
-    }
-    return dist;
-}
-
-// Levenshtein over code points, any length up to SLOW_LIMIT (two-row DP in scratch).
-__device__ int lev_long(const StrView &a, const StrView &b) {
-    uint32_t cb[SLOW_LIMIT];
-    int32_t row[SLOW_LIMIT + 1];
-    int nb = 0;
-    for (int j = 0; j < b.n; ++j) {
-        uint32_t w = b.p[j];
-        if (w >= 0xD800 && w < 0xDC00 && j + 1 < b.n) {
-            w = 0x10000 + ((w - 0xD800) << 10) + (b.p[j + 1] - 0xDC00);
-            ++j;
-        }
-        cb[nb++] = w;
-    }
-    for (int j = 0; j <= nb; ++j) row[j] = j;
-    int i = 0;
-    for (int u = 0; u < a.n; ++u) {
-        uint32_t w = a.p[u];
-        if (w >= 0xD800 && w < 0xDC00 && u + 1 < a.n) {
-            w = 0x10000 + ((w - 0xD800) << 10) + (a.p[u + 1] - 0xDC00);
-            ++u;
-        }
-        ++i;
-        int diag = row[0];
-        row[0] = i;
-        for (int j = 1; j <= nb; ++j) {
-            int up = row[j];
-            int best = diag + (w != cb[j - 1] ? 1 : 0);
-            if (up + 1 < best) best = up + 1;
-            if (row[j - 1] + 1 < best) best = row[j - 1] + 1;
-            row[j] = best;
-            diag = up;
-        }
-    }
-    return row[nb];
-}
-
-__device__ inline void stage(uint16_t *slot, const StrView &s) {
-    for (int i = 0; i < s.n; ++i) slot[i * G_THREADS] = s.p[i];
-}
-
 struct Memo {
     int jw_key, lev_key;
     double jw;
     int lev;
-    int staged_a, staged_b;  // operand ids currently in LDS slots 0 / 1
+    int staged_a, staged_b;  // operand ids currently in the LDS slots
 };
 
-// Evaluate one WHEN predicate.  Returns KT / KF / KN; sets *defer if the fast pass cannot.
-template <bool SLOW>
+// One WHEN predicate.  Sets *slow when the exact pass needs the global-memory pass.
+template <int MODE>
 __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, int32_t y, uint16_t *slot_a,
-                         uint16_t *slot_b, Memo &mm, bool *defer) {
-    uint32_t st = 0;  // Kleene stack, 2 bits per entry
+                         uint16_t *slot_b, Memo &mm, bool *slow) {
+    uint32_t st = 0;  // stack of truth values, 2 bits per entry
     for (int k = 0; k < count; ++k) {
         const spk_instr in = A.instr[first + k];
         int r = KN;
@@ -384,7 +261,7 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
             case SPK_OP_NOTNULL: {
                 const spk_operand &o = A.ops[in.a];
                 bool isnull;
-                if (o.kind == 0 && ((o.side ? A.cols1 : A.cols0)[o.col].kind == COL_NUM)) {
+                if (o.kind == 2 || (o.kind == 0 && (o.side ? A.cols1 : A.cols0)[o.col].kind == COL_NUM)) {
                     double v;
                     isnull = !get_num(A, o, x, y, v);
                 } else {
@@ -403,8 +280,7 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
                 } else if (in.op == SPK_OP_ABSDIFF) {
                     r = cmpd(fabs(a - b), in.t, in.cmp);
                 } else {
-                    double mx = a > b ? a : b;
-                    double d = fabs(mx);
+                    double d = fabs(a > b ? a : b);
                     r = d == 0.0 ? KN : cmpd(fabs(a - b) / d, in.t, in.cmp);
                 }
                 break;
@@ -413,8 +289,7 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
                 StrView a = get_str(A, A.ops[in.a], x, y), b = get_str(A, A.ops[in.b], x, y);
                 if (a.null || b.null) { r = KN; break; }
                 if (in.cmp == SPK_CMP_EQ || in.cmp == SPK_CMP_NE) {
-                    bool eq = units_equal(a, b);
-                    r = (eq == (in.cmp == SPK_CMP_EQ)) ? KT : KF;
+                    r = (units_equal(a, b) == (in.cmp == SPK_CMP_EQ)) ? KT : KF;
                 } else {
                     r = cmpd((double)str_order(a, b), 0.0, in.cmp);
                 }
@@ -433,15 +308,21 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
                     double v;
                     if (a.n == b.n && units_equal(a, b)) {
                         v = a.n > 0 ? 1.0 : 0.0;  // identical strings: m = n, t = 0 -> exactly 1.0
-                    } else if (SLOW) {
+                    } else if (MODE == M_FILTER) {
+                        const double hi = jw_upper(a, b);
+                        if (hi < 0.0) {
+                            v = 0.0;  // no common unit: m = 0
+                        } else {
+                            r = decide(0.0, hi + 1e-12, in.cmp, in.t);  // margin >> rounding of either side
+                            break;
+                        }
+                    } else if (MODE == M_SLOW) {
                         if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) { atomicOr(A.err, 1); v = 0.0; }
                         else if (a.n <= 64 && b.n <= 64) v = jw_small(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n);
                         else v = jw_long(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n);
                     } else {
-                        if (a.n > MAXU || b.n > MAXU) { *defer = true; return KN; }
-                        if (mm.staged_a != in.a) { stage(slot_a, a); mm.staged_a = in.a; }
-                        if (mm.staged_b != in.b) { stage(slot_b, b); mm.staged_b = in.b; }
-                        v = jw_small(LdsAcc{slot_a}, a.n, LdsAcc{slot_b}, b.n);
+                        if (a.n > 64 || b.n > 64) { *slow = true; return KN; }
+                        v = jw_exact(a, b);
                     }
                     mm.jw = v;
                     mm.jw_key = key;
@@ -453,29 +334,30 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
             case SPK_OP_LEVRATIO: {
                 StrView a = get_str(A, A.ops[in.a], x, y), b = get_str(A, A.ops[in.b], x, y);
                 if (a.null || b.null) { r = KN; break; }
+                const double den = (double)(a.ncp + b.ncp) / 2.0;
+                if (in.op == SPK_OP_LEVRATIO && den == 0.0) { r = KN; break; }
                 const int key = in.a * 4096 + in.b;
                 if (mm.lev_key != key) {
                     int v;
                     if (a.n == b.n && units_equal(a, b)) {
                         v = 0;
-                    } else if (SLOW) {
+                    } else if (MODE == M_FILTER) {
+                        const int lo = lev_lower(a, b);
+                        const int hi = a.ncp > b.ncp ? a.ncp : b.ncp;
+                        if (in.op == SPK_OP_LEV) r = decide((double)lo, (double)hi, in.cmp, in.t);
+                        else r = decide((double)lo / den, (double)hi / den, in.cmp, in.t);
+                        break;
+                    } else if (MODE == M_SLOW) {
                         if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) { atomicOr(A.err, 1); v = 0; }
                         else v = lev_long(a, b);
                     } else {
-                        if (a.n > MAXU || b.n > MAXU || a.ncp != a.n || b.ncp != b.n) { *defer = true; return KN; }
-                        if (mm.staged_a != in.a) { stage(slot_a, a); mm.staged_a = in.a; }
-                        if (mm.staged_b != in.b) { stage(slot_b, b); mm.staged_b = in.b; }
-                        v = lev_myers(LdsAcc{slot_a}, a.n, LdsAcc{slot_b}, b.n);
+                        if (a.n > 64 || b.n > 64 || a.ncp != a.n || b.ncp != b.n) { *slow = true; return KN; }
+                        v = lev_exact(a, b);
                     }
                     mm.lev = v;
                     mm.lev_key = key;
                 }
-                if (in.op == SPK_OP_LEV) {
-                    r = cmpd((double)mm.lev, in.t, in.cmp);
-                } else {
-                    double den = (double)(a.ncp + b.ncp) / 2.0;
-                    r = den == 0.0 ? KN : cmpd((double)mm.lev / den, in.t, in.cmp);
-                }
+                r = in.op == SPK_OP_LEV ? cmpd((double)mm.lev, in.t, in.cmp) : cmpd((double)mm.lev / den, in.t, in.cmp);
                 break;
             }
             default: atomicOr(A.err, 2); r = KN; break;
@@ -485,58 +367,308 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
     return (int)(st & 3);
 }
 
-template <bool SLOW>
-__device__ bool eval_pair(const GammaArgs &A, int64_t p, uint16_t *slot_a, uint16_t *slot_b, uint32_t &code) {
-    const int32_t x = A.pl[p], y = A.pr[p];
-    uint32_t acc = 0;
-    bool defer = false;
-    for (int k = 0; k < A.K; ++k) {
-        const spk_column_program prog = A.progs[k];
-        Memo mm{-1, -1, 0.0, 0, -1, -1};
-        int level = prog.else_level;
-        for (int w = 0; w < prog.n_when; ++w) {
-            const int wi = prog.first_when + w;
-            int r = eval_pred<SLOW>(A, A.when_first[wi], A.when_n[wi], x, y, slot_a, slot_b, mm, &defer);
-            if (!SLOW && defer) return false;
-            if (r == KT) {
-                level = A.when_level[wi];
-                break;
+template <int MODE>
+__device__ int eval_column(const GammaArgs &A, int k, int32_t x, int32_t y, uint16_t *slot_a, uint16_t *slot_b,
+                           int &level) {
+    const spk_column_program prog = A.progs[k];
+    Memo mm{-1, -1, 0.0, 0, -1, -1};
+    for (int w = 0; w < prog.n_when; ++w) {
+        const int wi = prog.first_when + w;
+        bool slow = false;
+        const int r = eval_pred<MODE>(A, A.when_first[wi], A.when_n[wi], x, y, slot_a, slot_b, mm, &slow);
+        if (slow) return ST_NEEDS_SLOW;
+        if (r == KU) return ST_UNDECIDED;
+        if (r == KT) {
+            level = A.when_level[wi];
+            return ST_DONE;
+        }
+    }
+    level = prog.else_level;
+    return ST_DONE;
+}
+
+// Append `val` for every lane with `want`; one atomic per wave.  Call with the whole wave converged.
+__device__ inline void wave_append(int32_t *list, unsigned int *count, bool want, int32_t val) {
+    const unsigned long long mask = __ballot(want);
+    if (!mask) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll(mask) - 1;
+    unsigned int base = 0;
+    if (lane == leader) base = atomicAdd(count, (unsigned int)__popcll(mask));
+    base = __shfl(base, leader);
+    if (want) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = val;
+}
+
+// Work lists of the filter pass.  Each workgroup owns one contiguous region of pair ordinals and
+// appends the region's undecided pairs of column k to work[k][region start ...] under a counter
+// in LDS: no device-scope atomic on a shared counter (those serialise at ~12 ns each across the
+// whole chip), deterministic list order, and a region's rows stay in one XCD's L2.
+struct Region {
+    int64_t r0, r1;  // pair ordinals [r0, r1)
+};
+
+__device__ inline Region my_region(const GammaArgs &A) {
+    const int64_t r0 = (int64_t)blockIdx.x * A.region_len;
+    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
+    return Region{r0, r1};
+}
+
+__device__ inline int32_t *region_list(const GammaArgs &A, int k, const Region &r) {
+    return A.work + (int64_t)k * A.P + r.r0;
+}
+
+// ---- simple columns in the filter pass ----------------------------------------------------------
+// Upper bound of jaro_winkler_sim(a, b) for unequal rows from their records alone (jw_upper with
+// the prefix bounded by the four head units: exact below 4, else by the shorter length).
+__device__ inline double jw_upper_meta(const RecMeta &a, const RecMeta &b) {
+    const int lf = a.len16, ls = b.len16;
+    const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
+    if (lmn == 0) return -1.0;
+    const SketchSums ss = sketch_sums(a.sketch, b.sketch);
+    const int M = ss.saturated ? lmn : (ss.sum_min < lmn ? ss.sum_min : lmn);
+    if (M == 0) return -1.0;
+    const uint64_t d = a.head ^ b.head;
+    const int cp = d ? (__ffsll((unsigned long long)d) - 1) / 16 : 4;
+    const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
+    // M/lf + M/ls with one division; the caller's 1e-12 margin covers the few-ulp difference from
+    // the reference's operation order (a bound only has to be >= the true value)
+    const double j = ((double)M * (double)(lf + ls) / ((double)lf * (double)ls) + 1.0) * (1.0 / 3.0);
+    if (j < 0.7) return j;
+    const double pw = lmx > 10 ? (double)prefix / (double)lmx : 0.1 * (double)prefix;
+    return j + pw * (1.0 - j);
+}
+
+__device__ inline int lev_lower_meta(const RecMeta &a, const RecMeta &b) {
+    const int na = meta_cplen(a), nb = meta_cplen(b);
+    int lb = na > nb ? na - nb : nb - na;
+    if (na == a.len16 && nb == b.len16) {
+        const SketchSums ss = sketch_sums(a.sketch, b.sketch);
+        const int bag = (ss.sum_a > ss.sum_b ? ss.sum_a : ss.sum_b) - ss.sum_min;
+        if (bag > lb) lb = bag;
+    }
+    return lb;
+}
+
+// 1 equal, 0 unequal, -1 needs the units (hash match on rows without dictionary ids).
+__device__ inline int meta_equal(const RecMeta &a, const RecMeta &b) {
+    if (a.cpf & b.cpf & CPF_ID) return a.key == b.key ? 1 : 0;
+    const bool keyed = ((a.cpf | b.cpf) & CPF_ID) == 0;
+    if (a.len16 != b.len16 || a.head != b.head || (keyed && a.key != b.key)) return 0;
+    return a.len16 <= 4 ? 1 : -1;
+}
+
+__device__ int simple_str(const SimpleCol &sc, const RecMeta &a, const RecMeta &b, int &level) {
+    if (a.len16 < 0 || b.len16 < 0) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    const int eq = meta_equal(a, b);
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int op = sc.op[i], cmp = sc.cmp[i];
+        const double t = sc.t[i];
+        int r;
+        if (op == SPK_OP_STR_CMP) {
+            r = eq < 0 ? KU : (((eq == 1) == (cmp == SPK_CMP_EQ)) ? KT : KF);
+        } else if (op == SPK_OP_JW) {
+            if (eq == 1) {
+                r = cmpd(a.len16 > 0 ? 1.0 : 0.0, t, cmp);
+            } else if (eq == 0) {
+                const double hi = jw_upper_meta(a, b);
+                r = hi < 0.0 ? cmpd(0.0, t, cmp) : decide(0.0, hi + 1e-12, cmp, t);
+            } else {
+                r = KU;
+            }
+        } else {  // SPK_OP_LEV / SPK_OP_LEVRATIO
+            const int na = meta_cplen(a), nb = meta_cplen(b);
+            const double den = (double)(na + nb) / 2.0;
+            if (op == SPK_OP_LEVRATIO && den == 0.0) {
+                r = KN;
+            } else if (eq == 1) {
+                r = cmpd(0.0, t, cmp);  // 0 / den == 0
+            } else if (eq == 0) {
+                const double lo = (double)lev_lower_meta(a, b), hi = (double)(na > nb ? na : nb);
+                r = op == SPK_OP_LEV ? decide(lo, hi, cmp, t) : decide(lo / den, hi / den, cmp, t);
+            } else {
+                r = KU;
             }
         }
-        acc += (uint32_t)(level + 1) * (uint32_t)A.stride[k];
-    }
-    code = acc;
-    return true;
-}
-
-__device__ inline void store_code(const GammaArgs &A, int64_t p, uint32_t code) {
-    if (A.code_bytes == 2) reinterpret_cast<uint16_t *>(A.codes)[p] = (uint16_t)code;
-    else reinterpret_cast<uint32_t *>(A.codes)[p] = code;
-}
-
-__global__ __launch_bounds__(G_THREADS) void k_gamma_fast(GammaArgs A) {
-    __shared__ uint16_t lds[2][MAXU][G_THREADS];
-    uint16_t *slot_a = &lds[0][0][threadIdx.x];
-    uint16_t *slot_b = &lds[1][0][threadIdx.x];
-    const int64_t stride = (int64_t)gridDim.x * G_THREADS;
-    for (int64_t p = (int64_t)blockIdx.x * G_THREADS + threadIdx.x; p < A.P; p += stride) {
-        uint32_t code;
-        if (eval_pair<false>(A, p, slot_a, slot_b, code)) {
-            store_code(A, p, code);
-        } else {
-            unsigned int i = atomicAdd(A.defer_count, 1u);
-            A.defer_list[i] = (int32_t)p;
+        if (r == KU) return ST_UNDECIDED;
+        if (r == KT) {
+            level = sc.level[i];
+            return ST_DONE;
         }
     }
+    level = sc.else_level;
+    return ST_DONE;
 }
 
-__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A) {
+__device__ int simple_num(const SimpleCol &sc, bool va, double a, bool vb, double b) {
+    if (!va || !vb) return sc.null_level;
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int op = sc.op[i], cmp = sc.cmp[i];
+        int r;
+        if (op == SPK_OP_NUM_CMP) {
+            r = cmpd(a, b, cmp);
+        } else if (op == SPK_OP_ABSDIFF) {
+            r = cmpd(fabs(a - b), sc.t[i], cmp);
+        } else {  // SPK_OP_PERCDIFF
+            const double d = fabs(a > b ? a : b);
+            r = d == 0.0 ? KN : cmpd(fabs(a - b) / d, sc.t[i], cmp);
+        }
+        if (r == KT) return sc.level[i];
+    }
+    return sc.else_level;
+}
+
+// Filter pass, simple columns: initialises code32[p] with their levels.  The column descriptors
+// and the table pointers are staged in LDS once per workgroup: read from global memory inside the
+// divergent per-pair code they would be per-lane vector loads on the critical path of every pair.
+struct SimpleSrc {
+    const RecMeta *m0, *m1;
+    const double *v0, *v1;
+    const uint8_t *ok0, *ok1;
+};
+
+__global__ __launch_bounds__(F_THREADS) void k_gamma_simple(GammaArgs A) {
+    __shared__ SimpleCol s_sc[MAX_SIMPLE];
+    __shared__ SimpleSrc s_src[MAX_SIMPLE];
+    __shared__ unsigned int s_cnt[MAX_SIMPLE];
+    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) {
+        const SimpleCol sc = A.simple[i];
+        const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
+        s_sc[i] = sc;
+        s_src[i] = SimpleSrc{c0.meta, c1.meta, c0.val, c1.val, c0.valid, c1.valid};
+        s_cnt[i] = 0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const Region R = my_region(A);
+    for (int64_t base = R.r0 + (threadIdx.x & ~63); base < R.r1; base += F_THREADS) {  // wave-uniform
+        const int64_t p = base + lane;
+        const bool active = p < R.r1;
+        const int32_t x = active ? A.pl[p] : 0;  // inactive lanes read row 0 harmlessly
+        const int32_t y = active ? A.pr[p] : 0;
+        uint32_t acc = 0;
+        for (int g = 0; g < A.n_simple; g += SIMPLE_GROUP) {
+            // issue every record load of the group before the first use
+            RecMeta ma[SIMPLE_GROUP], mb[SIMPLE_GROUP];
+            double va[SIMPLE_GROUP], vb[SIMPLE_GROUP];
+            bool oka[SIMPLE_GROUP], okb[SIMPLE_GROUP];
+#pragma unroll
+            for (int j = 0; j < SIMPLE_GROUP; ++j) {
+                if (g + j < A.n_simple) {
+                    const SimpleSrc &src = s_src[g + j];
+                    if (s_sc[g + j].kind == SK_STR) {
+                        ma[j] = src.m0[x];
+                        mb[j] = src.m1[y];
+                    } else {
+                        oka[j] = src.ok0[x] != 0;
+                        okb[j] = src.ok1[y] != 0;
+                        va[j] = src.v0[x];
+                        vb[j] = src.v1[y];
+                    }
+                }
+            }
+            // one copy of the evaluation code: slot 0 is evaluated, then the slots rotate down
+            const int n_here = A.n_simple - g < SIMPLE_GROUP ? A.n_simple - g : SIMPLE_GROUP;
+            for (int j = 0; j < n_here; ++j) {
+                const SimpleCol &sc = s_sc[g + j];
+                bool undecided = false;
+                if (active) {
+                    int level;
+                    if (sc.kind == SK_STR) {
+                        if (simple_str(sc, ma[0], mb[0], level) != ST_DONE) undecided = true;
+                    } else {
+                        level = simple_num(sc, oka[0], va[0], okb[0], vb[0]);
+                    }
+                    if (!undecided) acc += (uint32_t)(level + 1) * (uint32_t)sc.stride;
+                }
+                wave_append(region_list(A, sc.k, R), &s_cnt[g + j], undecided, (int32_t)p);
+#pragma unroll
+                for (int q = 0; q + 1 < SIMPLE_GROUP; ++q) {
+                    ma[q] = ma[q + 1];
+                    mb[q] = mb[q + 1];
+                    va[q] = va[q + 1];
+                    vb[q] = vb[q + 1];
+                    oka[q] = oka[q + 1];
+                    okb[q] = okb[q + 1];
+                }
+            }
+        }
+        if (active) A.code32[p] = acc;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
+        A.region_count[(int64_t)s_sc[i].k * A.n_regions + blockIdx.x] = s_cnt[i];
+}
+
+// Filter pass, every other column through the interpreter: adds to code32[p].
+__global__ __launch_bounds__(F_THREADS) void k_gamma_filter(GammaArgs A) {
+    __shared__ unsigned int s_cnt[MAX_SIMPLE];
+    for (int i = threadIdx.x; i < A.n_complex; i += F_THREADS) s_cnt[i] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const Region R = my_region(A);
+    for (int64_t base = R.r0 + (threadIdx.x & ~63); base < R.r1; base += F_THREADS) {  // wave-uniform
+        const int64_t p = base + lane;
+        const bool active = p < R.r1;
+        int32_t x = 0, y = 0;
+        if (active) {
+            x = A.pl[p];
+            y = A.pr[p];
+        }
+        uint32_t acc = 0;
+        for (int i = 0; i < A.n_complex; ++i) {
+            const int k = A.complex_k[i];
+            bool undecided = false;
+            if (active) {
+                int level = 0;
+                const int st = eval_column<M_FILTER>(A, k, x, y, nullptr, nullptr, level);
+                if (st == ST_DONE) acc += (uint32_t)(level + 1) * (uint32_t)A.stride[k];
+                else undecided = true;
+            }
+            wave_append(region_list(A, k, R), &s_cnt[i], undecided, (int32_t)p);
+        }
+        if (active) A.code32[p] += acc;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < A.n_complex; i += F_THREADS)
+        A.region_count[(int64_t)A.complex_k[i] * A.n_regions + blockIdx.x] = s_cnt[i];
+}
+
+// Exact pass over column k: workgroup b takes region b's list.
+__global__ __launch_bounds__(X_THREADS) void k_gamma_exact(GammaArgs A, int k) {
+    uint16_t *slot_a = nullptr, *slot_b = nullptr;  // the exact pass works from registers and L1/L2
+    const Region R = my_region(A);
+    const int32_t *items = region_list(A, k, R);
+    const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
+    for (int64_t base = 0; base < n; base += X_THREADS) {  // block-uniform trip count
+        const int64_t i = base + threadIdx.x;
+        bool to_slow = false;
+        int32_t p = 0;
+        if (i < n) {
+            p = items[i];
+            int level = 0;
+            const int st = eval_column<M_EXACT>(A, k, A.pl[p], A.pr[p], slot_a, slot_b, level);
+            if (st == ST_DONE) atomicAdd(&A.code32[p], (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+            else to_slow = true;
+        }
+        wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k, const int32_t *items, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (i >= A.n_work) return;
-    const int64_t p = A.work[i];
-    uint32_t code = 0;
-    eval_pair<true>(A, p, nullptr, nullptr, code);
-    store_code(A, p, code);
+    if (i >= n) return;
+    const int32_t p = items[i];
+    int level = 0;
+    eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level);
+    atomicAdd(&A.code32[p], (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+}
+
+__global__ void k_pack16(int64_t n, const uint32_t *__restrict__ in, uint16_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint16_t)in[i];
 }
 
 __global__ void k_codes_from_gammas(int64_t n, int K, const int8_t *__restrict__ g, const int64_t *__restrict__ stride,
@@ -608,6 +740,51 @@ static std::vector<uint16_t> utf8_to_utf16(const uint8_t *b, int64_t n, int32_t 
     return out;
 }
 
+// Recognise a simple column (see SimpleCol); false leaves it to the interpreter.
+static bool classify_simple(int k, const spk_column_program &prog, const int32_t *wf, const int32_t *wn,
+                            const int32_t *wl, const spk_instr *instr, const spk_operand *ops, const Table &t0,
+                            const Table &t1, const std::vector<int64_t> &stride, SimpleCol *out) {
+    if (prog.n_when < 1 || prog.n_when - 1 > MAX_TESTS) return false;
+    const int w0 = prog.first_when;
+    if (wn[w0] != 3) return false;
+    const spk_instr *n = instr + wf[w0];
+    if (n[0].op != SPK_OP_ISNULL || n[1].op != SPK_OP_ISNULL || n[2].op != SPK_OP_OR) return false;
+    auto plain = [&](int i, int side) {
+        const spk_operand &o = ops[i];
+        return o.kind == 0 && o.side == side && o.lit < 0 && !o.has_num_default && o.substr_start == 0;
+    };
+    int a = n[0].a, b = n[1].a;
+    if (plain(b, 0) && plain(a, 1)) std::swap(a, b);
+    if (!plain(a, 0) || !plain(b, 1) || ops[a].col != ops[b].col) return false;
+    const int col = ops[a].col;
+    const ColKind ka = t0.cols[col]->kind, kb = t1.cols[col]->kind;
+    if (ka != kb || (ka != COL_STR && ka != COL_NUM)) return false;
+    SimpleCol s{};
+    s.k = k;
+    s.kind = ka == COL_STR ? SK_STR : SK_NUM;
+    s.col = col;
+    s.null_level = wl[w0];
+    s.else_level = prog.else_level;
+    s.n_tests = prog.n_when - 1;
+    s.stride = stride[k];
+    for (int i = 0; i < s.n_tests; ++i) {
+        const int w = w0 + 1 + i;
+        if (wn[w] != 1) return false;
+        const spk_instr &in = instr[wf[w]];
+        if (in.a != a || in.b != b) return false;
+        const bool str_op = (in.op == SPK_OP_STR_CMP && (in.cmp == SPK_CMP_EQ || in.cmp == SPK_CMP_NE)) ||
+                            in.op == SPK_OP_JW || in.op == SPK_OP_LEV || in.op == SPK_OP_LEVRATIO;
+        const bool num_op = in.op == SPK_OP_NUM_CMP || in.op == SPK_OP_ABSDIFF || in.op == SPK_OP_PERCDIFF;
+        if (!(s.kind == SK_STR ? str_op : num_op)) return false;
+        s.op[i] = in.op;
+        s.cmp[i] = in.cmp;
+        s.level[i] = wl[w];
+        s.t[i] = in.t;
+    }
+    *out = s;
+    return true;
+}
+
 extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *cols, int n_when,
                           const int32_t *when_first_instr, const int32_t *when_n_instr, const int32_t *when_level,
                           int n_instr, const spk_instr *instr, int n_operands, const spk_operand *operands, int n_lits,
@@ -646,12 +823,13 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     }
     for (int i = 0; i < n_instr; ++i) {
         const spk_instr &in = instr[i];
-        bool binop = in.op == SPK_OP_AND || in.op == SPK_OP_OR || in.op == SPK_OP_NOT || in.op == SPK_OP_CONST;
-        if (!binop) {
+        bool logical = in.op == SPK_OP_AND || in.op == SPK_OP_OR || in.op == SPK_OP_NOT || in.op == SPK_OP_CONST;
+        if (!logical) {
             SPK_REQUIRE(in.a >= 0 && in.a < n_operands, SPK_E_INVALID, "spk_gammas: operand index");
             bool two = !(in.op == SPK_OP_ISNULL || in.op == SPK_OP_NOTNULL || in.op == SPK_OP_LEN);
             if (two) SPK_REQUIRE(in.b >= 0 && in.b < n_operands, SPK_E_INVALID, "spk_gammas: operand index");
         }
+        if (in.op == SPK_OP_CONST) SPK_REQUIRE(in.i0 >= 0 && in.i0 <= 2, SPK_E_INVALID, "spk_gammas: constant");
     }
     SPK_TRY(set_pattern_space(ctx, n_cols, nlev.data()));
 
@@ -667,7 +845,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         lcp.push_back(ncp);
         lu.insert(lu.end(), u.begin(), u.end());
     }
-    lu.push_back(0);
+    lu.resize(lu.size() + 8, 0);  // 4-unit vector reads past a literal's end stay in the buffer
     loff.push_back((int64_t)lu.size());
     llen.push_back(0);
     lcp.push_back(0);
@@ -675,20 +853,20 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_TRY(ensure_desc(ctx, t0));
     SPK_TRY(ensure_desc(ctx, t1));
     DevBuf<spk_column_program> d_prog;
-    DevBuf<int32_t> d_wf, d_wn, d_wl, d_defer;
+    DevBuf<int32_t> d_wf, d_wn, d_wl;
     DevBuf<spk_instr> d_instr;
     DevBuf<spk_operand> d_ops;
     DevBuf<uint16_t> d_lu;
-    DevBuf<int64_t> d_loff, d_stride;
+    DevBuf<int64_t> d_loff, d_stride, d_slow_off;
     DevBuf<int32_t> d_llen, d_lcp;
-    DevBuf<unsigned int> d_cnt;
     DevBuf<int> d_err;
     auto up = [&](auto &buf, const auto *src, size_t n) -> int {
         SPK_TRY(buf.alloc(n ? n : 1));
         if (n) SPK_HIP(hipMemcpyAsync(buf.p, src, n * sizeof(*src), hipMemcpyHostToDevice, ctx->stream));
         return SPK_OK;
     };
-    SPK_TRY(up(d_prog, cols, (size_t)n_cols));
+    const int K = n_cols;
+    SPK_TRY(up(d_prog, cols, (size_t)K));
     SPK_TRY(up(d_wf, when_first_instr, (size_t)n_when));
     SPK_TRY(up(d_wn, when_n_instr, (size_t)n_when));
     SPK_TRY(up(d_wl, when_level, (size_t)n_when));
@@ -699,13 +877,34 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_TRY(up(d_llen, llen.data(), llen.size()));
     SPK_TRY(up(d_lcp, lcp.data(), lcp.size()));
     SPK_TRY(up(d_stride, ctx->stride.data(), ctx->stride.size()));
-    SPK_TRY(d_cnt.alloc(1));
+    std::vector<SimpleCol> simple;
+    std::vector<int32_t> complex_k;
+    for (int k = 0; k < K; ++k) {
+        SimpleCol s;
+        if (ctx->simple_columns &&
+            classify_simple(k, cols[k], when_first_instr, when_n_instr, when_level, instr, operands, t0, t1,
+                            ctx->stride, &s))
+            simple.push_back(s);
+        else
+            complex_k.push_back(k);
+    }
+    DevBuf<SimpleCol> d_simple;
+    DevBuf<int32_t> d_complex;
+    SPK_TRY(up(d_simple, simple.data(), simple.size()));
+    SPK_TRY(up(d_complex, complex_k.data(), complex_k.size()));
     SPK_TRY(d_err.alloc(1));
-    SPK_HIP(hipMemsetAsync(d_cnt.p, 0, sizeof(unsigned int), ctx->stream));
-    SPK_HIP(hipMemsetAsync(d_err.p, 0, sizeof(int), ctx->stream));
     const int64_t P = ctx->n_pairs;
+    SPK_TRY(ctx->code32.alloc((size_t)P + 1));
+    SPK_TRY(ctx->work.alloc((size_t)K * (size_t)P + 1));
+    SPK_TRY(ctx->work_count.alloc((size_t)K));
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
-    SPK_TRY(d_defer.alloc((size_t)P + 1));
+    // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
+    const int n_regions = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (P + F_THREADS - 1) / F_THREADS));
+    const int64_t region_len = ((P + n_regions - 1) / n_regions + 63) / 64 * 64;
+    SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions));
+    SPK_HIP(hipMemsetAsync(ctx->region_count.p, 0, sizeof(unsigned int) * K * n_regions, ctx->stream));
+    SPK_HIP(hipMemsetAsync(ctx->work_count.p, 0, sizeof(unsigned int) * K, ctx->stream));
+    SPK_HIP(hipMemsetAsync(d_err.p, 0, sizeof(int), ctx->stream));
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -713,7 +912,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.pl = ctx->pl.p;
     A.pr = ctx->pr.p;
     A.P = P;
-    A.K = n_cols;
+    A.K = K;
     A.progs = d_prog.p;
     A.when_first = d_wf.p;
     A.when_n = d_wn.p;
@@ -725,26 +924,65 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.lit_len = d_llen.p;
     A.lit_cplen = d_lcp.p;
     A.stride = d_stride.p;
-    A.codes = ctx->codes.p;
-    A.code_bytes = ctx->code_bytes;
-    A.defer_list = d_defer.p;
-    A.defer_count = d_cnt.p;
+    A.code32 = ctx->code32.p;
+    A.work = ctx->work.p;
+    A.region_count = ctx->region_count.p;
+    A.region_len = region_len;
+    A.n_regions = n_regions;
+    A.slow_count = ctx->work_count.p;
     A.err = d_err.p;
+    A.simple = d_simple.p;
+    A.n_simple = (int)simple.size();
+    A.complex_k = d_complex.p;
+    A.n_complex = (int)complex_k.size();
+    ctx->last_simple = (int)simple.size();
 
     SPK_TRY(ctx->begin(K_GAMMA));
     if (P > 0) {
-        int64_t blocks = (P + G_THREADS - 1) / G_THREADS;
-        if (blocks > 256 * 16) blocks = 256 * 16;
-        k_gamma_fast<<<(unsigned)blocks, G_THREADS, 0, ctx->stream>>>(A);
+        k_gamma_simple<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
+        SPK_HIP(hipGetLastError());
+        if (A.n_complex) {
+            k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
+            SPK_HIP(hipGetLastError());
+        }
+    }
+    std::vector<unsigned int> rc((size_t)K * n_regions, 0);
+    SPK_HIP(hipMemcpyAsync(rc.data(), ctx->region_count.p, sizeof(unsigned int) * rc.size(), hipMemcpyDeviceToHost,
+                           ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<int64_t> counts((size_t)2 * K, 0);
+    for (int k = 0; k < K; ++k)
+        for (int b = 0; b < n_regions; ++b) counts[k] += rc[(size_t)k * n_regions + b];
+    std::vector<int64_t> slow_off(K + 1, 0);
+    for (int k = 0; k < K; ++k) slow_off[k + 1] = slow_off[k] + counts[k];
+    SPK_TRY(ctx->slow.alloc((size_t)slow_off[K] + 1));
+    SPK_TRY(up(d_slow_off, slow_off.data(), slow_off.size()));
+    A.slow = ctx->slow.p;
+    A.slow_off = d_slow_off.p;
+    for (int k = 0; k < K; ++k) {
+        if (!counts[k]) continue;
+        k_gamma_exact<<<(unsigned)n_regions, X_THREADS, 0, ctx->stream>>>(A, k);
         SPK_HIP(hipGetLastError());
     }
-    unsigned int n_def = 0;
-    SPK_HIP(hipMemcpyAsync(&n_def, d_cnt.p, sizeof(n_def), hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<unsigned int> slow_counts((size_t)K, 0);
+    SPK_HIP(hipMemcpyAsync(slow_counts.data(), ctx->work_count.p, sizeof(unsigned int) * K, hipMemcpyDeviceToHost,
+                           ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
-    if (n_def) {
-        A.work = d_defer.p;
-        A.n_work = n_def;
-        k_gamma_slow<<<(unsigned)((n_def + 63) / 64), 64, 0, ctx->stream>>>(A);
+    for (int k = 0; k < K; ++k) counts[K + k] = slow_counts[k];
+    int64_t n_slow = 0;
+    for (int k = 0; k < K; ++k) {
+        const unsigned int ns = counts[K + k];
+        n_slow += ns;
+        if (!ns) continue;
+        k_gamma_slow<<<(unsigned)((ns + 63) / 64), 64, 0, ctx->stream>>>(A, k, ctx->slow.p + slow_off[k], ns);
+        SPK_HIP(hipGetLastError());
+    }
+    if (P > 0) {
+        if (ctx->code_bytes == 2)
+            k_pack16<<<(unsigned)((P + 255) / 256), 256, 0, ctx->stream>>>(P, ctx->code32.p,
+                                                                         reinterpret_cast<uint16_t *>(ctx->codes.p));
+        else
+            SPK_HIP(hipMemcpyAsync(ctx->codes.p, ctx->code32.p, (size_t)P * 4, hipMemcpyDeviceToDevice, ctx->stream));
         SPK_HIP(hipGetLastError());
     }
     SPK_TRY(ctx->end(K_GAMMA));
@@ -755,7 +993,8 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_REQUIRE(!(err & 2), SPK_E_INVALID, "spk_gammas: unknown instruction");
     ctx->codes_valid = true;
     ctx->mpat_valid = false;
-    ctx->last_deferred = (int64_t)n_def;
+    ctx->last_deferred = n_slow;
+    ctx->last_exact.assign(counts.begin(), counts.begin() + K);
     return SPK_OK;
 }
 
@@ -808,7 +1047,7 @@ extern "C" int spk_gammas_copy(spk_ctx *ctx, int64_t start, int64_t count, int8_
 }
 
 // ---- the jar's UDFs as bulk device functions (JaroWinklerSimilarity.call, Spark levenshtein) -----
-// Same device code as the comparison kernel: LDS-staged jw_small / lev_myers for short strings,
+// Same device code as the comparison passes: LDS-staged jw_small / lev_myers for short strings,
 // the global-memory jw_long / lev_long for the rest.
 struct UdfArgs {
     int64_t n;
@@ -820,14 +1059,15 @@ struct UdfArgs {
     int *err;
 };
 
-__global__ __launch_bounds__(G_THREADS) void k_udf(UdfArgs U) {
-    __shared__ uint16_t lds[2][MAXU][G_THREADS];
+__global__ __launch_bounds__(U_THREADS) void k_udf(UdfArgs U) {
+    __shared__ uint16_t lds[2][MAXU][U_THREADS];
     uint16_t *slot_a = &lds[0][0][threadIdx.x];
     uint16_t *slot_b = &lds[1][0][threadIdx.x];
-    int64_t p = (int64_t)blockIdx.x * G_THREADS + threadIdx.x;
+    int64_t p = (int64_t)blockIdx.x * U_THREADS + threadIdx.x;
     if (p >= U.n) return;
-    StrView a{U.u16 + U.off[2 * p], (int32_t)(U.off[2 * p + 1] - U.off[2 * p]), U.cp[2 * p], 0, 0, 0};
-    StrView b{U.u16 + U.off[2 * p + 1], (int32_t)(U.off[2 * p + 2] - U.off[2 * p + 1]), U.cp[2 * p + 1], 0, 0, 0};
+    const StrView a = plain_view(U.u16 + U.off[2 * p], (int32_t)(U.off[2 * p + 1] - U.off[2 * p]), U.cp[2 * p]);
+    const StrView b =
+        plain_view(U.u16 + U.off[2 * p + 1], (int32_t)(U.off[2 * p + 2] - U.off[2 * p + 1]), U.cp[2 * p + 1]);
     if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) {
         atomicOr(U.err, 1);
         U.out[p] = NAN;
@@ -836,11 +1076,9 @@ __global__ __launch_bounds__(G_THREADS) void k_udf(UdfArgs U) {
     if (U.op == 0) {
         double v;
         if (a.n <= MAXU && b.n <= MAXU) {
-            stage(slot_a, a);
-            stage(slot_b, b);
-            v = jw_small(LdsAcc{slot_a}, a.n, LdsAcc{slot_b}, b.n);
-        } else if (a.n <= 64 && b.n <= 64) {
-            v = jw_small(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n);
+            stage<U_THREADS>(slot_a, a);
+            stage<U_THREADS>(slot_b, b);
+            v = jw_small(LdsAcc<U_THREADS>{slot_a}, a.n, LdsAcc<U_THREADS>{slot_b}, b.n);
         } else {
             v = jw_long(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n);
         }
@@ -848,9 +1086,9 @@ __global__ __launch_bounds__(G_THREADS) void k_udf(UdfArgs U) {
     } else {
         int v;
         if (a.n <= MAXU && b.n <= MAXU && a.ncp == a.n && b.ncp == b.n) {
-            stage(slot_a, a);
-            stage(slot_b, b);
-            v = lev_myers(LdsAcc{slot_a}, a.n, LdsAcc{slot_b}, b.n);
+            stage<U_THREADS>(slot_a, a);
+            stage<U_THREADS>(slot_b, b);
+            v = lev_myers(LdsAcc<U_THREADS>{slot_a}, a.n, LdsAcc<U_THREADS>{slot_b}, b.n);
         } else {
             v = lev_long(a, b);
         }
@@ -893,7 +1131,7 @@ static int run_udf(spk_ctx *ctx, int op, int64_t n, const int64_t *l_off, const 
     SPK_HIP(hipMemsetAsync(d_err.p, 0, sizeof(int), ctx->stream));
     if (n) {
         UdfArgs U{n, d_u.p, d_off.p, d_cp.p, op, d_out.p, d_err.p};
-        k_udf<<<(unsigned)((n + G_THREADS - 1) / G_THREADS), G_THREADS, 0, ctx->stream>>>(U);
+        k_udf<<<(unsigned)((n + U_THREADS - 1) / U_THREADS), U_THREADS, 0, ctx->stream>>>(U);
         SPK_HIP(hipGetLastError());
         SPK_HIP(hipMemcpyAsync(out, d_out.p, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
@@ -923,5 +1161,23 @@ extern "C" int spk_n_patterns(spk_ctx *ctx, int64_t *out) {
 extern "C" int spk_gammas_deferred(spk_ctx *ctx, int64_t *out) {
     SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
     *out = ctx->last_deferred;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n) {
+    SPK_REQUIRE(ctx && out && n >= (int)ctx->last_exact.size(), SPK_E_INVALID, "spk_gammas_exact_counts: bad args");
+    for (size_t k = 0; k < ctx->last_exact.size(); ++k) out[k] = ctx->last_exact[k];
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->simple_columns = on != 0;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_simple_count(spk_ctx *ctx, int *out) {
+    SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
+    *out = ctx->last_simple;
     return SPK_OK;
 }

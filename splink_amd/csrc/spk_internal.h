@@ -38,19 +38,44 @@ void set_error(const std::string &msg);
     } while (0)
 
 // ---- device column layout ---------------------------------------------------------------
-// String columns keep the UTF-16 code units of every row at the row's UTF-8 byte offset
-// (UTF-16 never needs more units than UTF-8 has bytes), so no scan is needed on upload.
+// String columns keep the UTF-16 code units of row i at a 4-unit (8-byte) aligned start derived
+// from its UTF-8 byte offset, (off8[i] + 3i + 3) & ~3: UTF-16 never needs more units than UTF-8
+// has bytes, so the starts are monotone, rows never overlap and no scan is needed on upload.
+// Each row also has a 32-byte metadata record (two 16-byte loads) that holds everything the
+// comparison filter needs -- NULL flag, lengths, equality key, sketch and the first four units --
+// so most (pair, column) cells are decided without touching the units at all.
 enum ColKind : int32_t { COL_NONE = 0, COL_STR = 1, COL_NUM = 2 };
+
+struct alignas(16) RecMeta {
+    uint32_t key;     // dictionary id of the value (CPF_ID: equal iff the strings are) or a 32-bit
+                      // FNV-1a fold of the units (unequal keys prove unequal strings)
+    int32_t len16;    // UTF-16 length, -1 = NULL
+    uint64_t sketch;  // nibbles 0..14: saturating per-bucket unit counts; nibble 15: saturation flag
+    uint64_t head;    // units 0..3, zero beyond len16
+    uint32_t off4;    // first UTF-16 unit of the row / 4 (rows start 8-byte aligned)
+    uint32_t cpf;     // bits 0..23: code-point length; bit 24: bit-planes valid (<= 64 units, all < 256);
+                      // bit 25: `key` is an exact dictionary id
+};
+static_assert(sizeof(RecMeta) == 32, "RecMeta layout");
+constexpr uint32_t CPF_PLANES = 1u << 24;
+constexpr uint32_t CPF_ID = 1u << 25;
+__host__ __device__ inline int32_t meta_cplen(const RecMeta &m) { return (int32_t)(m.cpf & 0xFFFFFFu); }
+__host__ __device__ inline int64_t meta_off(const RecMeta &m) { return (int64_t)m.off4 * 4; }
+
+// Bit-planes of a row whose units are all < 256 and that has <= 64 units: plane b (0..7) holds
+// bit b of unit i at bit i.  The Levenshtein / Jaro-Winkler match masks of a character c are then
+// AND_b (bit b of c ? plane_b : ~plane_b), eight register ops instead of a scan of the string.
+constexpr int N_PLANES = 8;
+
+__host__ __device__ inline uint32_t sketch_bucket(uint32_t u) { return ((u * 2654435761u) >> 16) % 15u; }
 
 struct ColDesc {
     int32_t kind;
     int32_t pad;
-    const uint16_t *units;  // COL_STR
-    const int64_t *off;     // row start (in units)
-    const int32_t *len16;   // UTF-16 length, -1 = NULL
-    const int32_t *cplen;   // code-point length
-    const uint64_t *hash;   // FNV-1a over the units (inequality fast path)
-    const double *val;      // COL_NUM
+    const uint16_t *units;   // COL_STR
+    const RecMeta *meta;     // COL_STR
+    const uint64_t *planes;  // COL_STR, [n][N_PLANES]
+    const double *val;       // COL_NUM
     const uint8_t *valid;   // COL_NUM
 };
 
@@ -85,9 +110,8 @@ struct DevBuf {
 struct Column {
     ColKind kind = COL_NONE;
     DevBuf<uint16_t> units;
-    DevBuf<int64_t> off;
-    DevBuf<int32_t> len16, cplen;
-    DevBuf<uint64_t> hash;
+    DevBuf<RecMeta> meta;
+    DevBuf<uint64_t> planes;
     DevBuf<double> val;
     DevBuf<uint8_t> valid;
 };
@@ -127,6 +151,15 @@ struct spk_ctx {
     int64_t n_patterns = 0;
     bool codes_valid = false;
     int64_t last_deferred = 0;
+    std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
+    bool simple_columns = true;       // template-shaped columns take the record-only filter
+    int last_simple = 0;
+
+    // comparison-vector work buffers (reused across calls)
+    spk::DevBuf<uint32_t> code32;
+    spk::DevBuf<int32_t> work, slow;
+    spk::DevBuf<unsigned int> work_count;    // [K] slow-pass list lengths
+    spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
     // EM state
     spk::DevBuf<uint64_t> hist;

@@ -1,0 +1,452 @@
+// Device string similarity: the jar's Jaro-Winkler (commons-text 1.4 JaroWinklerDistance,
+// SURVEY.md §2.3) and Spark's Levenshtein, exact, plus the cheap bounds the comparison filter
+// pass uses to decide most (pair, column) cells without running them.
+//
+// Exactness: jw_finish evaluates the reference's expression in its exact operation order; the
+// library is compiled with -ffp-contract=off so no FMA contraction changes the rounding.
+#pragma once
+
+#include <cmath>
+
+#include "spk_internal.h"
+
+namespace spk {
+
+constexpr int MAXU = 64;          // LDS staging capacity per string (UTF-16 units), exact pass
+constexpr int SLOW_LIMIT = 1024;  // global-memory pass capacity per string
+
+struct StrView {
+    const uint16_t *p = nullptr;
+    int32_t n = 0;     // UTF-16 units
+    int32_t ncp = 0;   // code points
+    int32_t null = 1;
+    int32_t has_meta = 0;   // key / sketch valid
+    int32_t exact_key = 0;  // column + 1 when `key` is that column's dictionary id, else 0
+    uint32_t key = 0;
+    uint64_t sketch = 0;
+    const uint64_t *planes = nullptr;  // N_PLANES bit-planes of the whole row, or null
+};
+
+__device__ inline StrView plain_view(const uint16_t *p, int32_t n, int32_t ncp) {
+    StrView s;
+    s.p = p;
+    s.n = n;
+    s.ncp = ncp;
+    s.null = 0;
+    return s;
+}
+
+// ---- accessors ---------------------------------------------------------------------------
+template <int STRIDE>
+struct LdsAcc {
+    const uint16_t *b;
+    __device__ uint16_t operator[](int i) const { return b[i * STRIDE]; }
+};
+struct GlbAcc {
+    const uint16_t *p;
+    __device__ uint16_t operator[](int i) const { return p[i]; }
+};
+
+template <int STRIDE>
+__device__ inline void stage(uint16_t *slot, const StrView &s) {
+    for (int i = 0; i < s.n; ++i) slot[i * STRIDE] = s.p[i];
+}
+
+__device__ inline bool aligned8(const uint16_t *p) { return ((uintptr_t)p & 7u) == 0; }
+
+// Units [0, lim) compared four at a time when both rows start 8-byte aligned (column rows do;
+// substr / literal views may not).  Reads stay inside the row's padded slot.
+__device__ inline int common_prefix(const uint16_t *a, const uint16_t *b, int lim) {
+    if (aligned8(a) && aligned8(b)) {
+        for (int i = 0; i < lim; i += 4) {
+            const uint64_t d = *reinterpret_cast<const uint64_t *>(a + i) ^ *reinterpret_cast<const uint64_t *>(b + i);
+            if (d) {
+                const int k = i + (__ffsll((unsigned long long)d) - 1) / 16;
+                return k < lim ? k : lim;
+            }
+        }
+        return lim;
+    }
+    int i = 0;
+    while (i < lim && a[i] == b[i]) ++i;
+    return i;
+}
+
+// Exact string equality: dictionary ids when both rows carry them, else hash then units.
+__device__ inline bool units_equal(const StrView &a, const StrView &b) {
+    if (a.n != b.n) return false;
+    if (a.has_meta && b.has_meta) {
+        // ids are equal iff the strings are, within one column's id space only
+        if (a.exact_key && a.exact_key == b.exact_key) return a.key == b.key;
+        if (!a.exact_key && !b.exact_key && a.key != b.key) return false;
+    }
+    return common_prefix(a.p, b.p, a.n) == a.n;
+}
+
+// Sequential reader of UTF-16 units: one aligned 8-byte load per four units.  A word is loaded
+// only when one of its units is consumed, so the reader never touches memory past the aligned
+// word holding the last unit read (safe for unpadded literal buffers too).
+struct UnitReader {
+    const uint64_t *q;
+    uint64_t w;
+    int pos;
+    bool live;
+    __device__ explicit UnitReader(const uint16_t *p) {
+        const uintptr_t a = (uintptr_t)p;
+        q = reinterpret_cast<const uint64_t *>(a & ~(uintptr_t)7);
+        pos = (int)((a & 7u) >> 1);
+        w = 0;
+        live = false;
+    }
+    __device__ uint32_t next() {
+        if (!live) {
+            w = *q;
+            live = true;
+        }
+        const uint32_t c = (uint32_t)(w >> (16 * pos)) & 0xFFFFu;
+        if (++pos == 4) {
+            pos = 0;
+            ++q;
+            live = false;
+        }
+        return c;
+    }
+};
+
+// ---- Jaro-Winkler (exact) ----------------------------------------------------------------------
+// apply(): m = matches, t = transpositions / 2 (integer), prefix not capped, max length lmx.
+__device__ inline double jw_finish(int m, int t, int prefix, int lf, int ls, int lmx) {
+    if (m == 0) return 0.0;
+    double md = (double)m;
+    double j = ((md / (double)lf + md / (double)ls) + (md - (double)(t / 2)) / md) / 3.0;
+    if (j < 0.7) return j;
+    double w = 1.0 / (double)lmx;
+    if (w > 0.1) w = 0.1;
+    return j + (w * (double)prefix) * (1.0 - j);
+}
+
+// matches(): greedy first free match inside the window, strings of <= 64 units (bit-mask flags).
+template <class Acc>
+__device__ double jw_small(Acc first, int lf, Acc second, int ls) {
+    const bool fmax = lf > ls;
+    const Acc mx = fmax ? first : second;
+    const Acc mn = fmax ? second : first;
+    const int lmx = fmax ? lf : ls, lmn = fmax ? ls : lf;
+    const int range = lmx / 2 - 1 > 0 ? lmx / 2 - 1 : 0;
+    uint64_t flags = 0, matched = 0;
+    int m = 0;
+    for (int mi = 0; mi < lmn; ++mi) {
+        const uint16_t c = mn[mi];
+        const int lo = mi - range > 0 ? mi - range : 0;
+        const int hi = mi + range + 1 < lmx ? mi + range + 1 : lmx;
+        for (int xi = lo; xi < hi; ++xi) {
+            if (!((flags >> xi) & 1ull) && mx[xi] == c) {
+                flags |= 1ull << xi;
+                matched |= 1ull << mi;
+                ++m;
+                break;
+            }
+        }
+    }
+    if (m == 0) return 0.0;
+    int t = 0;
+    uint64_t fm = flags, mm = matched;
+    while (mm) {
+        int i = __ffsll((unsigned long long)mm) - 1;
+        int x = __ffsll((unsigned long long)fm) - 1;
+        t += mn[i] != mx[x];
+        mm &= mm - 1;
+        fm &= fm - 1;
+    }
+    int prefix = 0;
+    for (int mi = 0; mi < lmn; ++mi) {
+        if (first[mi] == second[mi]) ++prefix;
+        else break;
+    }
+    return jw_finish(m, t, prefix, lf, ls, lmx);
+}
+
+// Same algorithm for any length up to SLOW_LIMIT (flag words in scratch).
+__device__ inline double jw_long(GlbAcc first, int lf, GlbAcc second, int ls) {
+    const bool fmax = lf > ls;
+    const GlbAcc mx = fmax ? first : second;
+    const GlbAcc mn = fmax ? second : first;
+    const int lmx = fmax ? lf : ls, lmn = fmax ? ls : lf;
+    const int range = lmx / 2 - 1 > 0 ? lmx / 2 - 1 : 0;
+    uint64_t flags[SLOW_LIMIT / 64], matched[SLOW_LIMIT / 64];
+    for (int i = 0; i < SLOW_LIMIT / 64; ++i) flags[i] = matched[i] = 0;
+    int m = 0;
+    for (int mi = 0; mi < lmn; ++mi) {
+        const uint16_t c = mn[mi];
+        const int lo = mi - range > 0 ? mi - range : 0;
+        const int hi = mi + range + 1 < lmx ? mi + range + 1 : lmx;
+        for (int xi = lo; xi < hi; ++xi) {
+            if (!((flags[xi >> 6] >> (xi & 63)) & 1ull) && mx[xi] == c) {
+                flags[xi >> 6] |= 1ull << (xi & 63);
+                matched[mi >> 6] |= 1ull << (mi & 63);
+                ++m;
+                break;
+            }
+        }
+    }
+    if (m == 0) return 0.0;
+    int t = 0, xi = 0;
+    for (int mi = 0; mi < lmn; ++mi) {
+        if (!((matched[mi >> 6] >> (mi & 63)) & 1ull)) continue;
+        while (!((flags[xi >> 6] >> (xi & 63)) & 1ull)) ++xi;
+        t += mn[mi] != mx[xi];
+        ++xi;
+    }
+    int prefix = 0;
+    for (int mi = 0; mi < lmn; ++mi) {
+        if (first[mi] == second[mi]) ++prefix;
+        else break;
+    }
+    return jw_finish(m, t, prefix, lf, ls, lmx);
+}
+
+// ---- Levenshtein (exact) -----------------------------------------------------------------------
+// Myers 1999 bit-parallel, pattern <= 64 symbols.
+template <class Acc>
+__device__ int lev_myers(Acc pat, int m, Acc txt, int n) {
+    if (m == 0) return n;
+    if (n == 0) return m;
+    uint64_t vp = ~0ull, vn = 0;
+    const uint64_t hib = 1ull << (m - 1);
+    int dist = m;
+    for (int j = 0; j < n; ++j) {
+        const uint16_t c = txt[j];
+        uint64_t eq = 0;
+        for (int i = 0; i < m; ++i) eq |= (uint64_t)(pat[i] == c) << i;
+        const uint64_t x = eq | vn;
+        const uint64_t d0 = (((x & vp) + vp) ^ vp) | x;
+        uint64_t hp = vn | ~(d0 | vp);
+        uint64_t hn = d0 & vp;
+        dist += (hp & hib) ? 1 : 0;
+        dist -= (hn & hib) ? 1 : 0;
+        hp = (hp << 1) | 1ull;
+        hn = hn << 1;
+        vp = hn | ~(d0 | hp);
+        vn = hp & d0;
+    }
+    return dist;
+}
+
+// Code points, any length up to SLOW_LIMIT (two-row DP in scratch).
+__device__ inline int lev_long(const StrView &a, const StrView &b) {
+    uint32_t cb[SLOW_LIMIT];
+    int32_t row[SLOW_LIMIT + 1];
+    int nb = 0;
+    for (int j = 0; j < b.n; ++j) {
+        uint32_t w = b.p[j];
+        if (w >= 0xD800 && w < 0xDC00 && j + 1 < b.n) {
+            w = 0x10000 + ((w - 0xD800) << 10) + (b.p[j + 1] - 0xDC00);
+            ++j;
+        }
+        cb[nb++] = w;
+    }
+    for (int j = 0; j <= nb; ++j) row[j] = j;
+    int i = 0;
+    for (int u = 0; u < a.n; ++u) {
+        uint32_t w = a.p[u];
+        if (w >= 0xD800 && w < 0xDC00 && u + 1 < a.n) {
+            w = 0x10000 + ((w - 0xD800) << 10) + (a.p[u + 1] - 0xDC00);
+            ++u;
+        }
+        ++i;
+        int diag = row[0];
+        row[0] = i;
+        for (int j = 1; j <= nb; ++j) {
+            int up = row[j];
+            int best = diag + (w != cb[j - 1] ? 1 : 0);
+            if (up + 1 < best) best = up + 1;
+            if (row[j - 1] + 1 < best) best = row[j - 1] + 1;
+            row[j] = best;
+            diag = up;
+        }
+    }
+    return row[nb];
+}
+
+// ---- bounds for the filter pass ---------------------------------------------------------------
+// A sketch holds 15 saturating 4-bit counts of the string's units per bucket (nibbles 0..14) and
+// a saturation flag (nibble 15).  For two strings with sketches a, b:
+//   Σ_b min(a_b, b_b)  >= the multiset intersection >= the Jaro match count m   (no saturation)
+//   max(Σa, Σb) - Σ min >= ... is <= the bag distance <= Levenshtein distance (saturation-safe)
+struct SketchSums {
+    int sum_a, sum_b, sum_min;
+    bool saturated;
+};
+
+__device__ inline int byte_sum(uint64_t x) { return (int)((x * 0x0101010101010101ull) >> 56); }
+
+__device__ inline uint64_t byte_min(uint64_t a, uint64_t b) {  // per byte, values <= 15
+    const uint64_t H = 0x8080808080808080ull;
+    const uint64_t ge = (((a | H) - b) & H) >> 7;  // 0x01 where a >= b
+    const uint64_t mge = ge * 0xFFull;
+    return (a & ~mge) | (b & mge);
+}
+
+__device__ inline SketchSums sketch_sums(uint64_t sa, uint64_t sb) {
+    const uint64_t L = 0x0F0F0F0F0F0F0F0Full, LO = 0x000F0F0F0F0F0F0Full;  // LO drops nibble 15
+    const uint64_t ae = sa & L, ao = (sa >> 4) & LO, be = sb & L, bo = (sb >> 4) & LO;
+    SketchSums s;
+    s.sum_a = byte_sum(ae) + byte_sum(ao);
+    s.sum_b = byte_sum(be) + byte_sum(bo);
+    s.sum_min = byte_sum(byte_min(ae, be)) + byte_sum(byte_min(ao, bo));
+    s.saturated = ((sa | sb) >> 60) != 0;
+    return s;
+}
+
+__device__ inline uint64_t view_sketch(const StrView &s) {
+    if (s.has_meta) return s.sketch;
+    uint64_t sk = 0;
+    for (int i = 0; i < s.n; ++i) {
+        const uint32_t b = sketch_bucket(s.p[i]);
+        if (((sk >> (4 * b)) & 15ull) == 15ull) sk |= 1ull << 60;
+        else sk += 1ull << (4 * b);
+    }
+    return sk;
+}
+
+// Upper bound of jaro_winkler_sim(first, second) for unequal strings.  m <= M from the sketches;
+// j <= ((M/lf + M/ls) + 1)/3 since (m - t)/m <= 1; jw = f(j) is non-decreasing in j for the
+// actual prefix.  Returns -1 when the bound proves m == 0 (so jw is exactly 0.0).
+__device__ inline double jw_upper(const StrView &first, const StrView &second) {
+    const int lf = first.n, ls = second.n;
+    const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
+    if (lmn == 0) return -1.0;
+    const SketchSums ss = sketch_sums(view_sketch(first), view_sketch(second));
+    int M = ss.saturated ? lmn : (ss.sum_min < lmn ? ss.sum_min : lmn);
+    if (M == 0) return -1.0;
+    const int prefix = common_prefix(first.p, second.p, lmn);
+    const double md = (double)M;
+    const double j = ((md / (double)lf + md / (double)ls) + 1.0) / 3.0;
+    if (j < 0.7) return j;
+    double w = 1.0 / (double)lmx;
+    if (w > 0.1) w = 0.1;
+    return j + (w * (double)prefix) * (1.0 - j);
+}
+
+// Lower bound of the code-point Levenshtein distance of unequal strings.
+__device__ inline int lev_lower(const StrView &a, const StrView &b) {
+    int lb = a.ncp > b.ncp ? a.ncp - b.ncp : b.ncp - a.ncp;
+    if (a.ncp == a.n && b.ncp == b.n) {  // BMP: units are code points, so the bag bound holds
+        const SketchSums ss = sketch_sums(view_sketch(a), view_sketch(b));
+        const int bag = (ss.sum_a > ss.sum_b ? ss.sum_a : ss.sum_b) - ss.sum_min;
+        if (bag > lb) lb = bag;
+    }
+    return lb;
+}
+
+// ---- bit-plane kernels (exact) -----------------------------------------------------------------
+template <typename W>
+__device__ inline W mask_below(int k) {  // bits [0, k)
+    return k >= (int)(8 * sizeof(W)) ? ~(W)0 : (((W)1 << k) - (W)1);
+}
+
+// Positions i of a plane-encoded string with unit i == c (garbage above the string's length).
+template <typename W>
+__device__ inline W eq_mask(const W (&pl)[N_PLANES], uint32_t c) {
+    W eq = c < 256u ? ~(W)0 : (W)0;
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) eq &= pl[b] ^ ((W)((c >> b) & 1u) - (W)1);
+    return eq;
+}
+
+// commons-text matches() with the longer string as bit-planes (<= 64 units).  mxp / mnp are the
+// longer / shorter strings' units, first / second the original argument order.
+template <typename W>
+__device__ double jw_planes(const uint64_t *mx_planes, const uint16_t *mxp, int lmx, const uint16_t *mnp, int lmn,
+                            const uint16_t *first, int lf, const uint16_t *second, int ls) {
+    W pl[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)mx_planes[b];
+    const int range = lmx / 2 - 1 > 0 ? lmx / 2 - 1 : 0;
+    W flags = 0;
+    uint64_t matched = 0;
+    int m = 0;
+    UnitReader rd(mnp);
+    for (int mi = 0; mi < lmn; ++mi) {
+        const int lo = mi - range > 0 ? mi - range : 0;
+        const int hi = mi + range + 1 < lmx ? mi + range + 1 : lmx;
+        const W cand = eq_mask<W>(pl, rd.next()) & mask_below<W>(hi) & ~mask_below<W>(lo) & ~flags;
+        if (cand) {
+            flags |= cand & (~cand + (W)1);  // lowest set bit: the first free match in the window
+            matched |= 1ull << mi;
+            ++m;
+        }
+    }
+    if (m == 0) return 0.0;
+    int t = 0;
+    uint64_t mm = matched, fm = (uint64_t)flags;
+    while (mm) {
+        const int i = __ffsll((unsigned long long)mm) - 1;
+        const int x = __ffsll((unsigned long long)fm) - 1;
+        t += mnp[i] != mxp[x];
+        mm &= mm - 1;
+        fm &= fm - 1;
+    }
+    return jw_finish(m, t, common_prefix(first, second, lmn), lf, ls, lmx);
+}
+
+// Myers 1999 with the pattern's match masks from its bit-planes, shifted by `shift` units.
+template <typename W>
+__device__ int lev_planes(const uint64_t *planes, int shift, int m, const uint16_t *txt, int n) {
+    W pl[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)(planes[b] >> shift);
+    W vp = ~(W)0, vn = 0;
+    const W hib = (W)1 << (m - 1);
+    int dist = m;
+    UnitReader rd(txt);
+    for (int j = 0; j < n; ++j) {
+        const W x = eq_mask<W>(pl, rd.next()) | vn;
+        const W d0 = (((x & vp) + vp) ^ vp) | x;
+        W hp = vn | ~(d0 | vp);
+        W hn = d0 & vp;
+        dist += (hp & hib) ? 1 : 0;
+        dist -= (hn & hib) ? 1 : 0;
+        hp = (hp << 1) | (W)1;
+        hn = hn << 1;
+        vp = hn | ~(d0 | hp);
+        vn = hp & d0;
+    }
+    return dist;
+}
+
+// Exact Jaro-Winkler for unequal strings of <= 64 units, without LDS.
+__device__ inline double jw_exact(const StrView &a, const StrView &b) {
+    const bool fmax = a.n > b.n;  // commons-text: max = first only if strictly longer
+    const StrView &mx = fmax ? a : b;
+    const StrView &mn = fmax ? b : a;
+    if (mx.planes) {
+        if (mx.n <= 32) return jw_planes<uint32_t>(mx.planes, mx.p, mx.n, mn.p, mn.n, a.p, a.n, b.p, b.n);
+        return jw_planes<uint64_t>(mx.planes, mx.p, mx.n, mn.p, mn.n, a.p, a.n, b.p, b.n);
+    }
+    return jw_small(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n);
+}
+
+// Exact code-point Levenshtein of unequal BMP strings of <= 64 units, without LDS: common prefix
+// and suffix are stripped (exact for unit-cost edit distance), then bit-parallel on the rest.
+__device__ inline int lev_exact(const StrView &a, const StrView &b) {
+    const int mn = a.n < b.n ? a.n : b.n;
+    const int pre = common_prefix(a.p, b.p, mn);
+    int suf = 0;
+    while (suf < mn - pre && a.p[a.n - 1 - suf] == b.p[b.n - 1 - suf]) ++suf;
+    const int la = a.n - pre - suf, lb = b.n - pre - suf;
+    if (la == 0) return lb;
+    if (lb == 0) return la;
+    // pattern: the longer trimmed string if it has planes (fewer text steps), else the other
+    const bool a_pat = a.planes && (la >= lb || !b.planes);
+    const StrView &pat = a_pat ? a : b;
+    const StrView &txt = a_pat ? b : a;
+    const int m = a_pat ? la : lb, n = a_pat ? lb : la;
+    if (pat.planes) {
+        if (m <= 32) return lev_planes<uint32_t>(pat.planes, pre, m, txt.p + pre, n);
+        return lev_planes<uint64_t>(pat.planes, pre, m, txt.p + pre, n);
+    }
+    return lev_myers(GlbAcc{a.p + pre}, la, GlbAcc{b.p + pre}, lb);
+}
+
+}  // namespace spk

@@ -200,25 +200,62 @@ def test_blocking_and_gammas_at_scale(amd, shards):
     from splink_amd.settings import complete_settings_dict
     df = _synthetic(30000, seed=11, surname_vocab=800, first_vocab=400, city_vocab=100)
     st = complete_settings_dict(cfg_settings(2), amd)
-    exp = _pandas_block(df, [["surname"], ["dob"]])
     rows = []
     codes = []
+    table = None
     for s in range(shards):
         job = Job("dedupe_only", [df], "unique_id", 0, shard=(s, shards))
         job.block(st["blocking_rules"])
+        if table is None:
+            table = job.tables[0]  # pair rows index the job's blocking-key clustered table
+            assert sorted(table["unique_id"]) == sorted(df["unique_id"])
+        assert job.tables[0]["unique_id"].equals(table["unique_id"])
         l, r = job.pair_rows()
         rows.append(np.stack([l, r], axis=1))
         job.gammas(st)
         codes.append(job.gammas_host())
+    exp = _pandas_block(table, [["surname"], ["dob"]])
     got_pairs = np.concatenate(rows)
     order = np.lexsort((got_pairs[:, 1], got_pairs[:, 0]))
     assert len(got_pairs) == len(exp)
     assert (got_pairs[order] == exp).all()
     gam = np.concatenate(codes)
-    cols = [orc.StrCol(df[c].tolist()) for c in ["first_name", "surname", "dob", "city", "email"]]
+    cols = [orc.StrCol(table[c].tolist()) for c in ["first_name", "surname", "dob", "city", "email"]]
     specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
     ref = orc.template_gammas(specs, cols, cols, got_pairs[:, 0], got_pairs[:, 1])
     assert (gam == ref).all()
+
+
+def test_simple_columns_match_interpreter(amd):
+    """The record-only filter for template-shaped columns and the general interpreter agree."""
+    from splink_amd.engine import Job
+    from splink_amd.synthetic import cfg_settings
+    from splink_amd.settings import complete_settings_dict
+    df = _synthetic(20000, seed=13, surname_vocab=500, first_vocab=300, city_vocab=80)
+    df["dob_num"] = pd.to_numeric(df["dob"].str.replace("-", ""), errors="coerce")
+    st = cfg_settings(2)
+    from splink_amd import case_statements as cs
+    extra = [("dob_abs4", cs.sql_gen_case_stmt_numeric_abs_4("dob_num", "dob_abs4", 1, 500), 4),
+             ("dob_perc3", cs.sql_gen_case_stmt_numeric_perc_3("dob_num", "dob_perc3"), 3),
+             ("dob_eq2", cs.sql_gen_case_stmt_numeric_2("dob_num", "dob_eq2"), 2),
+             ("email4", cs.sql_gen_case_stmt_levenshtein_4("email", "email4"), 4),
+             ("sn4", cs.sql_gen_gammas_case_stmt_jaro_4("surname", "sn4", 0.94, 0.88, 0.7), 4),
+             ("fn2", cs.sql_gen_gammas_case_stmt_jaro_2("first_name", "fn2"), 2),
+             ("city2", cs.sql_gen_case_smnt_strict_equality_2("city", "city2"), 2)]
+    for name, expr, L in extra:
+        st["comparison_columns"].append({"custom_name": name, "custom_columns_used": [name], "num_levels": L,
+                                         "case_expression": expr})
+    st = complete_settings_dict(st, amd)
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    assert job.ctx.gammas_simple_count() == len(st["comparison_columns"])
+    fast = job.gammas_host()
+    job.ctx.gammas_set_simple(False)
+    job.gammas(st)
+    assert job.ctx.gammas_simple_count() == 0
+    slow = job.gammas_host()
+    assert (fast == slow).all()
 
 
 def test_em_at_scale_matches_oracle(amd):
@@ -247,6 +284,32 @@ def test_em_at_scale_matches_oracle(amd):
             assert all(rel_close(a, b) for a, b in zip(u, u_o[k]))
     mp = job.score(params.params["λ"], params._level_probabilities())
     assert np.allclose(mp, mp_o, rtol=1e-9, atol=0)
+
+
+def test_cross_column_equality(amd):
+    """Dictionary ids are per column: `a_l = b_r` must compare strings, not ids of two spaces."""
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(5))
+    vocab_a = ["x", "yy", "zzz", "shared", None]
+    vocab_b = ["shared", "zzz", "q", None]
+    n = 400
+    pick = lambda v: rng.choice(np.array(v, dtype=object), n)  # noqa: E731
+    df = pd.DataFrame({"a_l": pick(vocab_a), "a_r": pick(vocab_a), "b_l": pick(vocab_b), "b_r": pick(vocab_b)})
+    expr = ("case when a_l is null or b_r is null then -1 when a_l = b_r then 2 "
+            "when a_l = a_r then 1 else 0 end")
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "x", "custom_columns_used": ["a", "b"], "num_levels": 3, "case_expression": expr}]}
+    got = add_gammas(df, st, amd).gamma_matrix()[:, 0]
+    for k, (al, ar, br) in enumerate(zip(df.a_l, df.a_r, df.b_r)):
+        if al is None or br is None:
+            want = -1
+        elif al == br:
+            want = 2
+        elif al == ar:
+            want = 1
+        else:
+            want = 0
+        assert got[k] == want, (al, br, ar)
 
 
 def test_edge_cases(amd):
