@@ -43,11 +43,6 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
 // points, hash the units and build the bucket sketch used by the comparison filters.
 // Surrogate-encoded (CESU / "surrogatepass") 3-byte sequences decode to lone surrogate units,
 // exactly as a Java String would hold them.
-__device__ inline void sketch_add(uint64_t &sk, uint32_t unit) {
-    const uint32_t b = sketch_bucket(unit);
-    if (((sk >> (4 * b)) & 15ull) == 15ull) sk |= 1ull << 60;  // saturated: flag nibble 15
-    else sk += 1ull << (4 * b);
-}
 
 __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const uint8_t *__restrict__ bytes,
                               const uint8_t *__restrict__ valid, uint16_t *__restrict__ units,

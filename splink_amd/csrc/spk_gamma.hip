@@ -424,16 +424,16 @@ __device__ inline double jw_upper_meta(const RecMeta &a, const RecMeta &b) {
     const int lf = a.len16, ls = b.len16;
     const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
     if (lmn == 0) return -1.0;
-    const SketchSums ss = sketch_sums(a.sketch, b.sketch);
-    const int M = ss.saturated ? lmn : (ss.sum_min < lmn ? ss.sum_min : lmn);
+    const int M = sketch_inter_ub(a.sketch, b.sketch, lf, ls);
     if (M == 0) return -1.0;
     const uint64_t d = a.head ^ b.head;
     const int cp = d ? (__ffsll((unsigned long long)d) - 1) / 16 : 4;
     const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
     // M/lf + M/ls with one division; the caller's 1e-12 margin covers the few-ulp difference from
-    // the reference's operation order (a bound only has to be >= the true value)
+    // the reference's operation order (a bound only has to be >= the true value), and the Winkler
+    // boost is applied unless j is clearly below its 0.7 threshold
     const double j = ((double)M * (double)(lf + ls) / ((double)lf * (double)ls) + 1.0) * (1.0 / 3.0);
-    if (j < 0.7) return j;
+    if (j < 0.7 - 1e-9) return j;
     const double pw = lmx > 10 ? (double)prefix / (double)lmx : 0.1 * (double)prefix;
     return j + pw * (1.0 - j);
 }
@@ -441,9 +441,8 @@ __device__ inline double jw_upper_meta(const RecMeta &a, const RecMeta &b) {
 __device__ inline int lev_lower_meta(const RecMeta &a, const RecMeta &b) {
     const int na = meta_cplen(a), nb = meta_cplen(b);
     int lb = na > nb ? na - nb : nb - na;
-    if (na == a.len16 && nb == b.len16) {
-        const SketchSums ss = sketch_sums(a.sketch, b.sketch);
-        const int bag = (ss.sum_a > ss.sum_b ? ss.sum_a : ss.sum_b) - ss.sum_min;
+    if (na == a.len16 && nb == b.len16) {  // BMP: units are code points, so the bag bound holds
+        const int bag = (na > nb ? na : nb) - sketch_inter_ub(a.sketch, b.sketch, na, nb);
         if (bag > lb) lb = bag;
     }
     return lb;

@@ -50,7 +50,7 @@ struct alignas(16) RecMeta {
     uint32_t key;     // dictionary id of the value (CPF_ID: equal iff the strings are) or a 32-bit
                       // FNV-1a fold of the units (unequal keys prove unequal strings)
     int32_t len16;    // UTF-16 length, -1 = NULL
-    uint64_t sketch;  // nibbles 0..14: saturating per-bucket unit counts; nibble 15: saturation flag
+    uint64_t sketch;  // unit sketch (sketch_bucket / sketch_add)
     uint64_t head;    // units 0..3, zero beyond len16
     uint32_t off4;    // first UTF-16 unit of the row / 4 (rows start 8-byte aligned)
     uint32_t cpf;     // bits 0..23: code-point length; bit 24: bit-planes valid (<= 64 units, all < 256);
@@ -67,7 +67,28 @@ __host__ __device__ inline int64_t meta_off(const RecMeta &m) { return (int64_t)
 // AND_b (bit b of c ? plane_b : ~plane_b), eight register ops instead of a scan of the string.
 constexpr int N_PLANES = 8;
 
-__host__ __device__ inline uint32_t sketch_bucket(uint32_t u) { return ((u * 2654435761u) >> 16) % 15u; }
+// Unit sketch: 32 buckets of saturating 2-bit unit counts (0, 1, 2, >=3) held as two bit-planes,
+// bits 0..31 the low count bit and bits 32..63 the high count bit of each bucket.  ASCII letters
+// get a bucket each (case folded), digits three, other ASCII three; other units are hashed.
+// Merging units into a bucket only raises the per-bucket minima, so the multiset-intersection
+// bound derived from two sketches (sketch_inter_ub) holds for any bucket map.
+__host__ __device__ inline uint32_t sketch_bucket(uint32_t u) {
+    if (u < 128u) {
+        if (u >= 'a' && u <= 'z') return u - 'a';
+        if (u >= 'A' && u <= 'Z') return u - 'A';
+        if (u >= '0' && u <= '9') return 26u + (u - '0') % 3u;
+        return 29u + u % 3u;
+    }
+    return ((u * 2654435761u) >> 16) & 31u;
+}
+
+__host__ __device__ inline void sketch_add(uint64_t &sk, uint32_t unit) {
+    const uint32_t b = sketch_bucket(unit);
+    const uint64_t lo = 1ull << b, hi = 1ull << (32 + b);
+    if ((sk & lo) && (sk & hi)) return;  // saturated at 3
+    if (sk & lo) sk = (sk & ~lo) | hi;   // 1 -> 2
+    else sk |= lo;                       // 0 -> 1, 2 -> 3
+}
 
 struct ColDesc {
     int32_t kind;

@@ -269,43 +269,31 @@ __device__ inline int lev_long(const StrView &a, const StrView &b) {
 }
 
 // ---- bounds for the filter pass ---------------------------------------------------------------
-// A sketch holds 15 saturating 4-bit counts of the string's units per bucket (nibbles 0..14) and
-// a saturation flag (nibble 15).  For two strings with sketches a, b:
-//   Σ_b min(a_b, b_b)  >= the multiset intersection >= the Jaro match count m   (no saturation)
-//   max(Σa, Σb) - Σ min >= ... is <= the bag distance <= Levenshtein distance (saturation-safe)
-struct SketchSums {
-    int sum_a, sum_b, sum_min;
-    bool saturated;
-};
-
-__device__ inline int byte_sum(uint64_t x) { return (int)((x * 0x0101010101010101ull) >> 56); }
-
-__device__ inline uint64_t byte_min(uint64_t a, uint64_t b) {  // per byte, values <= 15
-    const uint64_t H = 0x8080808080808080ull;
-    const uint64_t ge = (((a | H) - b) & H) >> 7;  // 0x01 where a >= b
-    const uint64_t mge = ge * 0xFFull;
-    return (a & ~mge) | (b & mge);
-}
-
-__device__ inline SketchSums sketch_sums(uint64_t sa, uint64_t sb) {
-    const uint64_t L = 0x0F0F0F0F0F0F0F0Full, LO = 0x000F0F0F0F0F0F0Full;  // LO drops nibble 15
-    const uint64_t ae = sa & L, ao = (sa >> 4) & LO, be = sb & L, bo = (sb >> 4) & LO;
-    SketchSums s;
-    s.sum_a = byte_sum(ae) + byte_sum(ao);
-    s.sum_b = byte_sum(be) + byte_sum(bo);
-    s.sum_min = byte_sum(byte_min(ae, be)) + byte_sum(byte_min(ao, bo));
-    s.saturated = ((sa | sb) >> 60) != 0;
-    return s;
+// Upper bound of the multiset intersection |a ∩ b| of two unit strings of la / lb units from
+// their sketches (spk_internal.h): Σ over buckets of min(count_a, count_b), exact per bucket unless
+// both counts are saturated; those buckets together hold at most what the other buckets leave of
+// either length.  |a ∩ b| bounds the Jaro match count m from above, and max(la, lb) - |a ∩ b| (the
+// bag distance) bounds the Levenshtein distance from below.
+__device__ inline int sketch_inter_ub(uint64_t sa, uint64_t sb, int la, int lb) {
+    const uint32_t aL = (uint32_t)sa, aH = (uint32_t)(sa >> 32);
+    const uint32_t bL = (uint32_t)sb, bH = (uint32_t)(sb >> 32);
+    const uint32_t gt = (aH & ~bH) | (~(aH ^ bH) & aL & ~bL);  // buckets where count_a > count_b
+    const uint32_t mL = (aL & ~gt) | (bL & gt), mH = (aH & ~gt) | (bH & gt);
+    const uint32_t both_sat = aL & aH & bL & bH, rest = ~both_sat;
+    int inter = __builtin_popcount(mL & rest) + 2 * __builtin_popcount(mH & rest);
+    if (both_sat) {
+        const int ra = la - (__builtin_popcount(aL & rest) + 2 * __builtin_popcount(aH & rest));
+        const int rb = lb - (__builtin_popcount(bL & rest) + 2 * __builtin_popcount(bH & rest));
+        inter += ra < rb ? ra : rb;
+    }
+    const int lmn = la < lb ? la : lb;
+    return inter < lmn ? inter : lmn;
 }
 
 __device__ inline uint64_t view_sketch(const StrView &s) {
     if (s.has_meta) return s.sketch;
     uint64_t sk = 0;
-    for (int i = 0; i < s.n; ++i) {
-        const uint32_t b = sketch_bucket(s.p[i]);
-        if (((sk >> (4 * b)) & 15ull) == 15ull) sk |= 1ull << 60;
-        else sk += 1ull << (4 * b);
-    }
+    for (int i = 0; i < s.n; ++i) sketch_add(sk, s.p[i]);
     return sk;
 }
 
@@ -316,8 +304,7 @@ __device__ inline double jw_upper(const StrView &first, const StrView &second) {
     const int lf = first.n, ls = second.n;
     const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
     if (lmn == 0) return -1.0;
-    const SketchSums ss = sketch_sums(view_sketch(first), view_sketch(second));
-    int M = ss.saturated ? lmn : (ss.sum_min < lmn ? ss.sum_min : lmn);
+    const int M = sketch_inter_ub(view_sketch(first), view_sketch(second), lf, ls);
     if (M == 0) return -1.0;
     const int prefix = common_prefix(first.p, second.p, lmn);
     const double md = (double)M;
@@ -332,8 +319,7 @@ __device__ inline double jw_upper(const StrView &first, const StrView &second) {
 __device__ inline int lev_lower(const StrView &a, const StrView &b) {
     int lb = a.ncp > b.ncp ? a.ncp - b.ncp : b.ncp - a.ncp;
     if (a.ncp == a.n && b.ncp == b.n) {  // BMP: units are code points, so the bag bound holds
-        const SketchSums ss = sketch_sums(view_sketch(a), view_sketch(b));
-        const int bag = (ss.sum_a > ss.sum_b ? ss.sum_a : ss.sum_b) - ss.sum_min;
+        const int bag = (a.n > b.n ? a.n : b.n) - sketch_inter_ub(view_sketch(a), view_sketch(b), a.n, b.n);
         if (bag > lb) lb = bag;
     }
     return lb;
