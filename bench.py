@@ -58,6 +58,7 @@ def main():
         torch.cuda.set_device(0)
 
     from splink_amd import _native as N
+    from splink_amd import distributed as D
     from splink_amd.engine import Job, m_step_rows
     from splink_amd.params import Params
     from splink_amd.session import AmdSession
@@ -93,9 +94,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize()
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
+        D.barrier()
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -111,16 +110,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     local_pairs = job.n_pairs
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        p = torch.tensor([local_pairs], dtype=torch.int64, device=f"cuda:{local}")
-        dist.all_reduce(p)
-        total_pairs = int(p.item())
-    else:
-        total_pairs = local_pairs
+    elapsed = D.max_over_ranks(elapsed)
+    total_pairs = D.sum_over_ranks(local_pairs)
     ms_per_step = elapsed * 1000.0 / args.steps
 
     # ---- full job (blocking excluded from the metric): score pass for the record
@@ -146,11 +137,11 @@ def main():
         rec_bytes += int(s.str.len().sum()) * 2 + 8 * 3 * len(df)  # UTF-16 units + offset/len/hash per row
     gamma_bytes = local_pairs * (8 + code_bytes) + rec_bytes
     em_bytes = local_pairs * code_bytes
-    roofline = {"bound": "hbm", "kernel": "k_gamma_fast (+deferred k_gamma_slow)",
+    roofline = {"bound": "hbm", "kernel": "spk_gammas pass (k_gamma_simple + k_gamma_exact per column + k_pack16)",
                 "achieved": gamma_bytes / (g_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gamma_bytes / (g_ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                 "algorithmic_bytes_per_launch": gamma_bytes, "avg_launch_ms": g_ms,
-                "note": "comparison kernel is VALU/LDS-bound (string work); HBM fraction shown per the contract"}
+                "note": "comparison pass is VALU / gather-latency bound (string work), not HBM-bound; its HBM fraction is shown per the contract"}
     em_roofline = {"bound": "hbm", "kernel": "k_hist", "achieved": em_bytes / (h_ms / 1e3) / 1e9,
                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": em_bytes / (h_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                    "algorithmic_bytes_per_launch": em_bytes, "avg_launch_ms": h_ms}

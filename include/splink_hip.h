@@ -184,6 +184,9 @@ int spk_levenshtein(spk_ctx *ctx, int64_t n, const int64_t *l_offsets, const uin
  * d_hist, a DEVICE buffer (NULL = context-owned).  The histogram is the sufficient statistic of
  * the E+M step; callers sharding pairs over GPUs all-reduce it (exact integer sum). */
 int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist);
+/* Histogram kernel choice (same result): 1 = lane-private LDS counters when the pattern space fits
+ * (default), 0 = wave-ballot aggregation into one LDS histogram.  For testing and measurement. */
+int spk_em_set_lane_histogram(spk_ctx *ctx, int on);
 /* E-step per pattern with the reference's literal arithmetic, then the M-step sums:
  * out_stats (host) = [Σmp, rows, non-null rows, Σ ln(λΠm + (1-λ)Πu), non-null ln rows] + per column k,
  * per level v in -1..L_k-1:

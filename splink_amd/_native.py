@@ -43,7 +43,7 @@ EXPORTS = [
     "spk_pairs_count", "spk_pairs_copy", "spk_pairs_load", "spk_gammas", "spk_gammas_copy", "spk_gammas_load",
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
-    "spk_gammas_set_simple", "spk_gammas_simple_count",
+    "spk_gammas_set_simple", "spk_gammas_simple_count", "spk_em_set_lane_histogram",
 ]
 
 
@@ -240,6 +240,9 @@ class Context:
         n = ctypes.c_int(0)
         check(self._lib.spk_gammas_simple_count(self._h, ctypes.byref(n)), "spk_gammas_simple_count")
         return n.value
+
+    def em_set_lane_histogram(self, on: bool):
+        check(self._lib.spk_em_set_lane_histogram(self._h, ctypes.c_int(1 if on else 0)), "spk_em_set_lane_histogram")
 
     def em_histogram(self, d_hist_ptr: int = 0):
         check(self._lib.spk_em_histogram(self._h, ctypes.c_void_p(d_hist_ptr)), "spk_em_histogram")

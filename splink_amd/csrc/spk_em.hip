@@ -3,8 +3,8 @@
 //
 // The E-step's match_probability is a function of the comparison vector only, so the M-step's
 // sufficient statistic is the histogram of codes.  Each EM iteration streams every pair's code
-// once (HBM-bound: 2 or 4 bytes per pair) into an LDS-privatised histogram with wave-level
-// aggregation of equal codes, then evaluates mp per pattern with the reference's literal
+// once (HBM-bound: 2 or 4 bytes per pair) into an LDS-privatised histogram (lane-private counters,
+// k_hist_lanes; wave-level aggregation of equal codes for large pattern spaces, k_hist), then evaluates mp per pattern with the reference's literal
 // arithmetic and reduces the per-(column, level) sums in a fixed order (deterministic, and
 // identical for any sharding of pairs over GPUs since the histogram is an exact integer sum).
 #include <cmath>
@@ -74,6 +74,68 @@ __global__ __launch_bounds__(H_THREADS) void k_hist(const CodeT *__restrict__ co
             uint32_t v = sh[b];
             if (v) atomicAdd(&ghist[b], (unsigned long long)v);
         }
+    }
+}
+
+// Histogram with lane-private LDS counters, for pattern spaces with n_pat x 4 copies x 4 B <= 80 KiB.  Counter
+// (bin, copy) lives at word bin * R + copy with copy = lane % R, R = 64 / 32 / 16 / 8 / 4 copies:
+// with R = 64 every lane of a wave hits its own bank (64 x 4-byte banks) whatever the codes are, so
+// one code costs one conflict-free `ds_add_u32` and a couple of VALU ops -- no ballots, no
+// serialisation on the few dominant patterns.  Smaller R (larger pattern spaces) admits at most
+// 64 / R lanes per bank.  Waves of a workgroup share the copies (atomics; different instructions
+// never bank-conflict).  Codes are streamed as 16-byte vectors, four loads in flight per lane.
+constexpr int HL_THREADS = 512;
+constexpr int HL_LDS_BYTES = 80 * 1024;  // two workgroups per CU
+constexpr int HL_UNROLL = 4;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename CodeT, int R>
+__global__ __launch_bounds__(HL_THREADS) void k_hist_lanes(const CodeT *__restrict__ codes, int64_t P, int n_pat,
+                                                           unsigned long long *__restrict__ ghist) {
+    extern __shared__ uint32_t sh[];
+    for (int b = threadIdx.x; b < n_pat * R; b += HL_THREADS) sh[b] = 0;
+    __syncthreads();
+    constexpr int VEC = 16 / sizeof(CodeT);
+    constexpr int BITS = 8 * sizeof(CodeT);
+    const uint32_t copy = threadIdx.x & (R - 1);
+    const u32x4 *cv = reinterpret_cast<const u32x4 *>(codes);
+    const int64_t n_vec = P / VEC;
+    const int64_t stride = (int64_t)gridDim.x * HL_THREADS;
+    int64_t v = (int64_t)blockIdx.x * HL_THREADS + threadIdx.x;
+    auto count_word = [&](uint32_t w) {
+#pragma unroll
+        for (int j = 0; j < 32 / BITS; ++j) {
+            const uint32_t c = BITS == 32 ? w : ((w >> (BITS * j)) & ((1u << BITS) - 1u));
+            atomicAdd(&sh[c * R + copy], 1u);
+        }
+    };
+    for (; v + (HL_UNROLL - 1) * stride < n_vec; v += HL_UNROLL * stride) {
+        u32x4 w[HL_UNROLL];
+#pragma unroll
+        for (int u = 0; u < HL_UNROLL; ++u) w[u] = __builtin_nontemporal_load(cv + v + u * stride);
+#pragma unroll
+        for (int u = 0; u < HL_UNROLL; ++u) {
+            count_word(w[u].x);
+            count_word(w[u].y);
+            count_word(w[u].z);
+            count_word(w[u].w);
+        }
+    }
+    for (; v < n_vec; v += stride) {
+        const u32x4 w = cv[v];
+        count_word(w.x);
+        count_word(w.y);
+        count_word(w.z);
+        count_word(w.w);
+    }
+    if (blockIdx.x == 0)  // tail (P not a multiple of VEC)
+        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
+        if (s) atomicAdd(&ghist[b], (unsigned long long)s);
     }
 }
 
@@ -280,6 +342,12 @@ static int compute_mpat(spk_ctx *ctx, double lambda, double one_minus, const dou
 
 using namespace spk;
 
+extern "C" int spk_em_set_lane_histogram(spk_ctx *ctx, int on) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->hist_lanes = on != 0;
+    return SPK_OK;
+}
+
 extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
     SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_histogram: no gammas");
@@ -299,7 +367,32 @@ extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     if (blocks < 1) blocks = 1;
     const bool lds = n_pat <= H_LDS_BINS;
     size_t shm = lds ? (size_t)n_pat * 4 : 0;
-    if (ctx->code_bytes == 2) {
+    int R = 64;
+    while (R >= 4 && (int64_t)n_pat * R * 4 > HL_LDS_BYTES) R >>= 1;
+    if (R >= 4 && ctx->hist_lanes) {
+        int n_cu = 256;
+        (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+        const int64_t vecs = P / vec;
+        int64_t g = (vecs + HL_THREADS - 1) / HL_THREADS;
+        if (g > 2 * (int64_t)n_cu) g = 2 * (int64_t)n_cu;
+        if (g < 1) g = 1;
+        const size_t sh = (size_t)n_pat * R * 4;
+        const auto *c16 = reinterpret_cast<const uint16_t *>(ctx->codes.p);
+        const auto *c32 = reinterpret_cast<const uint32_t *>(ctx->codes.p);
+#define SPK_HL(RR)                                                                                              \
+    case RR:                                                                                                     \
+        if (ctx->code_bytes == 2) k_hist_lanes<uint16_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c16, P, (int)n_pat, h); \
+        else k_hist_lanes<uint32_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c32, P, (int)n_pat, h);   \
+        break;
+        switch (R) {
+            SPK_HL(64)
+            SPK_HL(32)
+            SPK_HL(16)
+            SPK_HL(8)
+            SPK_HL(4)
+        }
+#undef SPK_HL
+    } else if (ctx->code_bytes == 2) {
         if (lds) k_hist<uint16_t, true><<<(unsigned)blocks, H_THREADS, shm, ctx->stream>>>(
             reinterpret_cast<const uint16_t *>(ctx->codes.p), P, (int)n_pat, h);
         else k_hist<uint16_t, false><<<(unsigned)blocks, H_THREADS, 0, ctx->stream>>>(

@@ -187,6 +187,7 @@ struct spk_ctx {
     spk::DevBuf<double> mpat, llpat, stats, mu;
     spk::DevBuf<double> mp;  // per-pair scores (final E-step)
     bool mpat_valid = false;
+    bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
 
     // timing
     bool timing = false;

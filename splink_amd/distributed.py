@@ -1,0 +1,65 @@
+"""Multi-GPU plumbing: one process per GPU, candidate pairs sharded by ordinal, one exchange per EM iteration.
+
+The reference's only cross-executor traffic on this path is Spark's shuffle of the partial
+GROUP BY (maximisation_step.py:54-58) and the `collect()` of the tiny result (:36, :88).  Here
+each rank holds the whole record table, generates only its slice of the global candidate-ordinal
+space (spk_block shard / n_shards), and the only data-path collective is the all-reduce of the
+comparison-pattern histogram (an exact integer sum, so every rank computes bit-identical
+parameters whatever the rank count).  With the `nccl` backend that is RCCL over xGMI; with
+`gloo` (CPU tests) the same code runs on host tensors.
+"""
+from __future__ import annotations
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+    except Exception:  # pragma: no cover - torch always ships distributed on ROCm builds
+        return None
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def shard() -> tuple:
+    """(rank, world_size) of this process; (0, 1) without an initialised process group."""
+    dist = _dist()
+    if dist is None or dist.get_world_size() <= 1:
+        return 0, 1
+    return dist.get_rank(), dist.get_world_size()
+
+
+def allreduce_histogram_(hist):
+    """In-place sum of a pattern histogram (int64 tensor, device or host) over all ranks."""
+    dist = _dist()
+    if dist is not None and dist.get_world_size() > 1:
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+    return hist
+
+
+def _reduce_scalar(x, op, dtype):
+    import torch
+    dist = _dist()
+    if dist is None or dist.get_world_size() <= 1:
+        return x
+    dev = "cpu" if dist.get_backend() == "gloo" else f"cuda:{torch.cuda.current_device()}"
+    t = torch.tensor([x], dtype=dtype, device=dev)
+    dist.all_reduce(t, op=op)
+    return t.item()
+
+
+def max_over_ranks(x: float) -> float:
+    """Wall time of a step = the slowest rank's (bench.py contract)."""
+    import torch
+    dist = _dist()
+    return float(_reduce_scalar(float(x), dist.ReduceOp.MAX if dist else None, torch.float64))
+
+
+def sum_over_ranks(n: int) -> int:
+    import torch
+    dist = _dist()
+    return int(_reduce_scalar(int(n), dist.ReduceOp.SUM if dist else None, torch.int64))
+
+
+def barrier():
+    dist = _dist()
+    if dist is not None and dist.get_world_size() > 1:
+        dist.barrier()

@@ -18,6 +18,7 @@ import numpy as np
 import pandas as pd
 
 from . import _native as N
+from . import distributed as D
 from . import table as T
 from .compiler import CompiledComparisons, Schema, compile_comparisons, compile_rule
 
@@ -36,13 +37,7 @@ def session_device(spark) -> int:
 
 def distributed_shard():
     """(rank, world_size) when running under torch.distributed with >1 rank, else (0, 1)."""
-    try:
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            return dist.get_rank(), dist.get_world_size()
-    except Exception:
-        pass
-    return 0, 1
+    return D.shard()
 
 
 def quantise(p):
@@ -269,11 +264,10 @@ class Job:
         rank, world = distributed_shard()
         if world > 1:
             import torch
-            import torch.distributed as dist
             n_pat = self.ctx.n_patterns()
             hist = torch.zeros(n_pat, dtype=torch.int64, device=f"cuda:{self.device}")
             self.ctx.em_histogram(hist.data_ptr())
-            dist.all_reduce(hist)
+            D.allreduce_histogram_(hist)
             torch.cuda.synchronize(self.device)
             return self.ctx.em_finalize(hist.data_ptr(), lam_d, one_minus, m, u, n_stats)
         self.ctx.em_histogram(0)

@@ -327,3 +327,32 @@ def test_edge_cases(amd):
     df = pd.DataFrame({"unique_id": [1, 1, 2], "name": ["a", "a", "a"]})
     out = Splink(copy.deepcopy(st), amd, df=df).get_scored_comparisons().toPandas()
     assert sorted(zip(out.unique_id_l, out.unique_id_r)) == [(1, 2), (1, 2)]
+
+
+@pytest.mark.parametrize("n_levels", [[2], [3, 3, 2, 2, 3], [4, 4, 4, 4, 4], [5, 5, 5, 5, 5, 5, 5], [4] * 9])
+def test_em_histogram_kernels_agree(amd, n_levels):
+    """Lane-private (R = 64 .. 4 copies) and wave-ballot histograms give the same pattern counts,
+    from 3 to 2M patterns (uint16 and uint32 codes), skewed towards one dominant pattern."""
+    from splink_amd import _native as N
+    rng = np.random.Generator(np.random.PCG64(len(n_levels) * 7 + n_levels[0]))
+    P = 1_000_003  # not a multiple of the 16-byte vector
+    g = np.zeros((P, len(n_levels)), dtype=np.int8)
+    for k, L in enumerate(n_levels):
+        dominant = rng.random(P) < 0.8
+        g[:, k] = np.where(dominant, 0, rng.integers(-1, L, P)).astype(np.int8)
+    ctx = N.Context(0)
+    ctx.gammas_load(n_levels, g)
+    n_pat = ctx.n_patterns()
+    stride = np.cumprod([1] + [L + 1 for L in n_levels[:-1]])
+    codes = ((g.astype(np.int64) + 1) * stride).sum(axis=1)
+    want = np.bincount(codes, minlength=n_pat)
+    got = []
+    for lanes in (True, False):
+        ctx.em_set_lane_histogram(lanes)
+        hist = np.zeros(n_pat, dtype=np.uint64)
+        import torch
+        d = torch.zeros(n_pat, dtype=torch.int64, device="cuda:0")
+        ctx.em_histogram(d.data_ptr())
+        hist[:] = d.cpu().numpy().astype(np.uint64)
+        got.append(hist)
+    assert (got[0] == want).all() and (got[1] == want).all()
