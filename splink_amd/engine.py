@@ -265,8 +265,13 @@ class Job:
         if world > 1:
             import torch
             n_pat = self.ctx.n_patterns()
-            hist = torch.zeros(n_pat, dtype=torch.int64, device=f"cuda:{self.device}")
-            self.ctx.em_histogram(hist.data_ptr())
+            hist = getattr(self, "_hist_dev", None)
+            if hist is None or hist.numel() != n_pat:
+                hist = torch.empty(n_pat, dtype=torch.int64, device=f"cuda:{self.device}")
+                # the buffer is written on the context's stream: torch's allocation work must be done
+                torch.cuda.synchronize(self.device)
+                self._hist_dev = hist
+            self.ctx.em_histogram(hist.data_ptr())  # zeroes, fills and synchronises its stream
             D.allreduce_histogram_(hist)
             torch.cuda.synchronize(self.device)
             return self.ctx.em_finalize(hist.data_ptr(), lam_d, one_minus, m, u, n_stats)

@@ -351,8 +351,9 @@ def test_em_histogram_kernels_agree(amd, n_levels):
         ctx.em_set_lane_histogram(lanes)
         hist = np.zeros(n_pat, dtype=np.uint64)
         import torch
-        d = torch.zeros(n_pat, dtype=torch.int64, device="cuda:0")
-        ctx.em_histogram(d.data_ptr())
+        d = torch.full((n_pat,), -1, dtype=torch.int64, device="cuda:0")
+        torch.cuda.synchronize()  # torch's fill runs on its own stream
+        ctx.em_histogram(d.data_ptr())  # zeroes the buffer itself
         hist[:] = d.cpu().numpy().astype(np.uint64)
         got.append(hist)
     assert (got[0] == want).all() and (got[1] == want).all()
