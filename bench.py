@@ -137,7 +137,7 @@ def main():
         rec_bytes += int(s.str.len().sum()) * 2 + 8 * 3 * len(df)  # UTF-16 units + offset/len/hash per row
     gamma_bytes = local_pairs * (8 + code_bytes) + rec_bytes
     em_bytes = local_pairs * code_bytes
-    roofline = {"bound": "hbm", "kernel": "spk_gammas pass (k_gamma_simple + k_gamma_exact per column + k_pack16)",
+    roofline = {"bound": "hbm", "kernel": "spk_gammas pass (k_gamma_simple + k_gamma_exact per undecided column)",
                 "achieved": gamma_bytes / (g_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gamma_bytes / (g_ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                 "algorithmic_bytes_per_launch": gamma_bytes, "avg_launch_ms": g_ms,

@@ -155,6 +155,7 @@ int spk_ctx_create(int device, spk_ctx **out) {
                 std::string("libsplink_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     spk_ctx *c = new spk_ctx();
     c->device = device;
+    c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -178,6 +179,7 @@ void spk_ctx_destroy(spk_ctx *ctx) {
         (void)hipEventDestroy(ctx->ev0[k]);
         (void)hipEventDestroy(ctx->ev1[k]);
     }
+    if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     hipStream_t own = ctx->own_stream;
     delete ctx;
     if (own) (void)hipStreamDestroy(own);

@@ -8,6 +8,7 @@
 // arithmetic and reduces the per-(column, level) sums in a fixed order (deterministic, and
 // identical for any sharding of pairs over GPUs since the histogram is an exact integer sum).
 #include <cmath>
+#include <cstring>
 
 #include "spk_internal.h"
 
@@ -84,14 +85,14 @@ __global__ __launch_bounds__(H_THREADS) void k_hist(const CodeT *__restrict__ co
 // serialisation on the few dominant patterns.  Smaller R (larger pattern spaces) admits at most
 // 64 / R lanes per bank.  Waves of a workgroup share the copies (atomics; different instructions
 // never bank-conflict).  Codes are streamed as 16-byte vectors, four loads in flight per lane.
-constexpr int HL_THREADS = 512;
-constexpr int HL_LDS_BYTES = 80 * 1024;  // two workgroups per CU
+constexpr int HL_THREADS = 1024;
+constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS
 constexpr int HL_UNROLL = 4;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <typename CodeT, int R>
 __global__ __launch_bounds__(HL_THREADS) void k_hist_lanes(const CodeT *__restrict__ codes, int64_t P, int n_pat,
-                                                           unsigned long long *__restrict__ ghist) {
+                                                           uint32_t *__restrict__ part) {
     extern __shared__ uint32_t sh[];
     for (int b = threadIdx.x; b < n_pat * R; b += HL_THREADS) sh[b] = 0;
     __syncthreads();
@@ -132,77 +133,127 @@ __global__ __launch_bounds__(HL_THREADS) void k_hist_lanes(const CodeT *__restri
         for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
     __syncthreads();
     for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
-        uint64_t s = 0;
+        uint32_t s = 0;
 #pragma unroll
         for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
-        if (s) atomicAdd(&ghist[b], (unsigned long long)s);
+        part[(int64_t)blockIdx.x * n_pat + b] = (uint32_t)s;
     }
 }
 
+// hist[b] = Σ_w part[w][b]: one 256-thread block per bin, fixed-order tree -- deterministic, no
+// atomics, no memset (the loop over hundreds of partials is spread over the block's lanes).
+constexpr int HR_THREADS = 256;
+__global__ __launch_bounds__(HR_THREADS) void k_hist_reduce(const uint32_t *__restrict__ part, int n_part, int n_pat,
+                                                            unsigned long long *__restrict__ hist) {
+    __shared__ unsigned long long s[HR_THREADS];
+    const int b = blockIdx.x;
+    unsigned long long acc = 0;
+    for (int w = threadIdx.x; w < n_part; w += HR_THREADS) acc += part[(int64_t)w * n_pat + b];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = HR_THREADS / 2; off > 0; off >>= 1) {
+        if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) hist[b] = s[0];
+}
+
+// Comparison-pattern arithmetic.  The pattern space description (mixed-radix strides, levels,
+// offsets into the flattened m / u) and -- for up to PA_INLINE_MU levels, every template setting --
+// the m / u tables themselves travel in the kernel arguments: no per-iteration uploads.
+constexpr int PA_MAXK = 64;
+constexpr int PA_INLINE_MU = 96;
+
 struct PatArgs {
     int K;
-    int64_t n_pat;
-    const int64_t *stride;
-    const int32_t *nlev;
-    const int32_t *moff;  // offset of column k in the flattened m/u arrays
-    const double *m, *u;
+    int n_pat;  // <= 2^31 (set_pattern_space)
+    int n_slots;
+    int tot;    // Σ L_k
     double lambda, one_minus;
+    const double *mu_dev;  // [m | u] (tot each) when tot > PA_INLINE_MU, else null
+    int32_t stride[PA_MAXK];
+    int16_t moff[PA_MAXK];
+    uint8_t nlev[PA_MAXK];
+    double mu[2 * PA_INLINE_MU];
 };
+static_assert(sizeof(PatArgs) <= 4096 && sizeof(PatArgs) % 4 == 0, "kernel argument size");
 
-// mp per pattern: (λ·m1·…·mK) / ((λ·m1·…·mK) + ((1-λ)·u1·…·uK)), left-associative products,
+__device__ inline int pa_gamma(const PatArgs &A, int p, int k) { return (p / A.stride[k]) % (A.nlev[k] + 1) - 1; }
+__device__ inline double pa_m(const PatArgs &A, int i) { return A.mu_dev ? A.mu_dev[i] : A.mu[i]; }
+__device__ inline double pa_u(const PatArgs &A, int i) { return A.mu_dev ? A.mu_dev[A.tot + i] : A.mu[A.tot + i]; }
+
+// mp of pattern p: (λ·m1·…·mK) / ((λ·m1·…·mK) + ((1-λ)·u1·…·uK)), left-associative products,
 // γ = -1 contributes 1.0; a zero denominator is NULL (NaN) as in Spark (expectation_step.py:167-185).
-__global__ void k_pattern_mp(PatArgs A, double *__restrict__ mpat, double *__restrict__ llpat) {
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= A.n_pat) return;
+// *ll = ln(λΠm + (1-λ)Πu), NULL for ln(<= 0) (expectation_step.py:224-256).
+__device__ inline double pattern_mp(const PatArgs &A, int p, double *ll) {
     double num = A.lambda;
     for (int k = 0; k < A.K; ++k) {
-        int g = (int)((p / A.stride[k]) % (A.nlev[k] + 1)) - 1;
-        num = num * (g < 0 ? 1.0 : A.m[A.moff[k] + g]);
+        const int g = pa_gamma(A, p, k);
+        num = num * (g < 0 ? 1.0 : pa_m(A, A.moff[k] + g));
     }
     double den = A.one_minus;
     for (int k = 0; k < A.K; ++k) {
-        int g = (int)((p / A.stride[k]) % (A.nlev[k] + 1)) - 1;
-        den = den * (g < 0 ? 1.0 : A.u[A.moff[k] + g]);
+        const int g = pa_gamma(A, p, k);
+        den = den * (g < 0 ? 1.0 : pa_u(A, A.moff[k] + g));
     }
-    double d = num + den;
-    mpat[p] = d == 0.0 ? NAN : num / d;
-    llpat[p] = d > 0.0 ? log(d) : NAN;  // ln(λΠm + (1-λ)Πu), NULL for ln(<= 0) (expectation_step.py:224-256)
+    const double d = num + den;
+    *ll = d > 0.0 ? log(d) : NAN;
+    return d == 0.0 ? NAN : num / d;
+}
+
+// The arguments are indexed per lane (column tables, m / u by level): stage them in LDS once per
+// block instead of letting dynamic indexing of the kernel-argument struct spill it to scratch.
+__device__ inline const PatArgs &stage_args(const PatArgs &A, PatArgs *sA) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&A);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(sA);
+    for (int i = threadIdx.x; i < (int)(sizeof(PatArgs) / 4); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    return *sA;
+}
+
+// One thread per pattern (the per-pattern chain of table lookups is latency-bound: spread it).
+__global__ void k_pattern_mp(PatArgs A0, double *__restrict__ mpat, double *__restrict__ llpat) {
+    __shared__ PatArgs sA;
+    const PatArgs &A = stage_args(A0, &sA);
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= A.n_pat) return;
+    double ll;
+    mpat[p] = pattern_mp(A, p, &ll);
+    if (llpat) llpat[p] = ll;
 }
 
 constexpr int S_THREADS = 256;
 constexpr int N_HEAD = 5;  // [Σmp, rows, non-null rows, Σ ln(...), non-null ln rows]
 
-// One block per statistics slot: slot 0 = totals, slot 1 + s = (column k, level v) in order.
-// Each thread sums a fixed strided subset of patterns; a fixed LDS tree finishes: deterministic.
-__global__ __launch_bounds__(S_THREADS) void k_stats(PatArgs A, const unsigned long long *__restrict__ hist,
-                                                     const double *__restrict__ mpat,
-                                                     const double *__restrict__ llpat,
-                                                     const int32_t *__restrict__ slot_k,
-                                                     const int32_t *__restrict__ slot_v, double *__restrict__ out) {
+// E-step per pattern + the M-step sums, one block per statistics slot: slot 0 = totals, slot 1 + s =
+// (column k, level v) in (k, v) order.  Each thread sums a fixed strided subset of patterns; a fixed
+// LDS tree finishes: deterministic, and the same for any sharding of pairs (integer histogram).
+__global__ __launch_bounds__(S_THREADS) void k_em_stats(PatArgs A0, const unsigned long long *__restrict__ hist,
+                                                        const double *__restrict__ mpat,
+                                                        const double *__restrict__ llpat, double *__restrict__ out) {
     __shared__ double s[6][S_THREADS];
+    __shared__ PatArgs sA;
+    const PatArgs &A = stage_args(A0, &sA);
     const int slot = blockIdx.x;
     int kk = -1, vv = 0;
     if (slot > 0) {
-        kk = slot_k[slot - 1];
-        vv = slot_v[slot - 1];
+        int r = slot - 1;
+        for (kk = 0; kk < A.K && r > A.nlev[kk]; ++kk) r -= A.nlev[kk] + 1;
+        vv = r - 1;
     }
     double rows = 0, nn = 0, sm = 0, s1 = 0, sll = 0, nll = 0;
-    for (int64_t p = threadIdx.x; p < A.n_pat; p += S_THREADS) {
-        unsigned long long c = hist[p];
+    for (int p = threadIdx.x; p < A.n_pat; p += S_THREADS) {
+        const unsigned long long c = hist[p];
         if (!c) continue;
-        if (kk >= 0) {
-            int g = (int)((p / A.stride[kk]) % (A.nlev[kk] + 1)) - 1;
-            if (g != vv) continue;
-        }
-        double cd = (double)c;
-        double mp = mpat[p];
+        if (kk >= 0 && pa_gamma(A, p, kk) != vv) continue;
+        const double cd = (double)c;
+        const double mp = mpat[p], ll = llpat[p];
         rows += cd;
         if (!isnan(mp)) {
             nn += cd;
             sm += cd * mp;
             s1 += cd * (1.0 - mp);
         }
-        double ll = llpat[p];
         if (!isnan(ll)) {
             nll += cd;
             sll += cd * ll;
@@ -297,44 +348,37 @@ __global__ void k_tf_apply(TfApply T, int64_t start, int64_t n, const int32_t *_
     out[i] = d == 0.0 ? NAN : a / d;
 }
 
-static int upload_tables(spk_ctx *ctx, const double *m, const double *u, DevBuf<int64_t> &d_stride,
-                         DevBuf<int32_t> &d_nlev, DevBuf<int32_t> &d_moff, PatArgs &A) {
-    int K = ctx->K;
-    std::vector<int32_t> moff(K);
-    int tot = 0;
-    for (int k = 0; k < K; ++k) {
-        moff[k] = tot;
-        tot += ctx->n_levels[k];
-    }
-    SPK_TRY(ctx->mu.alloc((size_t)2 * tot + 2));
-    SPK_TRY(d_stride.alloc((size_t)K));
-    SPK_TRY(d_nlev.alloc((size_t)K));
-    SPK_TRY(d_moff.alloc((size_t)K));
-    SPK_HIP(hipMemcpyAsync(ctx->mu.p, m, (size_t)tot * 8, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemcpyAsync(ctx->mu.p + tot, u, (size_t)tot * 8, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemcpyAsync(d_stride.p, ctx->stride.data(), (size_t)K * 8, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemcpyAsync(d_nlev.p, ctx->n_levels.data(), (size_t)K * 4, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemcpyAsync(d_moff.p, moff.data(), (size_t)K * 4, hipMemcpyHostToDevice, ctx->stream));
+// Pattern arguments for the current pattern space and m / u (one upload only for large tables).
+static int pat_args(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u, PatArgs &A) {
+    const int K = ctx->K;
+    SPK_REQUIRE(K <= PA_MAXK, SPK_E_LIMIT, "too many comparison columns");
     A.K = K;
-    A.n_pat = ctx->n_patterns;
-    A.stride = d_stride.p;
-    A.nlev = d_nlev.p;
-    A.moff = d_moff.p;
-    A.m = ctx->mu.p;
-    A.u = ctx->mu.p + tot;
-    return SPK_OK;
-}
-
-static int compute_mpat(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u, PatArgs &A,
-                        DevBuf<int64_t> &d_stride, DevBuf<int32_t> &d_nlev, DevBuf<int32_t> &d_moff) {
-    SPK_TRY(upload_tables(ctx, m, u, d_stride, d_nlev, d_moff, A));
+    A.n_pat = (int)ctx->n_patterns;
     A.lambda = lambda;
     A.one_minus = one_minus;
-    SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
-    SPK_TRY(ctx->llpat.alloc((size_t)ctx->n_patterns));
-    k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat.p, ctx->llpat.p);
-    SPK_HIP(hipGetLastError());
-    ctx->mpat_valid = true;
+    int tot = 0, slots = 0;
+    for (int k = 0; k < K; ++k) {
+        A.stride[k] = (int32_t)ctx->stride[k];
+        A.nlev[k] = (uint8_t)ctx->n_levels[k];
+        A.moff[k] = (int16_t)tot;
+        tot += ctx->n_levels[k];
+        slots += ctx->n_levels[k] + 1;
+    }
+    A.tot = tot;
+    A.n_slots = slots;
+    A.mu_dev = nullptr;
+    if (tot <= PA_INLINE_MU) {
+        for (int i = 0; i < tot; ++i) {
+            A.mu[i] = m[i];
+            A.mu[tot + i] = u[i];
+        }
+    } else {
+        SPK_TRY(ctx->mu.alloc((size_t)2 * tot));
+        SPK_HIP(hipMemcpyAsync(ctx->mu.p, m, (size_t)tot * 8, hipMemcpyHostToDevice, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(ctx->mu.p + tot, u, (size_t)tot * 8, hipMemcpyHostToDevice, ctx->stream));
+        SPK_HIP(hipStreamSynchronize(ctx->stream));  // pageable source: complete before returning
+        A.mu_dev = ctx->mu.p;
+    }
     return SPK_OK;
 }
 
@@ -358,31 +402,29 @@ extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
         SPK_TRY(ctx->hist.alloc((size_t)n_pat));
         h = reinterpret_cast<unsigned long long *>(ctx->hist.p);
     }
-    SPK_TRY(ctx->begin(K_EMHIST));
-    SPK_HIP(hipMemsetAsync(h, 0, (size_t)n_pat * 8, ctx->stream));
     const int64_t P = ctx->n_pairs;
     const int vec = 16 / ctx->code_bytes;
-    int64_t blocks = (P / vec + H_THREADS - 1) / H_THREADS;
-    if (blocks > 256 * 4) blocks = 256 * 4;
-    if (blocks < 1) blocks = 1;
-    const bool lds = n_pat <= H_LDS_BINS;
-    size_t shm = lds ? (size_t)n_pat * 4 : 0;
     int R = 64;
-    while (R >= 4 && (int64_t)n_pat * R * 4 > HL_LDS_BYTES) R >>= 1;
+    while (R >= 4 && n_pat * R * 4 > HL_LDS_BYTES) R >>= 1;
+    SPK_TRY(ctx->begin(K_EMHIST));
     if (R >= 4 && ctx->hist_lanes) {
-        int n_cu = 256;
-        (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+        // one 1024-thread workgroup per CU, per-workgroup partial counts, fixed-order reduction
+        int64_t g = ctx->n_cu;
         const int64_t vecs = P / vec;
-        int64_t g = (vecs + HL_THREADS - 1) / HL_THREADS;
-        if (g > 2 * (int64_t)n_cu) g = 2 * (int64_t)n_cu;
+        if (g > (vecs + HL_THREADS - 1) / HL_THREADS) g = (vecs + HL_THREADS - 1) / HL_THREADS;
         if (g < 1) g = 1;
+        while (P / g >= ((int64_t)1 << 31)) g *= 2;  // uint32 partial counts
+        SPK_TRY(ctx->hist_part.alloc((size_t)(g * n_pat)));
         const size_t sh = (size_t)n_pat * R * 4;
         const auto *c16 = reinterpret_cast<const uint16_t *>(ctx->codes.p);
         const auto *c32 = reinterpret_cast<const uint32_t *>(ctx->codes.p);
-#define SPK_HL(RR)                                                                                              \
-    case RR:                                                                                                     \
-        if (ctx->code_bytes == 2) k_hist_lanes<uint16_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c16, P, (int)n_pat, h); \
-        else k_hist_lanes<uint32_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c32, P, (int)n_pat, h);   \
+        uint32_t *part = ctx->hist_part.p;
+#define SPK_HL(RR)                                                                                           \
+    case RR:                                                                                                  \
+        if (ctx->code_bytes == 2)                                                                             \
+            k_hist_lanes<uint16_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c16, P, (int)n_pat, part); \
+        else                                                                                                  \
+            k_hist_lanes<uint32_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c32, P, (int)n_pat, part); \
         break;
         switch (R) {
             SPK_HL(64)
@@ -392,16 +434,26 @@ extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
             SPK_HL(4)
         }
 #undef SPK_HL
-    } else if (ctx->code_bytes == 2) {
-        if (lds) k_hist<uint16_t, true><<<(unsigned)blocks, H_THREADS, shm, ctx->stream>>>(
-            reinterpret_cast<const uint16_t *>(ctx->codes.p), P, (int)n_pat, h);
-        else k_hist<uint16_t, false><<<(unsigned)blocks, H_THREADS, 0, ctx->stream>>>(
-            reinterpret_cast<const uint16_t *>(ctx->codes.p), P, (int)n_pat, h);
+        SPK_HIP(hipGetLastError());
+        k_hist_reduce<<<(unsigned)n_pat, HR_THREADS, 0, ctx->stream>>>(part, (int)g, (int)n_pat, h);
     } else {
-        if (lds) k_hist<uint32_t, true><<<(unsigned)blocks, H_THREADS, shm, ctx->stream>>>(
-            reinterpret_cast<const uint32_t *>(ctx->codes.p), P, (int)n_pat, h);
-        else k_hist<uint32_t, false><<<(unsigned)blocks, H_THREADS, 0, ctx->stream>>>(
-            reinterpret_cast<const uint32_t *>(ctx->codes.p), P, (int)n_pat, h);
+        SPK_HIP(hipMemsetAsync(h, 0, (size_t)n_pat * 8, ctx->stream));
+        int64_t blocks = (P / vec + H_THREADS - 1) / H_THREADS;
+        if (blocks > 4 * (int64_t)ctx->n_cu) blocks = 4 * (int64_t)ctx->n_cu;
+        if (blocks < 1) blocks = 1;
+        const bool lds = n_pat <= H_LDS_BINS;
+        const size_t shm = lds ? (size_t)n_pat * 4 : 0;
+        if (ctx->code_bytes == 2) {
+            if (lds) k_hist<uint16_t, true><<<(unsigned)blocks, H_THREADS, shm, ctx->stream>>>(
+                reinterpret_cast<const uint16_t *>(ctx->codes.p), P, (int)n_pat, h);
+            else k_hist<uint16_t, false><<<(unsigned)blocks, H_THREADS, 0, ctx->stream>>>(
+                reinterpret_cast<const uint16_t *>(ctx->codes.p), P, (int)n_pat, h);
+        } else {
+            if (lds) k_hist<uint32_t, true><<<(unsigned)blocks, H_THREADS, shm, ctx->stream>>>(
+                reinterpret_cast<const uint32_t *>(ctx->codes.p), P, (int)n_pat, h);
+            else k_hist<uint32_t, false><<<(unsigned)blocks, H_THREADS, 0, ctx->stream>>>(
+                reinterpret_cast<const uint32_t *>(ctx->codes.p), P, (int)n_pat, h);
+        }
     }
     SPK_HIP(hipGetLastError());
     SPK_TRY(ctx->end(K_EMHIST));
@@ -414,33 +466,24 @@ extern "C" int spk_em_finalize(spk_ctx *ctx, const uint64_t *d_hist, double lamb
     SPK_REQUIRE(ctx && m && u && out_stats, SPK_E_INVALID, "spk_em_finalize: null arg");
     SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_finalize: no gammas");
     SPK_HIP(hipSetDevice(ctx->device));
-    int n_slots = 0;
-    std::vector<int32_t> sk, sv;
-    for (int k = 0; k < ctx->K; ++k)
-        for (int v = -1; v < ctx->n_levels[k]; ++v) {
-            sk.push_back(k);
-            sv.push_back(v);
-            ++n_slots;
-        }
-    SPK_REQUIRE(n_stats == N_HEAD + 4 * n_slots, SPK_E_INVALID, "spk_em_finalize: n_stats mismatch");
+    PatArgs A;
+    SPK_TRY(pat_args(ctx, lambda, one_minus, m, u, A));
+    SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_finalize: n_stats mismatch");
     const unsigned long long *h = reinterpret_cast<const unsigned long long *>(d_hist ? d_hist : ctx->hist.p);
     SPK_REQUIRE(h, SPK_E_STATE, "spk_em_finalize: no histogram");
-    SPK_TRY(ctx->begin(K_EMFIN));
-    PatArgs A{};
-    DevBuf<int64_t> d_stride;
-    DevBuf<int32_t> d_nlev, d_moff, d_sk, d_sv;
-    SPK_TRY(compute_mpat(ctx, lambda, one_minus, m, u, A, d_stride, d_nlev, d_moff));
-    SPK_TRY(d_sk.alloc((size_t)n_slots));
-    SPK_TRY(d_sv.alloc((size_t)n_slots));
     SPK_TRY(ctx->stats.alloc((size_t)n_stats));
-    SPK_HIP(hipMemcpyAsync(d_sk.p, sk.data(), (size_t)n_slots * 4, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemcpyAsync(d_sv.p, sv.data(), (size_t)n_slots * 4, hipMemcpyHostToDevice, ctx->stream));
-    k_stats<<<(unsigned)(n_slots + 1), S_THREADS, 0, ctx->stream>>>(A, h, ctx->mpat.p, ctx->llpat.p, d_sk.p, d_sv.p,
-                                                                     ctx->stats.p);
+    SPK_TRY(ctx->pinned_stats(n_stats));
+    SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
+    SPK_TRY(ctx->llpat.alloc((size_t)ctx->n_patterns));
+    SPK_TRY(ctx->begin(K_EMFIN));
+    k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat.p, ctx->llpat.p);
+    k_em_stats<<<(unsigned)(A.n_slots + 1), S_THREADS, 0, ctx->stream>>>(A, h, ctx->mpat.p, ctx->llpat.p,
+                                                                          ctx->stats.p);
     SPK_HIP(hipGetLastError());
     SPK_TRY(ctx->end(K_EMFIN));
-    SPK_HIP(hipMemcpyAsync(out_stats, ctx->stats.p, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(ctx->h_stats, ctx->stats.p, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(out_stats, ctx->h_stats, (size_t)n_stats * 8);
     return SPK_OK;
 }
 
@@ -450,12 +493,14 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
     SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_score: no gammas");
     SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_score: range");
     SPK_HIP(hipSetDevice(ctx->device));
-    PatArgs A{};
-    DevBuf<int64_t> d_stride;
-    DevBuf<int32_t> d_nlev, d_moff;
-    SPK_TRY(compute_mpat(ctx, lambda, one_minus, m, u, A, d_stride, d_nlev, d_moff));
+    PatArgs A;
+    SPK_TRY(pat_args(ctx, lambda, one_minus, m, u, A));
+    SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
     SPK_TRY(ctx->mp.alloc((size_t)ctx->n_pairs + 1));
     SPK_TRY(ctx->begin(K_SCORE));
+    k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat.p, nullptr);
+    SPK_HIP(hipGetLastError());
+    ctx->mpat_valid = true;
     if (count) {
         unsigned g = (unsigned)((count + 255) / 256);
         if (ctx->code_bytes == 2)

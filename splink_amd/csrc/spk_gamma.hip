@@ -19,10 +19,12 @@
 //      32-bit masks when the (trimmed) pattern fits.  Strings beyond 64 units, and surrogate
 //      strings under Levenshtein, go to
 //   3. the global-memory pass (two-row DP / flag words in scratch, any length up to SLOW_LIMIT).
-// Passes 2 and 3 add their level into a 32-bit code per pair; a pack pass writes the final
-// code = Σ_k (γ_k + 1) · Π_{j<k}(L_j + 1) as uint16 when the pattern space fits, else uint32.
+// The filter pass writes each pair's code = Σ_k (γ_k + 1) · Π_{j<k}(L_j + 1) over the columns it
+// decided (uint16 when the pattern space fits, else uint32); passes 2 and 3 add the rest in place.
 // Bounds are exact decisions (never approximations), so the result is the exact evaluation.
 #include <algorithm>
+#include <cstring>
+#include <type_traits>
 #include <cmath>
 
 #include "spk_strsim.h"
@@ -70,7 +72,8 @@ struct GammaArgs {
     const int64_t *lit_off;
     const int32_t *lit_len, *lit_cplen;
     const int64_t *stride;
-    uint32_t *code32;
+    void *codes;                  // packed code per pair: uint16 (code16) or uint32
+    int code16;
     int32_t *work;                // [K][P] pair indices per column needing the exact pass, by region
     unsigned int *region_count;   // [K][n_regions] list length of each region
     int64_t region_len;           // pair ordinals per region (one filter workgroup each)
@@ -84,6 +87,23 @@ struct GammaArgs {
     const int32_t *complex_k;  // ... and the columns the interpreter evaluates
     int n_complex;
 };
+
+// Codes are written in place: the filter pass sets each pair's code, the exact / slow passes of
+// column k add to it.  A pair occurs at most once in column k's lists and the passes are ordered
+// launches on one stream, so the read-modify-write needs no atomic -- and a 2-byte store leaves
+// the neighbouring pair's code alone.
+__device__ inline void code_set(const GammaArgs &A, int64_t p, uint32_t v) {
+    if (A.code16) static_cast<uint16_t *>(A.codes)[p] = (uint16_t)v;
+    else static_cast<uint32_t *>(A.codes)[p] = v;
+}
+__device__ inline void code_add(const GammaArgs &A, int64_t p, uint32_t d) {
+    if (A.code16) {
+        uint16_t *c = static_cast<uint16_t *>(A.codes) + p;
+        *c = (uint16_t)(*c + d);
+    } else {
+        static_cast<uint32_t *>(A.codes)[p] += d;
+    }
+}
 
 enum : int { KF = 0, KT = 1, KN = 2, KU = 3 };  // false, true, NULL, undecided (filter pass)
 
@@ -519,7 +539,7 @@ __device__ int simple_num(const SimpleCol &sc, bool va, double a, bool vb, doubl
     return sc.else_level;
 }
 
-// Filter pass, simple columns: initialises code32[p] with their levels.  The column descriptors
+// Filter pass, simple columns: initialises code[p] with their levels.  The column descriptors
 // and the table pointers are staged in LDS once per workgroup: read from global memory inside the
 // divergent per-pair code they would be per-lane vector loads on the critical path of every pair.
 struct SimpleSrc {
@@ -594,14 +614,14 @@ __global__ __launch_bounds__(F_THREADS) void k_gamma_simple(GammaArgs A) {
                 }
             }
         }
-        if (active) A.code32[p] = acc;
+        if (active) code_set(A, p, acc);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
         A.region_count[(int64_t)s_sc[i].k * A.n_regions + blockIdx.x] = s_cnt[i];
 }
 
-// Filter pass, every other column through the interpreter: adds to code32[p].
+// Filter pass, every other column through the interpreter: adds to code[p].
 __global__ __launch_bounds__(F_THREADS) void k_gamma_filter(GammaArgs A) {
     __shared__ unsigned int s_cnt[MAX_SIMPLE];
     for (int i = threadIdx.x; i < A.n_complex; i += F_THREADS) s_cnt[i] = 0;
@@ -628,7 +648,7 @@ __global__ __launch_bounds__(F_THREADS) void k_gamma_filter(GammaArgs A) {
             }
             wave_append(region_list(A, k, R), &s_cnt[i], undecided, (int32_t)p);
         }
-        if (active) A.code32[p] += acc;
+        if (active) code_add(A, p, acc);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < A.n_complex; i += F_THREADS)
@@ -649,10 +669,124 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_exact(GammaArgs A, int k) {
             p = items[i];
             int level = 0;
             const int st = eval_column<M_EXACT>(A, k, A.pl[p], A.pr[p], slot_a, slot_b, level);
-            if (st == ST_DONE) atomicAdd(&A.code32[p], (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+            if (st == ST_DONE) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
             else to_slow = true;
         }
         wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
+    }
+}
+
+// Exact pass over a simple string column (the template shapes): the tests run straight on the two
+// rows' records, bit-planes and units -- no interpreter, no re-evaluation of the NULL / equality
+// branches the filter pass already settled, each similarity computed at most once.  Levenshtein
+// tests of the `<=` / `<` kind need the distance only up to the largest value any of them accepts
+// (lev_cut), so the bit-parallel scan stops as soon as the distance provably exceeds it.
+__device__ inline int simple_lev_cut(const SimpleCol &sc, int ncp_a, int ncp_b) {
+    const double den = (double)(ncp_a + ncp_b) / 2.0;
+    int cut = 0;
+    for (int i = 0; i < sc.n_tests; ++i) {
+        if (sc.op[i] != SPK_OP_LEV && sc.op[i] != SPK_OP_LEVRATIO) continue;
+        if (sc.cmp[i] != SPK_CMP_LE && sc.cmp[i] != SPK_CMP_LT) return 1 << 30;
+        // every v > bound fails `v cmp t` (resp. `v / den cmp t`): one unit of margin over t * den
+        const double lim = sc.op[i] == SPK_OP_LEV ? sc.t[i] : sc.t[i] * den;
+        if (!(lim < 1e9)) return 1 << 30;
+        const int bound = lim < 0.0 ? 0 : (int)floor(lim) + 1;
+        cut = bound > cut ? bound : cut;
+    }
+    return cut;
+}
+
+__device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x,
+                            int32_t y, int &level) {
+    const RecMeta ma = c0.meta[x], mb = c1.meta[y];
+    if (ma.len16 < 0 || mb.len16 < 0) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    const StrView a = row_view(c0, ma, x, sc.col), b = row_view(c1, mb, y, sc.col);
+    int eq = meta_equal(ma, mb);
+    if (eq < 0) eq = units_equal(a, b) ? 1 : 0;
+    double jw = -1.0;
+    int lev = -1;
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int op = sc.op[i], cmp = sc.cmp[i];
+        const double t = sc.t[i];
+        int r;
+        if (op == SPK_OP_STR_CMP) {
+            r = ((eq == 1) == (cmp == SPK_CMP_EQ)) ? KT : KF;
+        } else if (op == SPK_OP_JW) {
+            if (jw < 0.0) {
+                if (eq == 1) jw = a.n > 0 ? 1.0 : 0.0;
+                else if (a.n > 64 || b.n > 64) return ST_NEEDS_SLOW;
+                else jw = jw_exact(a, b);
+            }
+            r = cmpd(jw, t, cmp);
+        } else {  // SPK_OP_LEV / SPK_OP_LEVRATIO
+            const double den = (double)(a.ncp + b.ncp) / 2.0;
+            if (op == SPK_OP_LEVRATIO && den == 0.0) {
+                r = KN;
+            } else {
+                if (lev < 0) {
+                    if (eq == 1) lev = 0;
+                    else if (a.n > 64 || b.n > 64 || a.ncp != a.n || b.ncp != b.n) return ST_NEEDS_SLOW;
+                    else lev = lev_exact(a, b, simple_lev_cut(sc, a.ncp, b.ncp));
+                }
+                r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
+            }
+        }
+        if (r == KT) {
+            level = sc.level[i];
+            return ST_DONE;
+        }
+    }
+    level = sc.else_level;
+    return ST_DONE;
+}
+
+__global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, int si) {
+    __shared__ SimpleCol s_sc;
+    __shared__ ColDesc s_c0, s_c1;
+    if (threadIdx.x == 0) {
+        s_sc = A.simple[si];
+        s_c0 = A.cols0[s_sc.col];
+        s_c1 = A.cols1[s_sc.col];
+    }
+    __syncthreads();
+    const SimpleCol &sc = s_sc;
+    const int k = sc.k;
+    const Region R = my_region(A);
+    const int32_t *items = region_list(A, k, R);
+    const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
+    // software pipeline: the next item's pair rows are in flight while this one is evaluated
+    int64_t i = threadIdx.x;
+    int32_t p = 0, x = 0, y = 0;
+    if (i < n) {
+        p = items[i];
+        x = A.pl[p];
+        y = A.pr[p];
+    }
+    for (int64_t base = 0; base < n; base += X_THREADS) {  // block-uniform trip count
+        const bool have = i < n;
+        const int64_t i2 = i + X_THREADS;
+        int32_t p2 = 0, x2 = 0, y2 = 0;
+        if (i2 < n) {
+            p2 = items[i2];
+            x2 = A.pl[p2];
+            y2 = A.pr[p2];
+        }
+        bool to_slow = false;
+        if (have) {
+            int level = 0;
+            if (simple_exact(A, sc, s_c0, s_c1, x, y, level) == ST_DONE)
+                code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
+            else
+                to_slow = true;
+        }
+        wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
+        i = i2;
+        p = p2;
+        x = x2;
+        y = y2;
     }
 }
 
@@ -662,12 +796,7 @@ __global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k, const int
     const int32_t p = items[i];
     int level = 0;
     eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level);
-    atomicAdd(&A.code32[p], (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
-}
-
-__global__ void k_pack16(int64_t n, const uint32_t *__restrict__ in, uint16_t *__restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = (uint16_t)in[i];
+    code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
 }
 
 __global__ void k_codes_from_gammas(int64_t n, int K, const int8_t *__restrict__ g, const int64_t *__restrict__ stride,
@@ -830,6 +959,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         }
         if (in.op == SPK_OP_CONST) SPK_REQUIRE(in.i0 >= 0 && in.i0 <= 2, SPK_E_INVALID, "spk_gammas: constant");
     }
+    ctx->codes_valid = false;  // codes are rewritten in place below
     SPK_TRY(set_pattern_space(ctx, n_cols, nlev.data()));
 
     // ---- literals -> UTF-16
@@ -851,49 +981,40 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
 
     SPK_TRY(ensure_desc(ctx, t0));
     SPK_TRY(ensure_desc(ctx, t1));
-    DevBuf<spk_column_program> d_prog;
-    DevBuf<int32_t> d_wf, d_wn, d_wl;
-    DevBuf<spk_instr> d_instr;
-    DevBuf<spk_operand> d_ops;
-    DevBuf<uint16_t> d_lu;
-    DevBuf<int64_t> d_loff, d_stride, d_slow_off;
-    DevBuf<int32_t> d_llen, d_lcp;
-    DevBuf<int> d_err;
-    auto up = [&](auto &buf, const auto *src, size_t n) -> int {
-        SPK_TRY(buf.alloc(n ? n : 1));
-        if (n) SPK_HIP(hipMemcpyAsync(buf.p, src, n * sizeof(*src), hipMemcpyHostToDevice, ctx->stream));
-        return SPK_OK;
-    };
     const int K = n_cols;
-    SPK_TRY(up(d_prog, cols, (size_t)K));
-    SPK_TRY(up(d_wf, when_first_instr, (size_t)n_when));
-    SPK_TRY(up(d_wn, when_n_instr, (size_t)n_when));
-    SPK_TRY(up(d_wl, when_level, (size_t)n_when));
-    SPK_TRY(up(d_instr, instr, (size_t)n_instr));
-    SPK_TRY(up(d_ops, operands, (size_t)n_operands));
-    SPK_TRY(up(d_lu, lu.data(), lu.size()));
-    SPK_TRY(up(d_loff, loff.data(), loff.size()));
-    SPK_TRY(up(d_llen, llen.data(), llen.size()));
-    SPK_TRY(up(d_lcp, lcp.data(), lcp.size()));
-    SPK_TRY(up(d_stride, ctx->stride.data(), ctx->stride.size()));
     std::vector<SimpleCol> simple;
     std::vector<int32_t> complex_k;
     for (int k = 0; k < K; ++k) {
-        SimpleCol s;
+        SimpleCol sc;
         if (ctx->simple_columns &&
             classify_simple(k, cols[k], when_first_instr, when_n_instr, when_level, instr, operands, t0, t1,
-                            ctx->stride, &s))
-            simple.push_back(s);
+                            ctx->stride, &sc))
+            simple.push_back(sc);
         else
             complex_k.push_back(k);
     }
-    DevBuf<SimpleCol> d_simple;
-    DevBuf<int32_t> d_complex;
-    SPK_TRY(up(d_simple, simple.data(), simple.size()));
-    SPK_TRY(up(d_complex, complex_k.data(), complex_k.size()));
-    SPK_TRY(d_err.alloc(1));
+    // Every program array goes up in one packed copy into a buffer the context keeps.
+    std::vector<uint8_t> blob;
+    auto put = [&](const auto *src, size_t n) -> size_t {
+        const size_t off = (blob.size() + 15) & ~(size_t)15;
+        blob.resize(off + (n ? n : 1) * sizeof(*src), 0);
+        if (n) std::memcpy(blob.data() + off, src, n * sizeof(*src));
+        return off;
+    };
+    const size_t o_prog = put(cols, (size_t)K), o_wf = put(when_first_instr, (size_t)n_when),
+                 o_wn = put(when_n_instr, (size_t)n_when), o_wl = put(when_level, (size_t)n_when),
+                 o_instr = put(instr, (size_t)n_instr), o_ops = put(operands, (size_t)n_operands),
+                 o_lu = put(lu.data(), lu.size()), o_loff = put(loff.data(), loff.size()),
+                 o_llen = put(llen.data(), llen.size()), o_lcp = put(lcp.data(), lcp.size()),
+                 o_stride = put(ctx->stride.data(), ctx->stride.size()), o_simple = put(simple.data(), simple.size()),
+                 o_complex = put(complex_k.data(), complex_k.size());
+    const int32_t zero = 0;
+    const size_t o_err = put(&zero, 1);
+    SPK_TRY(ctx->prog_blob.alloc(blob.size()));
+    SPK_HIP(hipMemcpyAsync(ctx->prog_blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, ctx->stream));
+    uint8_t *base = ctx->prog_blob.p;
+    auto at = [&](auto *&dst, size_t off) { dst = reinterpret_cast<std::remove_reference_t<decltype(dst)>>(base + off); };
     const int64_t P = ctx->n_pairs;
-    SPK_TRY(ctx->code32.alloc((size_t)P + 1));
     SPK_TRY(ctx->work.alloc((size_t)K * (size_t)P + 1));
     SPK_TRY(ctx->work_count.alloc((size_t)K));
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
@@ -903,7 +1024,6 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions));
     SPK_HIP(hipMemsetAsync(ctx->region_count.p, 0, sizeof(unsigned int) * K * n_regions, ctx->stream));
     SPK_HIP(hipMemsetAsync(ctx->work_count.p, 0, sizeof(unsigned int) * K, ctx->stream));
-    SPK_HIP(hipMemsetAsync(d_err.p, 0, sizeof(int), ctx->stream));
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -912,27 +1032,28 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.pr = ctx->pr.p;
     A.P = P;
     A.K = K;
-    A.progs = d_prog.p;
-    A.when_first = d_wf.p;
-    A.when_n = d_wn.p;
-    A.when_level = d_wl.p;
-    A.instr = d_instr.p;
-    A.ops = d_ops.p;
-    A.lit_units = d_lu.p;
-    A.lit_off = d_loff.p;
-    A.lit_len = d_llen.p;
-    A.lit_cplen = d_lcp.p;
-    A.stride = d_stride.p;
-    A.code32 = ctx->code32.p;
+    at(A.progs, o_prog);
+    at(A.when_first, o_wf);
+    at(A.when_n, o_wn);
+    at(A.when_level, o_wl);
+    at(A.instr, o_instr);
+    at(A.ops, o_ops);
+    at(A.lit_units, o_lu);
+    at(A.lit_off, o_loff);
+    at(A.lit_len, o_llen);
+    at(A.lit_cplen, o_lcp);
+    at(A.stride, o_stride);
+    at(A.simple, o_simple);
+    at(A.complex_k, o_complex);
+    at(A.err, o_err);
+    A.codes = ctx->codes.p;
+    A.code16 = ctx->code_bytes == 2;
     A.work = ctx->work.p;
     A.region_count = ctx->region_count.p;
     A.region_len = region_len;
     A.n_regions = n_regions;
     A.slow_count = ctx->work_count.p;
-    A.err = d_err.p;
-    A.simple = d_simple.p;
     A.n_simple = (int)simple.size();
-    A.complex_k = d_complex.p;
     A.n_complex = (int)complex_k.size();
     ctx->last_simple = (int)simple.size();
 
@@ -955,12 +1076,18 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     std::vector<int64_t> slow_off(K + 1, 0);
     for (int k = 0; k < K; ++k) slow_off[k + 1] = slow_off[k] + counts[k];
     SPK_TRY(ctx->slow.alloc((size_t)slow_off[K] + 1));
-    SPK_TRY(up(d_slow_off, slow_off.data(), slow_off.size()));
+    SPK_TRY(ctx->slow_off.alloc(slow_off.size()));
+    SPK_HIP(hipMemcpyAsync(ctx->slow_off.p, slow_off.data(), slow_off.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     A.slow = ctx->slow.p;
-    A.slow_off = d_slow_off.p;
+    A.slow_off = ctx->slow_off.p;
+    std::vector<int> simple_of(K, -1);
+    for (size_t i = 0; i < simple.size(); ++i) simple_of[simple[i].k] = (int)i;
     for (int k = 0; k < K; ++k) {
         if (!counts[k]) continue;
-        k_gamma_exact<<<(unsigned)n_regions, X_THREADS, 0, ctx->stream>>>(A, k);
+        if (simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR)
+            k_gamma_exact_simple<<<(unsigned)n_regions, X_THREADS, 0, ctx->stream>>>(A, simple_of[k]);
+        else
+            k_gamma_exact<<<(unsigned)n_regions, X_THREADS, 0, ctx->stream>>>(A, k);
         SPK_HIP(hipGetLastError());
     }
     std::vector<unsigned int> slow_counts((size_t)K, 0);
@@ -976,17 +1103,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         k_gamma_slow<<<(unsigned)((ns + 63) / 64), 64, 0, ctx->stream>>>(A, k, ctx->slow.p + slow_off[k], ns);
         SPK_HIP(hipGetLastError());
     }
-    if (P > 0) {
-        if (ctx->code_bytes == 2)
-            k_pack16<<<(unsigned)((P + 255) / 256), 256, 0, ctx->stream>>>(P, ctx->code32.p,
-                                                                         reinterpret_cast<uint16_t *>(ctx->codes.p));
-        else
-            SPK_HIP(hipMemcpyAsync(ctx->codes.p, ctx->code32.p, (size_t)P * 4, hipMemcpyDeviceToDevice, ctx->stream));
-        SPK_HIP(hipGetLastError());
-    }
     SPK_TRY(ctx->end(K_GAMMA));
     int err = 0;
-    SPK_HIP(hipMemcpyAsync(&err, d_err.p, sizeof(err), hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipMemcpyAsync(&err, A.err, sizeof(err), hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     SPK_REQUIRE(!(err & 1), SPK_E_LIMIT, "spk_gammas: a compared string exceeds 1024 UTF-16 units");
     SPK_REQUIRE(!(err & 2), SPK_E_INVALID, "spk_gammas: unknown instruction");
@@ -1127,7 +1246,6 @@ static int run_udf(spk_ctx *ctx, int op, int64_t n, const int64_t *l_off, const 
     SPK_HIP(hipMemcpyAsync(d_u.p, u.data(), u.size() * 2, hipMemcpyHostToDevice, ctx->stream));
     SPK_HIP(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     if (!cp.empty()) SPK_HIP(hipMemcpyAsync(d_cp.p, cp.data(), cp.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemsetAsync(d_err.p, 0, sizeof(int), ctx->stream));
     if (n) {
         UdfArgs U{n, d_u.p, d_off.p, d_cp.p, op, d_out.p, d_err.p};
         k_udf<<<(unsigned)((n + U_THREADS - 1) / U_THREADS), U_THREADS, 0, ctx->stream>>>(U);

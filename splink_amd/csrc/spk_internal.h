@@ -177,14 +177,32 @@ struct spk_ctx {
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)
-    spk::DevBuf<uint32_t> code32;
     spk::DevBuf<int32_t> work, slow;
+    spk::DevBuf<int64_t> slow_off;    // [K+1] slow-pass list offsets
+    spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)
     spk::DevBuf<unsigned int> work_count;    // [K] slow-pass list lengths
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
     // EM state
     spk::DevBuf<uint64_t> hist;
     spk::DevBuf<double> mpat, llpat, stats, mu;
+    spk::DevBuf<uint32_t> hist_part;  // per-workgroup pattern counts (k_hist_lanes)
+    double *h_stats = nullptr;        // pinned host copy of the statistics vector
+    size_t h_stats_n = 0;
+    int n_cu = 256;                   // compute units of the device (grid sizing)
+    int pinned_stats(size_t n) {
+        if (n <= h_stats_n) return SPK_OK;
+        if (h_stats) (void)hipHostFree(h_stats);
+        h_stats = nullptr;
+        h_stats_n = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&h_stats), n * 8, hipHostMallocDefault) != hipSuccess) {
+            h_stats = nullptr;
+            spk::set_error("hipHostMalloc failed");
+            return SPK_E_OOM;
+        }
+        h_stats_n = n;
+        return SPK_OK;
+    }
     spk::DevBuf<double> mp;  // per-pair scores (final E-step)
     bool mpat_valid = false;
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits

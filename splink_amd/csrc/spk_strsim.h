@@ -377,8 +377,11 @@ __device__ double jw_planes(const uint64_t *mx_planes, const uint16_t *mxp, int 
 }
 
 // Myers 1999 with the pattern's match masks from its bit-planes, shifted by `shift` units.
+// `cut`: the caller only distinguishes distances up to cut; once the score minus the text still to
+// come exceeds it (each remaining text unit lowers the final distance by at most one), the scan
+// stops and returns cut + 1.
 template <typename W>
-__device__ int lev_planes(const uint64_t *planes, int shift, int m, const uint16_t *txt, int n) {
+__device__ int lev_planes(const uint64_t *planes, int shift, int m, const uint16_t *txt, int n, int cut) {
     W pl[N_PLANES];
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)(planes[b] >> shift);
@@ -393,6 +396,7 @@ __device__ int lev_planes(const uint64_t *planes, int shift, int m, const uint16
         W hn = d0 & vp;
         dist += (hp & hib) ? 1 : 0;
         dist -= (hn & hib) ? 1 : 0;
+        if (dist - (n - 1 - j) > cut) return cut + 1;
         hp = (hp << 1) | (W)1;
         hn = hn << 1;
         vp = hn | ~(d0 | hp);
@@ -415,7 +419,7 @@ __device__ inline double jw_exact(const StrView &a, const StrView &b) {
 
 // Exact code-point Levenshtein of unequal BMP strings of <= 64 units, without LDS: common prefix
 // and suffix are stripped (exact for unit-cost edit distance), then bit-parallel on the rest.
-__device__ inline int lev_exact(const StrView &a, const StrView &b) {
+__device__ inline int lev_exact(const StrView &a, const StrView &b, int cut = 1 << 30) {
     const int mn = a.n < b.n ? a.n : b.n;
     const int pre = common_prefix(a.p, b.p, mn);
     int suf = 0;
@@ -429,8 +433,8 @@ __device__ inline int lev_exact(const StrView &a, const StrView &b) {
     const StrView &txt = a_pat ? b : a;
     const int m = a_pat ? la : lb, n = a_pat ? lb : la;
     if (pat.planes) {
-        if (m <= 32) return lev_planes<uint32_t>(pat.planes, pre, m, txt.p + pre, n);
-        return lev_planes<uint64_t>(pat.planes, pre, m, txt.p + pre, n);
+        if (m <= 32) return lev_planes<uint32_t>(pat.planes, pre, m, txt.p + pre, n, cut);
+        return lev_planes<uint64_t>(pat.planes, pre, m, txt.p + pre, n, cut);
     }
     return lev_myers(GlbAcc{a.p + pre}, la, GlbAcc{b.p + pre}, lb);
 }

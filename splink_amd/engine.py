@@ -11,6 +11,7 @@ histogram (an exact integer sum) with RCCL, so every rank computes identical par
 """
 from __future__ import annotations
 
+import json
 import os
 from typing import List, Optional
 
@@ -183,6 +184,7 @@ class Job:
             self.tables[side] = self.tables[side].take(perm).reset_index(drop=True)
             self.ctx.table_create(side, len(self.tables[side]), 8)
         self._col_index = {}
+        self._prog_cache = {}  # column uploads (and their indices) start again
         self._set_rank()
         p0 = perms[0]
         pr = perms.get(1, p0)
@@ -228,12 +230,22 @@ class Job:
         return self._pairs_host
 
     # ---- comparison vectors -----------------------------------------------------------------------
+    def _compiled(self, settings):
+        """The comparison program and its native buffers, compiled once per distinct comparison_columns."""
+        key = json.dumps(settings["comparison_columns"], sort_keys=True, default=str)
+        cache = self.__dict__.setdefault("_prog_cache", {})
+        if key not in cache:
+            prog = compile_comparisons(settings, self.schema)
+            index = {k: self.column_index(*k) for k in prog.columns}
+            lit_off, lit_bytes = prog.literal_buffers()
+            args = (prog.programs, prog.when_first, prog.when_n, prog.when_level, prog.instrs,
+                    prog.native_operands(index), lit_off, lit_bytes)
+            cache[key] = (prog, args)
+        return cache[key]
+
     def gammas(self, settings, token=None) -> CompiledComparisons:
-        prog = compile_comparisons(settings, self.schema)
-        index = {key: self.column_index(*key) for key in prog.columns}
-        lit_off, lit_bytes = prog.literal_buffers()
-        self.ctx.gammas(prog.programs, prog.when_first, prog.when_n, prog.when_level, prog.instrs,
-                        prog.native_operands(index), lit_off, lit_bytes)
+        prog, args = self._compiled(settings)
+        self.ctx.gammas(*args)
         self.codes_token = token if token is not None else object()
         self.code_meta = (prog.gamma_names, prog.n_levels)
         return prog
