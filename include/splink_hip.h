@@ -162,9 +162,12 @@ int spk_gammas_deferred(spk_ctx *ctx, int64_t *out);
  * and evaluated with the exact similarity (out[n], n >= number of columns). */
 int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
 /* Columns in the shape of the case_statements.py templates (NULL branch, then single-leaf tests
- * on the same two plain operands) are filtered straight from the row records; every other column
- * by the general interpreter.  on = 0 sends every column through the interpreter (same results;
- * for testing).  spk_gammas_simple_count: how many columns the last spk_gammas took as simple. */
+ * on the same two plain operands) are filtered from a packed per-row image of their fields; every
+ * other column by the general interpreter.  on = 1 (default): template columns through the
+ * column-batched filter; on = 2: through the register-resident row filter when the image row is
+ * short (<= 128 bytes); on = 0: every column through the interpreter.  All
+ * modes give identical results (for testing and measurement).  spk_gammas_simple_count: how many
+ * columns the last spk_gammas took as template columns. */
 int spk_gammas_set_simple(spk_ctx *ctx, int on);
 int spk_gammas_simple_count(spk_ctx *ctx, int *out);
 

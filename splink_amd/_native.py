@@ -233,8 +233,9 @@ class Context:
         check(self._lib.spk_gammas_exact_counts(self._h, _ptr(out), ctypes.c_int(len(out))), "spk_gammas_exact_counts")
         return out[:K].tolist()
 
-    def gammas_set_simple(self, on: bool):
-        check(self._lib.spk_gammas_set_simple(self._h, ctypes.c_int(1 if on else 0)), "spk_gammas_set_simple")
+    def gammas_set_simple(self, mode):
+        """1 / True: template-column filters (column-batched), 2: register-row filter when short, 0: interpreter."""
+        check(self._lib.spk_gammas_set_simple(self._h, ctypes.c_int(int(mode))), "spk_gammas_set_simple")
 
     def gammas_simple_count(self) -> int:
         n = ctypes.c_int(0)

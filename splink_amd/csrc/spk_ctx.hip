@@ -264,6 +264,7 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
                         "spk_table_add_utf8: value ids must lie in [0, 2^32) for non-NULL rows");
     }
     c->kind = COL_STR;
+    c->has_ids = value_ids != nullptr;
     DevBuf<uint8_t> d_bytes, d_valid;
     SPK_TRY(d_bytes.alloc((size_t)nbytes + 1));
     SPK_TRY(d_valid.alloc((size_t)n + 1));

@@ -46,9 +46,12 @@ enum Status { ST_DONE = 0, ST_UNDECIDED = 1, ST_NEEDS_SLOW = 2 };
 // these straight from the two rows' metadata records, loaded for several columns at once; every
 // other program runs through the general interpreter.  Both give identical levels.
 constexpr int MAX_TESTS = 6;
-constexpr int SIMPLE_GROUP = 4;  // simple columns whose row records are in flight together
 constexpr int MAX_SIMPLE = 64;   // = the column limit of set_pattern_space
 enum SimpleKind : int32_t { SK_STR = 1, SK_NUM = 2 };
+// Filter class of a simple column, chosen on the host: which row-image fields the filter reads and
+// which bound logic decides the column.  SC_GEN (strings) and SC_NUMRAW (numbers) read the
+// columns' own records instead of the row image.
+enum SimpleClass : int32_t { SC_GEN = 0, SC_EQ = 1, SC_JW = 2, SC_LEV = 3, SC_NUM = 4, SC_NUMRAW = 5 };
 struct SimpleCol {
     int32_t k;  // comparison column (position in the code)
     int32_t kind;
@@ -57,7 +60,36 @@ struct SimpleCol {
     int32_t op[MAX_TESTS], cmp[MAX_TESTS], level[MAX_TESTS];
     double t[MAX_TESTS];
     int64_t stride;
+    int32_t cls;      // SimpleClass
+    int32_t off;      // byte offset of the column's fields in a row-image row
+    int32_t off2;     // SC_JW: offset of the four head units
+    int32_t has_ids;  // both sides carry dictionary ids (equal keys = equal strings)
 };
+
+// ---- filter row image ----------------------------------------------------------------------------
+// The filter needs a few bytes per (row, column) -- equality key, lengths, unit sketch, head units --
+// but reading them from each column's own 32-byte records costs a cache line per row AND column,
+// and the pairs of a second blocking rule land on random rows.  So before the filter pass the
+// fields of every simple column are packed, per row, into one row of a row image (<= IMG_MAX
+// bytes, 16-byte aligned): a pair then reads two rows' lines whatever the number of columns.
+//   SC_EQ   8 B {key u32, lens u32}            SC_LEV 16 B {key, lens, sketch u64}
+//   SC_JW  16 B {key, lens, sketch} + 8 B head units at off2
+//   SC_NUM 16 B {value f64, valid u32, pad}
+// lens = UTF-16 length | code points << 16, each saturating at LEN_SAT; LENS_NULL = NULL.
+constexpr int IMG_MAX = 256;
+constexpr uint32_t LENS_NULL = 0xFFFFFFFFu;
+constexpr int LEN_SAT = 0xFFFE;
+// The comparison programs are read-only for the whole launch: reading them through the constant
+// address space lets wave-uniform reads become scalar loads (s_load) instead of per-lane vector
+// loads, which would compete with the row gathers for the texture addresser.
+typedef const __attribute__((address_space(4))) SimpleCol ConstSimpleCol;
+__device__ inline ConstSimpleCol *const_simple(const SimpleCol *p) { return (ConstSimpleCol *)p; }
+
+// Chunk-major image: the 16-byte chunk c of every row is contiguous, so the lanes of a wave that
+// read the same field of consecutive rows (a block's pairs) share a few cache lines.
+__host__ __device__ inline int64_t img_at(int64_t rows, int64_t row, int off) {
+    return ((int64_t)(off >> 4) * rows + row) * 16 + (off & 15);
+}
 
 struct GammaArgs {
     const ColDesc *cols0, *cols1;  // tables for operand side 0 (`_l`) and 1 (`_r`)
@@ -86,6 +118,10 @@ struct GammaArgs {
     int n_simple;
     const int32_t *complex_k;  // ... and the columns the interpreter evaluates
     int n_complex;
+    const uint8_t *img0, *img1;  // filter row images of the l- and r-side tables (k_build_image)
+    int64_t img_stride;          // bytes of one row's fields (a multiple of 16)
+    int64_t img_rows0, img_rows1;  // rows of each image (chunk-major layout: chunk c of row r at (c * rows + r) * 16)
+    int32_t slot_beg[17];        // k_gamma_rows: simple[slot_beg[s] .. slot_beg[s+1]) start at image byte 8 s
 };
 
 // Codes are written in place: the filter pass sets each pair's code, the exact / slow passes of
@@ -476,7 +512,8 @@ __device__ inline int meta_equal(const RecMeta &a, const RecMeta &b) {
     return a.len16 <= 4 ? 1 : -1;
 }
 
-__device__ int simple_str(const SimpleCol &sc, const RecMeta &a, const RecMeta &b, int &level) {
+template <class SC>
+__device__ __attribute__((always_inline)) inline int simple_str(const SC &sc, const RecMeta &a, const RecMeta &b, int &level) {
     if (a.len16 < 0 || b.len16 < 0) {
         level = sc.null_level;
         return ST_DONE;
@@ -521,7 +558,8 @@ __device__ int simple_str(const SimpleCol &sc, const RecMeta &a, const RecMeta &
     return ST_DONE;
 }
 
-__device__ int simple_num(const SimpleCol &sc, bool va, double a, bool vb, double b) {
+template <class SC>
+__device__ __attribute__((always_inline)) inline int simple_num(const SC &sc, bool va, double a, bool vb, double b) {
     if (!va || !vb) return sc.null_level;
     for (int i = 0; i < sc.n_tests; ++i) {
         const int op = sc.op[i], cmp = sc.cmp[i];
@@ -539,86 +577,464 @@ __device__ int simple_num(const SimpleCol &sc, bool va, double a, bool vb, doubl
     return sc.else_level;
 }
 
-// Filter pass, simple columns: initialises code[p] with their levels.  The column descriptors
-// and the table pointers are staged in LDS once per workgroup: read from global memory inside the
-// divergent per-pair code they would be per-lane vector loads on the critical path of every pair.
-struct SimpleSrc {
-    const RecMeta *m0, *m1;
-    const double *v0, *v1;
-    const uint8_t *ok0, *ok1;
-};
-
-__global__ __launch_bounds__(F_THREADS) void k_gamma_simple(GammaArgs A) {
-    __shared__ SimpleCol s_sc[MAX_SIMPLE];
-    __shared__ SimpleSrc s_src[MAX_SIMPLE];
-    __shared__ unsigned int s_cnt[MAX_SIMPLE];
-    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) {
-        const SimpleCol sc = A.simple[i];
-        const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
-        s_sc[i] = sc;
-        s_src[i] = SimpleSrc{c0.meta, c1.meta, c0.val, c1.val, c0.valid, c1.valid};
-        s_cnt[i] = 0;
+// rows_img: the image's row capacity (its chunk stride); rows [0, n) are filled.
+__global__ void k_build_image(int64_t n, const ColDesc *__restrict__ cols, const SimpleCol *__restrict__ simple,
+                              int n_simple, uint8_t *__restrict__ img, int64_t rows_img) {
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= n) return;
+    for (int j = 0; j < n_simple; ++j) {
+        const SimpleCol &sc = simple[j];
+        if (sc.cls == SC_GEN || sc.cls == SC_NUMRAW) continue;
+        const ColDesc &c = cols[sc.col];
+        if (sc.cls == SC_NUM) {
+            const bool ok = c.valid[row] != 0;
+            *reinterpret_cast<double *>(img + img_at(rows_img, row, sc.off)) = ok ? c.val[row] : 0.0;
+            *reinterpret_cast<uint2 *>(img + img_at(rows_img, row, sc.off + 8)) = make_uint2(ok ? 1u : 0u, 0u);
+            continue;
+        }
+        const RecMeta m = c.meta[row];
+        uint32_t lens = LENS_NULL;
+        if (m.len16 >= 0) {
+            const int l16 = m.len16 < LEN_SAT ? m.len16 : LEN_SAT;
+            const int lcp = meta_cplen(m) < LEN_SAT ? meta_cplen(m) : LEN_SAT;
+            lens = (uint32_t)l16 | ((uint32_t)lcp << 16);
+        }
+        *reinterpret_cast<uint2 *>(img + img_at(rows_img, row, sc.off)) = make_uint2(m.key, lens);
+        if (sc.cls != SC_EQ) *reinterpret_cast<uint64_t *>(img + img_at(rows_img, row, sc.off + 8)) = m.sketch;
+        if (sc.cls == SC_JW) *reinterpret_cast<uint64_t *>(img + img_at(rows_img, row, sc.off2)) = m.head;
     }
+}
+
+__device__ inline int lens_u16(uint32_t l) { return (int)(l & 0xFFFFu); }
+__device__ inline int lens_cp(uint32_t l) { return (int)(l >> 16); }
+__device__ inline uint64_t img_sketch(const uint4 &v) { return ((uint64_t)v.w << 32) | v.z; }
+
+// 1 equal, 0 unequal, -1 only the units can tell (equal hash keys without dictionary ids)
+template <class SC>
+__device__ inline int img_equal(const SC &sc, uint32_t ka, uint32_t la, uint32_t kb, uint32_t lb) {
+    if (la != lb || ka != kb) return 0;
+    return sc.has_ids ? 1 : -1;
+}
+
+template <class SC>
+__device__ inline int img_eq(const SC &sc, uint2 a, uint2 b, int &level) {
+    if (a.y == LENS_NULL || b.y == LENS_NULL) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    const int eq = img_equal(sc, a.x, a.y, b.x, b.y);
+    if (eq < 0) return ST_UNDECIDED;
+    for (int i = 0; i < sc.n_tests; ++i)
+        if ((eq == 1) == (sc.cmp[i] == SPK_CMP_EQ)) {
+            level = sc.level[i];
+            return ST_DONE;
+        }
+    level = sc.else_level;
+    return ST_DONE;
+}
+
+// jaro_winkler_sim(l, r) > / >= t tests.  Equal strings and strings without a common unit have
+// exact values (1.0 / 0.0); otherwise the upper bound from the sketches (m <= M, (m - t)/m <= 1)
+// and the head units (Winkler prefix) is evaluated in fp32 with a 1e-5 margin, far above its
+// rounding; a bound can only prove a test false, every other cell goes to the exact pass.
+template <class SC>
+__device__ inline int img_jw(const SC &sc, uint4 a, uint4 b, uint64_t ha, uint64_t hb, int &level) {
+    if (a.y == LENS_NULL || b.y == LENS_NULL) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    const int eq = img_equal(sc, a.x, a.y, b.x, b.y);
+    const int lf = lens_u16(a.y), ls = lens_u16(b.y);
+    if (eq < 0 || lf >= LEN_SAT || ls >= LEN_SAT) return ST_UNDECIDED;
+    double v = -1.0;  // the exact similarity when the records determine it
+    float hi = 0.f;   // else an upper bound
+    if (eq == 1) {
+        v = lf > 0 ? 1.0 : 0.0;
+    } else {
+        const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
+        const int M = lmn == 0 ? 0 : sketch_inter_ub(img_sketch(a), img_sketch(b), lf, ls);
+        if (M == 0) {
+            v = 0.0;
+        } else {
+            float j = ((float)M * (float)(lf + ls) / ((float)lf * (float)ls) + 1.0f) * (1.0f / 3.0f);
+            if (j >= 0.7f - 1e-4f) {
+                const uint64_t d = ha ^ hb;
+                const int cp = d ? (__ffsll((unsigned long long)d) - 1) >> 4 : 4;
+                const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
+                const float pw = (lmx > 10 ? 1.0f / (float)lmx : 0.1f) * (float)prefix;
+                j = j + pw * (1.0f - j);
+            }
+            hi = j + 1e-5f;
+        }
+    }
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const double t = sc.t[i];
+        int r;
+        if (v >= 0.0) r = cmpd(v, t, sc.cmp[i]);
+        else if (sc.cmp[i] == SPK_CMP_GT) r = 0.0 > t ? KT : ((double)hi <= t ? KF : KU);
+        else r = 0.0 >= t ? KT : ((double)hi < t ? KF : KU);  // SPK_CMP_GE
+        if (r == KU) return ST_UNDECIDED;
+        if (r == KT) {
+            level = sc.level[i];
+            return ST_DONE;
+        }
+    }
+    level = sc.else_level;
+    return ST_DONE;
+}
+
+// `=` / `<>` and levenshtein [ratio] tests: the distance lies in [max(length gap, bag distance),
+// max(length)].  The ratio test `lev / den <= t` (or `<`) is decided against t * den with one part
+// in 1e12 of margin instead of a division per pair; exact ties are left to the exact pass.
+template <class SC>
+__device__ inline int img_lev(const SC &sc, uint4 a, uint4 b, int &level) {
+    if (a.y == LENS_NULL || b.y == LENS_NULL) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    const int eq = img_equal(sc, a.x, a.y, b.x, b.y);
+    const int la = lens_u16(a.y), lb = lens_u16(b.y), na = lens_cp(a.y), nb = lens_cp(b.y);
+    if (eq < 0 || la >= LEN_SAT || lb >= LEN_SAT || na >= LEN_SAT || nb >= LEN_SAT) return ST_UNDECIDED;
+    int lo = 0, hi = 0;
+    if (eq == 0) {
+        lo = na > nb ? na - nb : nb - na;
+        if (na == la && nb == lb) {  // BMP: units are code points, so the bag bound holds
+            const int bag = (na > nb ? na : nb) - sketch_inter_ub(img_sketch(a), img_sketch(b), na, nb);
+            if (bag > lo) lo = bag;
+        }
+        hi = na > nb ? na : nb;
+    }
+    const double den = (double)(na + nb) / 2.0;
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int op = sc.op[i], cmp = sc.cmp[i];
+        const double t = sc.t[i];
+        int r;
+        if (op == SPK_OP_STR_CMP) {
+            r = ((eq == 1) == (cmp == SPK_CMP_EQ)) ? KT : KF;
+        } else if (op == SPK_OP_LEV) {
+            r = decide((double)lo, (double)hi, cmp, t);
+        } else if (den == 0.0) {
+            r = KN;
+        } else if (eq == 1) {
+            r = cmpd(0.0, t, cmp);
+        } else {
+            const double tl = t * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
+            const double tl_hi = up > dn ? up : dn, tl_lo = up > dn ? dn : up;
+            if (cmp == SPK_CMP_LE) r = (double)hi <= tl_lo ? KT : ((double)lo > tl_hi ? KF : KU);
+            else r = (double)hi < tl_lo ? KT : ((double)lo >= tl_hi ? KF : KU);  // SPK_CMP_LT
+        }
+        if (r == KU) return ST_UNDECIDED;
+        if (r == KT) {
+            level = sc.level[i];
+            return ST_DONE;
+        }
+    }
+    level = sc.else_level;
+    return ST_DONE;
+}
+
+__device__ inline double bits_to_double(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// Append the lanes' wanted values of F_PAIRS ballots to a list: one LDS atomic per call.  The wave
+// must be converged (lane 0 active).
+constexpr int F_PAIRS = 4;  // pairs per lane per iteration of the filter pass
+__device__ inline void wave_append_batch(int32_t *list, unsigned int *count, const bool (&want)[F_PAIRS],
+                                         const int64_t (&val)[F_PAIRS]) {
+    unsigned long long m[F_PAIRS];
+    unsigned int total = 0;
+#pragma unroll
+    for (int u = 0; u < F_PAIRS; ++u) {
+        m[u] = __ballot(want[u]);
+        total += (unsigned int)__popcll(m[u]);
+    }
+    if (!total) return;
+    const int lane = threadIdx.x & 63;
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(count, total);
+    base = __shfl(base, 0);
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int u = 0; u < F_PAIRS; ++u) {
+        if (want[u]) list[base + __popcll(m[u] & below)] = (int32_t)val[u];
+        base += (unsigned int)__popcll(m[u]);
+    }
+}
+
+// Filter pass, simple columns: initialises code[p] with their levels.  Each lane takes F_PAIRS
+// pairs per iteration and, column by column, issues the image loads of all of them before
+// evaluating any: the pass is bound by the latency of those gathers, so every round trip is
+// shared by F_PAIRS pairs.  The column loop is uniform across the wave, so the class dispatch and
+// the test parameters are scalar.
+__global__ __launch_bounds__(F_THREADS) void k_gamma_simple(GammaArgs A) {
+    __shared__ unsigned int s_cnt[MAX_SIMPLE];
+    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const Region R = my_region(A);
-    for (int64_t base = R.r0 + (threadIdx.x & ~63); base < R.r1; base += F_THREADS) {  // wave-uniform
-        const int64_t p = base + lane;
-        const bool active = p < R.r1;
-        const int32_t x = active ? A.pl[p] : 0;  // inactive lanes read row 0 harmlessly
-        const int32_t y = active ? A.pr[p] : 0;
-        uint32_t acc = 0;
-        for (int g = 0; g < A.n_simple; g += SIMPLE_GROUP) {
-            // issue every record load of the group before the first use
-            RecMeta ma[SIMPLE_GROUP], mb[SIMPLE_GROUP];
-            double va[SIMPLE_GROUP], vb[SIMPLE_GROUP];
-            bool oka[SIMPLE_GROUP], okb[SIMPLE_GROUP];
+    ConstSimpleCol *simple = const_simple(A.simple);
+    constexpr int64_t SPAN = 64 * F_PAIRS;
+    for (int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN; base < R.r1;
+         base += (int64_t)(F_THREADS / 64) * SPAN) {  // wave-uniform
+        int64_t p[F_PAIRS];
+        bool act[F_PAIRS];
+        int32_t x[F_PAIRS], y[F_PAIRS];
+        uint32_t acc[F_PAIRS];
 #pragma unroll
-            for (int j = 0; j < SIMPLE_GROUP; ++j) {
-                if (g + j < A.n_simple) {
-                    const SimpleSrc &src = s_src[g + j];
-                    if (s_sc[g + j].kind == SK_STR) {
-                        ma[j] = src.m0[x];
-                        mb[j] = src.m1[y];
-                    } else {
-                        oka[j] = src.ok0[x] != 0;
-                        okb[j] = src.ok1[y] != 0;
-                        va[j] = src.v0[x];
-                        vb[j] = src.v1[y];
-                    }
-                }
-            }
-            // one copy of the evaluation code: slot 0 is evaluated, then the slots rotate down
-            const int n_here = A.n_simple - g < SIMPLE_GROUP ? A.n_simple - g : SIMPLE_GROUP;
-            for (int j = 0; j < n_here; ++j) {
-                const SimpleCol &sc = s_sc[g + j];
-                bool undecided = false;
-                if (active) {
-                    int level;
-                    if (sc.kind == SK_STR) {
-                        if (simple_str(sc, ma[0], mb[0], level) != ST_DONE) undecided = true;
-                    } else {
-                        level = simple_num(sc, oka[0], va[0], okb[0], vb[0]);
-                    }
-                    if (!undecided) acc += (uint32_t)(level + 1) * (uint32_t)sc.stride;
-                }
-                wave_append(region_list(A, sc.k, R), &s_cnt[g + j], undecided, (int32_t)p);
-#pragma unroll
-                for (int q = 0; q + 1 < SIMPLE_GROUP; ++q) {
-                    ma[q] = ma[q + 1];
-                    mb[q] = mb[q + 1];
-                    va[q] = va[q + 1];
-                    vb[q] = vb[q + 1];
-                    oka[q] = oka[q + 1];
-                    okb[q] = okb[q + 1];
-                }
-            }
+        for (int u = 0; u < F_PAIRS; ++u) {
+            p[u] = base + u * 64 + lane;
+            act[u] = p[u] < R.r1;
+            x[u] = act[u] ? A.pl[p[u]] : 0;  // inactive lanes read row 0 harmlessly
+            y[u] = act[u] ? A.pr[p[u]] : 0;
+            acc[u] = 0;
         }
-        if (active) code_set(A, p, acc);
+        for (int j = 0; j < A.n_simple; ++j) {
+            ConstSimpleCol &sc = simple[j];
+            bool und[F_PAIRS];
+            int lev[F_PAIRS];
+#pragma unroll
+            for (int u = 0; u < F_PAIRS; ++u) {
+                und[u] = false;
+                lev[u] = 0;
+            }
+            switch (sc.cls) {
+                case SC_EQ: {
+                    uint2 va[F_PAIRS], vb[F_PAIRS];
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u) {
+                        va[u] = *reinterpret_cast<const uint2 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
+                        vb[u] = *reinterpret_cast<const uint2 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
+                    }
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u) und[u] = img_eq(sc, va[u], vb[u], lev[u]) != ST_DONE;
+                    break;
+                }
+                case SC_JW: {
+                    uint4 va[F_PAIRS], vb[F_PAIRS];
+                    uint64_t ha[F_PAIRS], hb[F_PAIRS];
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u) {
+                        va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
+                        vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
+                        ha[u] = *reinterpret_cast<const uint64_t *>(A.img0 + img_at(A.img_rows0, x[u], sc.off2));
+                        hb[u] = *reinterpret_cast<const uint64_t *>(A.img1 + img_at(A.img_rows1, y[u], sc.off2));
+                    }
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u) und[u] = img_jw(sc, va[u], vb[u], ha[u], hb[u], lev[u]) != ST_DONE;
+                    break;
+                }
+                case SC_LEV: {
+                    uint4 va[F_PAIRS], vb[F_PAIRS];
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u) {
+                        va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
+                        vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
+                    }
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u) und[u] = img_lev(sc, va[u], vb[u], lev[u]) != ST_DONE;
+                    break;
+                }
+                case SC_NUM: {
+                    uint4 va[F_PAIRS], vb[F_PAIRS];
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u) {
+                        va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
+                        vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
+                    }
+#pragma unroll
+                    for (int u = 0; u < F_PAIRS; ++u)
+                        lev[u] = simple_num(sc, va[u].z != 0, bits_to_double(va[u].x, va[u].y), vb[u].z != 0,
+                                            bits_to_double(vb[u].x, vb[u].y));
+                    break;
+                }
+                case SC_NUMRAW: {
+                    const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
+                    for (int u = 0; u < F_PAIRS; ++u)
+                        lev[u] = simple_num(sc, c0.valid[x[u]] != 0, c0.val[x[u]], c1.valid[y[u]] != 0, c1.val[y[u]]);
+                    break;
+                }
+                default: {  // SC_GEN: the full row records, one pair at a time (few registers)
+                    const RecMeta *m0 = A.cols0[sc.col].meta, *m1 = A.cols1[sc.col].meta;
+                    for (int u = 0; u < F_PAIRS; ++u) und[u] = simple_str(sc, m0[x[u]], m1[y[u]], lev[u]) != ST_DONE;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < F_PAIRS; ++u) {
+                und[u] = und[u] && act[u];
+                if (!und[u]) acc[u] += (uint32_t)(lev[u] + 1) * (uint32_t)sc.stride;
+            }
+            wave_append_batch(region_list(A, sc.k, R), &s_cnt[j], und, p);
+        }
+#pragma unroll
+        for (int u = 0; u < F_PAIRS; ++u)
+            if (act[u]) code_set(A, p[u], acc[u]);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
-        A.region_count[(int64_t)s_sc[i].k * A.n_regions + blockIdx.x] = s_cnt[i];
+        A.region_count[(int64_t)simple[i].k * A.n_regions + blockIdx.x] = s_cnt[i];
+}
+
+// Filter pass over rows held in registers: when the image row is at most ROW_MAXQ x 16 bytes,
+// each lane loads its RP pairs' two image rows whole, in one burst (2 x RP x NQ independent 16-byte
+// loads) and evaluates every column from registers -- one gather round trip per iteration
+// instead of one per column -- while the next iteration's pair rows are already in flight.
+// The column's 16-byte chunk is chosen by a wave-uniform index (scalar branches / selects).
+constexpr int ROW_MAXQ = 8;
+constexpr int RP = 2;
+
+// The columns whose fields start at 8-byte slot S of the image row, over the RP pairs' register rows.
+// S is a template parameter and the slots are visited in sequence (slot_cols<0> calls <1> ...), so
+// every row access -- chunk S / 2, half S % 2 -- has a compile-time index and the rows stay in
+// registers (a runtime chunk or half index would send them to scratch).  16-byte fields start at
+// even slots; JW heads sit in the low half of the next chunk (layout_image).
+template <int S, int NQ>
+__device__ __attribute__((always_inline)) inline void slot_cols(const GammaArgs &A, const Region &R,
+                                                                unsigned int *s_cnt, const uint4 (&ra)[RP][NQ],
+                                                                const uint4 (&rb)[RP][NQ], const int64_t (&p)[RP],
+                                                                const bool (&act)[RP], uint32_t (&acc)[RP]) {
+    if constexpr (S < 2 * NQ) {
+        constexpr int CQ = S / 2, HQ = CQ + 1 < NQ ? CQ + 1 : CQ;
+        const int lane = threadIdx.x & 63;
+        for (int j = A.slot_beg[S]; j < A.slot_beg[S + 1]; ++j) {
+            ConstSimpleCol &sc = const_simple(A.simple)[j];
+            bool und[RP];
+            int lev[RP];
+#pragma unroll
+            for (int u = 0; u < RP; ++u) {
+                und[u] = false;
+                lev[u] = 0;
+            }
+            if constexpr (S % 2 == 1) {  // only 8-byte EQ fields start at an odd slot
+#pragma unroll
+                for (int u = 0; u < RP; ++u)
+                    und[u] = img_eq(sc, make_uint2(ra[u][CQ].z, ra[u][CQ].w), make_uint2(rb[u][CQ].z, rb[u][CQ].w),
+                                    lev[u]) != ST_DONE;
+            } else {
+                switch (sc.cls) {
+                    case SC_EQ:
+#pragma unroll
+                        for (int u = 0; u < RP; ++u)
+                            und[u] = img_eq(sc, make_uint2(ra[u][CQ].x, ra[u][CQ].y),
+                                            make_uint2(rb[u][CQ].x, rb[u][CQ].y), lev[u]) != ST_DONE;
+                        break;
+                    case SC_JW:
+#pragma unroll
+                        for (int u = 0; u < RP; ++u)
+                            und[u] = img_jw(sc, ra[u][CQ], rb[u][CQ], ((uint64_t)ra[u][HQ].y << 32) | ra[u][HQ].x,
+                                            ((uint64_t)rb[u][HQ].y << 32) | rb[u][HQ].x, lev[u]) != ST_DONE;
+                        break;
+                    case SC_LEV:
+#pragma unroll
+                        for (int u = 0; u < RP; ++u) und[u] = img_lev(sc, ra[u][CQ], rb[u][CQ], lev[u]) != ST_DONE;
+                        break;
+                    default:  // SC_NUM
+#pragma unroll
+                        for (int u = 0; u < RP; ++u)
+                            lev[u] = simple_num(sc, ra[u][CQ].z != 0, bits_to_double(ra[u][CQ].x, ra[u][CQ].y),
+                                                rb[u][CQ].z != 0, bits_to_double(rb[u][CQ].x, rb[u][CQ].y));
+                        break;
+                }
+            }
+            unsigned long long m[RP];
+            unsigned int total = 0;
+#pragma unroll
+            for (int u = 0; u < RP; ++u) {
+                und[u] = und[u] && act[u];
+                if (!und[u]) acc[u] += (uint32_t)(lev[u] + 1) * (uint32_t)sc.stride;
+                m[u] = __ballot(und[u]);
+                total += (unsigned int)__popcll(m[u]);
+            }
+            if (total) {
+                int32_t *list = region_list(A, sc.k, R);
+                unsigned int b0 = 0;
+                if (lane == 0) b0 = atomicAdd(&s_cnt[j], total);
+                b0 = __shfl(b0, 0);
+                const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+                for (int u = 0; u < RP; ++u) {
+                    if (und[u]) list[b0 + __popcll(m[u] & below)] = (int32_t)p[u];
+                    b0 += (unsigned int)__popcll(m[u]);
+                }
+            }
+        }
+        slot_cols<S + 1, NQ>(A, R, s_cnt, ra, rb, p, act, acc);
+    }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(F_THREADS) void k_gamma_rows(GammaArgs A) {
+    __shared__ unsigned int s_cnt[MAX_SIMPLE];
+    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const Region R = my_region(A);
+    ConstSimpleCol *simple = const_simple(A.simple);
+    constexpr int64_t SPAN = 64 * RP;
+    constexpr int64_t STEP = (int64_t)(F_THREADS / 64) * SPAN;
+    int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN;
+    int32_t nx[RP], ny[RP];  // pair rows of the next iteration
+#pragma unroll
+    for (int u = 0; u < RP; ++u) {
+        const int64_t q = base + u * 64 + lane;
+        nx[u] = q < R.r1 ? A.pl[q] : 0;
+        ny[u] = q < R.r1 ? A.pr[q] : 0;
+    }
+    for (; base < R.r1; base += STEP) {  // wave-uniform
+        int64_t p[RP];
+        bool act[RP];
+        int32_t x[RP], y[RP];
+        uint32_t acc[RP];
+        uint4 ra[RP][NQ], rb[RP][NQ];
+#pragma unroll
+        for (int u = 0; u < RP; ++u) {
+            p[u] = base + u * 64 + lane;
+            act[u] = p[u] < R.r1;
+            x[u] = nx[u];
+            y[u] = ny[u];
+            acc[u] = 0;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                ra[u][k] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], 16 * k));
+                rb[u][k] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], 16 * k));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RP; ++u) {  // prefetch the next iteration's pair rows
+            const int64_t q = base + STEP + u * 64 + lane;
+            nx[u] = q < R.r1 ? A.pl[q] : 0;
+            ny[u] = q < R.r1 ? A.pr[q] : 0;
+        }
+        slot_cols<0, NQ>(A, R, s_cnt, ra, rb, p, act, acc);
+        // columns outside the image (records read directly), one pair at a time
+        for (int j = A.slot_beg[2 * NQ]; j < A.n_simple; ++j) {
+            ConstSimpleCol &sc = simple[j];
+            bool und[RP];
+            int lev[RP];
+            for (int u = 0; u < RP; ++u) {
+                und[u] = false;
+                lev[u] = 0;
+                if (sc.cls == SC_NUMRAW) {
+                    const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
+                    lev[u] = simple_num(sc, c0.valid[x[u]] != 0, c0.val[x[u]], c1.valid[y[u]] != 0, c1.val[y[u]]);
+                } else {
+                    und[u] = simple_str(sc, A.cols0[sc.col].meta[x[u]], A.cols1[sc.col].meta[y[u]], lev[u]) != ST_DONE;
+                }
+            }
+            bool w[RP];
+            for (int u = 0; u < RP; ++u) {
+                w[u] = und[u] && act[u];
+                if (!w[u]) acc[u] += (uint32_t)(lev[u] + 1) * (uint32_t)sc.stride;
+            }
+            for (int u = 0; u < RP; ++u) wave_append(region_list(A, sc.k, R), &s_cnt[j], w[u], (int32_t)p[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < RP; ++u)
+            if (act[u]) code_set(A, p[u], acc[u]);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
+        A.region_count[(int64_t)simple[i].k * A.n_regions + blockIdx.x] = s_cnt[i];
 }
 
 // Filter pass, every other column through the interpreter: adds to code[p].
@@ -869,6 +1285,99 @@ static std::vector<uint16_t> utf8_to_utf16(const uint8_t *b, int64_t n, int32_t 
 }
 
 // Recognise a simple column (see SimpleCol); false leaves it to the interpreter.
+static int32_t simple_class(const SimpleCol &s) {
+    if (s.kind == SK_NUM) return SC_NUM;
+    bool all_eq = true, all_jw = s.n_tests > 0, lev_ok = true;
+    int n_lev = 0;
+    for (int i = 0; i < s.n_tests; ++i) {
+        const int op = s.op[i], cmp = s.cmp[i];
+        all_eq = all_eq && op == SPK_OP_STR_CMP;
+        all_jw = all_jw && op == SPK_OP_JW && (cmp == SPK_CMP_GT || cmp == SPK_CMP_GE);
+        if (op == SPK_OP_LEV) {
+            ++n_lev;
+        } else if (op == SPK_OP_LEVRATIO) {
+            ++n_lev;
+            lev_ok = lev_ok && (cmp == SPK_CMP_LE || cmp == SPK_CMP_LT);
+        } else if (op != SPK_OP_STR_CMP) {
+            lev_ok = false;
+        }
+    }
+    if (all_eq) return SC_EQ;
+    if (all_jw) return SC_JW;
+    if (lev_ok && n_lev > 0) return SC_LEV;
+    return SC_GEN;
+}
+
+// Row-image offsets; returns the row stride (a multiple of 16), 0 when nothing uses the image.
+// JW fields take 24 B at a 16-byte boundary (key, lens, sketch; head units at off + 16, the low half
+// of the next chunk), LEV / NUM 16 B at a boundary, EQ 8 B in the gaps JW leaves, then at the end.
+// Columns that do not fit in IMG_MAX bytes keep reading their own records.
+static int64_t layout_image(std::vector<SimpleCol> &simple) {
+    int64_t off = 0;
+    std::vector<int64_t> gaps;  // free 8-byte slots
+    for (SimpleCol &s : simple) {
+        if (s.cls != SC_JW) continue;
+        if (off + 32 > IMG_MAX) {
+            s.cls = SC_GEN;
+            continue;
+        }
+        s.off = (int32_t)off;
+        s.off2 = (int32_t)(off + 16);
+        gaps.push_back(off + 24);
+        off += 32;
+    }
+    for (SimpleCol &s : simple) {
+        if (s.cls != SC_LEV && s.cls != SC_NUM) continue;
+        if (off + 16 > IMG_MAX) {
+            s.cls = s.cls == SC_NUM ? SC_NUMRAW : SC_GEN;
+            continue;
+        }
+        s.off = (int32_t)off;
+        off += 16;
+    }
+    size_t g = 0;
+    for (SimpleCol &s : simple) {
+        if (s.cls != SC_EQ) continue;
+        if (g < gaps.size()) {
+            s.off = (int32_t)gaps[g++];
+            continue;
+        }
+        if (off + 8 > IMG_MAX) {
+            s.cls = SC_GEN;
+            continue;
+        }
+        s.off = (int32_t)off;
+        off += 8;
+    }
+    int64_t end = off;
+    if (g < gaps.size() && gaps.back() + 8 == off) end = off - 8;  // trailing unused JW gap
+    return (end + 15) & ~(int64_t)15;
+}
+
+static int build_images(spk_ctx *ctx, Table &t0, Table &t1, GammaArgs &A, int64_t stride) {
+    A.img0 = A.img1 = nullptr;
+    A.img_stride = stride;
+    if (stride <= 0 || A.n_simple == 0) return SPK_OK;
+    Table *ts[2] = {&t0, &t1};
+    for (int s = 0; s < 2; ++s) {
+        if (s == 1 && &t1 == &t0) {
+            A.img1 = A.img0;
+            A.img_rows1 = A.img_rows0;
+            break;
+        }
+        Table &t = *ts[s];
+        SPK_TRY(ctx->img[s].alloc((size_t)(t.n + 1) * (size_t)stride));
+        if (t.n > 0) {
+            k_build_image<<<(unsigned)((t.n + 255) / 256), 256, 0, ctx->stream>>>(t.n, t.d_desc.p, A.simple, A.n_simple,
+                                                                                 ctx->img[s].p, t.n + 1);
+            SPK_HIP(hipGetLastError());
+        }
+        (s == 0 ? A.img0 : A.img1) = ctx->img[s].p;
+        (s == 0 ? A.img_rows0 : A.img_rows1) = t.n + 1;
+    }
+    return SPK_OK;
+}
+
 static bool classify_simple(int k, const spk_column_program &prog, const int32_t *wf, const int32_t *wn,
                             const int32_t *wl, const spk_instr *instr, const spk_operand *ops, const Table &t0,
                             const Table &t1, const std::vector<int64_t> &stride, SimpleCol *out) {
@@ -993,6 +1502,30 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         else
             complex_k.push_back(k);
     }
+    for (SimpleCol &sc : simple) {
+        sc.cls = simple_class(sc);
+        sc.has_ids = (t0.cols[sc.col]->has_ids && t1.cols[sc.col]->has_ids) ? 1 : 0;
+    }
+    const int64_t img_stride = layout_image(simple);
+    // image columns first, by field offset (the row filter walks the chunks in order), then the rest
+    std::stable_sort(simple.begin(), simple.end(), [](const SimpleCol &a, const SimpleCol &b) {
+        const bool ia = a.cls != SC_GEN && a.cls != SC_NUMRAW, ib = b.cls != SC_GEN && b.cls != SC_NUMRAW;
+        if (ia != ib) return ia;
+        return ia && a.off < b.off;
+    });
+    int32_t slot_beg[17];
+    {
+        // slot_beg[t] = first image column starting at 8-byte slot >= t; past the row, the end of them
+        int n_img = 0;
+        while (n_img < (int)simple.size() && simple[n_img].cls != SC_GEN && simple[n_img].cls != SC_NUMRAW) ++n_img;
+        int j = 0;
+        for (int t = 0; t <= 16; ++t) {
+            while (j < n_img && (simple[j].off >> 3) < t) ++j;
+            slot_beg[t] = j;
+        }
+        const int ns = (int)(img_stride / 8);
+        for (int t = ns; t <= 16; ++t) slot_beg[t] = n_img;
+    }
     // Every program array goes up in one packed copy into a buffer the context keeps.
     std::vector<uint8_t> blob;
     auto put = [&](const auto *src, size_t n) -> size_t {
@@ -1055,11 +1588,27 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.slow_count = ctx->work_count.p;
     A.n_simple = (int)simple.size();
     A.n_complex = (int)complex_k.size();
+    for (int t = 0; t <= 16; ++t) A.slot_beg[t] = slot_beg[t];
     ctx->last_simple = (int)simple.size();
 
     SPK_TRY(ctx->begin(K_GAMMA));
     if (P > 0) {
-        k_gamma_simple<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
+        SPK_TRY(build_images(ctx, t0, t1, A, img_stride));
+        const int nq = (int)(img_stride / 16);
+        if (ctx->row_filter && A.n_simple > 0 && nq >= 1 && nq <= ROW_MAXQ) {
+            switch (nq) {
+                case 1: k_gamma_rows<1><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 2: k_gamma_rows<2><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 3: k_gamma_rows<3><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 4: k_gamma_rows<4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 5: k_gamma_rows<5><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 6: k_gamma_rows<6><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 7: k_gamma_rows<7><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                default: k_gamma_rows<8><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+            }
+        } else {
+            k_gamma_simple<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
+        }
         SPK_HIP(hipGetLastError());
         if (A.n_complex) {
             k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
@@ -1290,6 +1839,7 @@ extern "C" int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n) {
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
     ctx->simple_columns = on != 0;
+    ctx->row_filter = on == 2;
     return SPK_OK;
 }
 

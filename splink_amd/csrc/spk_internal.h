@@ -135,6 +135,7 @@ struct Column {
     DevBuf<uint64_t> planes;
     DevBuf<double> val;
     DevBuf<uint8_t> valid;
+    bool has_ids = false;  // COL_STR: RecMeta.key is a dictionary id
 };
 
 struct Table {
@@ -174,11 +175,13 @@ struct spk_ctx {
     int64_t last_deferred = 0;
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
     bool simple_columns = true;       // template-shaped columns take the record-only filter
+    bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)
     spk::DevBuf<int32_t> work, slow;
     spk::DevBuf<int64_t> slow_off;    // [K+1] slow-pass list offsets
+    spk::DevBuf<uint8_t> img[2];      // filter row images of table 0 / table 1
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)
     spk::DevBuf<unsigned int> work_count;    // [K] slow-pass list lengths
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths

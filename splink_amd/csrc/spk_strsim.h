@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cmath>
+#include <type_traits>
 
 #include "spk_internal.h"
 
@@ -331,6 +332,7 @@ __device__ inline W mask_below(int k) {  // bits [0, k)
     return k >= (int)(8 * sizeof(W)) ? ~(W)0 : (((W)1 << k) - (W)1);
 }
 
+// Positions i of a plane-encoded string with unit i == c (garbage above the string's length).
 // Positions i of a plane-encoded string with unit i == c (garbage above the string's length).
 template <typename W>
 __device__ inline W eq_mask(const W (&pl)[N_PLANES], uint32_t c) {
