@@ -29,6 +29,9 @@ sys.path.insert(0, ROOT)
 warnings.filterwarnings("ignore")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
+# HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same command
+# (scripts_gpu_round.sh -> tools/traffic.py); the counters cannot be read inside a timed run.
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1_traffic.json")
 COLS = ["first_name", "surname", "dob", "city", "email"]
 
 
@@ -84,11 +87,20 @@ def main():
     job.gammas(st)  # uploads columns, first launch
     names, nlev = job.code_meta
 
+    host = {"gammas_call": [], "em_call": [], "m_step_host": []}
+
     def step():
+        t0 = time.perf_counter()
         job.gammas(st)
+        t1 = time.perf_counter()
         stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        t2 = time.perf_counter()
         lam, rows = m_step_rows(stats, names, nlev)
         params._update_params(lam, rows)
+        t3 = time.perf_counter()
+        host["gammas_call"].append((t1 - t0) * 1e3)
+        host["em_call"].append((t2 - t1) * 1e3)
+        host["m_step_host"].append((t3 - t2) * 1e3)
         ms = job.ctx.kernel_ms()
         return ms
 
@@ -99,6 +111,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    for v in host.values():
+        v.clear()
     gamma_ms, hist_ms, fin_ms = [], [], []
     barrier()
     t0 = time.perf_counter()
@@ -146,6 +160,15 @@ def main():
                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": em_bytes / (h_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                    "algorithmic_bytes_per_launch": em_bytes, "avg_launch_ms": h_ms}
 
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        with open(TRAFFIC_FILE) as f:
+            traffic = json.load(f)
+        roofline["traffic"] = traffic["gamma"]["traffic_bytes_per_call"]
+        em_roofline["traffic"] = traffic["em"]["traffic_bytes_per_call"]
+        roofline["traffic_source"] = em_roofline["traffic_source"] = (
+            os.path.relpath(TRAFFIC_FILE, ROOT) + ": rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command")
+
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(job, df, st, args.cpu_seconds)
@@ -170,7 +193,8 @@ def main():
         "roofline": roofline,
         "roofline_em": em_roofline,
         "breakdown_ms": {"gamma": g_ms, "em_hist": h_ms, "em_final": float(np.mean(fin_ms)), "score": score_ms,
-                         "block_device": block_kernel_ms, "block_wall_incl_host_prep": block_s * 1e3},
+                         "block_device": block_kernel_ms, "block_wall_incl_host_prep": block_s * 1e3,
+                         **{f"host_wall_{k}": float(np.mean(v)) for k, v in host.items()}},
         "deferred_pairs": job.ctx.gammas_deferred(),
         "exact_cells_per_column": dict(zip(names, job.ctx.gammas_exact_counts(len(names)))),
         "cpu_baseline": cpu,

@@ -122,6 +122,7 @@ struct GammaArgs {
     int64_t img_stride;          // bytes of one row's fields (a multiple of 16)
     int64_t img_rows0, img_rows1;  // rows of each image (chunk-major layout: chunk c of row r at (c * rows + r) * 16)
     int32_t slot_beg[17];        // k_gamma_rows: simple[slot_beg[s] .. slot_beg[s+1]) start at image byte 8 s
+    int xcd_swizzle;             // my_region: contiguous region ranges per XCD (n_regions % 8 == 0)
 };
 
 // Codes are written in place: the filter pass sets each pair's code, the exact / slow passes of
@@ -463,8 +464,15 @@ struct Region {
     int64_t r0, r1;  // pair ordinals [r0, r1)
 };
 
+// Workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8), each XCD with its own L2.  With
+// xcd_swizzle, workgroup b takes region (b % 8) * (n_regions / 8) + b / 8, so every XCD works
+// through one contiguous eighth of the pair ordinals: neighbouring pairs share blocks of rows, and
+// those rows then stay in one XCD's L2 instead of being fetched by all eight.  Per-region state
+// (region counts) stays indexed by blockIdx: every kernel maps blocks to regions through here.
 __device__ inline Region my_region(const GammaArgs &A) {
-    const int64_t r0 = (int64_t)blockIdx.x * A.region_len;
+    int64_t reg = blockIdx.x;
+    if (A.xcd_swizzle) reg = (int64_t)(blockIdx.x & 7u) * (A.n_regions >> 3) + (blockIdx.x >> 3);
+    const int64_t r0 = reg * A.region_len;
     const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
     return Region{r0, r1};
 }
@@ -1589,6 +1597,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.n_simple = (int)simple.size();
     A.n_complex = (int)complex_k.size();
     for (int t = 0; t <= 16; ++t) A.slot_beg[t] = slot_beg[t];
+    A.xcd_swizzle = ctx->xcd_swizzle && n_regions % 8 == 0 ? 1 : 0;
     ctx->last_simple = (int)simple.size();
 
     SPK_TRY(ctx->begin(K_GAMMA));

@@ -176,6 +176,7 @@ struct spk_ctx {
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
+    bool xcd_swizzle = true;          // comparison regions in contiguous ranges per XCD (SPK_XCD_SWIZZLE=0: off)
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)
