@@ -1,5 +1,4 @@
 // Context, record-table upload (UTF-8 -> UTF-16 on the device) and pair buffers.
-#include <cstdlib>
 #include <cstring>
 
 #include "spk_internal.h"
@@ -157,7 +156,6 @@ int spk_ctx_create(int device, spk_ctx **out) {
     spk_ctx *c = new spk_ctx();
     c->device = device;
     c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    if (const char *e = std::getenv("SPK_XCD_SWIZZLE")) c->xcd_swizzle = std::atoi(e) != 0;  // A/B measurement knob
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;

@@ -122,7 +122,6 @@ struct GammaArgs {
     int64_t img_stride;          // bytes of one row's fields (a multiple of 16)
     int64_t img_rows0, img_rows1;  // rows of each image (chunk-major layout: chunk c of row r at (c * rows + r) * 16)
     int32_t slot_beg[17];        // k_gamma_rows: simple[slot_beg[s] .. slot_beg[s+1]) start at image byte 8 s
-    int xcd_swizzle;             // my_region: contiguous region ranges per XCD (n_regions % 8 == 0)
 };
 
 // Codes are written in place: the filter pass sets each pair's code, the exact / slow passes of
@@ -464,15 +463,8 @@ struct Region {
     int64_t r0, r1;  // pair ordinals [r0, r1)
 };
 
-// Workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8), each XCD with its own L2.  With
-// xcd_swizzle, workgroup b takes region (b % 8) * (n_regions / 8) + b / 8, so every XCD works
-// through one contiguous eighth of the pair ordinals: neighbouring pairs share blocks of rows, and
-// those rows then stay in one XCD's L2 instead of being fetched by all eight.  Per-region state
-// (region counts) stays indexed by blockIdx: every kernel maps blocks to regions through here.
 __device__ inline Region my_region(const GammaArgs &A) {
-    int64_t reg = blockIdx.x;
-    if (A.xcd_swizzle) reg = (int64_t)(blockIdx.x & 7u) * (A.n_regions >> 3) + (blockIdx.x >> 3);
-    const int64_t r0 = reg * A.region_len;
+    const int64_t r0 = (int64_t)blockIdx.x * A.region_len;
     const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
     return Region{r0, r1};
 }
@@ -1079,13 +1071,23 @@ __global__ __launch_bounds__(F_THREADS) void k_gamma_filter(GammaArgs A) {
         A.region_count[(int64_t)A.complex_k[i] * A.n_regions + blockIdx.x] = s_cnt[i];
 }
 
-// Exact pass over column k: workgroup b takes region b's list.
-__global__ __launch_bounds__(X_THREADS) void k_gamma_exact(GammaArgs A, int k) {
-    uint16_t *slot_a = nullptr, *slot_b = nullptr;  // the exact pass works from registers and L1/L2
+// The exact passes run over column k's compacted work list -- every region's undecided pairs back
+// to back (k_compact) -- with a grid-stride loop, so every CU gets the same share of cells however
+// unevenly they fall over the regions (a region of one large block can hold several times the
+// average).  Block b of k_compact copies region b's list to its prefix offset.
+__global__ void k_compact(GammaArgs A, int k, const int64_t *__restrict__ pref, int32_t *__restrict__ out) {
     const Region R = my_region(A);
-    const int32_t *items = region_list(A, k, R);
+    const int32_t *src = region_list(A, k, R);
     const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
-    for (int64_t base = 0; base < n; base += X_THREADS) {  // block-uniform trip count
+    int32_t *dst = out + pref[blockIdx.x];
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+// Exact pass over column k through the interpreter.
+__global__ __launch_bounds__(X_THREADS) void k_gamma_exact(GammaArgs A, int k, const int32_t *items, int64_t n) {
+    uint16_t *slot_a = nullptr, *slot_b = nullptr;  // the exact pass works from registers and L1/L2
+    const int64_t stride = (int64_t)gridDim.x * X_THREADS;
+    for (int64_t base = (int64_t)blockIdx.x * X_THREADS; base < n; base += stride) {  // block-uniform
         const int64_t i = base + threadIdx.x;
         bool to_slow = false;
         int32_t p = 0;
@@ -1122,6 +1124,21 @@ __device__ inline int simple_lev_cut(const SimpleCol &sc, int ncp_a, int ncp_b) 
 
 __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x,
                             int32_t y, int &level) {
+    // Levenshtein columns: both rows' bit-planes are loaded with the records (same round trip; a
+    // row without planes reads zeros), and the distance is computed from them alone.
+    uint64_t pa[N_PLANES], pb[N_PLANES];
+    if (sc.cls == SC_LEV) {
+        const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
+        const uint4 *qb = reinterpret_cast<const uint4 *>(c1.planes + (int64_t)y * N_PLANES);
+#pragma unroll
+        for (int i = 0; i < N_PLANES / 2; ++i) {
+            const uint4 u = qa[i], v = qb[i];
+            pa[2 * i] = ((uint64_t)u.y << 32) | u.x;
+            pa[2 * i + 1] = ((uint64_t)u.w << 32) | u.z;
+            pb[2 * i] = ((uint64_t)v.y << 32) | v.x;
+            pb[2 * i + 1] = ((uint64_t)v.w << 32) | v.z;
+        }
+    }
     const RecMeta ma = c0.meta[x], mb = c1.meta[y];
     if (ma.len16 < 0 || mb.len16 < 0) {
         level = sc.null_level;
@@ -1153,7 +1170,18 @@ __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDe
                 if (lev < 0) {
                     if (eq == 1) lev = 0;
                     else if (a.n > 64 || b.n > 64 || a.ncp != a.n || b.ncp != b.n) return ST_NEEDS_SLOW;
-                    else lev = lev_exact(a, b, simple_lev_cut(sc, a.ncp, b.ncp));
+                    else if (a.planes && b.planes) {
+                        if (sc.cls != SC_LEV) {  // not preloaded
+#pragma unroll
+                            for (int q = 0; q < N_PLANES; ++q) {
+                                pa[q] = a.planes[q];
+                                pb[q] = b.planes[q];
+                            }
+                        }
+                        lev = lev_rows_planes(pa, a.n, pb, b.n, simple_lev_cut(sc, a.ncp, b.ncp));
+                    } else {
+                        lev = lev_exact(a, b, simple_lev_cut(sc, a.ncp, b.ncp));
+                    }
                 }
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
@@ -1167,7 +1195,8 @@ __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDe
     return ST_DONE;
 }
 
-__global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, int si) {
+__global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *items,
+                                                                   int64_t n) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
     if (threadIdx.x == 0) {
@@ -1178,20 +1207,18 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, i
     __syncthreads();
     const SimpleCol &sc = s_sc;
     const int k = sc.k;
-    const Region R = my_region(A);
-    const int32_t *items = region_list(A, k, R);
-    const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
+    const int64_t stride = (int64_t)gridDim.x * X_THREADS;
     // software pipeline: the next item's pair rows are in flight while this one is evaluated
-    int64_t i = threadIdx.x;
+    int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x;
     int32_t p = 0, x = 0, y = 0;
     if (i < n) {
         p = items[i];
         x = A.pl[p];
         y = A.pr[p];
     }
-    for (int64_t base = 0; base < n; base += X_THREADS) {  // block-uniform trip count
+    for (int64_t base = (int64_t)blockIdx.x * X_THREADS; base < n; base += stride) {  // block-uniform
         const bool have = i < n;
-        const int64_t i2 = i + X_THREADS;
+        const int64_t i2 = i + stride;
         int32_t p2 = 0, x2 = 0, y2 = 0;
         if (i2 < n) {
             p2 = items[i2];
@@ -1597,7 +1624,6 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.n_simple = (int)simple.size();
     A.n_complex = (int)complex_k.size();
     for (int t = 0; t <= 16; ++t) A.slot_beg[t] = slot_beg[t];
-    A.xcd_swizzle = ctx->xcd_swizzle && n_regions % 8 == 0 ? 1 : 0;
     ctx->last_simple = (int)simple.size();
 
     SPK_TRY(ctx->begin(K_GAMMA));
@@ -1640,12 +1666,33 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.slow_off = ctx->slow_off.p;
     std::vector<int> simple_of(K, -1);
     for (size_t i = 0; i < simple.size(); ++i) simple_of[simple[i].k] = (int)i;
+    // compacted work lists: per column, region b's list at prefix offset pref[k][b]
+    std::vector<int64_t> pref((size_t)K * (n_regions + 1), 0), list_base(K + 1, 0);
     for (int k = 0; k < K; ++k) {
-        if (!counts[k]) continue;
+        int64_t acc = 0;
+        for (int b = 0; b < n_regions; ++b) {
+            pref[(size_t)k * (n_regions + 1) + b] = acc;
+            acc += rc[(size_t)k * n_regions + b];
+        }
+        pref[(size_t)k * (n_regions + 1) + n_regions] = acc;
+        list_base[k + 1] = list_base[k] + acc;
+    }
+    if (list_base[K]) {
+        SPK_TRY(ctx->xlist.alloc((size_t)list_base[K]));
+        SPK_TRY(ctx->xpref.alloc(pref.size()));
+        SPK_HIP(hipMemcpyAsync(ctx->xpref.p, pref.data(), pref.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    for (int k = 0; k < K; ++k) {
+        const int64_t cnt = counts[k];
+        if (!cnt) continue;
+        int32_t *items = ctx->xlist.p + list_base[k];
+        k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1), items);
+        int64_t g = (cnt + X_THREADS - 1) / X_THREADS;
+        if (g > 8 * (int64_t)ctx->n_cu) g = 8 * (int64_t)ctx->n_cu;
         if (simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR)
-            k_gamma_exact_simple<<<(unsigned)n_regions, X_THREADS, 0, ctx->stream>>>(A, simple_of[k]);
+            k_gamma_exact_simple<<<(unsigned)g, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], items, cnt);
         else
-            k_gamma_exact<<<(unsigned)n_regions, X_THREADS, 0, ctx->stream>>>(A, k);
+            k_gamma_exact<<<(unsigned)g, X_THREADS, 0, ctx->stream>>>(A, k, items, cnt);
         SPK_HIP(hipGetLastError());
     }
     std::vector<unsigned int> slow_counts((size_t)K, 0);

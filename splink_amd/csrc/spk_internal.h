@@ -176,11 +176,12 @@ struct spk_ctx {
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
-    bool xcd_swizzle = true;          // comparison regions in contiguous ranges per XCD (SPK_XCD_SWIZZLE=0: off)
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)
     spk::DevBuf<int32_t> work, slow;
+    spk::DevBuf<int32_t> xlist;       // compacted exact-pass work lists, column after column
+    spk::DevBuf<int64_t> xpref;       // [K][regions + 1] offsets of each region's list in xlist
     spk::DevBuf<int64_t> slow_off;    // [K+1] slow-pass list offsets
     spk::DevBuf<uint8_t> img[2];      // filter row images of table 0 / table 1
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)

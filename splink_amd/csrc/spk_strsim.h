@@ -407,6 +407,82 @@ __device__ int lev_planes(const uint64_t *planes, int shift, int m, const uint16
     return dist;
 }
 
+// Myers 1999 with both strings as bit-planes: the pattern's match masks are AND_b(±plane_b) as in
+// lev_planes, and the text's units come out of the text's own planes bit-serially (bit j of plane b
+// is bit b of unit j), so the scan issues no memory access at all.  P / T are already shifted to the
+// first unit after the common prefix; bits past m (pattern) and n (text) are ignored.
+template <typename W>
+__device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
+                                       int cut) {
+    W pl[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
+    W vp = ~(W)0, vn = 0;
+    const W hib = (W)1 << (m - 1);
+    int dist = m;
+    for (int h = 0; h < 2 && 32 * h < n; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
+        uint32_t tw[N_PLANES];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        for (int jj = 0; jj < jn; ++jj) {
+            W eq = ~(W)0;
+#pragma unroll
+            for (int b = 0; b < N_PLANES; ++b) {
+                eq &= pl[b] ^ ((W)(tw[b] & 1u) - (W)1);
+                tw[b] >>= 1;
+            }
+            const W x = eq | vn;
+            const W d0 = (((x & vp) + vp) ^ vp) | x;
+            W hp = vn | ~(d0 | vp);
+            W hn = d0 & vp;
+            dist += (hp & hib) ? 1 : 0;
+            dist -= (hn & hib) ? 1 : 0;
+            if (dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
+            hp = (hp << 1) | (W)1;
+            hn = hn << 1;
+            vp = hn | ~(d0 | hp);
+            vn = hp & d0;
+        }
+    }
+    return dist;
+}
+
+// Code-point Levenshtein of two unequal rows that both carry bit-planes (<= 64 units, all < 256, so
+// units are code points), from the planes alone: the common prefix is the lowest set bit of
+// OR_b(a_b ^ b_b), the common suffix the highest of the same with both strings' ends aligned at bit
+// 63; both strips are exact for unit-cost edit distance.  The longer remainder is the pattern, so
+// the scan runs over the shorter one.  `cut` as in lev_planes.
+__device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
+                                      int cut) {
+    if (la == 0) return lb;
+    if (lb == 0) return la;
+    const int mn = la < lb ? la : lb;
+    uint64_t d = 0, e = 0;
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) {
+        d |= pa[b] ^ pb[b];
+        e |= (pa[b] << (64 - la)) ^ (pb[b] << (64 - lb));
+    }
+    int pre = d ? __ffsll((unsigned long long)d) - 1 : 64;
+    if (pre > mn) pre = mn;
+    int suf = e ? __clzll((long long)e) : 64;
+    if (suf > mn - pre) suf = mn - pre;
+    const int ra = la - pre - suf, rb = lb - pre - suf;
+    if (ra == 0) return rb;
+    if (rb == 0) return ra;
+    const bool a_pat = ra >= rb;
+    const int m = a_pat ? ra : rb, n = a_pat ? rb : ra;
+    uint64_t P[N_PLANES], T[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) {
+        P[b] = (a_pat ? pa[b] : pb[b]) >> pre;
+        T[b] = (a_pat ? pb[b] : pa[b]) >> pre;
+    }
+    if (m <= 32) return myers_plane_text<uint32_t>(P, m, T, n, cut);
+    return myers_plane_text<uint64_t>(P, m, T, n, cut);
+}
+
 // Exact Jaro-Winkler for unequal strings of <= 64 units, without LDS.
 __device__ inline double jw_exact(const StrView &a, const StrView &b) {
     const bool fmax = a.n > b.n;  // commons-text: max = first only if strictly longer

@@ -357,3 +357,65 @@ def test_em_histogram_kernels_agree(amd, n_levels):
         hist[:] = d.cpu().numpy().astype(np.uint64)
         got.append(hist)
     assert (got[0] == want).all() and (got[1] == want).all()
+
+
+def _mutate(rng, s, k, alpha):
+    s = list(s)
+    for _ in range(k):
+        op = int(rng.integers(3))
+        i = int(rng.integers(len(s) + 1))
+        if op == 0 or not s:
+            s.insert(i, alpha[int(rng.integers(len(alpha)))])
+        elif op == 1:
+            del s[min(i, len(s) - 1)]
+        else:
+            s[min(i, len(s) - 1)] = alpha[int(rng.integers(len(alpha)))]
+    return "".join(s)
+
+
+def test_levenshtein_levels_exact(amd):
+    """Exact Levenshtein in the template exact pass (bit-plane path, unit path and the global-memory
+    pass): six `<=` levels reveal the distance up to 5, a ratio column checks the division; lengths
+    straddle the 32- and 64-unit word sizes, with shared prefixes / suffixes, Latin-1 and
+    supplementary-plane characters and NULLs."""
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(21))
+    alpha = list("abcde") + ["é", "ü"]
+    left, right = [], []
+    for n in [0, 1, 2, 5, 17, 31, 32, 33, 40, 63, 64, 65, 80]:
+        for k in [0, 1, 2, 3, 5, 8]:
+            for rep in range(6):
+                a = "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), n))
+                if rep == 4:
+                    a = "prefix" + a + "suffix"
+                b = _mutate(rng, a, k, alpha)
+                if rep == 5 and n < 40:
+                    b = b + "\U0001F600"  # surrogate pair: code points != units
+                left.append(a)
+                right.append(b)
+    left += [None, "x", None]
+    right += ["x", None, None]
+    df = pd.DataFrame({"a_l": left, "a_r": right})
+    exact = ("case when a_l is null or a_r is null then -1 "
+             + " ".join(f"when levenshtein(a_l, a_r) <= {d} then {6 - d}" for d in range(6)) + " else 0 end")
+    ratio = ("case when a_l is null or a_r is null then -1 when a_l = a_r then 3 "
+             "when levenshtein(a_l, a_r)/((length(a_l) + length(a_r))/2) <= 0.2 then 2 "
+             "when levenshtein(a_l, a_r)/((length(a_l) + length(a_r))/2) <= 0.4 then 1 else 0 end")
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "lv", "custom_columns_used": ["a"], "num_levels": 7, "case_expression": exact,
+         "m_probabilities": [0.1, 0.1, 0.1, 0.1, 0.1, 0.2, 0.3], "u_probabilities": [0.4, 0.2, 0.1, 0.1, 0.1, 0.05, 0.05]},
+        {"custom_name": "lr", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": ratio}]}
+    got = add_gammas(df, st, amd).gamma_matrix()
+    for i, (a, b) in enumerate(zip(left, right)):
+        if a is None or b is None:
+            assert got[i, 0] == -1 and got[i, 1] == -1
+            continue
+        d = orc.levenshtein(a, b)
+        assert got[i, 0] == (6 - d if d <= 5 else 0), (a, b, d, got[i, 0])
+        if a == b:
+            want = 3
+        else:
+            den = (len(a) + len(b)) / 2.0
+            q = d / den if den else None
+            want = 2 if q is not None and q <= 0.2 else (1 if q is not None and q <= 0.4 else 0)
+        assert got[i, 1] == want, (a, b, d, got[i, 1])
