@@ -180,6 +180,7 @@ void spk_ctx_destroy(spk_ctx *ctx) {
         (void)hipEventDestroy(ctx->ev1[k]);
     }
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
+    if (ctx->h_info) (void)hipHostFree(ctx->h_info);
     hipStream_t own = ctx->own_stream;
     delete ctx;
     if (own) (void)hipStreamDestroy(own);

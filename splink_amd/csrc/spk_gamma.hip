@@ -1075,16 +1075,73 @@ __global__ __launch_bounds__(F_THREADS) void k_gamma_filter(GammaArgs A) {
 // to back (k_compact) -- with a grid-stride loop, so every CU gets the same share of cells however
 // unevenly they fall over the regions (a region of one large block can hold several times the
 // average).  Block b of k_compact copies region b's list to its prefix offset.
-__global__ void k_compact(GammaArgs A, int k, const int64_t *__restrict__ pref, int32_t *__restrict__ out) {
+//
+// The lists are sized on the device, so the pass needs no host round trip between the filter and
+// the exact kernels: k_prefix scans the region counts of every column (one workgroup) into
+// xpref[k][b] and xinfo = [col_base[K] | col_count[K] | overflow | total].  Column k's list
+// starts at xlist + col_base[k]; its slow-pass list (a subset) at the same offset in the second
+// half of xlist.  If the lists exceed the capacity, `overflow` makes every exact kernel a no-op
+// and the host re-runs the phase with room for `total` (codes are untouched until then).
+constexpr int PFX_THREADS = 1024;
+__global__ __launch_bounds__(PFX_THREADS) void k_prefix(const unsigned int *__restrict__ region_count, int K,
+                                                        int n_regions, int64_t cap, int64_t *__restrict__ xpref,
+                                                        int64_t *__restrict__ xinfo) {
+    __shared__ int64_t s[PFX_THREADS];
+    const int per = (n_regions + PFX_THREADS - 1) / PFX_THREADS;
+    const int b0 = threadIdx.x * per;
+    int64_t base = 0;
+    for (int k = 0; k < K; ++k) {
+        const unsigned int *rc = region_count + (int64_t)k * n_regions;
+        int64_t mine = 0;
+        for (int b = b0; b < b0 + per && b < n_regions; ++b) mine += rc[b];
+        s[threadIdx.x] = mine;
+        __syncthreads();
+        for (int off = 1; off < PFX_THREADS; off <<= 1) {
+            const int64_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+            __syncthreads();
+            s[threadIdx.x] += v;
+            __syncthreads();
+        }
+        int64_t acc = s[threadIdx.x] - mine;  // exclusive
+        int64_t *pf = xpref + (int64_t)k * (n_regions + 1);
+        for (int b = b0; b < b0 + per && b < n_regions; ++b) {
+            pf[b] = acc;
+            acc += rc[b];
+        }
+        const int64_t tot = s[PFX_THREADS - 1];
+        if (threadIdx.x == 0) {
+            pf[n_regions] = tot;
+            xinfo[k] = base;
+            xinfo[K + k] = tot;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        xinfo[2 * K] = base > cap ? 1 : 0;
+        xinfo[2 * K + 1] = base;
+    }
+}
+
+__global__ void k_compact(GammaArgs A, int k, const int64_t *__restrict__ pref, int32_t *__restrict__ xlist,
+                          const int64_t *__restrict__ xinfo) {
+    if (xinfo[2 * A.K]) return;  // overflow: the host re-runs the phase
     const Region R = my_region(A);
     const int32_t *src = region_list(A, k, R);
     const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
-    int32_t *dst = out + pref[blockIdx.x];
+    int32_t *dst = xlist + xinfo[k] + pref[blockIdx.x];
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
+__device__ inline int64_t exact_count(const GammaArgs &A, const int64_t *xinfo, int k) {
+    return xinfo[2 * A.K] ? 0 : xinfo[A.K + k];
+}
+
 // Exact pass over column k through the interpreter.
-__global__ __launch_bounds__(X_THREADS) void k_gamma_exact(GammaArgs A, int k, const int32_t *items, int64_t n) {
+__global__ __launch_bounds__(X_THREADS) void k_gamma_exact(GammaArgs A, int k, const int32_t *xlist,
+                                                            const int64_t *xinfo) {
+    const int64_t n = exact_count(A, xinfo, k);
+    const int32_t *items = xlist + xinfo[k];
     uint16_t *slot_a = nullptr, *slot_b = nullptr;  // the exact pass works from registers and L1/L2
     const int64_t stride = (int64_t)gridDim.x * X_THREADS;
     for (int64_t base = (int64_t)blockIdx.x * X_THREADS; base < n; base += stride) {  // block-uniform
@@ -1195,8 +1252,8 @@ __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDe
     return ST_DONE;
 }
 
-__global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *items,
-                                                                   int64_t n) {
+__global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
+                                                                   const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
     if (threadIdx.x == 0) {
@@ -1207,6 +1264,8 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, i
     __syncthreads();
     const SimpleCol &sc = s_sc;
     const int k = sc.k;
+    const int64_t n = exact_count(A, xinfo, k);
+    const int32_t *items = xlist + xinfo[k];
     const int64_t stride = (int64_t)gridDim.x * X_THREADS;
     // software pipeline: the next item's pair rows are in flight while this one is evaluated
     int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x;
@@ -1241,13 +1300,16 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, i
     }
 }
 
-__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k, const int32_t *items, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (i >= n) return;
-    const int32_t p = items[i];
-    int level = 0;
-    eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level);
-    code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+// Global-memory pass over column k's slow list (length on the device; usually empty).
+__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k) {
+    const int64_t n = A.slow_count[k];
+    const int32_t *items = A.slow + A.slow_off[k];
+    for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 64) {
+        const int32_t p = items[i];
+        int level = 0;
+        eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level);
+        code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+    }
 }
 
 __global__ void k_codes_from_gammas(int64_t n, int K, const int8_t *__restrict__ g, const int64_t *__restrict__ stride,
@@ -1650,68 +1712,62 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             SPK_HIP(hipGetLastError());
         }
     }
-    std::vector<unsigned int> rc((size_t)K * n_regions, 0);
-    SPK_HIP(hipMemcpyAsync(rc.data(), ctx->region_count.p, sizeof(unsigned int) * rc.size(), hipMemcpyDeviceToHost,
-                           ctx->stream));
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    std::vector<int64_t> counts((size_t)2 * K, 0);
-    for (int k = 0; k < K; ++k)
-        for (int b = 0; b < n_regions; ++b) counts[k] += rc[(size_t)k * n_regions + b];
-    std::vector<int64_t> slow_off(K + 1, 0);
-    for (int k = 0; k < K; ++k) slow_off[k + 1] = slow_off[k] + counts[k];
-    SPK_TRY(ctx->slow.alloc((size_t)slow_off[K] + 1));
-    SPK_TRY(ctx->slow_off.alloc(slow_off.size()));
-    SPK_HIP(hipMemcpyAsync(ctx->slow_off.p, slow_off.data(), slow_off.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    A.slow = ctx->slow.p;
-    A.slow_off = ctx->slow_off.p;
+    // ---- exact and slow passes, sized on the device (k_prefix): no host round trip
     std::vector<int> simple_of(K, -1);
     for (size_t i = 0; i < simple.size(); ++i) simple_of[simple[i].k] = (int)i;
-    // compacted work lists: per column, region b's list at prefix offset pref[k][b]
-    std::vector<int64_t> pref((size_t)K * (n_regions + 1), 0), list_base(K + 1, 0);
-    for (int k = 0; k < K; ++k) {
-        int64_t acc = 0;
-        for (int b = 0; b < n_regions; ++b) {
-            pref[(size_t)k * (n_regions + 1) + b] = acc;
-            acc += rc[(size_t)k * n_regions + b];
+    std::vector<char> may_exact(K, 1);  // columns whose filter can leave cells undecided
+    for (const SimpleCol &sc : simple)
+        if (sc.kind == SK_NUM || sc.cls == SC_NUM || sc.cls == SC_NUMRAW || (sc.cls == SC_EQ && sc.has_ids))
+            may_exact[sc.k] = 0;
+    const int n_info = 2 * K + 2;
+    SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions + 1)));
+    SPK_TRY(ctx->xinfo.alloc((size_t)n_info));
+    SPK_TRY(ctx->pinned_info((size_t)n_info + K + 1));  // + slow counts (uint32) + err word
+    int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(P, 1 << 16));
+    const int64_t g_exact = std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ctx->n_cu, (P + X_THREADS - 1) / X_THREADS));
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));
+        A.slow = ctx->xlist.p + cap;
+        A.slow_off = ctx->xinfo.p;
+        ctx->xcap = cap;
+        if (P > 0) {
+            k_prefix<<<1, PFX_THREADS, 0, ctx->stream>>>(ctx->region_count.p, K, n_regions, cap, ctx->xpref.p,
+                                                        ctx->xinfo.p);
+            for (int k = 0; k < K; ++k) {
+                if (!may_exact[k]) continue;
+                k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1),
+                                                                       ctx->xlist.p, ctx->xinfo.p);
+                if (simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR)
+                    k_gamma_exact_simple<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], ctx->xlist.p,
+                                                                                           ctx->xinfo.p);
+                else
+                    k_gamma_exact<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+                k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k);
+            }
+            SPK_HIP(hipGetLastError());
+        } else {
+            SPK_HIP(hipMemsetAsync(ctx->xinfo.p, 0, (size_t)n_info * 8, ctx->stream));
         }
-        pref[(size_t)k * (n_regions + 1) + n_regions] = acc;
-        list_base[k + 1] = list_base[k] + acc;
+        SPK_TRY(ctx->end(K_GAMMA));
+        SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_info * 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info, ctx->work_count.p, sizeof(unsigned int) * K, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info + K, A.err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        if (!ctx->h_info[2 * K]) break;
+        cap = ctx->h_info[2 * K + 1];  // exact lists did not fit: nothing ran, grow and redo the phase
+        SPK_REQUIRE(attempt == 0, SPK_E_STATE, "spk_gammas: exact work list sizing failed");
     }
-    if (list_base[K]) {
-        SPK_TRY(ctx->xlist.alloc((size_t)list_base[K]));
-        SPK_TRY(ctx->xpref.alloc(pref.size()));
-        SPK_HIP(hipMemcpyAsync(ctx->xpref.p, pref.data(), pref.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    }
-    for (int k = 0; k < K; ++k) {
-        const int64_t cnt = counts[k];
-        if (!cnt) continue;
-        int32_t *items = ctx->xlist.p + list_base[k];
-        k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1), items);
-        int64_t g = (cnt + X_THREADS - 1) / X_THREADS;
-        if (g > 8 * (int64_t)ctx->n_cu) g = 8 * (int64_t)ctx->n_cu;
-        if (simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR)
-            k_gamma_exact_simple<<<(unsigned)g, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], items, cnt);
-        else
-            k_gamma_exact<<<(unsigned)g, X_THREADS, 0, ctx->stream>>>(A, k, items, cnt);
-        SPK_HIP(hipGetLastError());
-    }
-    std::vector<unsigned int> slow_counts((size_t)K, 0);
-    SPK_HIP(hipMemcpyAsync(slow_counts.data(), ctx->work_count.p, sizeof(unsigned int) * K, hipMemcpyDeviceToHost,
-                           ctx->stream));
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    for (int k = 0; k < K; ++k) counts[K + k] = slow_counts[k];
+    std::vector<int64_t> counts((size_t)2 * K, 0);
+    const unsigned int *h_slow = reinterpret_cast<const unsigned int *>(ctx->h_info + n_info);
     int64_t n_slow = 0;
     for (int k = 0; k < K; ++k) {
-        const unsigned int ns = counts[K + k];
-        n_slow += ns;
-        if (!ns) continue;
-        k_gamma_slow<<<(unsigned)((ns + 63) / 64), 64, 0, ctx->stream>>>(A, k, ctx->slow.p + slow_off[k], ns);
-        SPK_HIP(hipGetLastError());
+        counts[k] = ctx->h_info[K + k];
+        counts[K + k] = h_slow[k];
+        n_slow += h_slow[k];
     }
-    SPK_TRY(ctx->end(K_GAMMA));
     int err = 0;
-    SPK_HIP(hipMemcpyAsync(&err, A.err, sizeof(err), hipMemcpyDeviceToHost, ctx->stream));
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(&err, ctx->h_info + n_info + K, sizeof(err));
     SPK_REQUIRE(!(err & 1), SPK_E_LIMIT, "spk_gammas: a compared string exceeds 1024 UTF-16 units");
     SPK_REQUIRE(!(err & 2), SPK_E_INVALID, "spk_gammas: unknown instruction");
     ctx->codes_valid = true;

@@ -179,10 +179,26 @@ struct spk_ctx {
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)
-    spk::DevBuf<int32_t> work, slow;
-    spk::DevBuf<int32_t> xlist;       // compacted exact-pass work lists, column after column
-    spk::DevBuf<int64_t> xpref;       // [K][regions + 1] offsets of each region's list in xlist
-    spk::DevBuf<int64_t> slow_off;    // [K+1] slow-pass list offsets
+    spk::DevBuf<int32_t> work;
+    spk::DevBuf<int32_t> xlist;       // [2 x xcap]: compacted exact-pass lists, column after column | slow lists
+    spk::DevBuf<int64_t> xpref;       // [K][regions + 1] offsets of each region's list in its column's list
+    spk::DevBuf<int64_t> xinfo;       // [col_base K | col_count K | overflow | total] (k_prefix)
+    int64_t xcap = 0;
+    int64_t *h_info = nullptr;        // pinned readback of xinfo + slow counts
+    size_t h_info_n = 0;
+    int pinned_info(size_t n) {
+        if (n <= h_info_n) return SPK_OK;
+        if (h_info) (void)hipHostFree(h_info);
+        h_info = nullptr;
+        h_info_n = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&h_info), n * 8, hipHostMallocDefault) != hipSuccess) {
+            h_info = nullptr;
+            spk::set_error("hipHostMalloc failed");
+            return SPK_E_OOM;
+        }
+        h_info_n = n;
+        return SPK_OK;
+    }
     spk::DevBuf<uint8_t> img[2];      // filter row images of table 0 / table 1
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)
     spk::DevBuf<unsigned int> work_count;    // [K] slow-pass list lengths

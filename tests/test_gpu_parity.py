@@ -419,3 +419,28 @@ def test_levenshtein_levels_exact(amd):
             q = d / den if den else None
             want = 2 if q is not None and q <= 0.2 else (1 if q is not None and q <= 0.4 else 0)
         assert got[i, 1] == want, (a, b, d, got[i, 1])
+
+
+def test_exact_work_lists_grow(amd):
+    """More undecided cells than the exact-pass lists hold on the first try (3 columns x 40k pairs of
+    anagrams, which no length / letter-count bound decides): the lists are re-sized on the device
+    side and the pass re-run, with the same levels as the oracle."""
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(33))
+    n = 40000
+    base = np.array(list("abcdefghij"))
+    data = {}
+    for c in ("x", "y", "z"):
+        data[f"{c}_l"] = ["".join(rng.permutation(base)) for _ in range(n)]
+        data[f"{c}_r"] = ["".join(rng.permutation(base)) for _ in range(n)]
+    df = pd.DataFrame(data)
+    expr = ("case when {c}_l is null or {c}_r is null then -1 when levenshtein({c}_l, {c}_r) <= 5 then 2 "
+            "when levenshtein({c}_l, {c}_r) <= 7 then 1 else 0 end")
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": c, "custom_columns_used": [c], "num_levels": 3, "case_expression": expr.format(c=c)}
+        for c in ("x", "y", "z")]}
+    got = add_gammas(df, st, amd).gamma_matrix()
+    for j, c in enumerate(("x", "y", "z")):
+        d = np.array([orc.levenshtein(a, b) for a, b in zip(data[f"{c}_l"], data[f"{c}_r"])])
+        want = np.where(d <= 5, 2, np.where(d <= 7, 1, 0))
+        assert (got[:, j] == want).all(), c
