@@ -190,6 +190,28 @@ class Context:
         check(self._lib.spk_pairs_load(self._h, ctypes.c_int64(len(rows_l)), _ptr(rows_l), _ptr(rows_r)),
               "spk_pairs_load")
 
+    @staticmethod
+    def gammas_args(programs, when_first, when_n, when_level, instrs, operands, lit_offsets, lit_bytes):
+        """The spk_gammas argument list, converted once (cached by the caller across calls)."""
+        programs = np.ascontiguousarray(programs, dtype=PROGRAM_DTYPE)
+        wf = np.ascontiguousarray(when_first, dtype=np.int32)
+        wn = np.ascontiguousarray(when_n, dtype=np.int32)
+        wl = np.ascontiguousarray(when_level, dtype=np.int32)
+        instrs = np.ascontiguousarray(instrs, dtype=INSTR_DTYPE)
+        operands = np.ascontiguousarray(operands, dtype=OPERAND_DTYPE)
+        lo = np.ascontiguousarray(lit_offsets, dtype=np.int64)
+        lb = np.ascontiguousarray(lit_bytes, dtype=np.uint8)
+        if lb.size == 0:
+            lb = np.zeros(1, dtype=np.uint8)
+        keep = (programs, wf, wn, wl, instrs, operands, lo, lb)
+        c_args = (ctypes.c_int(len(programs)), _ptr(programs), ctypes.c_int(len(wf)), _ptr(wf), _ptr(wn), _ptr(wl),
+                  ctypes.c_int(len(instrs)), _ptr(instrs), ctypes.c_int(len(operands)), _ptr(operands),
+                  ctypes.c_int(len(lo) - 1), _ptr(lo), _ptr(lb))
+        return keep, c_args
+
+    def gammas_native(self, args):
+        check(self._lib.spk_gammas(self._h, *args[1]), "spk_gammas")
+
     def gammas(self, programs, when_first, when_n, when_level, instrs, operands, lit_offsets, lit_bytes):
         programs = np.ascontiguousarray(programs, dtype=PROGRAM_DTYPE)
         wf = np.ascontiguousarray(when_first, dtype=np.int32)

@@ -1904,6 +1904,7 @@ static int run_udf(spk_ctx *ctx, int op, int64_t n, const int64_t *l_off, const 
     SPK_TRY(d_cp.alloc(cp.size() + 1));
     SPK_TRY(d_out.alloc((size_t)n + 1));
     SPK_TRY(d_err.alloc(1));
+    SPK_HIP(hipMemsetAsync(d_err.p, 0, sizeof(int), ctx->stream));  // hipMalloc does not zero
     SPK_HIP(hipMemcpyAsync(d_u.p, u.data(), u.size() * 2, hipMemcpyHostToDevice, ctx->stream));
     SPK_HIP(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     if (!cp.empty()) SPK_HIP(hipMemcpyAsync(d_cp.p, cp.data(), cp.size() * 4, hipMemcpyHostToDevice, ctx->stream));

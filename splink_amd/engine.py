@@ -232,20 +232,22 @@ class Job:
     # ---- comparison vectors -----------------------------------------------------------------------
     def _compiled(self, settings):
         """The comparison program and its native buffers, compiled once per distinct comparison_columns."""
-        key = json.dumps(settings["comparison_columns"], sort_keys=True, default=str)
+        # the program depends only on each column's name, level count and CASE text
+        key = tuple((c.get("col_name"), c.get("custom_name"), c.get("num_levels"), c.get("case_expression"))
+                    for c in settings["comparison_columns"])
         cache = self.__dict__.setdefault("_prog_cache", {})
         if key not in cache:
             prog = compile_comparisons(settings, self.schema)
             index = {k: self.column_index(*k) for k in prog.columns}
             lit_off, lit_bytes = prog.literal_buffers()
-            args = (prog.programs, prog.when_first, prog.when_n, prog.when_level, prog.instrs,
-                    prog.native_operands(index), lit_off, lit_bytes)
+            args = N.Context.gammas_args(prog.programs, prog.when_first, prog.when_n, prog.when_level, prog.instrs,
+                                         prog.native_operands(index), lit_off, lit_bytes)
             cache[key] = (prog, args)
         return cache[key]
 
     def gammas(self, settings, token=None) -> CompiledComparisons:
         prog, args = self._compiled(settings)
-        self.ctx.gammas(*args)
+        self.ctx.gammas_native(args)
         self.codes_token = token if token is not None else object()
         self.code_meta = (prog.gamma_names, prog.n_levels)
         return prog
@@ -300,19 +302,29 @@ class Job:
         return self.ctx.score(float(lam), float(1 - lam), m, u, 0, self.n_pairs, want_host)
 
 
+def _sum_lr(xs):
+    acc = 0.0
+    for x in xs:
+        acc += x
+    return acc
+
+
 def m_step_rows(stats, gamma_names, n_levels):
     """λ and the collected π rows (maximisation_step.py:16-90) from the device statistics,
     with Spark's NULL and float32 semantics."""
+    stats = [float(x) for x in stats]
     S, rows, nn = stats[0], stats[1], stats[2]
     new_lambda = f32(S / rows) if (rows > 0 and nn > 0) else None
     out = []
     off = N_HEAD
     for name, L in zip(gamma_names, n_levels):
-        slots = np.asarray(stats[off: off + 4 * (L + 1)]).reshape(L + 1, 4)
+        slots = [stats[off + 4 * i: off + 4 * i + 4] for i in range(L + 1)]
         off += 4 * (L + 1)
         observed = slots[1:]
-        den_nonnull = observed[:, 1].sum() > 0
-        den_m, den_u = observed[:, 2].sum(), observed[:, 3].sum()
+        # the denominators sum the observed levels in level order, as numpy's pairwise sum did for
+        # these short vectors (<= 8 terms: plain left-to-right addition)
+        den_nonnull = sum(o[1] for o in observed) > 0
+        den_m, den_u = _sum_lr([o[2] for o in observed]), _sum_lr([o[3] for o in observed])
         for v in range(-1, L):
             r, nnv, sm, su = slots[v + 1]
             if r == 0:
