@@ -1181,21 +1181,7 @@ __device__ inline int simple_lev_cut(const SimpleCol &sc, int ncp_a, int ncp_b) 
 
 __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x,
                             int32_t y, int &level) {
-    // Levenshtein columns: both rows' bit-planes are loaded with the records (same round trip; a
-    // row without planes reads zeros), and the distance is computed from them alone.
     uint64_t pa[N_PLANES], pb[N_PLANES];
-    if (sc.cls == SC_LEV) {
-        const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
-        const uint4 *qb = reinterpret_cast<const uint4 *>(c1.planes + (int64_t)y * N_PLANES);
-#pragma unroll
-        for (int i = 0; i < N_PLANES / 2; ++i) {
-            const uint4 u = qa[i], v = qb[i];
-            pa[2 * i] = ((uint64_t)u.y << 32) | u.x;
-            pa[2 * i + 1] = ((uint64_t)u.w << 32) | u.z;
-            pb[2 * i] = ((uint64_t)v.y << 32) | v.x;
-            pb[2 * i + 1] = ((uint64_t)v.w << 32) | v.z;
-        }
-    }
     const RecMeta ma = c0.meta[x], mb = c1.meta[y];
     if (ma.len16 < 0 || mb.len16 < 0) {
         level = sc.null_level;
@@ -1228,12 +1214,10 @@ __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDe
                     if (eq == 1) lev = 0;
                     else if (a.n > 64 || b.n > 64 || a.ncp != a.n || b.ncp != b.n) return ST_NEEDS_SLOW;
                     else if (a.planes && b.planes) {
-                        if (sc.cls != SC_LEV) {  // not preloaded
 #pragma unroll
-                            for (int q = 0; q < N_PLANES; ++q) {
-                                pa[q] = a.planes[q];
-                                pb[q] = b.planes[q];
-                            }
+                        for (int q = 0; q < N_PLANES; ++q) {
+                            pa[q] = a.planes[q];
+                            pb[q] = b.planes[q];
                         }
                         lev = lev_rows_planes(pa, a.n, pb, b.n, simple_lev_cut(sc, a.ncp, b.ncp));
                     } else {
@@ -1252,7 +1236,67 @@ __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDe
     return ST_DONE;
 }
 
-__global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
+// Exact pass cell of a Levenshtein-class template column (tests: `=` / `<>`, levenshtein [ratio]):
+// both rows' bit-planes are loaded in the same round trip as the records and the distance comes
+// from them alone (lev_rows_planes).  Rows without planes (> 64 units or a unit >= 256) go to the
+// global-memory pass.  A kernel of its own, so its register budget is not the JW path's.
+__device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level) {
+    uint64_t pa[N_PLANES], pb[N_PLANES];
+    {
+        const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
+        const uint4 *qb = reinterpret_cast<const uint4 *>(c1.planes + (int64_t)y * N_PLANES);
+#pragma unroll
+        for (int i = 0; i < N_PLANES / 2; ++i) {
+            const uint4 u = qa[i], v = qb[i];
+            pa[2 * i] = ((uint64_t)u.y << 32) | u.x;
+            pa[2 * i + 1] = ((uint64_t)u.w << 32) | u.z;
+            pb[2 * i] = ((uint64_t)v.y << 32) | v.x;
+            pb[2 * i + 1] = ((uint64_t)v.w << 32) | v.z;
+        }
+    }
+    const RecMeta ma = c0.meta[x], mb = c1.meta[y];
+    if (ma.len16 < 0 || mb.len16 < 0) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    int eq = meta_equal(ma, mb);
+    if (eq < 0) eq = units_equal(row_view(c0, ma, x, sc.col), row_view(c1, mb, y, sc.col)) ? 1 : 0;
+    const int na = meta_cplen(ma), nb = meta_cplen(mb);
+    const bool planes = (ma.cpf & mb.cpf & CPF_PLANES) != 0;
+    int lev = -1;
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int op = sc.op[i], cmp = sc.cmp[i];
+        const double t = sc.t[i];
+        int r;
+        if (op == SPK_OP_STR_CMP) {
+            r = ((eq == 1) == (cmp == SPK_CMP_EQ)) ? KT : KF;
+        } else {
+            const double den = (double)(na + nb) / 2.0;
+            if (op == SPK_OP_LEVRATIO && den == 0.0) {
+                r = KN;
+            } else {
+                if (lev < 0) {
+                    if (eq == 1) lev = 0;
+                    else if (!planes) return ST_NEEDS_SLOW;
+                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb));
+                }
+                r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
+            }
+        }
+        if (r == KT) {
+            level = sc.level[i];
+            return ST_DONE;
+        }
+    }
+    level = sc.else_level;
+    return ST_DONE;
+}
+
+// The Levenshtein variant is latency-bound (record + plane loads per cell): it keeps registers to
+// LEV_WAVES waves per SIMD so enough cells are in flight.
+constexpr int LEV_WAVES = 1;
+template <bool LEV>
+__global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : 1) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
                                                                    const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
@@ -1287,7 +1331,8 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_exact_simple(GammaArgs A, i
         bool to_slow = false;
         if (have) {
             int level = 0;
-            if (simple_exact(A, sc, s_c0, s_c1, x, y, level) == ST_DONE)
+            const int st = LEV ? lev_cell(sc, s_c0, s_c1, x, y, level) : simple_exact(A, sc, s_c0, s_c1, x, y, level);
+            if (st == ST_DONE)
                 code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
             else
                 to_slow = true;
@@ -1737,9 +1782,12 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 if (!may_exact[k]) continue;
                 k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1),
                                                                        ctx->xlist.p, ctx->xinfo.p);
-                if (simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR)
-                    k_gamma_exact_simple<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], ctx->xlist.p,
-                                                                                           ctx->xinfo.p);
+                if (simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV)
+                    k_gamma_exact_simple<true><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
+                        A, simple_of[k], ctx->xlist.p, ctx->xinfo.p);
+                else if (simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR)
+                    k_gamma_exact_simple<false><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
+                        A, simple_of[k], ctx->xlist.p, ctx->xinfo.p);
                 else
                     k_gamma_exact<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
                 k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k);

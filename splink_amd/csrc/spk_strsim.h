@@ -407,16 +407,25 @@ __device__ int lev_planes(const uint64_t *planes, int shift, int m, const uint16
     return dist;
 }
 
-// Myers 1999 with both strings as bit-planes: the pattern's match masks are AND_b(±plane_b) as in
-// lev_planes, and the text's units come out of the text's own planes bit-serially (bit j of plane b
-// is bit b of unit j), so the scan issues no memory access at all.  P / T are already shifted to the
-// first unit after the common prefix; bits past m (pattern) and n (text) are ignored.
+// Myers 1999 with both strings as bit-planes: the pattern's match mask for text unit j is
+// AND_b(bit b of unit j ? plane_b : ~plane_b), and bit b of unit j is bit j of the text's plane b,
+// so the scan issues no memory access at all.  Per plane and unit: one signed bit-field extract
+// (0 or all ones), one bit-select between the plane and its complement, one AND.  P / T are shifted
+// to the first unit after the common prefix; bits past m (pattern) and n (text) are ignored.
+template <typename W>
+__device__ inline W lane_mask(uint32_t m32) {  // 0 / all ones -> W
+    return sizeof(W) == 4 ? (W)m32 : (W)(((uint64_t)m32 << 32) | m32);
+}
+
 template <typename W>
 __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
                                        int cut) {
-    W pl[N_PLANES];
+    W pl[N_PLANES], npl[N_PLANES];
 #pragma unroll
-    for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
+    for (int b = 0; b < N_PLANES; ++b) {
+        pl[b] = (W)P[b];
+        npl[b] = ~pl[b];
+    }
     W vp = ~(W)0, vn = 0;
     const W hib = (W)1 << (m - 1);
     int dist = m;
@@ -429,8 +438,8 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
             W eq = ~(W)0;
 #pragma unroll
             for (int b = 0; b < N_PLANES; ++b) {
-                eq &= pl[b] ^ ((W)(tw[b] & 1u) - (W)1);
-                tw[b] >>= 1;
+                const W mb = lane_mask<W>((uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1));
+                eq &= (mb & pl[b]) | (~mb & npl[b]);
             }
             const W x = eq | vn;
             const W d0 = (((x & vp) + vp) ^ vp) | x;
@@ -479,7 +488,8 @@ __device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, co
         P[b] = (a_pat ? pa[b] : pb[b]) >> pre;
         T[b] = (a_pat ? pb[b] : pa[b]) >> pre;
     }
-    if (m <= 32) return myers_plane_text<uint32_t>(P, m, T, n, cut);
+    // one word width for all active lanes: a wave that mixed both would run both loops
+    if (!__any(m > 32)) return myers_plane_text<uint32_t>(P, m, T, n, cut);
     return myers_plane_text<uint64_t>(P, m, T, n, cut);
 }
 
