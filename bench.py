@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--records", type=int, default=1_000_000, help="records at N=1 (scaled by sqrt(N))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--em-scale", type=int, default=8,
+                    help="separate E/M streaming row: the run's comparison vectors tiled this many times (0 = off)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,6 +175,10 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(job, df, st, args.cpu_seconds)
 
+    em_scale = None
+    if world == 1 and args.em_scale > 0:
+        em_scale = em_streaming(job, names, nlev, params, args.em_scale)
+
     out = {
         "metric": "candidate pairs scored/sec (gammas+E+M per iter)",
         "value": total_pairs / (ms_per_step / 1e3),
@@ -198,12 +204,52 @@ def main():
         "deferred_pairs": job.ctx.gammas_deferred(),
         "exact_cells_per_column": dict(zip(names, job.ctx.gammas_exact_counts(len(names)))),
         "cpu_baseline": cpu,
+        "em_at_scale": em_scale,
     }
     print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
+
+
+def em_streaming(job, names, nlev, params, reps, iters=10):
+    """Separate labelled row (never the headline): the E/M kernels at a per-GPU pair count where
+    launch ramp and fixed costs no longer dominate -- the run's own comparison vectors tiled `reps`
+    times (cfg4 puts ~125-250M pairs on each GPU, cfg5 ~1.25B).  Reports k_hist (2 B/pair) and the
+    final scoring pass k_score (2 + 8 B/pair) against HBM peak, the per-iteration re-streaming EM
+    rate, and the O(#patterns) finalize alone (the iteration-invariant 'pattern-count' EM cost)."""
+    g = job.gammas_host()
+    big = np.tile(g, (reps, 1))
+    del g
+    job.load_gammas(names, nlev, big)
+    P = big.shape[0]
+    del big
+    cb = 2 if job.ctx.n_patterns() <= 65536 else 4
+    lam, lp = params.params["λ"], params._level_probabilities()
+    for _ in range(2):
+        job.em_stats(lam, lp)
+    hist, fin = [], []
+    for _ in range(iters):
+        job.em_stats(lam, lp)
+        ms = job.ctx.kernel_ms()
+        hist.append(ms["em_hist"])
+        fin.append(ms["em_final"])
+    sc = []
+    for _ in range(3):
+        job.score(lam, lp, want_host=False)
+        sc.append(job.ctx.kernel_ms()["score"])
+    h, f, s = float(np.median(hist)), float(np.median(fin)), float(np.median(sc[1:]))
+    hb, sb = P * cb, P * (cb + 8)
+    return {"pairs": P, "source": f"the run's comparison vectors tiled x{reps}",
+            "k_hist": {"bound": "hbm", "avg_launch_ms": h, "algorithmic_bytes_per_launch": hb,
+                       "achieved": hb / (h / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": hb / (h / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "k_score": {"bound": "hbm", "avg_launch_ms": s, "algorithmic_bytes_per_launch": sb,
+                        "achieved": sb / (s / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": sb / (s / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "em_restream_pairs_per_s": P / ((h + f) / 1e3),
+            "pattern_count_em_ms_per_iter": f}
 
 
 def cpu_baseline(job, df, st, seconds):

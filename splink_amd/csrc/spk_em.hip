@@ -110,10 +110,23 @@ __global__ __launch_bounds__(HL_THREADS) void k_hist_lanes(const CodeT *__restri
             atomicAdd(&sh[c * R + copy], 1u);
         }
     };
-    for (; v + (HL_UNROLL - 1) * stride < n_vec; v += HL_UNROLL * stride) {
-        u32x4 w[HL_UNROLL];
+    // Software-pipelined: the next group's HL_UNROLL loads are issued before the current group's
+    // LDS counts, so every lane keeps 2 x HL_UNROLL x 16 B in flight while it counts.
+    const int64_t step = HL_UNROLL * stride;
+    bool have = v + (HL_UNROLL - 1) * stride < n_vec;
+    u32x4 w[HL_UNROLL];
+    if (have) {
 #pragma unroll
         for (int u = 0; u < HL_UNROLL; ++u) w[u] = __builtin_nontemporal_load(cv + v + u * stride);
+    }
+    while (have) {
+        const int64_t vn = v + step;
+        const bool hn = vn + (HL_UNROLL - 1) * stride < n_vec;
+        u32x4 x[HL_UNROLL];
+        if (hn) {
+#pragma unroll
+            for (int u = 0; u < HL_UNROLL; ++u) x[u] = __builtin_nontemporal_load(cv + vn + u * stride);
+        }
 #pragma unroll
         for (int u = 0; u < HL_UNROLL; ++u) {
             count_word(w[u].x);
@@ -121,6 +134,10 @@ __global__ __launch_bounds__(HL_THREADS) void k_hist_lanes(const CodeT *__restri
             count_word(w[u].z);
             count_word(w[u].w);
         }
+#pragma unroll
+        for (int u = 0; u < HL_UNROLL; ++u) w[u] = x[u];
+        v = vn;
+        have = hn;
     }
     for (; v < n_vec; v += stride) {
         const u32x4 w = cv[v];
@@ -288,12 +305,55 @@ __global__ __launch_bounds__(S_THREADS) void k_em_stats(PatArgs A0, const unsign
     }
 }
 
-template <typename CodeT>
-__global__ void k_score(const CodeT *__restrict__ codes, int64_t start, int64_t n, const double *__restrict__ mpat,
-                        double *__restrict__ mp) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    mp[i] = mpat[codes[start + i]];
+// Final E-step: mp[i] = mpat[code[i]] for pairs [start, start + n).  Each lane turns two codes into
+// one 16-byte store of two doubles, so a wave instruction writes 1 KiB contiguous (the 8 B/pair of
+// output is the dominant stream); the per-pattern table sits in LDS when it fits.  The odd pair at
+// either end (when start or start + n is odd) is written by lane 0 of block 0.
+constexpr int SC_THREADS = 256;
+constexpr int SC_UNROLL = 4;
+constexpr int SC_LDS_PAT = 4096;
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <typename CodeT, bool LDS>
+__global__ __launch_bounds__(SC_THREADS) void k_score(const CodeT *__restrict__ codes, int64_t start, int64_t n,
+                                                      const double *__restrict__ mpat, int n_pat,
+                                                      double *__restrict__ mp) {
+    __shared__ double tab[LDS ? SC_LDS_PAT : 1];
+    if (LDS) {
+        for (int b = threadIdx.x; b < n_pat; b += SC_THREADS) tab[b] = mpat[b];
+        __syncthreads();
+    }
+    const double *T = LDS ? tab : mpat;
+    const int64_t head = start & 1;
+    const int64_t n2 = (n - head) / 2;  // pairs of pairs, from the even ordinal start + head
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (head && n > 0) mp[0] = T[codes[start]];
+        if (n - head > 2 * n2) mp[n - 1] = T[codes[start + n - 1]];
+    }
+    typedef CodeT code2 __attribute__((ext_vector_type(2)));
+    const code2 *c = reinterpret_cast<const code2 *>(codes + start + head);
+    f64x2 *out = reinterpret_cast<f64x2 *>(mp + head);
+    const int64_t stride = (int64_t)gridDim.x * SC_THREADS;
+    int64_t v = (int64_t)blockIdx.x * SC_THREADS + threadIdx.x;
+    for (; v + (SC_UNROLL - 1) * stride < n2; v += SC_UNROLL * stride) {
+        code2 a[SC_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SC_UNROLL; ++u) a[u] = __builtin_nontemporal_load(c + v + u * stride);
+#pragma unroll
+        for (int u = 0; u < SC_UNROLL; ++u) {
+            f64x2 o;
+            o.x = T[a[u].x];
+            o.y = T[a[u].y];
+            __builtin_nontemporal_store(o, out + v + u * stride);
+        }
+    }
+    for (; v < n2; v += stride) {
+        const code2 a = c[v];
+        f64x2 o;
+        o.x = T[a.x];
+        o.y = T[a.y];
+        __builtin_nontemporal_store(o, out + v);
+    }
 }
 
 __global__ void k_tf_accumulate(int64_t P, const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
@@ -502,13 +562,21 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
     SPK_HIP(hipGetLastError());
     ctx->mpat_valid = true;
     if (count) {
-        unsigned g = (unsigned)((count + 255) / 256);
-        if (ctx->code_bytes == 2)
-            k_score<uint16_t><<<g, 256, 0, ctx->stream>>>(reinterpret_cast<const uint16_t *>(ctx->codes.p), start,
-                                                          count, ctx->mpat.p, ctx->mp.p + start);
-        else
-            k_score<uint32_t><<<g, 256, 0, ctx->stream>>>(reinterpret_cast<const uint32_t *>(ctx->codes.p), start,
-                                                          count, ctx->mpat.p, ctx->mp.p + start);
+        int64_t g = (count / 2 + SC_THREADS - 1) / SC_THREADS;
+        if (g > 8 * (int64_t)ctx->n_cu) g = 8 * (int64_t)ctx->n_cu;  // grid-stride: 8 workgroups per CU
+        if (g < 1) g = 1;
+        const int np = (int)ctx->n_patterns;
+        const bool lds = ctx->n_patterns <= SC_LDS_PAT;
+        const auto *c16 = reinterpret_cast<const uint16_t *>(ctx->codes.p);
+        const auto *c32 = reinterpret_cast<const uint32_t *>(ctx->codes.p);
+        double *o = ctx->mp.p + start;
+        if (ctx->code_bytes == 2) {
+            if (lds) k_score<uint16_t, true><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c16, start, count, ctx->mpat.p, np, o);
+            else k_score<uint16_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c16, start, count, ctx->mpat.p, np, o);
+        } else {
+            if (lds) k_score<uint32_t, true><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c32, start, count, ctx->mpat.p, np, o);
+            else k_score<uint32_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c32, start, count, ctx->mpat.p, np, o);
+        }
         SPK_HIP(hipGetLastError());
     }
     SPK_TRY(ctx->end(K_SCORE));

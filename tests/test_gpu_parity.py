@@ -284,6 +284,13 @@ def test_em_at_scale_matches_oracle(amd):
             assert all(rel_close(a, b) for a, b in zip(u, u_o[k]))
     mp = job.score(params.params["λ"], params._level_probabilities())
     assert np.allclose(mp, mp_o, rtol=1e-9, atol=0)
+    # ranges of the scoring kernel: odd / even start and length, single pairs, empty ranges
+    lam = params.params["λ"]
+    m_t, u_t = job.flat_tables(params._level_probabilities())
+    n = len(mp)
+    for start, count in [(0, 1), (1, 0), (1, 1), (1, 2), (1, 7), (2, 6), (3, n - 3), (n - 1, 1), (n - 2, 2)]:
+        got = job.ctx.score(float(lam), float(1 - lam), m_t, u_t, start, count)
+        assert np.array_equal(got, mp[start:start + count], equal_nan=True), (start, count)
 
 
 def test_cross_column_equality(amd):
