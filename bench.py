@@ -33,6 +33,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level
 # (scripts_gpu_round.sh -> tools/traffic.py); the counters cannot be read inside a timed run.
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1_traffic.json")
 COLS = ["first_name", "surname", "dob", "city", "email"]
+WORKLOADS = {2: "cfg2: synthetic person-record dedupe, 1M x sqrt(N) records, blocking surname|dob, "
+                "5 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3)",
+             5: "cfg5 columns at cfg2 size: synthetic person-record dedupe, 1M x sqrt(N) records, blocking "
+                "surname|dob, 6 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3, free-text address "
+                "30-128 chars Levenshtein-4)"}
 
 
 def log(*a):
@@ -45,6 +50,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--records", type=int, default=1_000_000, help="records at N=1 (scaled by sqrt(N))")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="2: the headline workload; 5: + free-text address Levenshtein-4 (cfg5's columns at cfg2's size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--em-scale", type=int, default=8,
@@ -71,10 +78,11 @@ def main():
 
     n_records = int(round(args.records * math.sqrt(world)))
     t0 = time.time()
-    df = make_records(n_records, surname_vocab=15000)[["unique_id"] + COLS]
+    cols = COLS + (["address"] if args.config == 5 else [])
+    df = make_records(n_records, surname_vocab=15000, with_address=args.config == 5)[["unique_id"] + cols]
     log(f"[rank {rank}] generated {n_records} records in {time.time() - t0:.1f}s")
 
-    settings = cfg_settings(2, max_iterations=10)
+    settings = cfg_settings(args.config, max_iterations=10)
     params = Params(settings, AmdSession(local))
     st = params.settings
 
@@ -148,7 +156,7 @@ def main():
     g_ms = float(np.mean(gamma_ms))
     h_ms = float(np.mean(hist_ms))
     rec_bytes = 0
-    for c in COLS:
+    for c in cols:
         s = df[c].dropna()
         rec_bytes += int(s.str.len().sum()) * 2 + 8 * 3 * len(df)  # UTF-16 units + offset/len/hash per row
     gamma_bytes = local_pairs * (8 + code_bytes) + rec_bytes
@@ -173,7 +181,7 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(job, df, st, args.cpu_seconds)
+        cpu = cpu_baseline(job, df, st, args.cpu_seconds, cols)
 
     em_scale = None
     if world == 1 and args.em_scale > 0:
@@ -192,9 +200,8 @@ def main():
         "vs_baseline": None,
         "dtype": "fp64",
         "data": "synthetic",
-        "config": {"workload": "cfg2: synthetic person-record dedupe, 1M x sqrt(N) records, blocking surname|dob, "
-                               "5 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3)",
-                   "records": n_records, "candidate_pairs": total_pairs, "comparison_columns": 5,
+        "config": {"workload": WORKLOADS[args.config],
+                   "records": n_records, "candidate_pairs": total_pairs, "comparison_columns": len(cols),
                    "parallelism": f"pair-ordinal shards x{world}, RCCL all-reduce of pattern histogram"},
         "roofline": roofline,
         "roofline_em": em_roofline,
@@ -252,7 +259,7 @@ def em_streaming(job, names, nlev, params, reps, iters=10):
             "pattern_count_em_ms_per_iter": f}
 
 
-def cpu_baseline(job, df, st, seconds):
+def cpu_baseline(job, df, st, seconds, col_names):
     """The CPU oracle (C/OpenMP restatement) on a bounded sample of the same pairs: γ + E + M."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
@@ -260,8 +267,9 @@ def cpu_baseline(job, df, st, seconds):
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     l, r = job.pair_rows()
     t = job.tables[0]  # pair rows index the job's (blocking-key clustered) table
-    cols = [orc.StrCol(t[c].tolist()) for c in COLS]
-    specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
+    cols = [orc.StrCol(t[c].tolist()) for c in col_names]
+    specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3]),
+             ("lev", 4, [0.2, 0.4])][:len(col_names)]
     lp = [(c["m_probabilities"], c["u_probabilities"]) for c in st["comparison_columns"]]
     nlev = [c["num_levels"] for c in st["comparison_columns"]]
     n = min(len(l), 200_000)
@@ -274,7 +282,7 @@ def cpu_baseline(job, df, st, seconds):
             break
         n = min(len(l), int(n * max(2.0, seconds / 2 / max(dt, 1e-3))))
     return {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of the same candidate pairs, gammas (5 template columns) + one E+M pass, "
+            "sample": f"first {n} of the same candidate pairs, gammas ({len(col_names)} template columns) + one E+M pass, "
                       f"oracle/splink_oracle.c OpenMP ({dt:.1f}s)"}
 
 

@@ -25,6 +25,7 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
             d.units = c->units.p;
             d.meta = c->meta.p;
             d.planes = c->planes.p;
+            d.planes_hi = c->planes_hi.n ? c->planes_hi.p : nullptr;
         } else if (c && c->kind == COL_NUM) {
             d.val = c->val.p;
             d.valid = c->valid.p;
@@ -47,7 +48,7 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
 __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const uint8_t *__restrict__ bytes,
                               const uint8_t *__restrict__ valid, uint16_t *__restrict__ units,
                               RecMeta *__restrict__ meta, uint64_t *__restrict__ planes,
-                              const int64_t *__restrict__ ids) {
+                              uint64_t *__restrict__ planes_hi, const int64_t *__restrict__ ids) {
     int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= n) return;
     RecMeta m;
@@ -61,6 +62,8 @@ __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const
         m.sketch = 0;
         meta[row] = m;
         for (int b = 0; b < N_PLANES; ++b) planes[row * N_PLANES + b] = 0;
+        if (planes_hi)
+            for (int b = 0; b < N_PLANES; ++b) planes_hi[row * N_PLANES + b] = 0;
         return;
     }
     int64_t b = off8[row], e = off8[row + 1];
@@ -93,20 +96,29 @@ __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const
         }
         ++nc;
     }
-    // bit-planes for short Latin-1 rows
-    uint64_t pl[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0};
-    bool ok = nu <= 64;
-    for (int i = 0; ok && i < nu; ++i) {
+    // bit-planes for Latin-1 rows of <= 64 units (one word) or, when the column has planes_hi,
+    // <= PLANES2_MAX units (two words)
+    uint64_t pl[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0}, ph[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool latin = nu <= (planes_hi ? PLANES2_MAX : 64);
+    for (int i = 0; latin && i < nu; ++i) {
         const uint32_t c = dst[i];
-        if (c >= 256) { ok = false; break; }
+        if (c >= 256) { latin = false; break; }
 #pragma unroll
-        for (int b = 0; b < N_PLANES; ++b) pl[b] |= (uint64_t)((c >> b) & 1u) << i;
+        for (int b = 0; b < N_PLANES; ++b) {
+            const uint64_t bit = (uint64_t)((c >> b) & 1u) << (i & 63);
+            if (i < 64) pl[b] |= bit;
+            else ph[b] |= bit;
+        }
     }
+    const bool ok = latin && nu <= 64, ok2 = latin && nu > 64;
 #pragma unroll
-    for (int b = 0; b < N_PLANES; ++b) planes[row * N_PLANES + b] = ok ? pl[b] : 0;
+    for (int b = 0; b < N_PLANES; ++b) planes[row * N_PLANES + b] = (ok || ok2) ? pl[b] : 0;
+    if (planes_hi)
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) planes_hi[row * N_PLANES + b] = ok2 ? ph[b] : 0;
     for (int i = 0; i < 4 && i < nu; ++i) m.head |= (uint64_t)dst[i] << (16 * i);
     m.len16 = nu;
-    m.cpf = (uint32_t)nc | (ok ? CPF_PLANES : 0u) | (ids ? CPF_ID : 0u);
+    m.cpf = (uint32_t)nc | (ok ? CPF_PLANES : 0u) | (ok2 ? CPF_PLANES2 : 0u) | (ids ? CPF_ID : 0u);
     h ^= (uint64_t)nu;
     m.key = ids ? (uint32_t)ids[row] : (uint32_t)(h ^ (h >> 32));
     m.sketch = sk;
@@ -272,6 +284,11 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
     SPK_TRY(c->units.alloc((size_t)(nbytes + 3 * n + 16)));
     SPK_TRY(c->meta.alloc((size_t)n + 1));
     SPK_TRY(c->planes.alloc((size_t)(n + 1) * N_PLANES));
+    // two-word planes only for columns that can have rows of more than 64 units (> 64 bytes)
+    bool long_rows = false;
+    for (int64_t i = 0; i < n && !long_rows; ++i) long_rows = offsets[i + 1] - offsets[i] > 64;
+    if (long_rows) SPK_TRY(c->planes_hi.alloc((size_t)(n + 1) * N_PLANES));
+    else c->planes_hi.release();
     DevBuf<int64_t> d_off8, d_ids;
     SPK_TRY(d_off8.alloc((size_t)n + 1));
     if (value_ids) {
@@ -286,6 +303,7 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
         int bs = 256;
         k_utf8_decode<<<(unsigned)((n + bs - 1) / bs), bs, 0, ctx->stream>>>(n, d_off8.p, d_bytes.p, d_valid.p,
                                                                           c->units.p, c->meta.p, c->planes.p,
+                                                                          long_rows ? c->planes_hi.p : nullptr,
                                                                           value_ids ? d_ids.p : nullptr);
         SPK_HIP(hipGetLastError());
     }

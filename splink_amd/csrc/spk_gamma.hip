@@ -1357,6 +1357,100 @@ __global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k) {
     }
 }
 
+// Slow list of a Levenshtein template column: cells whose rows are Latin-1 and at most
+// PLANES2_MAX units (CPF_PLANES / CPF_PLANES2) are exact from 128-bit planes in registers
+// (lev_rows_planes128) -- free-text columns such as cfg5's addresses land here; any other cell
+// (non-Latin-1 or longer rows) runs the global-memory evaluation of k_gamma_slow.
+__device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y,
+                           int &level) {
+    const RecMeta ma = c0.meta[x], mb = c1.meta[y];
+    if (ma.len16 < 0 || mb.len16 < 0) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    constexpr uint32_t ANY = CPF_PLANES | CPF_PLANES2;
+    if (!(ma.cpf & ANY) || !(mb.cpf & ANY)) return ST_NEEDS_SLOW;
+    if (((ma.cpf & CPF_PLANES2) && !c0.planes_hi) || ((mb.cpf & CPF_PLANES2) && !c1.planes_hi)) return ST_NEEDS_SLOW;
+    u128 pa[N_PLANES], pb[N_PLANES];
+    {
+        const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
+        const uint4 *qb = reinterpret_cast<const uint4 *>(c1.planes + (int64_t)y * N_PLANES);
+        uint4 ha[N_PLANES / 2], hb[N_PLANES / 2];
+#pragma unroll
+        for (int i = 0; i < N_PLANES / 2; ++i) ha[i] = hb[i] = make_uint4(0, 0, 0, 0);
+        if (ma.cpf & CPF_PLANES2) {
+            const uint4 *ra = reinterpret_cast<const uint4 *>(c0.planes_hi + (int64_t)x * N_PLANES);
+#pragma unroll
+            for (int i = 0; i < N_PLANES / 2; ++i) ha[i] = ra[i];
+        }
+        if (mb.cpf & CPF_PLANES2) {
+            const uint4 *rb = reinterpret_cast<const uint4 *>(c1.planes_hi + (int64_t)y * N_PLANES);
+#pragma unroll
+            for (int i = 0; i < N_PLANES / 2; ++i) hb[i] = rb[i];
+        }
+#pragma unroll
+        for (int i = 0; i < N_PLANES / 2; ++i) {
+            const uint4 u = qa[i], v = qb[i];
+            pa[2 * i] = ((u128)(((uint64_t)ha[i].y << 32) | ha[i].x) << 64) | (((uint64_t)u.y << 32) | u.x);
+            pa[2 * i + 1] = ((u128)(((uint64_t)ha[i].w << 32) | ha[i].z) << 64) | (((uint64_t)u.w << 32) | u.z);
+            pb[2 * i] = ((u128)(((uint64_t)hb[i].y << 32) | hb[i].x) << 64) | (((uint64_t)v.y << 32) | v.x);
+            pb[2 * i + 1] = ((u128)(((uint64_t)hb[i].w << 32) | hb[i].z) << 64) | (((uint64_t)v.w << 32) | v.z);
+        }
+    }
+    int eq = meta_equal(ma, mb);
+    if (eq < 0) {  // equal keys without dictionary ids: the planes are the units
+        eq = ma.len16 == mb.len16 ? 1 : 0;
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) eq &= pa[b] == pb[b] ? 1 : 0;
+    }
+    const int na = meta_cplen(ma), nb = meta_cplen(mb);  // = len16: Latin-1 rows
+    int lev = -1;
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int op = sc.op[i], cmp = sc.cmp[i];
+        const double t = sc.t[i];
+        int r;
+        if (op == SPK_OP_STR_CMP) {
+            r = ((eq == 1) == (cmp == SPK_CMP_EQ)) ? KT : KF;
+        } else {
+            const double den = (double)(na + nb) / 2.0;
+            if (op == SPK_OP_LEVRATIO && den == 0.0) {
+                r = KN;
+            } else {
+                if (lev < 0) lev = eq == 1 ? 0 : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb));
+                r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
+            }
+        }
+        if (r == KT) {
+            level = sc.level[i];
+            return ST_DONE;
+        }
+    }
+    level = sc.else_level;
+    return ST_DONE;
+}
+
+__global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int si) {
+    __shared__ SimpleCol s_sc;
+    __shared__ ColDesc s_c0, s_c1;
+    if (threadIdx.x == 0) {
+        s_sc = A.simple[si];
+        s_c0 = A.cols0[s_sc.col];
+        s_c1 = A.cols1[s_sc.col];
+    }
+    __syncthreads();
+    const int k = s_sc.k;
+    const int64_t n = A.slow_count[k];
+    const int32_t *items = A.slow + A.slow_off[k];
+    for (int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * X_THREADS) {
+        const int32_t p = items[i];
+        const int32_t x = A.pl[p], y = A.pr[p];
+        int level = 0;
+        if (lev_cell128(s_sc, s_c0, s_c1, x, y, level) != ST_DONE)
+            eval_column<M_SLOW>(A, k, x, y, nullptr, nullptr, level);
+        code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+    }
+}
+
 __global__ void k_codes_from_gammas(int64_t n, int K, const int8_t *__restrict__ g, const int64_t *__restrict__ stride,
                                     uint8_t *codes, int code_bytes) {
     int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1790,7 +1884,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                         A, simple_of[k], ctx->xlist.p, ctx->xinfo.p);
                 else
                     k_gamma_exact<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
-                k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k);
+                if (simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV)
+                    k_gamma_slow_lev<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k]);
+                else
+                    k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k);
             }
             SPK_HIP(hipGetLastError());
         } else {

@@ -54,11 +54,14 @@ struct alignas(16) RecMeta {
     uint64_t head;    // units 0..3, zero beyond len16
     uint32_t off4;    // first UTF-16 unit of the row / 4 (rows start 8-byte aligned)
     uint32_t cpf;     // bits 0..23: code-point length; bit 24: bit-planes valid (<= 64 units, all < 256);
-                      // bit 25: `key` is an exact dictionary id
+                      // bit 25: `key` is an exact dictionary id; bit 26: two-word bit-planes valid
+                      // (65..128 units, all < 256: units 0..63 in planes, 64..127 in planes_hi)
 };
 static_assert(sizeof(RecMeta) == 32, "RecMeta layout");
 constexpr uint32_t CPF_PLANES = 1u << 24;
 constexpr uint32_t CPF_ID = 1u << 25;
+constexpr uint32_t CPF_PLANES2 = 1u << 26;
+constexpr int PLANES2_MAX = 128;  // longest row with two-word planes
 __host__ __device__ inline int32_t meta_cplen(const RecMeta &m) { return (int32_t)(m.cpf & 0xFFFFFFu); }
 __host__ __device__ inline int64_t meta_off(const RecMeta &m) { return (int64_t)m.off4 * 4; }
 
@@ -96,6 +99,7 @@ struct ColDesc {
     const uint16_t *units;   // COL_STR
     const RecMeta *meta;     // COL_STR
     const uint64_t *planes;  // COL_STR, [n][N_PLANES]
+    const uint64_t *planes_hi;  // COL_STR, [n][N_PLANES] units 64..127 (CPF_PLANES2 rows), or null
     const double *val;       // COL_NUM
     const uint8_t *valid;   // COL_NUM
 };
@@ -133,6 +137,7 @@ struct Column {
     DevBuf<uint16_t> units;
     DevBuf<RecMeta> meta;
     DevBuf<uint64_t> planes;
+    DevBuf<uint64_t> planes_hi;  // allocated only when some row has more than 64 UTF-8 bytes
     DevBuf<double> val;
     DevBuf<uint8_t> valid;
     bool has_ids = false;  // COL_STR: RecMeta.key is a dictionary id

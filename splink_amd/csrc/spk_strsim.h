@@ -493,6 +493,100 @@ __device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, co
     return myers_plane_text<uint64_t>(P, m, T, n, cut);
 }
 
+// ---- rows of 65..128 units (CPF_PLANES2): the same scan over 128-bit plane words ----------------
+// The 128-bit add of Myers' D0 carries from word 0 into word 1 exactly as the multi-block form
+// (Hyyro 2003) propagates it; unsigned __int128 is two VGPR pairs and the compiler emits the
+// add-with-carry, funnel shifts and per-word logic.
+typedef unsigned __int128 u128;
+
+__device__ inline int ctz128(u128 v) {
+    const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+    return lo ? __ffsll((unsigned long long)lo) - 1 : (hi ? 64 + __ffsll((unsigned long long)hi) - 1 : 128);
+}
+
+__device__ inline int clz128(u128 v) {
+    const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+    return hi ? __clzll((long long)hi) : (lo ? 64 + __clzll((long long)lo) : 128);
+}
+
+__device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
+                                          int cut) {
+    u128 vp = ~(u128)0, vn = 0;
+    const u128 hib = (u128)1 << (m - 1);
+    int dist = m;
+    for (int h = 0; h < 4 && 32 * h < n; ++h) {  // text units [32h, 32h + 32)
+        uint32_t tw[N_PLANES];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        for (int jj = 0; jj < jn; ++jj) {
+            uint64_t e0 = ~0ull, e1 = ~0ull;
+#pragma unroll
+            for (int b = 0; b < N_PLANES; ++b) {
+                const uint32_t m32 = (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1);
+                const uint64_t mb = ((uint64_t)m32 << 32) | m32;
+                const uint64_t p0 = (uint64_t)P[b], p1 = (uint64_t)(P[b] >> 64);
+                e0 &= (mb & p0) | (~mb & ~p0);
+                e1 &= (mb & p1) | (~mb & ~p1);
+            }
+            const u128 x = (((u128)e1 << 64) | e0) | vn;
+            const u128 d0 = (((x & vp) + vp) ^ vp) | x;
+            u128 hp = vn | ~(d0 | vp);
+            u128 hn = d0 & vp;
+            dist += (hp & hib) ? 1 : 0;
+            dist -= (hn & hib) ? 1 : 0;
+            if (dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
+            hp = (hp << 1) | (u128)1;
+            hn = hn << 1;
+            vp = hn | ~(d0 | hp);
+            vn = hp & d0;
+        }
+    }
+    return dist;
+}
+
+// lev_rows_planes for rows of up to 128 units held as 128-bit planes (bits past a row's length are
+// zero).  After the common prefix and suffix are stripped, a pattern of <= 64 units runs the
+// one-word scan (the same word width for the whole wave), else the 128-bit one.
+__device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
+                                         int cut) {
+    if (la == 0) return lb;
+    if (lb == 0) return la;
+    const int mn = la < lb ? la : lb;
+    u128 d = 0, e = 0;
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) {
+        d |= pa[b] ^ pb[b];
+        e |= (pa[b] << (128 - la)) ^ (pb[b] << (128 - lb));
+    }
+    int pre = ctz128(d);
+    if (pre > mn) pre = mn;
+    int suf = clz128(e);
+    if (suf > mn - pre) suf = mn - pre;
+    const int ra = la - pre - suf, rb = lb - pre - suf;
+    if (ra == 0) return rb;
+    if (rb == 0) return ra;
+    const bool a_pat = ra >= rb;
+    const int m = a_pat ? ra : rb, n = a_pat ? rb : ra;
+    u128 P[N_PLANES], T[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) {
+        P[b] = (a_pat ? pa[b] : pb[b]) >> pre;
+        T[b] = (a_pat ? pb[b] : pa[b]) >> pre;
+    }
+    if (!__any(m > 64)) {
+        uint64_t P64[N_PLANES], T64[N_PLANES];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) {
+            P64[b] = (uint64_t)P[b];
+            T64[b] = (uint64_t)T[b];
+        }
+        if (!__any(m > 32)) return myers_plane_text<uint32_t>(P64, m, T64, n, cut);
+        return myers_plane_text<uint64_t>(P64, m, T64, n, cut);
+    }
+    return myers_plane_text128(P, m, T, n, cut);
+}
+
 // Exact Jaro-Winkler for unequal strings of <= 64 units, without LDS.
 __device__ inline double jw_exact(const StrView &a, const StrView &b) {
     const bool fmax = a.n > b.n;  // commons-text: max = first only if strictly longer

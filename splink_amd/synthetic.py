@@ -25,6 +25,11 @@ _CODAS = ["", "", "n", "r", "s", "l", "m", "th", "ck", "ll", "nd", "rt", "x"]
 _STREET_TYPES = ["Street", "Road", "Lane", "Avenue", "Close", "Drive", "Way", "Crescent"]
 _DOMAINS = ["example.com", "mail.co.uk", "post.net", "inbox.org", "webmail.com",
             "fastmail.io", "letters.uk", "corp.example", "home.net", "uni.ac.uk"]
+_BUILDINGS = ["House", "Court", "Mansions", "Lodge", "Tower", "Heights", "Place", "Gardens"]
+_NOTES = ["leave parcels with the neighbour at number 12", "ring the bell twice and wait",
+          "side entrance via the garden gate", "deliveries to the rear door after 6pm",
+          "third floor, lift out of order", "use the intercom, code at reception",
+          "opposite the old post office", "next to the primary school car park"]
 _ACCENTS = "éèêëáàâäíìîïóòôöúùûüçñ"
 _SUPPLEMENTARY = ["\U0001D400", "\U0001F600", "\U00020BB7", "\U0001D49C"]
 
@@ -113,16 +118,30 @@ def make_records(n: int, seed: int = SEED, surname_vocab: int = 15000, surname_s
                       zip(first, sur, e_num[cluster], e_dom[cluster])], dtype=object)
     cols = {"first_name": first, "surname": sur, "dob": dob, "city": city, "email": email}
     if with_address:
+        # free-text addresses of 30-128 characters (cfg5): flat / building, house and street, an
+        # optional district, city, postcode and an optional delivery note, per entity
         e_house = rng.integers(1, 400, size=n_ent)
         e_street = rng.integers(0, len(streets), size=n_ent)
         e_type = rng.integers(0, len(_STREET_TYPES), size=n_ent)
         e_flat = rng.integers(0, 60, size=n_ent)
+        e_bldg = rng.integers(0, len(streets), size=n_ent)
+        e_dist = rng.integers(0, len(cities), size=n_ent)
+        e_note = rng.integers(0, 2 * len(_NOTES), size=n_ent)
+        e_parts = rng.random((n_ent, 3))
         addr = []
         for i in range(n):
             e = cluster[i]
-            flat = f"Flat {e_flat[e]}, " if e_flat[e] < 20 else ""
-            addr.append(f"{flat}{e_house[e]} {streets[e_street[e]]} {_STREET_TYPES[e_type[e]]}, "
-                        f"{cities[e_city[e]]}, AB{e % 90 + 10} {e % 9}XY")
+            head = ""
+            if e_flat[e] < 20:
+                head = f"Flat {e_flat[e]}, "
+                if e_parts[e, 0] < 0.5:
+                    head += f"{streets[e_bldg[e]]} {_BUILDINGS[e_bldg[e] % len(_BUILDINGS)]}, "
+            dist = f"{cities[e_dist[e]]} District, " if e_parts[e, 1] < 0.5 else ""
+            a = (f"{head}{e_house[e]} {streets[e_street[e]]} {_STREET_TYPES[e_type[e]]}, {dist}"
+                 f"{cities[e_city[e]]}, AB{e % 90 + 10} {e % 9}XY")
+            if e_note[e] < len(_NOTES) and e_parts[e, 2] < 0.7:
+                a += f" ({_NOTES[e_note[e]]})"
+            addr.append(a[:128])
         cols["address"] = np.array(addr, dtype=object)
 
     # non-ASCII sprinkles on names
@@ -157,12 +176,14 @@ CONFIGS = {
     1: dict(n=1000, surname_vocab=100, first_vocab=300, city_vocab=80),
     2: dict(n=1_000_000, surname_vocab=15000),
     4: dict(n=20_000_000, surname_vocab=300000),
+    5: dict(n=100_000_000, surname_vocab=600000, with_address=True),
 }
 
 
 def cfg_settings(cfg: int = 2, max_iterations: int = 10) -> dict:
-    """Settings dict for configs 1/2/4: first/surname JW-3, dob/city exact-2, email Lev-3."""
-    return {
+    """Settings dict for configs 1/2/4: first/surname JW-3, dob/city exact-2, email Lev-3;
+    config 5 adds the free-text address column as Levenshtein-4 (case_statements.py:128-141)."""
+    st = {
         "link_type": "dedupe_only",
         "proportion_of_matches": 0.01,
         "max_iterations": max_iterations,
@@ -183,6 +204,9 @@ def cfg_settings(cfg: int = 2, max_iterations: int = 10) -> dict:
              "case_expression": _lev3("email")},
         ],
     }
+    if cfg == 5:
+        st["comparison_columns"].append({"col_name": "address", "num_levels": 4, "case_expression": _lev4("address")})
+    return st
 
 
 def _jw3(c):
@@ -200,4 +224,13 @@ def _lev3(c):
     return (f"case when {c}_l is null or {c}_r is null then -1 "
             f"when {c}_l = {c}_r then 2 "
             f"when levenshtein({c}_l, {c}_r)/((length({c}_l) + length({c}_r))/2) <= 0.3 then 1 "
+            f"else 0 end")
+
+
+def _lev4(c):
+    ratio = f"levenshtein({c}_l, {c}_r)/((length({c}_l) + length({c}_r))/2)"
+    return (f"case when {c}_l is null or {c}_r is null then -1 "
+            f"when {c}_l = {c}_r then 3 "
+            f"when {ratio} <= 0.2 then 2 "
+            f"when {ratio} <= 0.4 then 1 "
             f"else 0 end")

@@ -381,15 +381,15 @@ def _mutate(rng, s, k, alpha):
 
 
 def test_levenshtein_levels_exact(amd):
-    """Exact Levenshtein in the template exact pass (bit-plane path, unit path and the global-memory
-    pass): six `<=` levels reveal the distance up to 5, a ratio column checks the division; lengths
-    straddle the 32- and 64-unit word sizes, with shared prefixes / suffixes, Latin-1 and
-    supplementary-plane characters and NULLs."""
+    """Exact Levenshtein in the template exact pass (bit-plane path, unit path, the 128-bit plane path
+    of the slow list and the global-memory pass): six `<=` levels reveal the distance up to 5, a
+    ratio column checks the division; lengths straddle the 32-, 64- and 128-unit word sizes, with
+    shared prefixes / suffixes, Latin-1 and supplementary-plane characters and NULLs."""
     from splink_amd.gammas import add_gammas
     rng = np.random.Generator(np.random.PCG64(21))
     alpha = list("abcde") + ["é", "ü"]
     left, right = [], []
-    for n in [0, 1, 2, 5, 17, 31, 32, 33, 40, 63, 64, 65, 80]:
+    for n in [0, 1, 2, 5, 17, 31, 32, 33, 40, 63, 64, 65, 80, 100, 116, 127, 128, 129]:
         for k in [0, 1, 2, 3, 5, 8]:
             for rep in range(6):
                 a = "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), n))
@@ -451,3 +451,33 @@ def test_exact_work_lists_grow(amd):
         d = np.array([orc.levenshtein(a, b) for a, b in zip(data[f"{c}_l"], data[f"{c}_r"])])
         want = np.where(d <= 5, 2, np.where(d <= 7, 1, 0))
         assert (got[:, j] == want).all(), c
+
+
+def test_cfg5_address_column_at_scale(amd):
+    """cfg5's columns: blocking surname|dob over records with 30-128 character free-text addresses
+    (Levenshtein-4, case_statements.py:128-141) next to the five cfg2 columns -- pair set and every
+    gamma against the C oracle; most address cells are decided by the 128-bit plane path."""
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import cfg_settings, make_records
+    cols = ["first_name", "surname", "dob", "city", "email", "address"]
+    df = make_records(20000, seed=17, surname_vocab=400, first_vocab=300, city_vocab=60,
+                      with_address=True)[["unique_id"] + cols]
+    assert (df["address"].dropna().str.len() > 64).mean() > 0.2
+    st = complete_settings_dict(cfg_settings(5), amd)
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    table = job.tables[0]
+    l, r = job.pair_rows()
+    exp = _pandas_block(table, [["surname"], ["dob"]])
+    got_pairs = np.stack([l, r], axis=1)
+    order = np.lexsort((got_pairs[:, 1], got_pairs[:, 0]))
+    assert (got_pairs[order] == exp).all()
+    job.gammas(st)
+    gam = job.gammas_host()
+    ocols = [orc.StrCol(table[c].tolist()) for c in cols]
+    specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3]),
+             ("lev", 4, [0.2, 0.4])]
+    ref = orc.template_gammas(specs, ocols, ocols, l, r)
+    assert (gam == ref).all()
+    assert len(np.unique(gam[:, 5])) == 5  # every address level occurs
