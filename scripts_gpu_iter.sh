@@ -7,7 +7,7 @@ echo "pytest exit $rc" >> gpurun_out/tests_$T.log; tail -4 gpurun_out/tests_$T.l
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || exit 1
 cat gpurun_out/bench_$T.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$T -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/benchprof_$T.json 2> gpurun_out/benchprof_$T.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$T -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --em-scale 0 > gpurun_out/benchprof_$T.json 2> gpurun_out/benchprof_$T.err || exit 1
 if [ -n "$PMC" ]; then
   pass() { local n=$1; shift; timeout -s KILL 200 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d gpurun_out/pmc${n}_$T -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc${n}_$T.log 2>&1; }
   pass 1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY || exit 1

@@ -16,11 +16,11 @@ if [ "$2" != "skip-tests" ]; then
 fi
 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 1
 cat gpurun_out/bench_$TAG.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --em-scale 0 > gpurun_out/benchprof_$TAG.json 2> gpurun_out/benchprof_$TAG.err || exit 1
 if [ -n "$AB" ]; then
   timeout -k 10 300 python -u tools/ab_rules.py 1000000 $AB > gpurun_out/abrules_$TAG.log 2>&1 || exit 1
   cat gpurun_out/abrules_$TAG.log
 fi
-timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcf_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcf_$TAG.log 2>&1 || exit 1
-timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcw_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcw_$TAG.log 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcf_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --em-scale 0 > gpurun_out/pmcf_$TAG.log 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcw_$TAG -o run -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --em-scale 0 > gpurun_out/pmcw_$TAG.log 2>&1 || exit 1
 echo done

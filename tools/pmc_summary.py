@@ -1,6 +1,15 @@
 """Summarise rocprofv3 --pmc counter CSVs per kernel (per dispatch averages).
 
     python tools/pmc_summary.py gpurun_out/pmc1_TAG gpurun_out/pmc2_TAG ... [--match REGEX] [--json OUT]
+
+Derived figures (per dispatch, from the counter rows' own start / end timestamps, so the duration is
+the counted run's): gfx950 has 256 CUs x 4 SIMDs; a wave64 VALU instruction holds its SIMD for 4
+cycles, an SALU instruction 1, at the 2.4 GHz engine clock (MI355X_MICROARCH.md).
+  valu_util   = SQ_INSTS_VALU x 4 / (1024 SIMDs x cycles)       VALU issue share of the SIMDs
+  salu_util   = SQ_INSTS_SALU / (1024 x cycles)
+  wait_frac   = SQ_WAIT_ANY / SQ_WAVE_CYCLES                    share of wave time stalled
+  lds_conflict_rate = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS conflict cycles per LDS cycle
+  l2_hit      = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
 """
 import collections
 import csv
@@ -9,6 +18,25 @@ import json
 import os
 import re
 import sys
+
+
+N_SIMD, CLOCK_GHZ = 1024, 2.4
+
+
+def derive(c):
+    cyc = c.get("_dur_ns", 0.0) * CLOCK_GHZ
+    if cyc <= 0:
+        return
+    if "SQ_INSTS_VALU" in c:
+        c["valu_util"] = c["SQ_INSTS_VALU"] * 4 / (N_SIMD * cyc)
+    if "SQ_INSTS_SALU" in c:
+        c["salu_util"] = c["SQ_INSTS_SALU"] / (N_SIMD * cyc)
+    if c.get("SQ_WAVE_CYCLES"):
+        c["wait_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
+    if c.get("SQ_ACTIVE_INST_LDS"):
+        c["lds_conflict_rate"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_ACTIVE_INST_LDS"]
+    if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
+        c["l2_hit"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
 
 
 def main():
@@ -26,10 +54,12 @@ def main():
                 if match and not re.search(match, k):
                     continue
                 vals[k[:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                vals[k[:60]]["_dur_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     summary = {}
     for k, cs in vals.items():
         summary[k] = {c: sum(v) / len(v) for c, v in cs.items()}
-        summary[k]["dispatches"] = max(len(v) for v in cs.values())
+        summary[k]["dispatches"] = max(len(v) for c, v in cs.items() if c != "_dur_ns")
+        derive(summary[k])
     for k, cs in summary.items():
         print(k)
         for c, v in sorted(cs.items()):
