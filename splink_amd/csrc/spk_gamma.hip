@@ -767,7 +767,8 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
 // evaluating any: the pass is bound by the latency of those gathers, so every round trip is
 // shared by F_PAIRS pairs.  The column loop is uniform across the wave, so the class dispatch and
 // the test parameters are scalar.
-__global__ __launch_bounds__(F_THREADS) void k_gamma_simple(GammaArgs A) {
+template <int MINW>
+__global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     __shared__ unsigned int s_cnt[MAX_SIMPLE];
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
     __syncthreads();
@@ -1294,7 +1295,7 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
 
 // The Levenshtein variant is latency-bound (record + plane loads per cell): it keeps registers to
 // LEV_WAVES waves per SIMD so enough cells are in flight.
-constexpr int LEV_WAVES = 1;
+constexpr int LEV_WAVES = 5;
 template <bool LEV>
 __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : 1) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
                                                                    const int64_t *xinfo) {
@@ -1788,7 +1789,11 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_TRY(ctx->work_count.alloc((size_t)K));
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
     // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
-    const int n_regions = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (P + F_THREADS - 1) / F_THREADS));
+    // 20 regions (256-thread workgroups) per CU: four rounds of the 5 resident workgroups a CU holds
+    // at the filter's 96-VGPR cap, so the regions' uneven work evens out (measured best of 1280 ..
+    // 20480 on MI355X: 5120 regions 1.76 ms vs 2048 regions 1.86 ms for the cfg2 pass)
+    const int64_t max_regions = 20 * (int64_t)ctx->n_cu;
+    const int n_regions = (int)std::max<int64_t>(1, std::min<int64_t>(max_regions, (P + F_THREADS - 1) / F_THREADS));
     const int64_t region_len = ((P + n_regions - 1) / n_regions + 63) / 64 * 64;
     SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions));
     SPK_HIP(hipMemsetAsync(ctx->region_count.p, 0, sizeof(unsigned int) * K * n_regions, ctx->stream));
@@ -1843,7 +1848,12 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 default: k_gamma_rows<8><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
             }
         } else {
-            k_gamma_simple<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
+            switch (ctx->filter_waves) {  // waves per SIMD the filter is compiled for (register cap)
+                case 5: k_gamma_simple<5><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 6: k_gamma_simple<6><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 1: k_gamma_simple<1><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                default: k_gamma_simple<5><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+            }
         }
         SPK_HIP(hipGetLastError());
         if (A.n_complex) {
@@ -2098,6 +2108,7 @@ extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
     ctx->simple_columns = on != 0;
     ctx->row_filter = on == 2;
+    ctx->filter_waves = on == 3 ? 1 : (on == 4 ? 6 : 0);
     return SPK_OK;
 }
 

@@ -181,6 +181,7 @@ struct spk_ctx {
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
+    int filter_waves = 0;             // k_gamma_simple register cap: 0 = 5 waves per SIMD (96 VGPRs), 1 = none, 6
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)

@@ -16,7 +16,8 @@ job = Job("dedupe_only", [df], "unique_id", 0)
 job.ctx.enable_timing(True)
 job.block(st["blocking_rules"])
 ref = None
-for mode in (1, 2, 1, 2):
+MODES = [int(m) for m in os.environ.get("AB_MODES", "1,2,1,2").split(",")]
+for mode in MODES:
     job.ctx.gammas_set_simple(mode)
     job.gammas(st)
     ts = []
