@@ -242,6 +242,7 @@ int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols) {
     t.rank.release();
     t.n = n_rows;
     t.desc_dirty = true;
+    t.version = ++ctx->table_epoch;
     ctx->pairs_valid = false;
     ctx->codes_valid = false;
     return SPK_OK;
@@ -256,6 +257,7 @@ static int get_col(spk_ctx *ctx, int side, int col, Column **out) {
     delete t.cols[col];
     t.cols[col] = new Column();
     t.desc_dirty = true;
+    t.version = ++ctx->table_epoch;
     *out = t.cols[col];
     return SPK_OK;
 }

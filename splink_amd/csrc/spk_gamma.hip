@@ -739,13 +739,14 @@ __device__ inline double bits_to_double(uint32_t lo, uint32_t hi) {
 
 // Append the lanes' wanted values of F_PAIRS ballots to a list: one LDS atomic per call.  The wave
 // must be converged (lane 0 active).
-constexpr int F_PAIRS = 4;  // pairs per lane per iteration of the filter pass
-__device__ inline void wave_append_batch(int32_t *list, unsigned int *count, const bool (&want)[F_PAIRS],
-                                         const int64_t (&val)[F_PAIRS]) {
-    unsigned long long m[F_PAIRS];
+constexpr int F_PAIRS = 4;  // pairs per lane per iteration of the general filter (k_gamma_simple: a template parameter)
+template <int FP>
+__device__ inline void wave_append_batch(int32_t *list, unsigned int *count, const bool (&want)[FP],
+                                         const int64_t (&val)[FP]) {
+    unsigned long long m[FP];
     unsigned int total = 0;
 #pragma unroll
-    for (int u = 0; u < F_PAIRS; ++u) {
+    for (int u = 0; u < FP; ++u) {
         m[u] = __ballot(want[u]);
         total += (unsigned int)__popcll(m[u]);
     }
@@ -756,7 +757,7 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
     base = __shfl(base, 0);
     const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int u = 0; u < F_PAIRS; ++u) {
+    for (int u = 0; u < FP; ++u) {
         if (want[u]) list[base + __popcll(m[u] & below)] = (int32_t)val[u];
         base += (unsigned int)__popcll(m[u]);
     }
@@ -767,7 +768,7 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
 // evaluating any: the pass is bound by the latency of those gathers, so every round trip is
 // shared by F_PAIRS pairs.  The column loop is uniform across the wave, so the class dispatch and
 // the test parameters are scalar.
-template <int MINW>
+template <int MINW, int FP>
 __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     __shared__ unsigned int s_cnt[MAX_SIMPLE];
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
@@ -775,15 +776,15 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     const int lane = threadIdx.x & 63;
     const Region R = my_region(A);
     ConstSimpleCol *simple = const_simple(A.simple);
-    constexpr int64_t SPAN = 64 * F_PAIRS;
+    constexpr int64_t SPAN = 64 * FP;
     for (int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN; base < R.r1;
          base += (int64_t)(F_THREADS / 64) * SPAN) {  // wave-uniform
-        int64_t p[F_PAIRS];
-        bool act[F_PAIRS];
-        int32_t x[F_PAIRS], y[F_PAIRS];
-        uint32_t acc[F_PAIRS];
+        int64_t p[FP];
+        bool act[FP];
+        int32_t x[FP], y[FP];
+        uint32_t acc[FP];
 #pragma unroll
-        for (int u = 0; u < F_PAIRS; ++u) {
+        for (int u = 0; u < FP; ++u) {
             p[u] = base + u * 64 + lane;
             act[u] = p[u] < R.r1;
             x[u] = act[u] ? A.pl[p[u]] : 0;  // inactive lanes read row 0 harmlessly
@@ -792,83 +793,83 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
         }
         for (int j = 0; j < A.n_simple; ++j) {
             ConstSimpleCol &sc = simple[j];
-            bool und[F_PAIRS];
-            int lev[F_PAIRS];
+            bool und[FP];
+            int lev[FP];
 #pragma unroll
-            for (int u = 0; u < F_PAIRS; ++u) {
+            for (int u = 0; u < FP; ++u) {
                 und[u] = false;
                 lev[u] = 0;
             }
             switch (sc.cls) {
                 case SC_EQ: {
-                    uint2 va[F_PAIRS], vb[F_PAIRS];
+                    uint2 va[FP], vb[FP];
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u) {
+                    for (int u = 0; u < FP; ++u) {
                         va[u] = *reinterpret_cast<const uint2 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
                         vb[u] = *reinterpret_cast<const uint2 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
                     }
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u) und[u] = img_eq(sc, va[u], vb[u], lev[u]) != ST_DONE;
+                    for (int u = 0; u < FP; ++u) und[u] = img_eq(sc, va[u], vb[u], lev[u]) != ST_DONE;
                     break;
                 }
                 case SC_JW: {
-                    uint4 va[F_PAIRS], vb[F_PAIRS];
-                    uint64_t ha[F_PAIRS], hb[F_PAIRS];
+                    uint4 va[FP], vb[FP];
+                    uint64_t ha[FP], hb[FP];
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u) {
+                    for (int u = 0; u < FP; ++u) {
                         va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
                         vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
                         ha[u] = *reinterpret_cast<const uint64_t *>(A.img0 + img_at(A.img_rows0, x[u], sc.off2));
                         hb[u] = *reinterpret_cast<const uint64_t *>(A.img1 + img_at(A.img_rows1, y[u], sc.off2));
                     }
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u) und[u] = img_jw(sc, va[u], vb[u], ha[u], hb[u], lev[u]) != ST_DONE;
+                    for (int u = 0; u < FP; ++u) und[u] = img_jw(sc, va[u], vb[u], ha[u], hb[u], lev[u]) != ST_DONE;
                     break;
                 }
                 case SC_LEV: {
-                    uint4 va[F_PAIRS], vb[F_PAIRS];
+                    uint4 va[FP], vb[FP];
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u) {
+                    for (int u = 0; u < FP; ++u) {
                         va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
                         vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
                     }
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u) und[u] = img_lev(sc, va[u], vb[u], lev[u]) != ST_DONE;
+                    for (int u = 0; u < FP; ++u) und[u] = img_lev(sc, va[u], vb[u], lev[u]) != ST_DONE;
                     break;
                 }
                 case SC_NUM: {
-                    uint4 va[F_PAIRS], vb[F_PAIRS];
+                    uint4 va[FP], vb[FP];
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u) {
+                    for (int u = 0; u < FP; ++u) {
                         va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
                         vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
                     }
 #pragma unroll
-                    for (int u = 0; u < F_PAIRS; ++u)
+                    for (int u = 0; u < FP; ++u)
                         lev[u] = simple_num(sc, va[u].z != 0, bits_to_double(va[u].x, va[u].y), vb[u].z != 0,
                                             bits_to_double(vb[u].x, vb[u].y));
                     break;
                 }
                 case SC_NUMRAW: {
                     const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
-                    for (int u = 0; u < F_PAIRS; ++u)
+                    for (int u = 0; u < FP; ++u)
                         lev[u] = simple_num(sc, c0.valid[x[u]] != 0, c0.val[x[u]], c1.valid[y[u]] != 0, c1.val[y[u]]);
                     break;
                 }
                 default: {  // SC_GEN: the full row records, one pair at a time (few registers)
                     const RecMeta *m0 = A.cols0[sc.col].meta, *m1 = A.cols1[sc.col].meta;
-                    for (int u = 0; u < F_PAIRS; ++u) und[u] = simple_str(sc, m0[x[u]], m1[y[u]], lev[u]) != ST_DONE;
+                    for (int u = 0; u < FP; ++u) und[u] = simple_str(sc, m0[x[u]], m1[y[u]], lev[u]) != ST_DONE;
                 }
             }
 #pragma unroll
-            for (int u = 0; u < F_PAIRS; ++u) {
+            for (int u = 0; u < FP; ++u) {
                 und[u] = und[u] && act[u];
                 if (!und[u]) acc[u] += (uint32_t)(lev[u] + 1) * (uint32_t)sc.stride;
             }
             wave_append_batch(region_list(A, sc.k, R), &s_cnt[j], und, p);
         }
 #pragma unroll
-        for (int u = 0; u < F_PAIRS; ++u)
+        for (int u = 0; u < FP; ++u)
             if (act[u]) code_set(A, p[u], acc[u]);
     }
     __syncthreads();
@@ -1591,7 +1592,10 @@ static int64_t layout_image(std::vector<SimpleCol> &simple) {
     return (end + 15) & ~(int64_t)15;
 }
 
-static int build_images(spk_ctx *ctx, Table &t0, Table &t1, GammaArgs &A, int64_t stride) {
+// The image is a re-layout of the resident records for the current set of simple columns: it is
+// rebuilt only when a table (or one of its columns) was replaced or the column layout changed.
+static int build_images(spk_ctx *ctx, Table &t0, Table &t1, GammaArgs &A, int64_t stride,
+                        const std::vector<SimpleCol> &simple) {
     A.img0 = A.img1 = nullptr;
     A.img_stride = stride;
     if (stride <= 0 || A.n_simple == 0) return SPK_OK;
@@ -1603,8 +1607,17 @@ static int build_images(spk_ctx *ctx, Table &t0, Table &t1, GammaArgs &A, int64_
             break;
         }
         Table &t = *ts[s];
+        std::vector<int64_t> key = {(int64_t)t.version, t.n, stride};
+        for (const SimpleCol &sc : simple) {
+            key.push_back(sc.cls);
+            key.push_back(sc.col);
+            key.push_back(sc.off);
+            key.push_back(sc.off2);
+        }
+        const bool fresh = ctx->img[s].p && ctx->img_key[s] == key;
         SPK_TRY(ctx->img[s].alloc((size_t)(t.n + 1) * (size_t)stride));
-        if (t.n > 0) {
+        ctx->img_key[s] = key;
+        if (t.n > 0 && !fresh) {
             k_build_image<<<(unsigned)((t.n + 255) / 256), 256, 0, ctx->stream>>>(t.n, t.d_desc.p, A.simple, A.n_simple,
                                                                                  ctx->img[s].p, t.n + 1);
             SPK_HIP(hipGetLastError());
@@ -1834,7 +1847,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
 
     SPK_TRY(ctx->begin(K_GAMMA));
     if (P > 0) {
-        SPK_TRY(build_images(ctx, t0, t1, A, img_stride));
+        SPK_TRY(build_images(ctx, t0, t1, A, img_stride, simple));
         const int nq = (int)(img_stride / 16);
         if (ctx->row_filter && A.n_simple > 0 && nq >= 1 && nq <= ROW_MAXQ) {
             switch (nq) {
@@ -1848,11 +1861,15 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 default: k_gamma_rows<8><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
             }
         } else {
-            switch (ctx->filter_waves) {  // waves per SIMD the filter is compiled for (register cap)
-                case 5: k_gamma_simple<5><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 6: k_gamma_simple<6><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 1: k_gamma_simple<1><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                default: k_gamma_simple<5><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+            switch (ctx->filter_waves) {  // (waves per SIMD the filter is compiled for, pairs per lane)
+                case 1: k_gamma_simple<1, 4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 2: k_gamma_simple<6, 4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 3: k_gamma_simple<5, 4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 4: k_gamma_simple<8, 2><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                case 5: k_gamma_simple<5, 3><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+                // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
+                // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
+                default: k_gamma_simple<6, 3><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
             }
         }
         SPK_HIP(hipGetLastError());
@@ -2108,7 +2125,7 @@ extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
     ctx->simple_columns = on != 0;
     ctx->row_filter = on == 2;
-    ctx->filter_waves = on == 3 ? 1 : (on == 4 ? 6 : 0);
+    ctx->filter_waves = on >= 3 ? on - 2 : 0;  // A/B variants of the filter (tools/ab_gamma.py)
     return SPK_OK;
 }
 

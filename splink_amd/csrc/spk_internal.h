@@ -148,6 +148,7 @@ struct Table {
     std::vector<Column *> cols;
     DevBuf<ColDesc> d_desc;
     bool desc_dirty = true;
+    uint64_t version = 0;  // bumped (ctx-wide counter) whenever the table or one of its columns is replaced
     DevBuf<int64_t> rank;
     std::vector<DevBuf<int64_t> *> key[2];  // [which][rule]
     ~Table();
@@ -181,7 +182,7 @@ struct spk_ctx {
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
-    int filter_waves = 0;             // k_gamma_simple register cap: 0 = 5 waves per SIMD (96 VGPRs), 1 = none, 6
+    int filter_waves = 0;             // k_gamma_simple variant (waves per SIMD, pairs per lane): 0 = <6,3>; 1..5 A/B
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)
@@ -206,6 +207,8 @@ struct spk_ctx {
         return SPK_OK;
     }
     spk::DevBuf<uint8_t> img[2];      // filter row images of table 0 / table 1
+    std::vector<int64_t> img_key[2];  // what img[s] was built from: table version, rows, column layout
+    uint64_t table_epoch = 0;
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)
     spk::DevBuf<unsigned int> work_count;    // [K] slow-pass list lengths
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths

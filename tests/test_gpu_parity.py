@@ -481,3 +481,27 @@ def test_cfg5_address_column_at_scale(amd):
     ref = orc.template_gammas(specs, ocols, ocols, l, r)
     assert (gam == ref).all()
     assert len(np.unique(gam[:, 5])) == 5  # every address level occurs
+
+
+def test_row_image_rebuilt_when_layout_changes(amd):
+    """The filter's row image is kept across comparison passes of one context and rebuilt when the
+    simple-column layout or a table changes: alternating settings give the same codes every time."""
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import cfg_settings
+    df = _synthetic(8000, seed=19, surname_vocab=300, first_vocab=200, city_vocab=50)
+    st = complete_settings_dict(cfg_settings(2), amd)
+    st2 = copy.deepcopy(cfg_settings(2))
+    st2["comparison_columns"] = [st2["comparison_columns"][i] for i in (4, 0, 3)]  # email, first_name, city
+    st2 = complete_settings_dict(st2, amd)
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    g1 = job.gammas_host()
+    job.gammas(st2)
+    h1 = job.gammas_host()
+    assert (h1 == g1[:, [4, 0, 3]]).all()
+    job.gammas(st)
+    assert (job.gammas_host() == g1).all()
+    job.gammas(st2)
+    assert (job.gammas_host() == h1).all()
