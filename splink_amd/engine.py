@@ -203,7 +203,10 @@ class Job:
             spec = compile_rule(text, self.schema)
             per_term = []
             for lexpr, rexpr in spec.terms:
-                codes, _ = T.factorize_joint([self._key_values(t0, lexpr), self._key_values(tr, rexpr)])
+                kl = self._key_values(t0, lexpr)
+                # dedupe with a symmetric term (l.x = r.x): both sides read the same table and key
+                kr = kl if (tr is t0 and lexpr == rexpr) else self._key_values(tr, rexpr)
+                codes, _ = T.factorize_joint([kl, kr])
                 per_term.append(codes)
             rule_keys.append(T.combine_codes(per_term))
             symmetric.append(1 if spec.symmetric else 0)
