@@ -656,12 +656,15 @@ __device__ inline int img_jw(const SC &sc, uint4 a, uint4 b, uint64_t ha, uint64
         if (M == 0) {
             v = 0.0;
         } else {
-            float j = ((float)M * (float)(lf + ls) / ((float)lf * (float)ls) + 1.0f) * (1.0f / 3.0f);
+            // v_rcp_f32 (1 ulp) instead of IEEE divisions: the error (< 1e-6 on j) sits far inside
+            // the 1e-5 margin, so hi stays an upper bound
+            float j = ((float)M * (float)(lf + ls) * __builtin_amdgcn_rcpf((float)lf * (float)ls) + 1.0f) *
+                      (1.0f / 3.0f);
             if (j >= 0.7f - 1e-4f) {
                 const uint64_t d = ha ^ hb;
                 const int cp = d ? (__ffsll((unsigned long long)d) - 1) >> 4 : 4;
                 const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
-                const float pw = (lmx > 10 ? 1.0f / (float)lmx : 0.1f) * (float)prefix;
+                const float pw = (lmx > 10 ? __builtin_amdgcn_rcpf((float)lmx) : 0.1f) * (float)prefix;
                 j = j + pw * (1.0f - j);
             }
             hi = j + 1e-5f;

@@ -31,7 +31,13 @@ def allreduce_histogram_(hist):
     """In-place sum of a pattern histogram (int64 tensor, device or host) over all ranks."""
     dist = _dist()
     if dist is not None and dist.get_world_size() > 1:
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+        if hist.is_cuda and dist.get_backend() == "gloo":
+            # gloo rehearsal of the multi-GPU path (several ranks on one device): host staging
+            h = hist.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            hist.copy_(h)
+        else:
+            dist.all_reduce(hist, op=dist.ReduceOp.SUM)
     return hist
 
 

@@ -1,0 +1,54 @@
+"""One rank of tests/test_gpu_parity.py::test_sharded_ranks_match_single_process (run as a child process).
+
+Every rank uses cuda:0 with the gloo backend, so the sharded device path -- spk_block with
+shard=(rank, world), per-rank comparison vectors, the histogram all-reduce between
+spk_em_histogram and spk_em_finalize -- runs on a one-GPU box exactly as bench.py runs it per GPU.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from splink_amd.engine import Job, m_step_rows  # noqa: E402
+from splink_amd.params import Params  # noqa: E402
+from splink_amd.session import AmdSession  # noqa: E402
+from splink_amd.synthetic import cfg_settings, make_records  # noqa: E402
+
+COLS = ["first_name", "surname", "dob", "city", "email"]
+ITERS = 5
+
+
+def run(shard):
+    df = make_records(20000, seed=23, surname_vocab=500, first_vocab=300, city_vocab=80)[["unique_id"] + COLS]
+    params = Params(cfg_settings(2, max_iterations=ITERS), AmdSession(0))
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0, shard=shard)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    names, nlev = job.code_meta
+    for _ in range(ITERS):
+        stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        lam, rows = m_step_rows(stats, names, nlev)
+        params._update_params(lam, rows)
+    return {"n_pairs": int(job.n_pairs), "lambda": params.params["λ"],
+            "pi": [[list(m), list(u)] for m, u in params._level_probabilities()]}
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    out = run((rank, world))
+    with open(f"{sys.argv[1]}.{rank}", "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

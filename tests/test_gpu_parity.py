@@ -505,3 +505,35 @@ def test_row_image_rebuilt_when_layout_changes(amd):
     assert (job.gammas_host() == g1).all()
     job.gammas(st2)
     assert (job.gammas_host() == h1).all()
+
+
+def test_sharded_ranks_match_single_process(amd, tmp_path):
+    """Two ranks (child processes, gloo, both on cuda:0) run the sharded device path -- pair-ordinal
+    shards of spk_block, per-rank comparison vectors, histogram all-reduce per EM iteration --
+    and end with the same parameters, bit for bit, as one process over all pairs."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import gpu_dist_worker as W
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "rank")
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   LOCAL_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(here, "gpu_dist_worker.py"), out], env=env))
+    for p in procs:
+        assert p.wait(timeout=170) == 0
+    ranks = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    single = W.run((0, 1))
+    assert ranks[0]["n_pairs"] > 0 and ranks[1]["n_pairs"] > 0
+    assert ranks[0]["n_pairs"] + ranks[1]["n_pairs"] == single["n_pairs"]
+    for r in ranks:
+        assert r["lambda"] == single["lambda"]
+        assert r["pi"] == single["pi"]
