@@ -1434,7 +1434,11 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
     return ST_DONE;
 }
 
-__global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int si) {
+// Cells without planes on both rows are handed on (rest list: column k's exact-list region, free
+// once the exact pass ran, and counter slow_count[K + k]) to k_gamma_rest, so this kernel does not
+// carry the general interpreter's registers (the 128-bit scan alone holds ~100).
+__global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int si, int32_t *xlist,
+                                                              const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
     if (threadIdx.x == 0) {
@@ -1446,12 +1450,24 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int s
     const int k = s_sc.k;
     const int64_t n = A.slow_count[k];
     const int32_t *items = A.slow + A.slow_off[k];
+    int32_t *rest = xlist + xinfo[k];
     for (int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * X_THREADS) {
         const int32_t p = items[i];
-        const int32_t x = A.pl[p], y = A.pr[p];
         int level = 0;
-        if (lev_cell128(s_sc, s_c0, s_c1, x, y, level) != ST_DONE)
-            eval_column<M_SLOW>(A, k, x, y, nullptr, nullptr, level);
+        const bool done = lev_cell128(s_sc, s_c0, s_c1, A.pl[p], A.pr[p], level) == ST_DONE;
+        if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        wave_append(rest, A.slow_count + A.K + k, !done, p);
+    }
+}
+
+// The rest list of k_gamma_slow_lev through the global-memory evaluation.
+__global__ __launch_bounds__(64) void k_gamma_rest(GammaArgs A, int k, const int32_t *xlist, const int64_t *xinfo) {
+    const int64_t n = A.slow_count[A.K + k];
+    const int32_t *items = xlist + xinfo[k];
+    for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 64) {
+        const int32_t p = items[i];
+        int level = 0;
+        eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level);
         code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
     }
 }
@@ -1802,7 +1818,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     auto at = [&](auto *&dst, size_t off) { dst = reinterpret_cast<std::remove_reference_t<decltype(dst)>>(base + off); };
     const int64_t P = ctx->n_pairs;
     SPK_TRY(ctx->work.alloc((size_t)K * (size_t)P + 1));
-    SPK_TRY(ctx->work_count.alloc((size_t)K));
+    SPK_TRY(ctx->work_count.alloc((size_t)(2 * K)));  // slow-list lengths, then k_gamma_slow_lev's rest lists
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
     // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
     // 20 regions (256-thread workgroups) per CU: four rounds of the 5 resident workgroups a CU holds
@@ -1813,7 +1829,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     const int64_t region_len = ((P + n_regions - 1) / n_regions + 63) / 64 * 64;
     SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions));
     SPK_HIP(hipMemsetAsync(ctx->region_count.p, 0, sizeof(unsigned int) * K * n_regions, ctx->stream));
-    SPK_HIP(hipMemsetAsync(ctx->work_count.p, 0, sizeof(unsigned int) * K, ctx->stream));
+    SPK_HIP(hipMemsetAsync(ctx->work_count.p, 0, sizeof(unsigned int) * 2 * K, ctx->stream));
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -1914,9 +1930,11 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                         A, simple_of[k], ctx->xlist.p, ctx->xinfo.p);
                 else
                     k_gamma_exact<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
-                if (simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV)
-                    k_gamma_slow_lev<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k]);
-                else
+                if (simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV) {
+                    k_gamma_slow_lev<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], ctx->xlist.p,
+                                                                                         ctx->xinfo.p);
+                    k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+                } else
                     k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k);
             }
             SPK_HIP(hipGetLastError());

@@ -210,7 +210,7 @@ struct spk_ctx {
     std::vector<int64_t> img_key[2];  // what img[s] was built from: table version, rows, column layout
     uint64_t table_epoch = 0;
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)
-    spk::DevBuf<unsigned int> work_count;    // [K] slow-pass list lengths
+    spk::DevBuf<unsigned int> work_count;    // [2K] slow-pass list lengths, then slow-Levenshtein rest lists
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
     // EM state

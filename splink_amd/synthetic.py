@@ -141,7 +141,7 @@ def make_records(n: int, seed: int = SEED, surname_vocab: int = 15000, surname_s
                  f"{cities[e_city[e]]}, AB{e % 90 + 10} {e % 9}XY")
             if e_note[e] < len(_NOTES) and e_parts[e, 2] < 0.7:
                 a += f" ({_NOTES[e_note[e]]})"
-            addr.append(a[:128])
+            addr.append(a[:127])  # <= 128 characters after the one-edit corruption below
         cols["address"] = np.array(addr, dtype=object)
 
     # non-ASCII sprinkles on names
