@@ -417,15 +417,21 @@ __device__ inline W lane_mask(uint32_t m32) {  // 0 / all ones -> W
     return sizeof(W) == 4 ? (W)m32 : (W)(((uint64_t)m32 << 32) | m32);
 }
 
+// eq & XNOR(unit-bit mask, plane) as one 3-input bit op per dword (truth table 0x90 = S0 & ~(S1 ^ S2))
+__device__ inline uint32_t eq_plane(uint32_t eq, uint32_t mb, uint32_t pl) {
+    return __builtin_amdgcn_bitop3_b32(eq, mb, pl, 0x90);
+}
+__device__ inline uint64_t eq_plane(uint64_t eq, uint32_t mb, uint64_t pl) {
+    return ((uint64_t)eq_plane((uint32_t)(eq >> 32), mb, (uint32_t)(pl >> 32)) << 32) |
+           eq_plane((uint32_t)eq, mb, (uint32_t)pl);
+}
+
 template <typename W>
 __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
                                        int cut) {
-    W pl[N_PLANES], npl[N_PLANES];
+    W pl[N_PLANES];
 #pragma unroll
-    for (int b = 0; b < N_PLANES; ++b) {
-        pl[b] = (W)P[b];
-        npl[b] = ~pl[b];
-    }
+    for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
     W vp = ~(W)0, vn = 0;
     const W hib = (W)1 << (m - 1);
     int dist = m;
@@ -437,24 +443,25 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
         for (int jj = 0; jj < jn; ++jj) {
             W eq = ~(W)0;
 #pragma unroll
-            for (int b = 0; b < N_PLANES; ++b) {
-                const W mb = lane_mask<W>((uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1));
-                eq &= (mb & pl[b]) | (~mb & npl[b]);
-            }
+            for (int b = 0; b < N_PLANES; ++b)
+                eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), pl[b]);
             const W x = eq | vn;
             const W d0 = (((x & vp) + vp) ^ vp) | x;
             W hp = vn | ~(d0 | vp);
             W hn = d0 & vp;
             dist += (hp & hib) ? 1 : 0;
             dist -= (hn & hib) ? 1 : 0;
-            if (dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
+            // The bound dist - (units left) never decreases and ends at dist, so testing it every
+            // fourth unit plus clamping at the end returns cut + 1 for exactly the cells a per-unit
+            // test cuts.
+            if ((jj & 3) == 3 && dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
             hp = (hp << 1) | (W)1;
             hn = hn << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
         }
     }
-    return dist;
+    return dist > cut ? cut + 1 : dist;
 }
 
 // Code-point Levenshtein of two unequal rows that both carry bit-planes (<= 64 units, all < 256, so
@@ -524,10 +531,8 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
 #pragma unroll
             for (int b = 0; b < N_PLANES; ++b) {
                 const uint32_t m32 = (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1);
-                const uint64_t mb = ((uint64_t)m32 << 32) | m32;
-                const uint64_t p0 = (uint64_t)P[b], p1 = (uint64_t)(P[b] >> 64);
-                e0 &= (mb & p0) | (~mb & ~p0);
-                e1 &= (mb & p1) | (~mb & ~p1);
+                e0 = eq_plane(e0, m32, (uint64_t)P[b]);
+                e1 = eq_plane(e1, m32, (uint64_t)(P[b] >> 64));
             }
             const u128 x = (((u128)e1 << 64) | e0) | vn;
             const u128 d0 = (((x & vp) + vp) ^ vp) | x;
@@ -535,14 +540,14 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
             u128 hn = d0 & vp;
             dist += (hp & hib) ? 1 : 0;
             dist -= (hn & hib) ? 1 : 0;
-            if (dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
+            if ((jj & 3) == 3 && dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;  // as in myers_plane_text
             hp = (hp << 1) | (u128)1;
             hn = hn << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
         }
     }
-    return dist;
+    return dist > cut ? cut + 1 : dist;
 }
 
 // lev_rows_planes for rows of up to 128 units held as 128-bit planes (bits past a row's length are
