@@ -1091,7 +1091,11 @@ constexpr int PFX_THREADS = 1024;
 __global__ __launch_bounds__(PFX_THREADS) void k_prefix(const unsigned int *__restrict__ region_count, int K,
                                                         int n_regions, int64_t cap, int64_t *__restrict__ xpref,
                                                         int64_t *__restrict__ xinfo) {
-    __shared__ int64_t s[PFX_THREADS];
+    // per column: wave-level inclusive scans (shuffles) and one scan of the 16 wave totals, two
+    // barriers per column instead of a Hillis-Steele ladder of 20
+    constexpr int NW = PFX_THREADS / 64;
+    __shared__ int64_t wsum[NW];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int per = (n_regions + PFX_THREADS - 1) / PFX_THREADS;
     const int b0 = threadIdx.x * per;
     int64_t base = 0;
@@ -1099,28 +1103,38 @@ __global__ __launch_bounds__(PFX_THREADS) void k_prefix(const unsigned int *__re
         const unsigned int *rc = region_count + (int64_t)k * n_regions;
         int64_t mine = 0;
         for (int b = b0; b < b0 + per && b < n_regions; ++b) mine += rc[b];
-        s[threadIdx.x] = mine;
-        __syncthreads();
-        for (int off = 1; off < PFX_THREADS; off <<= 1) {
-            const int64_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
-            __syncthreads();
-            s[threadIdx.x] += v;
-            __syncthreads();
+        int64_t v = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t t = __shfl_up(v, off, 64);
+            if (lane >= off) v += t;
         }
-        int64_t acc = s[threadIdx.x] - mine;  // exclusive
+        if (lane == 63) wsum[wave] = v;
+        __syncthreads();
+        if (wave == 0) {
+            int64_t w = lane < NW ? wsum[lane] : 0;
+#pragma unroll
+            for (int off = 1; off < NW; off <<= 1) {
+                const int64_t t = __shfl_up(w, off, 64);
+                if (lane >= off) w += t;
+            }
+            if (lane < NW) wsum[lane] = w;
+        }
+        __syncthreads();
+        int64_t acc = v - mine + (wave > 0 ? wsum[wave - 1] : 0);  // exclusive
         int64_t *pf = xpref + (int64_t)k * (n_regions + 1);
         for (int b = b0; b < b0 + per && b < n_regions; ++b) {
             pf[b] = acc;
             acc += rc[b];
         }
-        const int64_t tot = s[PFX_THREADS - 1];
+        const int64_t tot = wsum[NW - 1];
         if (threadIdx.x == 0) {
             pf[n_regions] = tot;
             xinfo[k] = base;
             xinfo[K + k] = tot;
         }
         base += tot;
-        __syncthreads();
+        __syncthreads();  // wsum is rewritten by the next column
     }
     if (threadIdx.x == 0) {
         xinfo[2 * K] = base > cap ? 1 : 0;
@@ -1300,8 +1314,10 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
 // The Levenshtein variant is latency-bound (record + plane loads per cell): it keeps registers to
 // LEV_WAVES waves per SIMD so enough cells are in flight.
 constexpr int LEV_WAVES = 5;
+// The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD).
+constexpr int JW_WAVES = 1;
 template <bool LEV>
-__global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : 1) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
+__global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
                                                                    const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;

@@ -42,13 +42,30 @@ def distributed_shard():
 
 
 def quantise(p):
-    """The E-step renders each m / u as `cast({p:.35f} as double)` (expectation_step.py:212)."""
+    """The E-step renders each m / u as `cast({p:.35f} as double)` (expectation_step.py:212).
+
+    For |p| >= 1e-18 the 35 decimals hold >= 18 significant digits, and any correctly rounded decimal
+    of >= 17 significant digits parses back to the same double, so only smaller values (and NaN /
+    inf, which fail both tests) go through the text round trip."""
+    if p >= 1e-18 or p <= -1e-18 or p == 0:
+        return float(p)
     return float(f"{p:.35f}")
 
 
 def f32(x):
     """`cast(... as float)` of the M-step (maximisation_step.py:19, 68-69)."""
     return None if x is None else float(np.float32(x))
+
+
+def f32_many(xs):
+    """f32 over a list (one numpy conversion instead of one per value); None stays None."""
+    idx = [i for i, x in enumerate(xs) if x is not None]
+    out = [None] * len(xs)
+    if idx:
+        vals = np.array([xs[i] for i in idx], dtype=np.float64).astype(np.float32).tolist()
+        for i, v in zip(idx, vals):
+            out[i] = v
+    return out
 
 
 def columns_to_retain_blocking(settings) -> List[str]:
@@ -315,7 +332,7 @@ def _sum_lr(xs):
 def m_step_rows(stats, gamma_names, n_levels):
     """λ and the collected π rows (maximisation_step.py:16-90) from the device statistics,
     with Spark's NULL and float32 semantics."""
-    stats = [float(x) for x in stats]
+    stats = stats.tolist() if isinstance(stats, np.ndarray) else [float(x) for x in stats]
     S, rows, nn = stats[0], stats[1], stats[2]
     new_lambda = f32(S / rows) if (rows > 0 and nn > 0) else None
     out = []
@@ -335,8 +352,12 @@ def m_step_rows(stats, gamma_names, n_levels):
             if nnv == 0 or not den_nonnull:
                 pm = pu = None
             else:
-                pm = f32(sm / den_m) if den_m != 0 else None
-                pu = f32(su / den_u) if den_u != 0 else None
+                pm = sm / den_m if den_m != 0 else None
+                pu = su / den_u if den_u != 0 else None
             out.append({"gamma_value": v, "new_probability_match": pm, "new_probability_non_match": pu,
                         "gamma_col": name})
+    # Spark's float cast of every ratio, in one conversion
+    cast = f32_many([x for r in out for x in (r["new_probability_match"], r["new_probability_non_match"])])
+    for i, r in enumerate(out):
+        r["new_probability_match"], r["new_probability_non_match"] = cast[2 * i], cast[2 * i + 1]
     return new_lambda, out

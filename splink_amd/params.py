@@ -18,13 +18,18 @@ logger = logging.getLogger(__name__)
 
 
 
+_ATOMS = frozenset((str, int, float, bool, type(None)))
+
+
 def _copy_tree(x):
-    """copy.deepcopy for the params dict (dicts / lists of str, int, float, bool, None), several times faster."""
-    if isinstance(x, dict):
+    """copy.deepcopy for the params dict (dicts / lists of str, int, float, bool, None), several times
+    faster; any other type (a numpy scalar, a dict subclass) goes through copy.deepcopy."""
+    t = type(x)
+    if t is dict:
         return {k: _copy_tree(v) for k, v in x.items()}
-    if isinstance(x, list):
+    if t is list:
         return [_copy_tree(v) for v in x]
-    if isinstance(x, (str, int, float, bool)) or x is None:
+    if t in _ATOMS:
         return x
     return copy.deepcopy(x)
 
