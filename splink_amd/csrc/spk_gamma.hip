@@ -1088,21 +1088,38 @@ __global__ __launch_bounds__(F_THREADS) void k_gamma_filter(GammaArgs A) {
 // half of xlist.  If the lists exceed the capacity, `overflow` makes every exact kernel a no-op
 // and the host re-runs the phase with room for `total` (codes are untouched until then).
 constexpr int PFX_THREADS = 1024;
+constexpr int PFX_PER = 8;  // region counts a k_prefix thread keeps in registers
 __global__ __launch_bounds__(PFX_THREADS) void k_prefix(const unsigned int *__restrict__ region_count, int K,
                                                         int n_regions, int64_t cap, int64_t *__restrict__ xpref,
                                                         int64_t *__restrict__ xinfo) {
-    // per column: wave-level inclusive scans (shuffles) and one scan of the 16 wave totals, two
-    // barriers per column instead of a Hillis-Steele ladder of 20
+    // Per column: wave-level inclusive scans (shuffles) and one scan of the 16 wave totals, two
+    // barriers per column instead of a Hillis-Steele ladder of 20.  A thread's counts (<= PFX_PER of
+    // them, 5 at 20 regions per CU) stay in registers, and the next column's are loaded before this
+    // column's scan, so the K columns pay about one load latency instead of 2K.
     constexpr int NW = PFX_THREADS / 64;
     __shared__ int64_t wsum[NW];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int per = (n_regions + PFX_THREADS - 1) / PFX_THREADS;
     const int b0 = threadIdx.x * per;
+    const bool in_regs = per <= PFX_PER;  // block-uniform
+    auto load = [&](int k, unsigned int (&c)[PFX_PER]) {
+        const unsigned int *rc = region_count + (int64_t)k * n_regions;
+#pragma unroll
+        for (int q = 0; q < PFX_PER; ++q) c[q] = (q < per && b0 + q < n_regions) ? rc[b0 + q] : 0u;
+    };
+    unsigned int cur[PFX_PER], nxt[PFX_PER];
+    if (in_regs && K > 0) load(0, cur);
     int64_t base = 0;
     for (int k = 0; k < K; ++k) {
         const unsigned int *rc = region_count + (int64_t)k * n_regions;
         int64_t mine = 0;
-        for (int b = b0; b < b0 + per && b < n_regions; ++b) mine += rc[b];
+        if (in_regs) {
+            if (k + 1 < K) load(k + 1, nxt);
+#pragma unroll
+            for (int q = 0; q < PFX_PER; ++q) mine += cur[q];
+        } else {
+            for (int b = b0; b < b0 + per && b < n_regions; ++b) mine += rc[b];
+        }
         int64_t v = mine;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -1123,9 +1140,19 @@ __global__ __launch_bounds__(PFX_THREADS) void k_prefix(const unsigned int *__re
         __syncthreads();
         int64_t acc = v - mine + (wave > 0 ? wsum[wave - 1] : 0);  // exclusive
         int64_t *pf = xpref + (int64_t)k * (n_regions + 1);
-        for (int b = b0; b < b0 + per && b < n_regions; ++b) {
-            pf[b] = acc;
-            acc += rc[b];
+        if (in_regs) {
+#pragma unroll
+            for (int q = 0; q < PFX_PER; ++q) {
+                if (q < per && b0 + q < n_regions) pf[b0 + q] = acc;
+                acc += cur[q];
+            }
+#pragma unroll
+            for (int q = 0; q < PFX_PER; ++q) cur[q] = nxt[q];
+        } else {
+            for (int b = b0; b < b0 + per && b < n_regions; ++b) {
+                pf[b] = acc;
+                acc += rc[b];
+            }
         }
         const int64_t tot = wsum[NW - 1];
         if (threadIdx.x == 0) {
@@ -1314,7 +1341,8 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
 // The Levenshtein variant is latency-bound (record + plane loads per cell): it keeps registers to
 // LEV_WAVES waves per SIMD so enough cells are in flight.
 constexpr int LEV_WAVES = 5;
-// The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD).
+// The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD): capped at
+// 4 waves (128 VGPRs, 40 B of spills) it measured the same on MI355X (52.1 vs 52.3 us per call).
 constexpr int JW_WAVES = 1;
 template <bool LEV>
 __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
