@@ -183,6 +183,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(job, df, st, args.cpu_seconds, cols)
 
+    rates = string_rates(job, st, local_pairs, g_ms) if world == 1 else None
+
     em_scale = None
     if world == 1 and args.em_scale > 0:
         em_scale = em_streaming(job, names, nlev, params, args.em_scale)
@@ -211,6 +213,7 @@ def main():
         "deferred_pairs": job.ctx.gammas_deferred(),
         "exact_cells_per_column": dict(zip(names, job.ctx.gammas_exact_counts(len(names)))),
         "cpu_baseline": cpu,
+        "string_rates": rates,
         "em_at_scale": em_scale,
     }
     print(json.dumps(out), flush=True)
@@ -257,6 +260,33 @@ def em_streaming(job, names, nlev, params, reps, iters=10):
                         "frac": sb / (s / 1e3) / 1e9 / HBM_PEAK_GBS},
             "em_restream_pairs_per_s": P / ((h + f) / 1e3),
             "pattern_count_em_ms_per_iter": f}
+
+
+def string_rates(job, st, pairs, g_ms):
+    """Rates of the string work in one γ pass (Levenshtein GCUPS, JW comparisons/s).
+
+    `lev_effective_gcups` = Σ over every pair of len_l·len_r (code points) of each Levenshtein column,
+    i.e. the DP cells a full Wagner-Fischer pass would update, ÷ the whole γ-pass time: what the
+    filter bounds plus the bit-parallel exact pass stand in for.  It is an effective rate, not a count
+    of cells computed (most pairs are decided by the filter's bounds, the rest 32-64 cells per
+    word-op)."""
+    l, r = job.pair_rows()
+    t = job.tables[0]
+    sec = g_ms / 1e3
+    lev_cells, n_jw, n_lev = 0, 0, 0
+    for c in st["comparison_columns"]:
+        expr = (c.get("case_expression") or "").lower()
+        if "levenshtein" in expr:
+            n_lev += 1
+            ln = t[c["col_name"]].str.len().fillna(0).to_numpy(np.int64)
+            lev_cells += int(np.dot(ln[l], ln[r]))
+        elif "jaro_winkler" in expr:
+            n_jw += 1
+    K = len(st["comparison_columns"])
+    return {"comparisons_per_s": pairs * K / sec, "jw_comparisons_per_s": pairs * n_jw / sec,
+            "lev_comparisons_per_s": pairs * n_lev / sec, "lev_dp_cells_per_pass": lev_cells,
+            "lev_effective_gcups": lev_cells / sec / 1e9,
+            "note": "whole γ-pass time; effective GCUPS = Σ len_l·len_r over all pairs' Levenshtein columns ÷ that time"}
 
 
 def cpu_baseline(job, df, st, seconds, col_names):
