@@ -1340,6 +1340,56 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
 
 // The Levenshtein variant is latency-bound (record + plane loads per cell): it keeps registers to
 // LEV_WAVES waves per SIMD so enough cells are in flight.
+// Work bins of a Levenshtein cell: the scan runs over the shorter row (trip count) with a word as
+// wide as the longer one needs, and a wave runs as long as its slowest lane and at the widest word
+// any lane needs.  So each workgroup's 256 cells are regrouped by (longer > 32 units, shorter length)
+// before they are evaluated: lanes of a wave then get similar trip counts and most waves stay at
+// 32-bit words.  Only the assignment of cells to lanes changes; every cell is evaluated once, as
+// before.  Bin LEV_BINS - 1 also holds the empty slots past the end of the list.
+constexpr int LEV_BINS = 128;
+__device__ inline int lev_work_bin(int la, int lb) {
+    la = la < 0 ? 0 : la;
+    lb = lb < 0 ? 0 : lb;
+    const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
+    return (mx > 32 ? 64 : 0) + (mn < 63 ? mn : 63);
+}
+
+// Counting sort of the workgroup's (key, item) by key through LDS: one LDS atomic per lane, a
+// 128-bin exclusive scan in wave 0, one scatter and one gather.  Three barriers.
+__device__ inline void lev_sort_items(int key, bool &have, int32_t &p, int32_t &x, int32_t &y) {
+    __shared__ unsigned int s_bin[LEV_BINS];
+    __shared__ int32_t s_p[X_THREADS], s_x[X_THREADS], s_y[X_THREADS];
+    __shared__ uint8_t s_have[X_THREADS];
+    const int t = threadIdx.x;
+    if (t < LEV_BINS) s_bin[t] = 0;
+    __syncthreads();
+    const unsigned int r = atomicAdd(&s_bin[key], 1u);
+    __syncthreads();
+    if (t < 64) {  // wave 0: two bins per lane
+        const unsigned int a = s_bin[2 * t], b = s_bin[2 * t + 1];
+        unsigned int v = a + b;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned int u = __shfl_up(v, off, 64);
+            if (t >= off) v += u;
+        }
+        const unsigned int ex = v - a - b;
+        s_bin[2 * t] = ex;
+        s_bin[2 * t + 1] = ex + a;
+    }
+    __syncthreads();
+    const unsigned int pos = s_bin[key] + r;
+    s_p[pos] = p;
+    s_x[pos] = x;
+    s_y[pos] = y;
+    s_have[pos] = have ? 1 : 0;
+    __syncthreads();
+    p = s_p[t];
+    x = s_x[t];
+    y = s_y[t];
+    have = s_have[t] != 0;
+}
+
 constexpr int LEV_WAVES = 5;
 // The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD): capped at
 // 4 waves (128 VGPRs, 40 B of spills) it measured the same on MI355X (52.1 vs 52.3 us per call).
@@ -1360,23 +1410,31 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
     const int64_t n = exact_count(A, xinfo, k);
     const int32_t *items = xlist + xinfo[k];
     const int64_t stride = (int64_t)gridDim.x * X_THREADS;
-    // software pipeline: the next item's pair rows are in flight while this one is evaluated
+    // software pipeline: the next item's pair rows (and, for Levenshtein, the rows' lengths) are in
+    // flight while this one is evaluated
     int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x;
-    int32_t p = 0, x = 0, y = 0;
+    // Regroup by work bin only in free-text columns (rows past 64 units, so planes_hi exists): there the
+    // trip counts spread widely (cfg5 addresses: 2.98 -> 2.67 ms per call).  In short-string columns
+    // the sort's barriers cost more than it saves (cfg2 email: 475 -> 505 us), so they keep the old order.
+    const bool regroup = LEV && s_c0.planes_hi != nullptr && s_c1.planes_hi != nullptr;  // block-uniform
+    int32_t p = 0, x = 0, y = 0, key = LEV_BINS - 1;
     if (i < n) {
         p = items[i];
         x = A.pl[p];
         y = A.pr[p];
+        if (regroup) key = lev_work_bin(s_c0.meta[x].len16, s_c1.meta[y].len16);
     }
     for (int64_t base = (int64_t)blockIdx.x * X_THREADS; base < n; base += stride) {  // block-uniform
-        const bool have = i < n;
+        bool have = i < n;
         const int64_t i2 = i + stride;
-        int32_t p2 = 0, x2 = 0, y2 = 0;
+        int32_t p2 = 0, x2 = 0, y2 = 0, key2 = LEV_BINS - 1;
         if (i2 < n) {
             p2 = items[i2];
             x2 = A.pl[p2];
             y2 = A.pr[p2];
+            if (regroup) key2 = lev_work_bin(s_c0.meta[x2].len16, s_c1.meta[y2].len16);
         }
+        if (regroup) lev_sort_items(key, have, p, x, y);
         bool to_slow = false;
         if (have) {
             int level = 0;
@@ -1391,6 +1449,7 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
         p = p2;
         x = x2;
         y = y2;
+        key = key2;
     }
 }
 
@@ -1495,6 +1554,8 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int s
     const int64_t n = A.slow_count[k];
     const int32_t *items = A.slow + A.slow_off[k];
     int32_t *rest = xlist + xinfo[k];
+    // (regrouping these cells by work bin, as k_gamma_exact_simple does for free-text columns,
+    // measured no faster here: 2.43-2.47 ms per cfg5 call either way)
     for (int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * X_THREADS) {
         const int32_t p = items[i];
         int level = 0;
