@@ -73,6 +73,10 @@ int spk_table_add_float64(spk_ctx *ctx, int side, int col, const double *values,
 /* Order rank per row for the link-type predicate: dedupe `l.uid < r.uid` (blocking.py:136),
  * link_and_dedupe `(l.src < r.src) or (l.uid < r.uid and same src)` (:139).  Equal rank = equal key. */
 int spk_table_set_rank(spk_ctx *ctx, int side, const int64_t *rank);
+/* NULL unique ids (blocking.py:136, :139: `l.uid < r.uid` is NULL, so the pair is dropped, unless
+ * `l._source_table < r._source_table` holds).  divisor > 0 declares the rank layout
+ * rank = source * divisor + r with r = divisor - 1 for a row whose unique id is NULL; 0 = no NULL ids. */
+int spk_table_set_rank_null(spk_ctx *ctx, int side, int64_t divisor);
 /* Blocking key ids of rule `rule` for each row (-1 = NULL: the row never matches the rule).
  * which = 0: key of the row as the join's l-side; which = 1: as the r-side. */
 int spk_table_set_key(spk_ctx *ctx, int side, int rule, int which, const int64_t *keys);

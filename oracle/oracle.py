@@ -52,6 +52,7 @@ def _lib():
     lib.orc_gammas.restype = ctypes.c_int
     lib.orc_em_stats.restype = ctypes.c_int
     lib.orc_score.restype = None
+    lib.orc_log_likelihood.restype = None
     _LIB = lib
     return lib
 
@@ -87,19 +88,29 @@ class _StrColC(ctypes.Structure):
 
 
 class StrCol:
-    """A string column encoded as UTF-16 units and code points (the JW / Levenshtein alphabets)."""
+    """A string column encoded as UTF-16 units and code points (the JW / Levenshtein alphabets).
+
+    Built with whole-column codecs (one join + encode per alphabet), so a 1M-row column takes
+    well under a second; lone surrogates pass through as in a Java String."""
 
     def __init__(self, values):
         vals = [None if (v is None or (isinstance(v, float) and np.isnan(v))) else str(v) for v in values]
+        n = len(vals)
         self.valid = np.array([v is not None for v in vals], dtype=np.uint8)
-        u16 = [_u16(v) if v is not None else np.zeros(0, np.uint16) for v in vals]
-        u32 = [_u32(v) if v is not None else np.zeros(0, np.uint32) for v in vals]
-        self.off16 = np.zeros(len(vals) + 1, dtype=np.int64)
-        self.off32 = np.zeros(len(vals) + 1, dtype=np.int64)
-        self.off16[1:] = np.cumsum([len(a) for a in u16])
-        self.off32[1:] = np.cumsum([len(a) for a in u32])
-        self.u16 = np.concatenate(u16 + [np.zeros(1, np.uint16)])
-        self.u32 = np.concatenate(u32 + [np.zeros(1, np.uint32)])
+        strs = [v if v is not None else "" for v in vals]
+        len32 = np.fromiter((len(v) for v in strs), dtype=np.int64, count=n)
+        joined = "".join(strs)
+        u32 = np.frombuffer(joined.encode("utf-32-le", "surrogatepass"), dtype=np.uint32)
+        self.off32 = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(len32, out=self.off32[1:])
+        supp = (u32 >= 0x10000).astype(np.int64)
+        csupp = np.zeros(len(u32) + 1, dtype=np.int64)
+        np.cumsum(supp, out=csupp[1:])
+        self.off16 = self.off32 + csupp[self.off32]
+        self.u16 = np.concatenate([np.frombuffer(joined.encode("utf-16-le", "surrogatepass"), dtype=np.uint16),
+                                   np.zeros(1, np.uint16)])
+        self.u32 = np.concatenate([u32, np.zeros(1, np.uint32)])
+        assert self.off16[-1] == len(self.u16) - 1
         self.c = _StrColC(self.u16.ctypes.data, self.off16.ctypes.data, self.u32.ctypes.data,
                           self.off32.ctypes.data, self.valid.ctypes.data)
 
@@ -171,6 +182,22 @@ def score(gam, nlev, lam, m, u):
                      ctypes.c_double(float(repr(1 - lam))), mq.ctypes.data_as(ctypes.c_void_p),
                      uq.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p))
     return out
+
+
+def log_likelihood(gam, nlev, lam, m, u):
+    """get_overall_log_likelihood (expectation_step.py:224-272): Σ ln(λΠm + (1-λ)Πu) over the pairs,
+    None when every term is NULL (Spark's sum of no values)."""
+    gam = np.ascontiguousarray(gam, dtype=np.int8)
+    nlev = np.ascontiguousarray(nlev, dtype=np.int32)
+    mq = np.array([quantise(x) for row in m for x in row], dtype=np.float64)
+    uq = np.array([quantise(x) for row in u for x in row], dtype=np.float64)
+    out = np.zeros(2, dtype=np.float64)
+    _lib().orc_log_likelihood(ctypes.c_int(len(nlev)), nlev.ctypes.data_as(ctypes.c_void_p),
+                              ctypes.c_int64(gam.shape[0]), gam.ctypes.data_as(ctypes.c_void_p),
+                              ctypes.c_double(float(repr(lam))), ctypes.c_double(float(repr(1 - lam))),
+                              mq.ctypes.data_as(ctypes.c_void_p), uq.ctypes.data_as(ctypes.c_void_p),
+                              out.ctypes.data_as(ctypes.c_void_p))
+    return float(out[0]) if out[1] > 0 else None
 
 
 def m_step(stats, nlev):

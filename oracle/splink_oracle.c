@@ -261,6 +261,29 @@ int orc_em_stats(int K, const int *nlev, int64_t P, const int8_t *gam, double la
     return n_stats;
 }
 
+/* Log-likelihood of the parameters (expectation_step.py:224-272): Σ over pairs of
+ * ln(λ·Πm + (1-λ)·Πu), Spark's ln giving NULL (skipped by sum) for arguments <= 0.
+ * out[0] = the sum, out[1] = the number of non-NULL terms. */
+void orc_log_likelihood(int K, const int *nlev, int64_t P, const int8_t *gam, double lambda, double one_minus,
+                        const double *m, const double *u, double *out)
+{
+    int lvl_off[64];
+    int n_slots = 0;
+    for (int k = 0; k < K; k++) { lvl_off[k] = n_slots; n_slots += nlev[k] + 1; }
+    double sum = 0.0, cnt = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : sum, cnt)
+    for (int64_t p = 0; p < P; p++) {
+        const int8_t *g = gam + p * K;
+        double num = lambda, den = one_minus;
+        for (int k = 0; k < K; k++) num = num * (g[k] < 0 ? 1.0 : m[lvl_off[k] - k + g[k]]);
+        for (int k = 0; k < K; k++) den = den * (g[k] < 0 ? 1.0 : u[lvl_off[k] - k + g[k]]);
+        const double d = num + den;
+        if (d > 0.0) { sum += log(d); cnt += 1.0; }
+    }
+    out[0] = sum;
+    out[1] = cnt;
+}
+
 /* Final scoring pass: mp per pair (NaN where the reference yields NULL). */
 void orc_score(int K, const int *nlev, int64_t P, const int8_t *gam, double lambda, double one_minus,
                const double *m, const double *u, double *mp_out)

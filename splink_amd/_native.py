@@ -43,7 +43,7 @@ EXPORTS = [
     "spk_pairs_count", "spk_pairs_copy", "spk_pairs_load", "spk_gammas", "spk_gammas_copy", "spk_gammas_load",
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
-    "spk_gammas_set_simple", "spk_gammas_simple_count", "spk_em_set_lane_histogram",
+    "spk_gammas_set_simple", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
 ]
 
 
@@ -155,6 +155,10 @@ class Context:
     def table_set_rank(self, side, rank):
         rank = np.ascontiguousarray(rank, dtype=np.int64)
         check(self._lib.spk_table_set_rank(self._h, ctypes.c_int(side), _ptr(rank)), "spk_table_set_rank")
+
+    def table_set_rank_null(self, side, divisor):
+        check(self._lib.spk_table_set_rank_null(self._h, ctypes.c_int(side), ctypes.c_int64(divisor)),
+              "spk_table_set_rank_null")
 
     def table_set_key(self, side, rule, which, keys):
         keys = np.ascontiguousarray(keys, dtype=np.int64)

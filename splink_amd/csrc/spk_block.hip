@@ -94,6 +94,7 @@ struct EnumArgs {
     const int64_t *rankL, *rankR;
     int tri;
     int rank_filter;            // 1: keep rank(l) < rank(r) (dedupe / link_and_dedupe)
+    int64_t null_div;           // > 0: rank = src * null_div + r, r == null_div - 1 for a NULL unique id
     int rule;                   // index of this rule; rules [0, rule) exclude their pairs
     RuleKeys keys;
     int64_t *chunk_count;       // count pass output
@@ -172,6 +173,11 @@ __global__ __launch_bounds__(EN_THREADS) void k_enum(EnumArgs A) {
                 } else {
                     ok = rx < ry;
                 }
+                // `l.uid < r.uid` is NULL (the pair is dropped) when either unique id is NULL; pairs
+                // across the two sources of link_and_dedupe are kept by `l.src < r.src` alone
+                if (ok && A.null_div > 0 && rx / A.null_div == ry / A.null_div &&
+                    (rx % A.null_div == A.null_div - 1 || ry % A.null_div == A.null_div - 1))
+                    ok = false;
             }
             for (int j = 0; ok && j < A.rule; ++j) {
                 int64_t kl = A.keys.keyL[j][x];
@@ -392,6 +398,7 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         A.rankR = tr.rank.p;
         A.tri = P.tri;
         A.rank_filter = link_only ? 0 : 1;
+        A.null_div = tl.null_div;
         A.rule = r;
         A.chunk_count = counts[r]->p;
         k_enum<false><<<(unsigned)n_chunks[r], EN_THREADS, 0, ctx->stream>>>(A);
@@ -423,6 +430,7 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         A.rankR = tr.rank.p;
         A.tri = P.tri;
         A.rank_filter = link_only ? 0 : 1;
+        A.null_div = tl.null_div;
         A.rule = r;
         A.chunk_off = offs[r]->p;
         A.out_l = ctx->pl.p + rule_base[r];

@@ -240,6 +240,7 @@ int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols) {
         t.key[w].clear();
     }
     t.rank.release();
+    t.null_div = 0;
     t.n = n_rows;
     t.desc_dirty = true;
     t.version = ++ctx->table_epoch;
@@ -342,6 +343,12 @@ int spk_table_set_rank(spk_ctx *ctx, int side, const int64_t *rank) {
     SPK_TRY(t.rank.alloc((size_t)t.n + 1));
     if (t.n) SPK_HIP(hipMemcpyAsync(t.rank.p, rank, (size_t)t.n * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+int spk_table_set_rank_null(spk_ctx *ctx, int side, int64_t divisor) {
+    SPK_REQUIRE(ctx && (side == 0 || side == 1) && divisor >= 0, SPK_E_INVALID, "spk_table_set_rank_null: bad args");
+    ctx->table[side].null_div = divisor;
     return SPK_OK;
 }
 

@@ -1922,6 +1922,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     uint8_t *base = ctx->prog_blob.p;
     auto at = [&](auto *&dst, size_t off) { dst = reinterpret_cast<std::remove_reference_t<decltype(dst)>>(base + off); };
     const int64_t P = ctx->n_pairs;
+    // the filter's work lists and the exact passes hold pair ordinals as int32
+    SPK_REQUIRE(P <= (int64_t)INT32_MAX, SPK_E_LIMIT,
+                "spk_gammas: more than 2^31-1 pairs in one context (shard the pair set over more ranks)");
     SPK_TRY(ctx->work.alloc((size_t)K * (size_t)P + 1));
     SPK_TRY(ctx->work_count.alloc((size_t)(2 * K)));  // slow-list lengths, then k_gamma_slow_lev's rest lists
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));

@@ -150,6 +150,7 @@ struct Table {
     bool desc_dirty = true;
     uint64_t version = 0;  // bumped (ctx-wide counter) whenever the table or one of its columns is replaced
     DevBuf<int64_t> rank;
+    int64_t null_div = 0;  // rank layout for NULL unique ids (spk_table_set_rank_null), 0 = none
     std::vector<DevBuf<int64_t> *> key[2];  // [which][rule]
     ~Table();
 };

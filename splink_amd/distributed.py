@@ -41,6 +41,24 @@ def allreduce_histogram_(hist):
     return hist
 
 
+def allreduce_host_(arr):
+    """In-place sum over all ranks of a host numpy array (float64 / int64), e.g. the per-value
+    (Σmp, count) tables of the term-frequency adjustment (term_frequencies.py:49-65 groups over all
+    pairs, which are sharded here).  RCCL needs device tensors, so under `nccl` the array is staged
+    through the rank's GPU; under `gloo` it is reduced on the host."""
+    import numpy as np
+    import torch
+    dist = _dist()
+    if dist is None or dist.get_world_size() <= 1 or arr.size == 0:
+        return arr
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if dist.get_backend() != "gloo":
+        t = t.to(f"cuda:{torch.cuda.current_device()}")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    arr[...] = t.cpu().numpy()
+    return arr
+
+
 def _reduce_scalar(x, op, dtype):
     import torch
     dist = _dist()

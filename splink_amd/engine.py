@@ -122,20 +122,32 @@ class Job:
         return self.tables[1] if self.link_type == "link_only" else self.tables[0]
 
     def _set_rank(self):
+        """Order rank of every row for the link-type predicate (blocking.py:136, :139).  A NULL
+        unique id never satisfies `l.uid < r.uid`; its rows get the last rank of their source and
+        the kernel drops their same-source pairs (spk_table_set_rank_null)."""
         self._rank = None
         if self.link_type == "link_only":
             return
         t = self.tables[0]
         if self.uid not in t.columns:
             raise ValueError(f"unique_id_column_name {self.uid!r} is not a column of the input data")
-        uid_rank = T.dense_rank(t[self.uid].tolist())
+        col = t[self.uid]
+        if (pd.api.types.is_integer_dtype(col.dtype) and not pd.api.types.is_bool_dtype(col.dtype)
+                and not col.isna().any()):
+            uid_rank, nulls = T.dense_rank_array(col.to_numpy(dtype=np.int64))
+        else:
+            uid_rank, nulls = T.dense_rank(col.tolist())
+        n_distinct = int(uid_rank[~nulls].max()) + 1 if (~nulls).any() else 0
+        div = n_distinct + 1  # r in [0, n_distinct) for ids, n_distinct for NULL
+        r = np.where(nulls, n_distinct, uid_rank)
         if self.link_type == "link_and_dedupe":
             src = (t["_source_table"].to_numpy() == "right").astype(np.int64)
-            rank = src * (int(uid_rank.max()) + 1 if len(uid_rank) else 1) + uid_rank
+            rank = src * div + r
         else:
-            rank = uid_rank
+            rank = r
         self._rank = np.asarray(rank, dtype=np.int64)
         self.ctx.table_set_rank(0, self._rank)
+        self.ctx.table_set_rank_null(0, div if nulls.any() else 0)
 
     def column_index(self, name: str, form: str) -> int:
         key = (name, form)
@@ -283,6 +295,14 @@ class Job:
         return self.ctx.gammas_copy(len(names), 0, self.n_pairs)
 
     # ---- EM -------------------------------------------------------------------------------------------
+    def reduces_across_ranks(self) -> bool:
+        """True when this job holds one rank's shard of a pair set split over the process group:
+        its sufficient statistics (EM histogram, tf tables) must be summed over ranks.  A job whose
+        pairs are not sharded (a gamma table handed to iterate(), or a test's explicit shard without
+        a process group) keeps its statistics local."""
+        rank, world = distributed_shard()
+        return world > 1 and self.n_shards == world and self.shard == rank
+
     @staticmethod
     def flat_tables(level_probs):
         m = [quantise(p) for mk, _ in level_probs for p in mk]
@@ -295,8 +315,7 @@ class Job:
         m, u = self.flat_tables(level_probs)
         lam_d, one_minus = float(lam), float(1 - lam)
         n_stats = N_HEAD + 4 * sum(L + 1 for L in n_levels)
-        rank, world = distributed_shard()
-        if world > 1:
+        if self.reduces_across_ranks():
             import torch
             n_pat = self.ctx.n_patterns()
             hist = getattr(self, "_hist_dev", None)

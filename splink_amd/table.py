@@ -154,17 +154,31 @@ def combine_codes(code_lists):
     return [np.where(nulls[i], -1, acc[i]) for i in range(n_parts)]
 
 
-def dense_rank(values) -> np.ndarray:
-    """Dense rank of values (equal values -> equal rank), ordered like Spark compares them."""
+def dense_rank(values):
+    """Dense rank of the non-NULL values (equal values -> equal rank) in Spark's comparison order,
+    and the NULL mask.  Numbers (ints / floats, NULLs aside) compare numerically; anything else by
+    its string rendering in code-point order (= Spark's UTF-8 byte order)."""
     vals = list(values)
-    if all(isinstance(v, (int, np.integer, float, np.floating)) and not isinstance(v, bool) for v in vals):
-        arr = np.asarray(vals, dtype=np.float64 if any(isinstance(v, (float, np.floating)) for v in vals)
+    nulls = np.array([is_null_scalar(v) for v in vals], dtype=bool)
+    present = [v for v, n in zip(vals, nulls) if not n]
+    rank = np.zeros(len(vals), dtype=np.int64)
+    if present and all(isinstance(v, (int, np.integer, float, np.floating)) and not isinstance(v, (bool, np.bool_))
+                       for v in present):
+        arr = np.asarray(present, dtype=np.float64 if any(isinstance(v, (float, np.floating)) for v in present)
                          else np.int64)
         _, inv = np.unique(arr, return_inverse=True)
-        return inv.astype(np.int64)
-    keyed = [spark_str(v) if not is_null_scalar(v) else "" for v in vals]
-    order = {k: i for i, k in enumerate(sorted(set(keyed)))}
-    return np.array([order[k] for k in keyed], dtype=np.int64)
+        rank[~nulls] = inv.astype(np.int64)
+    elif present:
+        keyed = [spark_str(v) for v in present]
+        order = {k: i for i, k in enumerate(sorted(set(keyed)))}
+        rank[~nulls] = np.array([order[k] for k in keyed], dtype=np.int64)
+    return rank, nulls
+
+
+def dense_rank_array(values: np.ndarray):
+    """dense_rank for a numeric numpy array without NULLs (vectorised fast path)."""
+    _, inv = np.unique(values, return_inverse=True)
+    return inv.astype(np.int64).reshape(-1), np.zeros(len(values), dtype=bool)
 
 
 def spark_substr(s: str, pos: int, length: int) -> str:

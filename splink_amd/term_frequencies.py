@@ -13,6 +13,7 @@ from collections import OrderedDict
 import numpy as np
 import pandas as pd
 
+from . import distributed as D
 from . import table as T
 from .check_types import check_types
 from .frames import ExpectationFrame, SplinkDataFrame, _HostColumns, df_e_column_order
@@ -79,6 +80,10 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
         ids0 = codes[0]
         ids1 = codes[1] if len(codes) > 1 else codes[0]
         sums, counts = job.ctx.tf_accumulate(n_values, ids0, ids1)
+        if job.reduces_across_ranks():
+            # the reference groups over ALL pairs (:49-65); each rank holds one shard of them
+            D.allreduce_host_(sums)
+            D.allreduce_host_(counts)
         with np.errstate(invalid="ignore", divide="ignore"):
             adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
         tables.append(_bayes_pair(adj_lambda, one_minus))

@@ -47,7 +47,8 @@ from splink.case_statements import (  # noqa: E402
     sql_gen_case_stmt_numeric_abs_3, sql_gen_case_stmt_numeric_abs_4, sql_gen_case_stmt_numeric_perc_3,
     sql_gen_case_stmt_numeric_perc_4, sql_gen_gammas_case_stmt_jaro_2, sql_gen_gammas_case_stmt_jaro_3,
     sql_gen_gammas_case_stmt_jaro_4, sql_gen_gammas_name_inversion_4, sql_gen_case_stmt_numeric_2)
-from splink.expectation_step import _sql_gen_expected_match_prob, _sql_gen_gamma_prob_columns  # noqa: E402
+from splink.expectation_step import (  # noqa: E402
+    _sql_gen_expected_match_prob, _sql_gen_gamma_prob_columns, get_overall_log_likelihood)
 from splink.gammas import _sql_gen_add_gammas  # noqa: E402
 from splink.maximisation_step import (  # noqa: E402
     _sql_gen_intermediate_pi_aggregate, _sql_gen_new_lambda, _sql_gen_pi_df)
@@ -128,9 +129,15 @@ def f32(x):
     return None if x is None else float(np.float32(x))
 
 
+def spark_ln(x):
+    """Spark's ln: NULL for x <= 0 (and for NULL)."""
+    return None if x is None or x <= 0 else math.log(x)
+
+
 def connect():
     con = sqlite3.connect(":memory:")
     con.row_factory = sqlite3.Row
+    con.create_function("ln", 1, spark_ln, deterministic=True)
     con.create_function("jaro_winkler_sim", 2, py_jaro_winkler, deterministic=True)
     con.create_function("levenshtein", 2, py_levenshtein, deterministic=True)
     con.create_function("length", 1, py_length, deterministic=True)
@@ -148,6 +155,40 @@ class JaroSpark:
         @staticmethod
         def listFunctions():
             return [_Fn()]
+
+
+class SqliteFrame:
+    """The slice of a Spark DataFrame that the reference's get_overall_log_likelihood touches
+    (expectation_step.py:224-272): createOrReplaceTempView, groupby().sum(col).collect()."""
+
+    def __init__(self, con, sql):
+        self.con, self.sql = con, sql
+        self._agg = None
+
+    def createOrReplaceTempView(self, name):  # noqa: N802
+        self.con.execute(f"drop view if exists {name}")
+        self.con.execute(f"create temp view {name} as {self.sql}")
+
+    def groupby(self):
+        return self
+
+    def sum(self, col):
+        out = SqliteFrame(self.con, self.sql)
+        out._agg = col
+        return out
+
+    def collect(self):
+        return [[self.con.execute(f"select sum({self._agg}) from ({self.sql})").fetchone()[0]]]
+
+
+class SqliteSpark:
+    """spark.sql over the sqlite connection (lazy, like Spark)."""
+
+    def __init__(self, con):
+        self.con = con
+
+    def sql(self, sql):
+        return SqliteFrame(self.con, sql)
 
 
 def spark_for(jaro):
@@ -197,7 +238,7 @@ def params_snapshot(params):
 # --------------------------------------------------------------------------------------
 # Reference pipeline: block -> gammas -> EM (iterate.py semantics) -> final E (-> tf)
 # --------------------------------------------------------------------------------------
-def reference_pipeline(settings_in, jaro, df=None, df_l=None, df_r=None, df_gammas=None, tf=False):
+def reference_pipeline(settings_in, jaro, df=None, df_l=None, df_r=None, df_gammas=None, tf=False, ll=False):
     spark = spark_for(jaro)
     settings = complete_settings_dict(copy.deepcopy(settings_in), spark)
     con = connect()
@@ -239,20 +280,30 @@ def reference_pipeline(settings_in, jaro, df=None, df_l=None, df_r=None, df_gamm
     out["settings_completed"] = params.settings
     out["initial"] = params_snapshot(params)
     try:
-        _em(con, params, settings, out, tf)
+        _em(con, params, settings, out, tf, ll)
     except Exception as e:  # the reference itself fails here; record the error it raises
         out["error"] = type(e).__name__
     return out
 
 
-def _em(con, params, settings, out, tf):
+def _log_likelihood(con, params):
+    """The reference's own get_overall_log_likelihood (expectation_step.py:259-272) on df_wgp."""
+    return get_overall_log_likelihood(SqliteFrame(con, "select * from df_wgp"), params, SqliteSpark(con))
+
+
+def _em(con, params, settings, out, tf, ll=False):
     iters = []
     out["iterations"] = iters
+    lls = []
+    if ll:
+        out["log_likelihood"] = lls  # one per E-step (iterate.py:45-63 with compute_ll=True)
     for _ in range(settings["max_iterations"]):
         con.execute("drop table if exists df_wgp")
         con.execute("drop table if exists df_e")
         con.execute("drop table if exists df_intermediate")
         con.execute("create table df_wgp as " + _sql_gen_gamma_prob_columns(params, settings, "df_gammas"))
+        if ll:
+            lls.append(_log_likelihood(con, params))
         con.execute("create table df_e as " + _sql_gen_expected_match_prob(params, settings, "df_wgp"))
         con.execute("create table df_intermediate as " + _sql_gen_intermediate_pi_aggregate(params, "df_e"))
         new_lambda = f32(con.execute(_sql_gen_new_lambda("df_intermediate")).fetchone()[0])
@@ -270,6 +321,8 @@ def _em(con, params, settings, out, tf):
     con.execute("drop table if exists df_wgp")
     con.execute("drop table if exists df_e")
     con.execute("create table df_wgp as " + _sql_gen_gamma_prob_columns(params, settings, "df_gammas"))
+    if ll:
+        lls.append(_log_likelihood(con, params))
     con.execute("create table df_e as " + _sql_gen_expected_match_prob(params, settings, "df_wgp"))
     df_e = q(con, "select * from df_e")
     out["df_e_columns"] = list(df_e.columns)
@@ -489,6 +542,60 @@ def custom_settings():
     }
 
 
+def tiny_numbers_settings(max_iterations):  # reference tests/test_spark.py:137-150
+    return {
+        "link_type": "dedupe_only", "proportion_of_matches": 0.4,
+        "comparison_columns": [
+            {"col_name": "mob", "num_levels": 2,
+             "m_probabilities": [5.9380419956766985e-25, 1 - 5.9380419956766985e-25], "u_probabilities": [0.8, 0.2]},
+            {"col_name": "surname", "num_levels": 2}],
+        "blocking_rules": ["l.mob = r.mob", "l.surname = r.surname"],
+        "max_iterations": max_iterations,
+    }
+
+
+def edge_cases():
+    """Reference edge cases replayed as fixtures (VERDICT r1 'missing' 5)."""
+    out = {}
+    # first E-step with the settings' m / u (max_iterations = 0): the literal lists of
+    # tests/test_expectation.py:57-66 and tests/test_nulls.py:11
+    st = gamma_settings_1()
+    st["max_iterations"] = 0
+    g = reference_pipeline(st, False, df=test1_records(), ll=True)
+    want = [0.893617021, 0.705882353, 0.705882353, 0.189189189, 0.189189189, 0.893617021, 0.375, 0.375]
+    assert all(abs(a - b) < 1e-8 for a, b in zip(g["df_e"]["match_probability"], want)), g["df_e"]["match_probability"]
+    g["reference_literal_mp"] = want
+    out["first_estep_test1"] = g
+    st = gamma_settings_2()
+    st["max_iterations"] = 0
+    g = reference_pipeline(st, False, df=test2_records(), ll=True)
+    want = [0.322580645, 0.16, 0.1, 0.16, 0.1, 0.1]
+    assert all(abs(a - b) < 1e-8 for a, b in zip(g["df_e"]["match_probability"], want)), g["df_e"]["match_probability"]
+    g["reference_literal_mp"] = want
+    out["first_estep_nulls"] = g
+    # tests/test_spark.py:130-160 (m = 5.9e-25 through the 35-digit literal), the first E-step and 3 iterations
+    out["tiny_numbers_estep"] = reference_pipeline(tiny_numbers_settings(0), False, df=test1_records(), ll=True)
+    out["tiny_numbers_em"] = reference_pipeline(tiny_numbers_settings(3), False, df=test1_records(), ll=True)
+    # compute_ll through every iteration (expectation_step.py:52-57, 224-272)
+    out["ll_test1"] = reference_pipeline(gamma_settings_1(), False, df=test1_records(), ll=True)
+    out["ll_nulls"] = reference_pipeline(gamma_settings_2(), False, df=test2_records(), ll=True)
+    df1 = make_records(**CONFIGS[1])
+    out["ll_cfg1"] = reference_pipeline(cfg_settings(1, max_iterations=4), True,
+                                        df=df1[["unique_id", "first_name", "surname", "dob", "city", "email"]], ll=True)
+    # NULL unique ids: `l.uid < r.uid` is NULL, so same-source pairs with a NULL id are dropped
+    # (blocking.py:136, :139); link_and_dedupe keeps cross-source pairs through `l.src < r.src`
+    recs = pd.DataFrame({"unique_id": [1.0, None, 3.0, None, 5.0, 2.0],
+                         "surname": ["a", "a", "a", "b", "b", "a"], "first_name": ["x", "y", "x", "y", "x", "y"]})
+    st = {"link_type": "dedupe_only", "comparison_columns": [{"col_name": "first_name"}],
+          "blocking_rules": ["l.surname = r.surname"], "max_iterations": 1}
+    out["null_uid_dedupe"] = reference_pipeline(st, False, df=recs)
+    st = {"link_type": "link_and_dedupe", "comparison_columns": [{"col_name": "first_name"}, {"col_name": "surname"}],
+          "blocking_rules": ["l.surname = r.surname"], "max_iterations": 1}
+    out["null_uid_link_and_dedupe"] = reference_pipeline(st, False, df_l=recs.iloc[:3].reset_index(drop=True),
+                                                         df_r=recs.iloc[3:].reset_index(drop=True))
+    return out
+
+
 def main():
     # 1. conftest test1 (two EM iterations, substr custom expression), jaro off (spark="supress_warnings")
     dump("test1", reference_pipeline(gamma_settings_1(), False, df=test1_records()))
@@ -550,7 +657,16 @@ def main():
     st["comparison_columns"][1]["term_frequency_adjustments"] = True
     st["em_convergence"] = 1e-4
     dump("link_tf", reference_pipeline(st, True, df_l=left, df_r=right, tf=True))
+    # 10. edge cases, log-likelihood, NULL unique ids
+    dump("edge_cases", edge_cases())
+
+
+def main_edge_only():
+    dump("edge_cases", edge_cases())
 
 
 if __name__ == "__main__":
-    main()
+    if "--edge-only" in sys.argv:
+        main_edge_only()
+    else:
+        main()

@@ -116,3 +116,33 @@ def test_single_process_helpers_are_identity():
     assert D.sum_over_ranks(7) == 7 and D.max_over_ranks(2.5) == 2.5
     h = torch.arange(5)
     assert D.allreduce_histogram_(h) is h and h.tolist() == [0, 1, 2, 3, 4]
+
+
+def _tf_rank_main(rank, world, port, out_dir):
+    """Per-value (Σmp, count) tables of the tf adjustment summed over ranks (term_frequencies.py:49-65)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from splink_amd import distributed as D
+    rng = np.random.Generator(np.random.PCG64(3))
+    ids = rng.integers(0, 50, 4000)           # value id of each pair (both sides equal)
+    mp = rng.random(4000)
+    lo, hi = 4000 * rank // world, 4000 * (rank + 1) // world
+    sums = np.bincount(ids[lo:hi], weights=mp[lo:hi], minlength=50).astype(np.float64)
+    counts = np.bincount(ids[lo:hi], minlength=50).astype(np.int64)
+    D.allreduce_host_(sums)
+    D.allreduce_host_(counts)
+    np.savez(os.path.join(out_dir, f"tf{rank}.npz"), sums=sums, counts=counts)
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_tf_tables(tmp_path):
+    world = 2
+    mp.start_processes(_tf_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    rng = np.random.Generator(np.random.PCG64(3))
+    ids = rng.integers(0, 50, 4000)
+    mpv = rng.random(4000)
+    for k in range(world):
+        x = np.load(tmp_path / f"tf{k}.npz")
+        assert (x["counts"] == np.bincount(ids, minlength=50)).all()
+        assert np.allclose(x["sums"], np.bincount(ids, weights=mpv, minlength=50), rtol=1e-12, atol=0)

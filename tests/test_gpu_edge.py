@@ -1,0 +1,121 @@
+"""Reference edge cases on the HIP path (through the C ABI), against fixtures generated from the reference.
+
+* the first E-step lists of tests/test_expectation.py:57-66 and tests/test_nulls.py:11;
+* m = 5.9e-25 through the 35-digit literal (tests/test_spark.py:130-160);
+* the log-likelihood of every E-step of iterate(compute_ll=True) (expectation_step.py:52-57, 224-272);
+* manually_apply_fellegi_sunter_weights (splink/__init__.py:111-119), the save_state_fn hook
+  (splink/iterate.py:54-55) and load_from_json -> Splink (splink/__init__.py:175-194);
+* NULL unique ids in dedupe_only and link_and_dedupe (blocking.py:136, :139).
+"""
+import copy
+import json
+import warnings
+
+import pytest
+
+from conftest import load_golden
+from test_gpu_parity import check_history, compare_frames, frame, rel_close, run_linker, spark_for
+
+pytestmark = pytest.mark.gpu
+warnings.filterwarnings("ignore")
+
+EDGE_PIPELINES = ["first_estep_test1", "first_estep_nulls", "tiny_numbers_estep", "tiny_numbers_em",
+                  "null_uid_dedupe", "null_uid_link_and_dedupe", "ll_cfg1"]
+LL_CASES = ["first_estep_test1", "first_estep_nulls", "tiny_numbers_estep", "tiny_numbers_em", "ll_test1",
+            "ll_nulls", "ll_cfg1"]
+
+
+@pytest.fixture(scope="module")
+def amd():
+    from splink_amd import AmdSession, _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the -m gpu tests need an MI355X")
+    return AmdSession(0)
+
+
+@pytest.mark.parametrize("case", EDGE_PIPELINES)
+def test_edge_pipeline_matches_reference(case, amd):
+    g = load_golden("edge_cases")[case]
+    linker = run_linker(g, amd)
+    df_e = linker.get_scored_comparisons()
+    compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])
+    check_history(linker.params, g)
+    if "reference_literal_mp" in g:  # the reference tests' own literal lists
+        got = sorted(df_e.toPandas()["match_probability"].tolist())
+        assert got == pytest.approx(sorted(g["reference_literal_mp"]), abs=1e-8)
+
+
+@pytest.mark.parametrize("case", LL_CASES)
+def test_log_likelihood_every_estep(case, amd):
+    """iterate(compute_ll=True): params.params['log_likelihood'] after every E-step, kept in the
+    parameter history, equals the reference's get_overall_log_likelihood at 1e-9."""
+    from splink_amd import Params, add_gammas, block_using_rules, complete_settings_dict, iterate
+    g = load_golden("edge_cases")[case]
+    spark = spark_for(g["jaro"], amd)
+    settings = complete_settings_dict(copy.deepcopy(g["settings_in"]), spark)
+    params = Params(settings, spark)
+    df_c = block_using_rules(settings, spark, df=frame(g.get("df")), df_l=frame(g.get("df_l")),
+                             df_r=frame(g.get("df_r")))
+    df_g = add_gammas(df_c, settings, spark)
+    df_e = iterate(df_g, params, settings, spark, compute_ll=True)
+    got = [h["log_likelihood"] for h in params.param_history] + [params.params["log_likelihood"]]
+    assert len(got) == len(g["log_likelihood"])
+    for a, b in zip(got, g["log_likelihood"]):
+        assert rel_close(a, b), (a, b)
+    compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])
+
+
+def test_manually_apply_fellegi_sunter_weights(amd):
+    """Scores with the settings' m / u and no EM: the reference's first E-step (test_expectation.py:57-66)."""
+    from splink_amd import Splink
+    g = load_golden("edge_cases")["first_estep_test1"]
+    settings = copy.deepcopy(g["settings_in"])
+    settings["max_iterations"] = 7  # ignored: no EM runs
+    linker = Splink(settings, spark_for(g["jaro"], amd), df=frame(g["df"]))
+    df_e = linker.manually_apply_fellegi_sunter_weights()
+    compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])
+    assert linker.params.iteration == 1 and linker.params.param_history == []
+
+
+def test_save_state_fn_called_every_iteration(amd):
+    """iterate.py:54-55: save_state_fn(params, settings) after every M-step, before the convergence test."""
+    g = load_golden("test1")
+    seen = []
+
+    def save_state(params, settings):
+        seen.append((params.iteration, params.params["λ"], settings["max_iterations"]))
+
+    from splink_amd import Splink
+    linker = Splink(copy.deepcopy(g["settings_in"]), spark_for(g["jaro"], amd), df=frame(g["df"]),
+                    save_state_fn=save_state)
+    linker.get_scored_comparisons()
+    assert [s[0] for s in seen] == list(range(2, 2 + len(g["iterations"])))
+    for (_, lam, mi), it in zip(seen, g["iterations"]):
+        assert rel_close(lam, it["lambda"]) and mi == g["settings_in"]["max_iterations"]
+
+
+def test_load_from_json_resumes(amd, tmp_path):
+    """save_model_as_json after one iteration, load_from_json, one more iteration: the reference's
+    second-iteration parameters and scores (test_spark.py:211-221, 296-311)."""
+    from splink_amd import Splink, load_from_json
+    g = load_golden("test1")
+    spark = spark_for(g["jaro"], amd)
+    settings = copy.deepcopy(g["settings_in"])
+    settings["max_iterations"] = 1
+    linker = Splink(settings, spark, df=frame(g["df"]))
+    linker.get_scored_comparisons()
+    assert rel_close(linker.params.params["λ"], g["iterations"][0]["lambda"])
+    path = str(tmp_path / "model.json")
+    linker.save_model_as_json(path)
+    saved = json.load(open(path))
+    assert set(saved) == {"current_params", "historical_params", "settings"}
+    linker2 = load_from_json(path, spark, df=frame(g["df"]))
+    assert linker2.params.params == linker.params.params
+    df_e = linker2.get_scored_comparisons()
+    it2 = g["iterations"][1]
+    assert rel_close(linker2.params.params["λ"], it2["lambda"])
+    for gname, d in it2["pi"].items():
+        for i, (m, u) in enumerate(zip(d["m"], d["u"])):
+            assert rel_close(linker2.params.params["π"][gname]["prob_dist_match"][f"level_{i}"]["probability"], m)
+            assert rel_close(linker2.params.params["π"][gname]["prob_dist_non_match"][f"level_{i}"]["probability"], u)
+    compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])

@@ -68,6 +68,10 @@ def compare_frames(got: pd.DataFrame, exp: dict, columns):
 
 
 def check_history(params, g):
+    if not g["iterations"]:  # max_iterations = 0: the initial parameters, untouched
+        assert params.param_history == []
+        assert rel_close(params.params["λ"], g["initial"]["lambda"])
+        return
     hist = params.param_history[1:] + [params.params]
     assert len(hist) == len(g["iterations"])
     for p, it in zip(hist, g["iterations"]):
@@ -507,18 +511,14 @@ def test_row_image_rebuilt_when_layout_changes(amd):
     assert (job.gammas_host() == h1).all()
 
 
-def test_sharded_ranks_match_single_process(amd, tmp_path):
-    """Two ranks (child processes, gloo, both on cuda:0) run the sharded device path -- pair-ordinal
-    shards of spk_block, per-rank comparison vectors, histogram all-reduce per EM iteration --
-    and end with the same parameters, bit for bit, as one process over all pairs."""
+def _two_ranks(tmp_path, mode=None):
+    """Run tests/gpu_dist_worker.py as two gloo ranks on cuda:0; returns their JSON outputs."""
     import json
     import os
     import socket
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    sys.path.insert(0, here)
-    import gpu_dist_worker as W
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -527,13 +527,51 @@ def test_sharded_ranks_match_single_process(amd, tmp_path):
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    LOCAL_RANK="0")
-        procs.append(subprocess.Popen([sys.executable, os.path.join(here, "gpu_dist_worker.py"), out], env=env))
+        cmd = [sys.executable, os.path.join(here, "gpu_dist_worker.py"), out] + ([mode] if mode else [])
+        procs.append(subprocess.Popen(cmd, env=env))
     for p in procs:
         assert p.wait(timeout=170) == 0
-    ranks = [json.load(open(f"{out}.{r}")) for r in range(2)]
-    single = W.run((0, 1))
+    return [json.load(open(f"{out}.{r}")) for r in range(2)]
+
+
+def test_sharded_ranks_match_oracle(amd, tmp_path):
+    """Two ranks (child processes, gloo, both on cuda:0) run the sharded device path -- pair-ordinal
+    shards of spk_block, per-rank comparison vectors, histogram all-reduce per EM iteration -- and
+    end with the oracle's parameters (C restatement over all pairs, at 1e-9), and bit for bit with
+    one process over all pairs."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import gpu_dist_worker as W
+    ranks = _two_ranks(tmp_path)
+    single, job, (lam0, lp0), nlev = W.run((0, 1), want_job=True)
     assert ranks[0]["n_pairs"] > 0 and ranks[1]["n_pairs"] > 0
     assert ranks[0]["n_pairs"] + ranks[1]["n_pairs"] == single["n_pairs"]
-    for r in ranks:
-        assert r["lambda"] == single["lambda"]
-        assert r["pi"] == single["pi"]
+    # the oracle over every pair, independent of the device's comparison vectors and EM
+    l, r = job.pair_rows()
+    table = job.tables[0]
+    cols = [orc.StrCol(table[c].tolist()) for c in W.COLS]
+    specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
+    gam = orc.template_gammas(specs, cols, cols, l, r)
+    hist_o, _ = orc.em_iterate(gam, nlev, lam0, [m for m, _ in lp0], [u for _, u in lp0], W.ITERS, 1e-300)
+    lam_o, m_o, u_o = hist_o[-1]
+    for rk in ranks:
+        assert rel_close(rk["lambda"], lam_o)
+        for k, (m, u) in enumerate(rk["pi"]):
+            assert all(rel_close(a, b) for a, b in zip(m, m_o[k])), (k, m, m_o[k])
+            assert all(rel_close(a, b) for a, b in zip(u, u_o[k]))
+        assert rk["lambda"] == single["lambda"] and rk["pi"] == single["pi"]
+
+
+def test_sharded_link_tf_matches_reference(amd, tmp_path):
+    """link_only with term-frequency adjustment on two gloo ranks on cuda:0: each rank scores its
+    shard of the pairs; the EM histogram and the per-value tf (Σmp, count) tables are all-reduced
+    (term_frequencies.py:49-65 groups over all pairs).  The ranks' frames together are the golden."""
+    g = load_golden("link_tf")
+    ranks = _two_ranks(tmp_path, "link_tf")
+    assert all(rk["n_pairs"] > 0 for rk in ranks)
+    assert ranks[0]["lambda"] == ranks[1]["lambda"]
+    for key in ("df_e", "df_tf"):
+        cols = ranks[0][f"{key}_columns"]
+        both = pd.concat([pd.DataFrame(rk[key])[cols] for rk in ranks], ignore_index=True)
+        compare_frames(both, g[key], g[f"{key}_columns"])

@@ -1,0 +1,110 @@
+"""Parity at the configs' own sizes (the bench workloads), against the C oracle.
+
+* cfg2 (BASELINE configs[1]): 1M synthetic person records, blocking surname|dob -> 45,981,122 pairs.
+  Every comparison vector bit-exact against oracle.template_gammas, 10 EM iterations of λ / m / u and
+  the final match_probability at 1e-9 against oracle.em_iterate (case_statements.py:81-141,
+  expectation_step.py:167-185, maximisation_step.py:16-90).
+* cfg5's columns at 1M records: + the free-text address column (Levenshtein-4, 30-128 characters).
+* The pair set at full size through size-independent properties: every pair satisfies a rule and
+  the link predicate, no pair repeats, and the count equals the inclusion-exclusion count of the
+  two equi-joins computed from the key histograms.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+
+import oracle as orc
+from test_gpu_parity import rel_close
+
+pytestmark = pytest.mark.gpu
+
+COLS = ["first_name", "surname", "dob", "city", "email"]
+SPECS = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3]),
+         ("lev", 4, [0.2, 0.4])]
+N_RECORDS = 1_000_000
+CFG2_PAIRS = 45_981_122  # bench.py's headline workload (BENCH_r01.json config.candidate_pairs)
+
+
+@pytest.fixture(scope="module")
+def amd():
+    from splink_amd import AmdSession, _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the -m gpu tests need an MI355X")
+    return AmdSession(0)
+
+
+def _c2(n):
+    n = n.astype(np.int64)
+    return int((n * (n - 1) // 2).sum())
+
+
+def expected_pair_count(table):
+    """|surname join ∪ dob join| for dedupe with unique ids: Σ C(n_s, 2) + Σ C(n_d, 2) - Σ C(n_sd, 2)."""
+    s = table["surname"].dropna()
+    d = table["dob"].dropna()
+    both = table.dropna(subset=["surname", "dob"])
+    return (_c2(s.value_counts().to_numpy()) + _c2(d.value_counts().to_numpy())
+            - _c2(both.groupby(["surname", "dob"]).size().to_numpy()))
+
+
+def check_pair_properties(table, l, r):
+    uid = table["unique_id"].to_numpy()
+    assert (uid[l] < uid[r]).all()
+    sn, _ = pd.factorize(table["surname"])  # -1 = NULL
+    dob, _ = pd.factorize(table["dob"])
+    same_s = (sn[l] >= 0) & (sn[l] == sn[r])
+    same_d = (dob[l] >= 0) & (dob[l] == dob[r])
+    assert (same_s | same_d).all()
+    # rule order: surname pairs first, then dob pairs that are not surname pairs
+    n_s = int(same_s.sum())
+    assert same_s[:n_s].all() and not same_s[n_s:].any()
+    key = l.astype(np.int64) * len(table) + r.astype(np.int64)
+    assert len(np.unique(key)) == len(key)
+    assert len(key) == expected_pair_count(table)
+
+
+def run_full(amd, with_address, iters):
+    from splink_amd.engine import Job, m_step_rows
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    cols = COLS + (["address"] if with_address else [])
+    df = make_records(N_RECORDS, surname_vocab=15000, with_address=with_address)[["unique_id"] + cols]
+    params = Params(cfg_settings(5 if with_address else 2, max_iterations=iters), amd)
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    table = job.tables[0]
+    l, r = job.pair_rows()
+    check_pair_properties(table, l, r)
+    job.gammas(st)
+    gam = job.gammas_host()
+    ocols = [orc.StrCol(table[c].tolist()) for c in cols]
+    ref = orc.template_gammas(SPECS[:len(cols)], ocols, ocols, l, r)
+    bad = np.nonzero((gam != ref).any(axis=1))[0]
+    assert len(bad) == 0, (len(bad), bad[:5], gam[bad[:5]], ref[bad[:5]])
+    del ref, ocols
+    names, nlev = job.code_meta
+    lam0, lp0 = params.params["λ"], params._level_probabilities()
+    hist_o, mp_o = orc.em_iterate(gam, nlev, lam0, [m for m, _ in lp0], [u for _, u in lp0], iters, 1e-300)
+    assert len(hist_o) == iters
+    for lam_o, m_o, u_o in hist_o:
+        stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        new_lambda, rows = m_step_rows(stats, names, nlev)
+        params._update_params(new_lambda, rows)
+        assert rel_close(params.params["λ"], lam_o)
+        for k, (m, u) in enumerate(params._level_probabilities()):
+            assert all(rel_close(a, b) for a, b in zip(m, m_o[k])), (k, m, m_o[k])
+            assert all(rel_close(a, b) for a, b in zip(u, u_o[k])), (k, u, u_o[k])
+    mp = job.score(params.params["λ"], params._level_probabilities())
+    assert np.allclose(mp, mp_o, rtol=1e-9, atol=0, equal_nan=True)
+    return job
+
+
+def test_cfg2_full_size(amd):
+    job = run_full(amd, with_address=False, iters=10)
+    assert job.n_pairs == CFG2_PAIRS
+
+
+def test_cfg5_columns_full_size(amd):
+    job = run_full(amd, with_address=True, iters=3)
+    assert job.n_pairs > 40_000_000

@@ -155,3 +155,38 @@ def test_tf_adjust():
     exp = tf["tf_adjusted_match_prob"].astype(float).to_numpy()
     assert np.allclose(out, exp, rtol=1e-9, atol=0)
     assert np.allclose(adjs[0], tf["surname_adj"].astype(float).to_numpy(), rtol=1e-9, atol=0)
+
+
+EDGE = ["first_estep_test1", "first_estep_nulls", "tiny_numbers_estep", "tiny_numbers_em", "ll_test1", "ll_nulls",
+        "ll_cfg1", "null_uid_dedupe", "null_uid_link_and_dedupe"]
+
+
+def oracle_log_likelihoods(g, gam):
+    """One log-likelihood per E-step of iterate(compute_ll=True): the initial parameters, then the
+    parameters after each M-step (expectation_step.py:52-57; iterate.py:45-63)."""
+    names, nlev, lam, m, u, st = golden_params(g)
+    hist, _ = orc.em_iterate(gam, nlev, lam, m, u, st["max_iterations"], st["em_convergence"])
+    params = [(lam, m, u)] + list(hist)
+    return [orc.log_likelihood(gam, nlev, *p) for p in params]
+
+
+@pytest.mark.parametrize("case", EDGE)
+def test_edge_cases(case):
+    """Reference edge cases (tests/test_expectation.py:57-66, tests/test_nulls.py:11, tests/test_spark.py:130-160),
+    NULL unique ids, and the log-likelihood of every E-step (expectation_step.py:224-272)."""
+    g = load_golden("edge_cases")[case]
+    got, names, _, _ = run_oracle_pipeline(g)
+    exp = frame(g["gammas"])
+    assert len(got) == len(exp)
+    nan_none = lambda xs: [None if isinstance(v, float) and math.isnan(v) else v for v in xs]  # noqa: E731
+    for c in pair_keys(exp) + names:
+        assert nan_none(got[c].tolist()) == nan_none(exp[c].tolist()), c
+    gam = exp[names].to_numpy(np.int8)
+    _check_em(g, gam)
+    if "reference_literal_mp" in g:  # the reference's own hand-calculated lists (abs 1e-8)
+        assert g["df_e"]["match_probability"] == pytest.approx(g["reference_literal_mp"], abs=1e-8)
+    if "log_likelihood" in g:
+        lls = oracle_log_likelihoods(g, gam)
+        assert len(lls) == len(g["log_likelihood"])
+        for a, b in zip(lls, g["log_likelihood"]):
+            assert rel_close(a, b), (a, b)
