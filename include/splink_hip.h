@@ -81,6 +81,39 @@ int spk_table_set_rank_null(spk_ctx *ctx, int side, int64_t divisor);
  * which = 0: key of the row as the join's l-side; which = 1: as the r-side. */
 int spk_table_set_key(spk_ctx *ctx, int side, int rule, int which, const int64_t *keys);
 
+/* ---- device ingest (replaces the per-row key / value preparation that Spark does inside the
+ *      equi-joins of blocking.py:95-160 and the projections of gammas.py:65-89) ----------------
+ * Input columns are handed over once as Arrow buffers ("raw" columns, input row order, indexed by
+ * `raw`, borrowed for the call).  Everything derived from them is computed on the device. */
+int spk_raw_utf8(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const uint8_t *data, const uint8_t *valid);
+/* 8-byte values compared as bit patterns (int64 ids, canonical float64 bits, host-computed key ids). */
+int spk_raw_i64(spk_ctx *ctx, int raw, int64_t n, const int64_t *values, const uint8_t *valid);
+/* One equality term of a blocking rule: l-side column `raw_l` (table 0) = r-side column `raw_r` (the
+ * r table; -1 = the same column, a symmetric term), each with an optional Spark substr(start, len)
+ * on code points (len < 0 = none). */
+typedef struct {
+    int32_t raw_l, raw_r;
+    int32_t l_substr_start, l_substr_len;
+    int32_t r_substr_start, r_substr_len;
+} spk_key_term;
+/* Blocking key of rule `rule` (the conjunction of its terms; NULL if a term is NULL): hash, radix sort
+ * and verified dense ids on the device, one id space for both sides.  Same result as
+ * spk_table_set_key with host-computed ids (which stays available for other key expressions). */
+int spk_key_build(spk_ctx *ctx, int rule, int n_terms, const spk_key_term *terms);
+/* Rank for the link predicate from int64 unique ids (raw column, NULL allowed): dense rank, rows
+ * [right_from, n) being the 'right' source of link_and_dedupe (-1 = none).  Also sets the NULL-id
+ * layout of spk_table_set_rank_null. */
+int spk_rank_from_raw(spk_ctx *ctx, int raw_uid, int64_t right_from);
+/* Reorder the tables' rows by rule 0's key, then rank (NULL keys last), so a block's rows are
+ * contiguous on the device.  Keys and ranks move with the rows; comparison columns must be added
+ * after this (they are decoded through the permutation).  out_perm0 / out_perm1 (host, optional):
+ * input row of each table row. */
+int spk_cluster(spk_ctx *ctx, int32_t *out_perm0, int32_t *out_perm1);
+/* String comparison column `col` from raw column raw0 (table 0) and, for link_only, raw1 (table 1):
+ * decoded to UTF-16 through the tables' row permutations, with dictionary ids computed on the
+ * device in one id space for both sides. */
+int spk_table_add_raw_utf8(spk_ctx *ctx, int col, int raw0, int raw1);
+
 /* ---- blocking (replaces block_using_rules / cartesian_block, blocking.py:162-318) -- */
 /* Generates candidate pairs for rules 0..n_rules-1 in order, each excluding pairs an earlier
  * rule matched (`AND NOT ifnull(rule_j, false)`, :59-68), with the link-type predicate.

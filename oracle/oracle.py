@@ -94,7 +94,8 @@ class StrCol:
     well under a second; lone surrogates pass through as in a Java String."""
 
     def __init__(self, values):
-        vals = [None if (v is None or (isinstance(v, float) and np.isnan(v))) else str(v) for v in values]
+        vals = [None if (v is None or v is pd.NA or (isinstance(v, float) and np.isnan(v))) else str(v)
+                for v in values]
         n = len(vals)
         self.valid = np.array([v is not None for v in vals], dtype=np.uint8)
         strs = [v if v is not None else "" for v in vals]

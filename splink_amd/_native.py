@@ -30,6 +30,9 @@ INSTR_DTYPE = np.dtype([("op", "<i4"), ("a", "<i4"), ("b", "<i4"), ("cmp", "<i4"
                         ("t", "<f8")], align=True)
 PROGRAM_DTYPE = np.dtype([("n_levels", "<i4"), ("else_level", "<i4"), ("n_when", "<i4"), ("first_when", "<i4")],
                          align=True)
+KEY_TERM_DTYPE = np.dtype([("raw_l", "<i4"), ("raw_r", "<i4"), ("l_substr_start", "<i4"), ("l_substr_len", "<i4"),
+                           ("r_substr_start", "<i4"), ("r_substr_len", "<i4")], align=True)
+assert KEY_TERM_DTYPE.itemsize == 24
 assert OPERAND_DTYPE.itemsize == 40 and INSTR_DTYPE.itemsize == 32 and PROGRAM_DTYPE.itemsize == 16
 
 OP = {"ISNULL": 1, "NOTNULL": 2, "STR_CMP": 3, "NUM_CMP": 4, "JW": 5, "LEV": 6, "LEVRATIO": 7, "ABSDIFF": 8,
@@ -44,6 +47,7 @@ EXPORTS = [
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
     "spk_gammas_set_simple", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
+    "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
 ]
 
 
@@ -159,6 +163,45 @@ class Context:
     def table_set_rank_null(self, side, divisor):
         check(self._lib.spk_table_set_rank_null(self._h, ctypes.c_int(side), ctypes.c_int64(divisor)),
               "spk_table_set_rank_null")
+
+    # ---- device ingest ---------------------------------------------------------------------
+    def raw_utf8(self, raw, offsets, data, valid):
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, dtype=np.uint8)
+        valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        check(self._lib.spk_raw_utf8(self._h, ctypes.c_int(raw), ctypes.c_int64(len(offsets) - 1), _ptr(offsets),
+                                     _ptr(data), _ptr(valid)), "spk_raw_utf8")
+
+    def raw_i64(self, raw, values, valid):
+        values = np.ascontiguousarray(values, dtype=np.int64)
+        valid = np.ascontiguousarray(valid, dtype=np.uint8)
+        if values.size == 0:
+            values, valid = np.zeros(1, np.int64), np.zeros(1, np.uint8)
+            n = 0
+        else:
+            n = len(values)
+        check(self._lib.spk_raw_i64(self._h, ctypes.c_int(raw), ctypes.c_int64(n), _ptr(values), _ptr(valid)),
+              "spk_raw_i64")
+
+    def key_build(self, rule, terms):
+        t = np.array([tuple(x) for x in terms], dtype=KEY_TERM_DTYPE)
+        check(self._lib.spk_key_build(self._h, ctypes.c_int(rule), ctypes.c_int(len(t)), _ptr(t)), "spk_key_build")
+
+    def rank_from_raw(self, raw_uid, right_from=-1):
+        check(self._lib.spk_rank_from_raw(self._h, ctypes.c_int(raw_uid), ctypes.c_int64(right_from)),
+              "spk_rank_from_raw")
+
+    def cluster(self, n0, n1=None):
+        p0 = np.empty(max(n0, 1), dtype=np.int32)
+        p1 = np.empty(max(n1 or 0, 1), dtype=np.int32) if n1 is not None else None
+        check(self._lib.spk_cluster(self._h, _ptr(p0), _ptr(p1)), "spk_cluster")
+        return p0[:n0], (p1[:n1] if p1 is not None else None)
+
+    def table_add_raw_utf8(self, col, raw0, raw1=-1):
+        check(self._lib.spk_table_add_raw_utf8(self._h, ctypes.c_int(col), ctypes.c_int(raw0), ctypes.c_int(raw1)),
+              "spk_table_add_raw_utf8")
 
     def table_set_key(self, side, rule, which, keys):
         keys = np.ascontiguousarray(keys, dtype=np.int64)

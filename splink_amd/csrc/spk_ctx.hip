@@ -45,17 +45,21 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
 // Surrogate-encoded (CESU / "surrogatepass") 3-byte sequences decode to lone surrogate units,
 // exactly as a Java String would hold them.
 
-__global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const uint8_t *__restrict__ bytes,
+// perm (optional): row `row` of the table is row perm[row] of the source buffers (src_off / bytes /
+// valid / ids); off8 is then the layout of the permuted rows (exclusive scan of their byte lengths).
+__global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const int64_t *__restrict__ src_off,
+                              const int32_t *__restrict__ perm, const uint8_t *__restrict__ bytes,
                               const uint8_t *__restrict__ valid, uint16_t *__restrict__ units,
                               RecMeta *__restrict__ meta, uint64_t *__restrict__ planes,
                               uint64_t *__restrict__ planes_hi, const int64_t *__restrict__ ids) {
     int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= n) return;
+    const int64_t src = perm ? (int64_t)perm[row] : row;
     RecMeta m;
     const int64_t start = (off8[row] + 3 * row + 3) & ~(int64_t)3;
     m.off4 = (uint32_t)(start >> 2);
     m.head = 0;
-    if (!valid[row]) {
+    if (!valid[src]) {
         m.len16 = -1;
         m.cpf = 0;
         m.key = 0;
@@ -66,7 +70,8 @@ __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const
             for (int b = 0; b < N_PLANES; ++b) planes_hi[row * N_PLANES + b] = 0;
         return;
     }
-    int64_t b = off8[row], e = off8[row + 1];
+    const int64_t *so = src_off ? src_off : off8;
+    int64_t b = so[src], e = so[src + 1];
     uint16_t *dst = units + start;
     int32_t nu = 0, nc = 0;
     uint64_t h = 1469598103934665603ull, sk = 0;
@@ -120,9 +125,34 @@ __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const
     m.len16 = nu;
     m.cpf = (uint32_t)nc | (ok ? CPF_PLANES : 0u) | (ok2 ? CPF_PLANES2 : 0u) | (ids ? CPF_ID : 0u);
     h ^= (uint64_t)nu;
-    m.key = ids ? (uint32_t)ids[row] : (uint32_t)(h ^ (h >> 32));
+    m.key = ids ? (uint32_t)ids[src] : (uint32_t)(h ^ (h >> 32));
     m.sketch = sk;
     meta[row] = m;
+}
+
+int launch_utf8_decode(spk_ctx *ctx, int64_t n, const int64_t *off8, const int64_t *src_off, const int32_t *perm,
+                       const uint8_t *bytes, const uint8_t *valid, Column *c, bool long_rows, const int64_t *ids) {
+    if (n <= 0) return SPK_OK;
+    k_utf8_decode<<<(unsigned)((n + 255) / 256), 256, 0, ctx->stream>>>(n, off8, src_off, perm, bytes, valid, c->units.p,
+                                                                        c->meta.p, c->planes.p,
+                                                                        long_rows ? c->planes_hi.p : nullptr, ids);
+    SPK_HIP(hipGetLastError());
+    return SPK_OK;
+}
+
+
+int new_column(spk_ctx *ctx, int side, int col, Column **out) {
+    SPK_REQUIRE(ctx && (side == 0 || side == 1), SPK_E_INVALID, "bad side");
+    Table &t = ctx->table[side];
+    SPK_REQUIRE(t.n >= 0, SPK_E_STATE, "table not created");
+    SPK_REQUIRE(col >= 0 && col < 4096, SPK_E_INVALID, "column index out of range");
+    if (col >= (int)t.cols.size()) t.cols.resize((size_t)col + 1, nullptr);
+    delete t.cols[col];
+    t.cols[col] = new Column();
+    t.desc_dirty = true;
+    t.version = ++ctx->table_epoch;
+    *out = t.cols[col];
+    return SPK_OK;
 }
 
 }  // namespace spk
@@ -240,6 +270,7 @@ int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols) {
         t.key[w].clear();
     }
     t.rank.release();
+    t.perm.release();
     t.null_div = 0;
     t.n = n_rows;
     t.desc_dirty = true;
@@ -249,25 +280,12 @@ int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols) {
     return SPK_OK;
 }
 
-static int get_col(spk_ctx *ctx, int side, int col, Column **out) {
-    SPK_REQUIRE(ctx && (side == 0 || side == 1), SPK_E_INVALID, "bad side");
-    Table &t = ctx->table[side];
-    SPK_REQUIRE(t.n >= 0, SPK_E_STATE, "table not created");
-    SPK_REQUIRE(col >= 0 && col < 4096, SPK_E_INVALID, "column index out of range");
-    if (col >= (int)t.cols.size()) t.cols.resize((size_t)col + 1, nullptr);
-    delete t.cols[col];
-    t.cols[col] = new Column();
-    t.desc_dirty = true;
-    t.version = ++ctx->table_epoch;
-    *out = t.cols[col];
-    return SPK_OK;
-}
 
 int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, const uint8_t *data,
                        const uint8_t *valid, const int64_t *value_ids) {
     SPK_REQUIRE(offsets && valid, SPK_E_INVALID, "spk_table_add_utf8: null buffer");
     Column *c = nullptr;
-    SPK_TRY(get_col(ctx, side, col, &c));
+    SPK_TRY(new_column(ctx, side, col, &c));
     SPK_HIP(hipSetDevice(ctx->device));
     int64_t n = ctx->table[side].n;
     int64_t nbytes = offsets[n];
@@ -304,8 +322,8 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
     SPK_HIP(hipMemcpyAsync(d_off8.p, offsets, (size_t)(n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
     if (n) {
         int bs = 256;
-        k_utf8_decode<<<(unsigned)((n + bs - 1) / bs), bs, 0, ctx->stream>>>(n, d_off8.p, d_bytes.p, d_valid.p,
-                                                                          c->units.p, c->meta.p, c->planes.p,
+        k_utf8_decode<<<(unsigned)((n + bs - 1) / bs), bs, 0, ctx->stream>>>(n, d_off8.p, nullptr, nullptr, d_bytes.p,
+                                                                          d_valid.p, c->units.p, c->meta.p, c->planes.p,
                                                                           long_rows ? c->planes_hi.p : nullptr,
                                                                           value_ids ? d_ids.p : nullptr);
         SPK_HIP(hipGetLastError());
@@ -318,7 +336,7 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
 int spk_table_add_float64(spk_ctx *ctx, int side, int col, const double *values, const uint8_t *valid) {
     SPK_REQUIRE(values && valid, SPK_E_INVALID, "spk_table_add_float64: null buffer");
     Column *c = nullptr;
-    SPK_TRY(get_col(ctx, side, col, &c));
+    SPK_TRY(new_column(ctx, side, col, &c));
     SPK_HIP(hipSetDevice(ctx->device));
     int64_t n = ctx->table[side].n;
     c->kind = COL_NUM;

@@ -64,7 +64,17 @@ struct SimpleCol {
     int32_t off;      // byte offset of the column's fields in a row-image row
     int32_t off2;     // SC_JW: offset of the four head units
     int32_t has_ids;  // both sides carry dictionary ids (equal keys = equal strings)
+    // Per-test decision parameters, precomputed on the host (prepare_tests) so the filter decides
+    // every test with compares and selects only -- no divergent branches:
+    int32_t tflag[MAX_TESTS];  // TF_* bits
+    int32_t lev_a[MAX_TESTS];  // LEV (absolute): integer bound of the equivalent integer test
+    float jw_cf[MAX_TESTS];    // JW: an upper bound hi < jw_cf proves the test false
 };
+constexpr int32_t TF_ZERO = 1;     // the value 0.0 passes the test (JW of strings without a common unit; lev ratio 0)
+constexpr int32_t TF_ONE = 2;      // JW: the value 1.0 passes (equal non-empty strings)
+constexpr int32_t TF_GE = 4;       // LEV: the test is `lev >= lev_a` (else `lev <= lev_a`)
+constexpr int32_t TF_EXACT = 8;    // LEV `=` / `<>`: decided only when the bounds meet
+constexpr int32_t TF_EQ = 16;      // `=` (else `<>`)
 
 // ---- filter row image ----------------------------------------------------------------------------
 // The filter needs a few bytes per (row, column) -- equality key, lengths, unit sketch, head units --
@@ -154,6 +164,23 @@ __device__ inline int k_or(int a, int b) {
     return (a == KN || b == KN) ? KN : KF;
 }
 __device__ inline int k_not(int a) { return (a == KN || a == KU) ? a : (a == KT ? KF : KT); }
+
+// Fold one WHEN test into the branch chain: the first test that is TRUE (or UNDECIDED) ends it;
+// FALSE and NULL fall through to the next WHEN (a NULL predicate is a branch not taken).  r is
+// KF 0 / KT 1 / KN 2 / KU 3, so "ends the chain" is r & 1 and "undecided" r >> 1 on top: the chain
+// state stays in integer registers (VALU bit ops) instead of per-lane condition masks, and the
+// lanes of a wave never diverge over which test decided them.
+struct Chain {
+    int open = 1, und = 0, lvl;
+    __device__ explicit Chain(int else_level) : lvl(else_level) {}
+    __device__ __attribute__((always_inline)) void fold(int r, int lvl_i) {
+        const int hit = r & open;  // bit 0: TRUE / UNDECIDED while open
+        und |= hit & (r >> 1);
+        lvl += hit * (lvl_i - lvl);
+        open &= ~hit;
+    }
+};
+
 
 __device__ inline int cmpd(double a, double b, int cmp) {
     bool r;
@@ -560,21 +587,17 @@ __device__ __attribute__((always_inline)) inline int simple_str(const SC &sc, co
 
 template <class SC>
 __device__ __attribute__((always_inline)) inline int simple_num(const SC &sc, bool va, double a, bool vb, double b) {
-    if (!va || !vb) return sc.null_level;
+    Chain c(sc.else_level);
+    const double diff = fabs(a - b), big = fabs(a > b ? a : b);
     for (int i = 0; i < sc.n_tests; ++i) {
         const int op = sc.op[i], cmp = sc.cmp[i];
         int r;
-        if (op == SPK_OP_NUM_CMP) {
-            r = cmpd(a, b, cmp);
-        } else if (op == SPK_OP_ABSDIFF) {
-            r = cmpd(fabs(a - b), sc.t[i], cmp);
-        } else {  // SPK_OP_PERCDIFF
-            const double d = fabs(a > b ? a : b);
-            r = d == 0.0 ? KN : cmpd(fabs(a - b) / d, sc.t[i], cmp);
-        }
-        if (r == KT) return sc.level[i];
+        if (op == SPK_OP_NUM_CMP) r = cmpd(a, b, cmp);
+        else if (op == SPK_OP_ABSDIFF) r = cmpd(diff, sc.t[i], cmp);
+        else r = big == 0.0 ? KN : cmpd(diff / big, sc.t[i], cmp);  // SPK_OP_PERCDIFF
+        c.fold(r, sc.level[i]);
     }
-    return sc.else_level;
+    return (!va || !vb) ? sc.null_level : c.lvl;
 }
 
 // rows_img: the image's row capacity (its chunk stride); rows [0, n) are filled.
@@ -609,131 +632,112 @@ __device__ inline int lens_u16(uint32_t l) { return (int)(l & 0xFFFFu); }
 __device__ inline int lens_cp(uint32_t l) { return (int)(l >> 16); }
 __device__ inline uint64_t img_sketch(const uint4 &v) { return ((uint64_t)v.w << 32) | v.z; }
 
-// 1 equal, 0 unequal, -1 only the units can tell (equal hash keys without dictionary ids)
-template <class SC>
-__device__ inline int img_equal(const SC &sc, uint32_t ka, uint32_t la, uint32_t kb, uint32_t lb) {
-    if (la != lb || ka != kb) return 0;
-    return sc.has_ids ? 1 : -1;
+// sketch_inter_ub without the data-dependent branch (both saturated buckets add min(rest_a, rest_b)).
+__device__ __attribute__((always_inline)) inline int sketch_inter_ub_bf(uint64_t sa, uint64_t sb, int la, int lb) {
+    const uint32_t aL = (uint32_t)sa, aH = (uint32_t)(sa >> 32);
+    const uint32_t bL = (uint32_t)sb, bH = (uint32_t)(sb >> 32);
+    const uint32_t gt = (aH & ~bH) | (~(aH ^ bH) & aL & ~bL);
+    const uint32_t mL = (aL & ~gt) | (bL & gt), mH = (aH & ~gt) | (bH & gt);
+    const uint32_t both_sat = aL & aH & bL & bH, rest = ~both_sat;
+    int inter = __builtin_popcount(mL & rest) + 2 * __builtin_popcount(mH & rest);
+    const int ra = la - (__builtin_popcount(aL & rest) + 2 * __builtin_popcount(aH & rest));
+    const int rb = lb - (__builtin_popcount(bL & rest) + 2 * __builtin_popcount(bH & rest));
+    inter += both_sat ? (ra < rb ? ra : rb) : 0;
+    const int lmn = la < lb ? la : lb;
+    return inter < lmn ? inter : lmn;
 }
 
+// `=` / `<>` tests.  Equal keys prove equality with dictionary ids; without them only the units can tell.
 template <class SC>
 __device__ inline int img_eq(const SC &sc, uint2 a, uint2 b, int &level) {
-    if (a.y == LENS_NULL || b.y == LENS_NULL) {
-        level = sc.null_level;
-        return ST_DONE;
-    }
-    const int eq = img_equal(sc, a.x, a.y, b.x, b.y);
-    if (eq < 0) return ST_UNDECIDED;
-    for (int i = 0; i < sc.n_tests; ++i)
-        if ((eq == 1) == (sc.cmp[i] == SPK_CMP_EQ)) {
-            level = sc.level[i];
-            return ST_DONE;
-        }
-    level = sc.else_level;
-    return ST_DONE;
+    const bool nul = a.y == LENS_NULL || b.y == LENS_NULL;
+    const int same = (a.x == b.x) & (a.y == b.y);
+    Chain c(sc.else_level);
+    for (int i = 0; i < sc.n_tests; ++i) c.fold(same ^ ((sc.tflag[i] & TF_EQ) ? 0 : 1), sc.level[i]);
+    level = nul ? sc.null_level : c.lvl;
+    return (!nul && same && !sc.has_ids) ? ST_UNDECIDED : ST_DONE;
 }
 
 // jaro_winkler_sim(l, r) > / >= t tests.  Equal strings and strings without a common unit have
 // exact values (1.0 / 0.0); otherwise the upper bound from the sketches (m <= M, (m - t)/m <= 1)
 // and the head units (Winkler prefix) is evaluated in fp32 with a 1e-5 margin, far above its
-// rounding; a bound can only prove a test false, every other cell goes to the exact pass.
+// rounding; a bound can only prove a test false, every other cell goes to the exact pass.  The
+// float thresholds jw_cf are the doubles' exact float images (prepare_tests).  The bound is only
+// computed when some lane of the wave needs it (in the first rule's blocks every pair shares
+// the blocking key, so a wave of such pairs skips it for that column).
 template <class SC>
 __device__ inline int img_jw(const SC &sc, uint4 a, uint4 b, uint64_t ha, uint64_t hb, int &level) {
-    if (a.y == LENS_NULL || b.y == LENS_NULL) {
-        level = sc.null_level;
-        return ST_DONE;
-    }
-    const int eq = img_equal(sc, a.x, a.y, b.x, b.y);
+    const bool nul = a.y == LENS_NULL || b.y == LENS_NULL;
+    const bool same = a.x == b.x && a.y == b.y;
     const int lf = lens_u16(a.y), ls = lens_u16(b.y);
-    if (eq < 0 || lf >= LEN_SAT || ls >= LEN_SAT) return ST_UNDECIDED;
-    double v = -1.0;  // the exact similarity when the records determine it
-    float hi = 0.f;   // else an upper bound
-    if (eq == 1) {
-        v = lf > 0 ? 1.0 : 0.0;
-    } else {
-        const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
-        const int M = lmn == 0 ? 0 : sketch_inter_ub(img_sketch(a), img_sketch(b), lf, ls);
-        if (M == 0) {
-            v = 0.0;
-        } else {
-            // v_rcp_f32 (1 ulp) instead of IEEE divisions: the error (< 1e-6 on j) sits far inside
-            // the 1e-5 margin, so hi stays an upper bound
-            float j = ((float)M * (float)(lf + ls) * __builtin_amdgcn_rcpf((float)lf * (float)ls) + 1.0f) *
-                      (1.0f / 3.0f);
-            if (j >= 0.7f - 1e-4f) {
-                const uint64_t d = ha ^ hb;
-                const int cp = d ? (__ffsll((unsigned long long)d) - 1) >> 4 : 4;
-                const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
-                const float pw = (lmx > 10 ? __builtin_amdgcn_rcpf((float)lmx) : 0.1f) * (float)prefix;
-                j = j + pw * (1.0f - j);
-            }
-            hi = j + 1e-5f;
-        }
+    const bool und0 = (same && !sc.has_ids) || lf >= LEN_SAT || ls >= LEN_SAT;
+    const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
+    bool exact = same || lmn == 0;
+    float hi = 0.f;
+    if (__ballot(!exact) != 0ull) {  // wave-uniform
+        const int M = sketch_inter_ub_bf(img_sketch(a), img_sketch(b), lf, ls);
+        exact = exact || M == 0;
+        // v_rcp_f32 (1 ulp) instead of IEEE divisions: the error (< 1e-6 on j) sits far inside the
+        // 1e-5 margin, so hi stays an upper bound (the exact cases never read it)
+        const float j = ((float)M * (float)(lf + ls) * __builtin_amdgcn_rcpf((float)lf * (float)ls) + 1.0f) *
+                        (1.0f / 3.0f);
+        const uint64_t d = ha ^ hb;
+        const int cp = d ? (__ffsll((unsigned long long)d) - 1) >> 4 : 4;
+        const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
+        const float pw = (lmx > 10 ? __builtin_amdgcn_rcpf((float)lmx) : 0.1f) * (float)prefix;
+        hi = (j >= 0.7f - 1e-4f ? j + pw * (1.0f - j) : j) + 1e-5f;
     }
+    const bool one = same && lf > 0;
+    Chain c(sc.else_level);
     for (int i = 0; i < sc.n_tests; ++i) {
-        const double t = sc.t[i];
-        int r;
-        if (v >= 0.0) r = cmpd(v, t, sc.cmp[i]);
-        else if (sc.cmp[i] == SPK_CMP_GT) r = 0.0 > t ? KT : ((double)hi <= t ? KF : KU);
-        else r = 0.0 >= t ? KT : ((double)hi < t ? KF : KU);  // SPK_CMP_GE
-        if (r == KU) return ST_UNDECIDED;
-        if (r == KT) {
-            level = sc.level[i];
-            return ST_DONE;
-        }
+        const int f = sc.tflag[i];
+        const int r_exact = one ? ((f >> 1) & 1) : (f & TF_ZERO);   // TF_ONE / TF_ZERO -> KT / KF
+        const int r_bound = hi < sc.jw_cf[i] ? KF : ((f & TF_ZERO) ? KT : KU);
+        c.fold(exact ? r_exact : r_bound, sc.level[i]);
     }
-    level = sc.else_level;
-    return ST_DONE;
+    level = nul ? sc.null_level : c.lvl;
+    return (!nul && (und0 || c.und)) ? ST_UNDECIDED : ST_DONE;
 }
 
 // `=` / `<>` and levenshtein [ratio] tests: the distance lies in [max(length gap, bag distance),
-// max(length)].  The ratio test `lev / den <= t` (or `<`) is decided against t * den with one part
-// in 1e12 of margin instead of a division per pair; exact ties are left to the exact pass.
+// max(length)].  Absolute tests compare integer bounds (lev_a); the ratio test `lev / den <= t`
+// (or `<`) is decided against t * den with one part in 1e12 of margin instead of a division per
+// pair; exact ties are left to the exact pass.
 template <class SC>
 __device__ inline int img_lev(const SC &sc, uint4 a, uint4 b, int &level) {
-    if (a.y == LENS_NULL || b.y == LENS_NULL) {
-        level = sc.null_level;
-        return ST_DONE;
-    }
-    const int eq = img_equal(sc, a.x, a.y, b.x, b.y);
+    const bool nul = a.y == LENS_NULL || b.y == LENS_NULL;
+    const bool same = a.x == b.x && a.y == b.y;
     const int la = lens_u16(a.y), lb = lens_u16(b.y), na = lens_cp(a.y), nb = lens_cp(b.y);
-    if (eq < 0 || la >= LEN_SAT || lb >= LEN_SAT || na >= LEN_SAT || nb >= LEN_SAT) return ST_UNDECIDED;
-    int lo = 0, hi = 0;
-    if (eq == 0) {
-        lo = na > nb ? na - nb : nb - na;
-        if (na == la && nb == lb) {  // BMP: units are code points, so the bag bound holds
-            const int bag = (na > nb ? na : nb) - sketch_inter_ub(img_sketch(a), img_sketch(b), na, nb);
-            if (bag > lo) lo = bag;
-        }
-        hi = na > nb ? na : nb;
-    }
-    const double den = (double)(na + nb) / 2.0;
+    const bool und0 = (same && !sc.has_ids) || la >= LEN_SAT || lb >= LEN_SAT || na >= LEN_SAT || nb >= LEN_SAT;
+    const int gap = na > nb ? na - nb : nb - na, mx = na > nb ? na : nb;
+    // BMP rows: units are code points, so the bag bound holds
+    const bool bmp = na == la && nb == lb && !same;
+    int bag = 0;
+    if (__ballot(bmp) != 0ull) bag = bmp ? mx - sketch_inter_ub_bf(img_sketch(a), img_sketch(b), na, nb) : 0;
+    const int lo = same ? 0 : (bag > gap ? bag : gap), hi = same ? 0 : mx;
+    const double den = (double)(na + nb) * 0.5;
+    Chain c(sc.else_level);
     for (int i = 0; i < sc.n_tests; ++i) {
-        const int op = sc.op[i], cmp = sc.cmp[i];
-        const double t = sc.t[i];
+        const int op = sc.op[i], f = sc.tflag[i];
         int r;
-        if (op == SPK_OP_STR_CMP) {
-            r = ((eq == 1) == (cmp == SPK_CMP_EQ)) ? KT : KF;
+        if (op == SPK_OP_STR_CMP) {  // wave-uniform branches on the test kind
+            r = (int)same ^ ((f & TF_EQ) ? 0 : 1);
         } else if (op == SPK_OP_LEV) {
-            r = decide((double)lo, (double)hi, cmp, t);
-        } else if (den == 0.0) {
-            r = KN;
-        } else if (eq == 1) {
-            r = cmpd(0.0, t, cmp);
+            const int A = sc.lev_a[i];
+            if (f & TF_EXACT) r = lo == hi ? cmpd((double)lo, sc.t[i], sc.cmp[i]) : KU;
+            else if (f & TF_GE) r = lo >= A ? KT : (hi < A ? KF : KU);
+            else r = hi <= A ? KT : (lo > A ? KF : KU);
         } else {
-            const double tl = t * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
+            const double tl = sc.t[i] * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
             const double tl_hi = up > dn ? up : dn, tl_lo = up > dn ? dn : up;
-            if (cmp == SPK_CMP_LE) r = (double)hi <= tl_lo ? KT : ((double)lo > tl_hi ? KF : KU);
-            else r = (double)hi < tl_lo ? KT : ((double)lo >= tl_hi ? KF : KU);  // SPK_CMP_LT
+            const int rr = sc.cmp[i] == SPK_CMP_LE ? ((double)hi <= tl_lo ? KT : ((double)lo > tl_hi ? KF : KU))
+                                                   : ((double)hi < tl_lo ? KT : ((double)lo >= tl_hi ? KF : KU));
+            r = den == 0.0 ? KN : (same ? (f & TF_ZERO) : rr);
         }
-        if (r == KU) return ST_UNDECIDED;
-        if (r == KT) {
-            level = sc.level[i];
-            return ST_DONE;
-        }
+        c.fold(r, sc.level[i]);
     }
-    level = sc.else_level;
-    return ST_DONE;
+    level = nul ? sc.null_level : c.lvl;
+    return (!nul && (und0 || c.und)) ? ST_UNDECIDED : ST_DONE;
 }
 
 __device__ inline double bits_to_double(uint32_t lo, uint32_t hi) {
@@ -780,8 +784,18 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     const Region R = my_region(A);
     ConstSimpleCol *simple = const_simple(A.simple);
     constexpr int64_t SPAN = 64 * FP;
-    for (int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN; base < R.r1;
-         base += (int64_t)(F_THREADS / 64) * SPAN) {  // wave-uniform
+    constexpr int64_t STEP = (int64_t)(F_THREADS / 64) * SPAN;
+    int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN;
+    // the pair rows of the next iteration are loaded while this one's columns are evaluated, so the
+    // image gathers do not wait behind the pair-array load
+    int32_t nx[FP], ny[FP];
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        const int64_t q = base + u * 64 + lane;
+        nx[u] = q < R.r1 ? A.pl[q] : 0;  // inactive lanes read row 0 harmlessly
+        ny[u] = q < R.r1 ? A.pr[q] : 0;
+    }
+    for (; base < R.r1; base += STEP) {  // wave-uniform
         int64_t p[FP];
         bool act[FP];
         int32_t x[FP], y[FP];
@@ -790,9 +804,12 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
         for (int u = 0; u < FP; ++u) {
             p[u] = base + u * 64 + lane;
             act[u] = p[u] < R.r1;
-            x[u] = act[u] ? A.pl[p[u]] : 0;  // inactive lanes read row 0 harmlessly
-            y[u] = act[u] ? A.pr[p[u]] : 0;
+            x[u] = nx[u];
+            y[u] = ny[u];
             acc[u] = 0;
+            const int64_t q = p[u] + STEP;
+            nx[u] = q < R.r1 ? A.pl[q] : 0;
+            ny[u] = q < R.r1 ? A.pr[q] : 0;
         }
         for (int j = 0; j < A.n_simple; ++j) {
             ConstSimpleCol &sc = simple[j];
@@ -1646,6 +1663,55 @@ static std::vector<uint16_t> utf8_to_utf16(const uint8_t *b, int64_t n, int32_t 
     return out;
 }
 
+static bool host_cmp(double a, double b, int cmp) {
+    switch (cmp) {
+        case SPK_CMP_EQ: return a == b;
+        case SPK_CMP_NE: return a != b;
+        case SPK_CMP_LT: return a < b;
+        case SPK_CMP_LE: return a <= b;
+        case SPK_CMP_GT: return a > b;
+        default: return a >= b;
+    }
+}
+
+static int32_t clamp_i32(double v) { return (int32_t)std::max(-1073741824.0, std::min(1073741824.0, v)); }
+
+// The filter's per-test decision parameters (SimpleCol.tflag / lev_a / jw_cf), so the device decides
+// each test with compares and selects only.
+static void prepare_tests(SimpleCol &s) {
+    for (int i = 0; i < s.n_tests; ++i) {
+        const int op = s.op[i], cmp = s.cmp[i];
+        const double t = s.t[i];
+        int32_t f = 0;
+        if (op == SPK_OP_STR_CMP) f |= cmp == SPK_CMP_EQ ? TF_EQ : 0;
+        if (op == SPK_OP_JW || op == SPK_OP_LEVRATIO) {
+            f |= host_cmp(0.0, t, cmp) ? TF_ZERO : 0;
+            f |= host_cmp(1.0, t, cmp) ? TF_ONE : 0;
+        }
+        s.lev_a[i] = 0;
+        s.jw_cf[i] = 0.f;
+        if (op == SPK_OP_LEV) {  // integer v: v cmp t as v >= A or v <= A
+            switch (cmp) {
+                case SPK_CMP_GT: f |= TF_GE; s.lev_a[i] = clamp_i32(std::floor(t) + 1.0); break;
+                case SPK_CMP_GE: f |= TF_GE; s.lev_a[i] = clamp_i32(std::ceil(t)); break;
+                case SPK_CMP_LT: s.lev_a[i] = clamp_i32(std::ceil(t) - 1.0); break;
+                case SPK_CMP_LE: s.lev_a[i] = clamp_i32(std::floor(t)); break;
+                default: f |= TF_EXACT; break;
+            }
+        }
+        if (op == SPK_OP_JW) {
+            // an fp32 upper bound hi (of a double value) proves `v > t` false iff hi <= t, i.e. hi <=
+            // the largest float <= t; `v >= t` false iff hi < t, i.e. hi < the smallest float >= t
+            float fl = (float)t;
+            if ((double)fl > t) fl = std::nextafter(fl, -INFINITY);
+            float fu = (float)t;
+            if ((double)fu < t) fu = std::nextafter(fu, INFINITY);
+            s.jw_cf[i] = cmp == SPK_CMP_GT ? std::nextafter(fl, INFINITY) : fu;
+        }
+        s.tflag[i] = f;
+    }
+}
+
 // Recognise a simple column (see SimpleCol); false leaves it to the interpreter.
 static int32_t simple_class(const SimpleCol &s) {
     if (s.kind == SK_NUM) return SC_NUM;
@@ -1878,6 +1944,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     }
     for (SimpleCol &sc : simple) {
         sc.cls = simple_class(sc);
+        prepare_tests(sc);
         sc.has_ids = (t0.cols[sc.col]->has_ids && t1.cols[sc.col]->has_ids) ? 1 : 0;
     }
     const int64_t img_stride = layout_image(simple);

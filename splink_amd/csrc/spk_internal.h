@@ -143,8 +143,22 @@ struct Column {
     bool has_ids = false;  // COL_STR: RecMeta.key is a dictionary id
 };
 
+// An input column as handed over (Arrow buffers), kept on the device in input row order: the source
+// of blocking keys, dictionary ids and (through a table's row permutation) comparison columns.
+enum RawKind : int32_t { RAW_UTF8 = 1, RAW_I64 = 2 };
+struct RawCol {
+    RawKind kind = RAW_UTF8;
+    int64_t n = 0;
+    int64_t max_len = 0;     // longest value in bytes (UTF-8)
+    DevBuf<int64_t> off;     // RAW_UTF8: n + 1 byte offsets
+    DevBuf<uint8_t> bytes;   // RAW_UTF8
+    DevBuf<int64_t> i64;     // RAW_I64: values (compared as 8-byte patterns)
+    DevBuf<uint8_t> valid;   // 1 = non-NULL
+};
+
 struct Table {
     int64_t n = -1;
+    DevBuf<int32_t> perm;    // row i of the table is input row perm[i] (spk_cluster); empty = identity
     std::vector<Column *> cols;
     DevBuf<ColDesc> d_desc;
     bool desc_dirty = true;
@@ -235,6 +249,10 @@ struct spk_ctx {
         return SPK_OK;
     }
     spk::DevBuf<double> mp;  // per-pair scores (final E-step)
+    std::vector<spk::RawCol *> raw;  // device copies of the input columns (spk_raw_*)
+    ~spk_ctx() {
+        for (spk::RawCol *r : raw) delete r;
+    }
     bool mpat_valid = false;
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
 
@@ -250,4 +268,7 @@ struct spk_ctx {
 
 namespace spk {
 int ensure_desc(spk_ctx *ctx, Table &t);
+int new_column(spk_ctx *ctx, int side, int col, Column **out);
+int launch_utf8_decode(spk_ctx *ctx, int64_t n, const int64_t *off8, const int64_t *src_off, const int32_t *perm,
+                       const uint8_t *bytes, const uint8_t *valid, Column *c, bool long_rows, const int64_t *ids);
 }

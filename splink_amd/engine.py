@@ -82,31 +82,42 @@ def columns_to_retain_blocking(settings) -> List[str]:
 
 
 class Job:
-    """Record tables + pairs + codes living on one GPU."""
+    """Record tables + pairs + codes living on one GPU.
+
+    `inputs` are the tables as given (input row order).  Their columns go to the device once as
+    Arrow buffers (spk_raw_*); blocking keys, dictionary ids, unique-id ranks and the clustering of
+    the rows by the first rule's key are computed there (spk_key_build, spk_rank_from_raw,
+    spk_cluster).  Device row i of side s is input row perm[s][i]; `tables` are the inputs in that
+    order (materialised on demand, for output columns and checks)."""
 
     def __init__(self, link_type: str, tables: List[pd.DataFrame], unique_id_col: str, device: int,
                  shard=(0, 1), cluster: bool = True):
         self.link_type = link_type
         self.cluster = cluster
-        self.tables = [t.reset_index(drop=True) for t in tables]
+        self.inputs = [t.reset_index(drop=True) for t in tables]
+        self.perm = [None] * len(self.inputs)
+        self._views = {}
+        self._host_cols = {}
         self.uid = unique_id_col
         self.device = device
         self.shard, self.n_shards = shard
         self.ctx = N.Context(device)
         self.ctx.set_link_type(N.LINK_TYPES[link_type])
         forms = {}
-        for t in reversed(self.tables):
+        for t in reversed(self.inputs):
             for c in t.columns:
                 forms[c] = T.natural_form(t[c])
         self.schema = Schema(forms)
         self._col_index = {}
-        for side, t in enumerate(self.tables):
+        self._raw = {}
+        for side, t in enumerate(self.inputs):
             self.ctx.table_create(side, len(t), 8)
         self.n_pairs = 0
         self.n_candidates = 0
         self._pairs_host = None
         self.codes_token = None
         self.code_meta = None
+        self.timings = {}
         self._set_rank()
 
     @classmethod
@@ -118,35 +129,84 @@ class Job:
         return job
 
     # ---- tables --------------------------------------------------------------------------------
+    @property
+    def tables(self) -> List[pd.DataFrame]:
+        """The input tables in device row order (pair rows index these)."""
+        return [self.table_view(s) for s in range(len(self.inputs))]
+
+    def table_view(self, side: int) -> pd.DataFrame:
+        if self.perm[side] is None:
+            return self.inputs[side]
+        if side not in self._views:
+            self._views[side] = self.inputs[side].take(self.perm[side]).reset_index(drop=True)
+        return self._views[side]
+
+    def r_side(self) -> int:
+        return 1 if self.link_type == "link_only" else 0
+
     def r_table(self) -> pd.DataFrame:
-        return self.tables[1] if self.link_type == "link_only" else self.tables[0]
+        return self.table_view(self.r_side())
+
+    def host_values(self, side: int, name: str) -> np.ndarray:
+        """Column `name` of side `side` as a numpy array in device row order."""
+        key = (side, name)
+        if key not in self._host_cols:
+            col = self.inputs[side][name]
+            if isinstance(col.dtype, pd.api.extensions.ExtensionDtype):  # Arrow / nullable: NULL as None
+                v = col.to_numpy(dtype=object, na_value=None)
+            else:
+                v = col.to_numpy()
+            self._host_cols[key] = v if self.perm[side] is None else v[self.perm[side]]
+        return self._host_cols[key]
+
+    def _new_raw(self) -> int:
+        return len(self._raw)
+
+    def raw_utf8(self, side: int, name: str) -> int:
+        """Raw string column (input row order) on the device, uploaded once."""
+        key = (side, name, "utf8")
+        if key not in self._raw:
+            off, data, valid = T.arrow_utf8(self.inputs[side][name])
+            rid = self._new_raw()
+            self.ctx.raw_utf8(rid, off, data, valid)
+            self._raw[key] = rid
+        return self._raw[key]
+
+    def raw_i64(self, key, values, valid) -> int:
+        if key not in self._raw:
+            rid = self._new_raw()
+            self.ctx.raw_i64(rid, values, valid)
+            self._raw[key] = rid
+        return self._raw[key]
 
     def _set_rank(self):
         """Order rank of every row for the link-type predicate (blocking.py:136, :139).  A NULL
         unique id never satisfies `l.uid < r.uid`; its rows get the last rank of their source and
-        the kernel drops their same-source pairs (spk_table_set_rank_null)."""
-        self._rank = None
+        the kernel drops their same-source pairs (spk_table_set_rank_null).  Integer ids are ranked
+        on the device (spk_rank_from_raw); others in Spark's order on the host."""
         if self.link_type == "link_only":
             return
-        t = self.tables[0]
+        t = self.inputs[0]
         if self.uid not in t.columns:
             raise ValueError(f"unique_id_column_name {self.uid!r} is not a column of the input data")
         col = t[self.uid]
-        if (pd.api.types.is_integer_dtype(col.dtype) and not pd.api.types.is_bool_dtype(col.dtype)
-                and not col.isna().any()):
-            uid_rank, nulls = T.dense_rank_array(col.to_numpy(dtype=np.int64))
-        else:
-            uid_rank, nulls = T.dense_rank(col.tolist())
+        right_from = -1
+        if self.link_type == "link_and_dedupe":
+            src = (t["_source_table"].to_numpy() == "right")
+            right_from = int(np.argmax(src)) if src.any() else len(t)
+            assert src[right_from:].all(), "link_and_dedupe: the right table's rows follow the left table's"
+        if pd.api.types.is_integer_dtype(col.dtype) and not pd.api.types.is_bool_dtype(col.dtype):
+            vals, valid = T.numeric_key_bits(col)
+            self.ctx.rank_from_raw(self.raw_i64(("uid",), vals, valid), right_from)
+            return
+        uid_rank, nulls = T.dense_rank(col.tolist())
         n_distinct = int(uid_rank[~nulls].max()) + 1 if (~nulls).any() else 0
         div = n_distinct + 1  # r in [0, n_distinct) for ids, n_distinct for NULL
         r = np.where(nulls, n_distinct, uid_rank)
+        rank = r
         if self.link_type == "link_and_dedupe":
-            src = (t["_source_table"].to_numpy() == "right").astype(np.int64)
-            rank = src * div + r
-        else:
-            rank = r
-        self._rank = np.asarray(rank, dtype=np.int64)
-        self.ctx.table_set_rank(0, self._rank)
+            rank = (np.arange(len(t)) >= right_from).astype(np.int64) * div + r
+        self.ctx.table_set_rank(0, np.asarray(rank, dtype=np.int64))
         self.ctx.table_set_rank_null(0, div if nulls.any() else 0)
 
     def column_index(self, name: str, form: str) -> int:
@@ -156,19 +216,18 @@ class Job:
         idx = len(self._col_index)
         sides = [0, 1] if self.link_type == "link_only" else [0]
         for side in sides:
-            if name not in self.tables[side].columns:
+            if name not in self.inputs[side].columns:
                 raise ValueError(f"column {name!r} is missing from input table {side}")
-        ids = None
         if form == "str":
-            # dictionary ids in one id space for both sides: string equality becomes one integer compare
-            ids, _ = T.factorize_joint([pd.Series(T.to_strings(self.tables[s][name]), dtype=object) for s in sides])
-        for i, side in enumerate(sides):
-            t = self.tables[side]
-            if form == "str":
-                off, data, valid = T.encode_utf8(t[name])
-                self.ctx.table_add_utf8(side, idx, off, data, valid, ids[i])
-            else:
-                vals, valid = T.encode_float64(t[name])
+            # decoded on the device through the row permutation; dictionary ids computed there, in one
+            # id space for both sides (string equality = one integer compare)
+            raws = [self.raw_utf8(side, name) for side in sides]
+            self.ctx.table_add_raw_utf8(idx, raws[0], raws[1] if len(raws) > 1 else -1)
+        else:
+            for side in sides:
+                vals, valid = T.encode_float64(self.inputs[side][name])
+                if self.perm[side] is not None:
+                    vals, valid = vals[self.perm[side]], valid[self.perm[side]]
                 self.ctx.table_add_float64(side, idx, vals, valid)
         self._col_index[key] = idx
         return idx
@@ -196,56 +255,68 @@ class Job:
             out.append(x)
         return pd.Series(out, dtype=object)
 
-    def _cluster(self, rule_keys):
-        """Reorder the record tables by the first rule's blocking key (then rank), so a block's
-        rows are contiguous on the device: the comparison pass reads a block's records from a few
-        cache lines instead of one random line per row.  Pair rows then index the reordered tables;
-        the pair set and its ordinal order do not change (blocking sorts by key and rank anyway)."""
-        key_l, key_r = rule_keys[0]
-        sides = [(0, key_l)] + ([(1, key_r)] if self.link_type == "link_only" else [])
-        perms = {}
-        for side, key in sides:
-            n = len(self.tables[side])
-            nulls_last = np.where(key < 0, np.iinfo(np.int64).max, key)
-            rank = self._rank if (side == 0 and self._rank is not None) else np.arange(n, dtype=np.int64)
-            perms[side] = np.lexsort((np.arange(n), rank, nulls_last))
-        for side, perm in perms.items():
-            self.tables[side] = self.tables[side].take(perm).reset_index(drop=True)
-            self.ctx.table_create(side, len(self.tables[side]), 8)
-        self._col_index = {}
-        self._prog_cache = {}  # column uploads (and their indices) start again
-        self._set_rank()
-        p0 = perms[0]
-        pr = perms.get(1, p0)
-        return [(kl[p0], kr[pr]) for kl, kr in rule_keys]
+    @staticmethod
+    def _substr_of(kexpr):
+        """(start, len) of a key expression that is a column or one substr of it; None otherwise."""
+        if not kexpr.transforms:
+            return (0, -1)
+        if len(kexpr.transforms) == 1 and kexpr.transforms[0][0] == "substr" and kexpr.transforms[0][2] >= 0:
+            return (int(kexpr.transforms[0][1]), int(min(kexpr.transforms[0][2], 2 ** 31 - 1)))
+        return None
+
+    def _term(self, r, i, lexpr, rexpr, symmetric):
+        """spk_key_term of one `l.a = r.b` term.  String columns (optionally under one substr) and plain
+        numeric columns are keyed on the device from their raw buffers; other expressions (lower /
+        upper / trim, mixed types) get their key ids on the host, uploaded as an int64 raw column."""
+        s0, s1 = 0, self.r_side()
+        fl, fr = self.schema.form(lexpr.column), self.schema.form(rexpr.column)
+        sl, sr = self._substr_of(lexpr), self._substr_of(rexpr)
+        same_raw = symmetric and self.link_type != "link_only"
+        if fl == fr == "str" and sl is not None and sr is not None:
+            raw_l = self.raw_utf8(s0, lexpr.column)
+            raw_r = -1 if same_raw else self.raw_utf8(s1, rexpr.column)
+            return (raw_l, raw_r, sl[0], sl[1], sr[0], sr[1])
+        cl, cr = self.inputs[s0][lexpr.column], self.inputs[s1][rexpr.column]
+        if fl == fr == "num" and not lexpr.transforms and not rexpr.transforms:
+            ints = all(pd.api.types.is_integer_dtype(c.dtype) and not pd.api.types.is_bool_dtype(c.dtype)
+                       for c in (cl, cr))
+            conv = (lambda c: T.numeric_key_bits(c)) if ints else \
+                (lambda c: T.numeric_key_bits(pd.to_numeric(c, errors="coerce").astype(np.float64)))
+            raw_l = self.raw_i64((s0, lexpr.column, "num", ints), *conv(cl))
+            raw_r = -1 if same_raw else self.raw_i64((s1, rexpr.column, "num", ints), *conv(cr))
+            return (raw_l, raw_r, 0, -1, 0, -1)
+        kl = self._key_values(self.inputs[s0], lexpr)
+        kr = kl if same_raw else self._key_values(self.inputs[s1], rexpr)
+        codes, _ = T.factorize_joint([kl, kr])
+        raw_l = self.raw_i64(("key", r, i, "l"), codes[0], codes[0] >= 0)
+        raw_r = -1 if same_raw else self.raw_i64(("key", r, i, "r"), codes[1], codes[1] >= 0)
+        return (raw_l, raw_r, 0, -1, 0, -1)
 
     def block(self, rules: List[str]):
-        t0, tr = self.tables[0], self.r_table()
+        import time
+        t_start = time.perf_counter()
+        n0, nr = len(self.inputs[0]), len(self.inputs[self.r_side()])
         symmetric = []
         if not rules:
-            self.ctx.table_set_key(0, 0, 0, np.zeros(len(t0), dtype=np.int64))
-            side_r = 1 if self.link_type == "link_only" else 0
-            self.ctx.table_set_key(side_r, 0, 1, np.zeros(len(tr), dtype=np.int64))
+            self.ctx.table_set_key(0, 0, 0, np.zeros(n0, dtype=np.int64))
+            self.ctx.table_set_key(self.r_side(), 0, 1, np.zeros(nr, dtype=np.int64))
             symmetric = [1]
-        rule_keys = []
-        for text in rules:
+        for r, text in enumerate(rules):
             spec = compile_rule(text, self.schema)
-            per_term = []
-            for lexpr, rexpr in spec.terms:
-                kl = self._key_values(t0, lexpr)
-                # dedupe with a symmetric term (l.x = r.x): both sides read the same table and key
-                kr = kl if (tr is t0 and lexpr == rexpr) else self._key_values(tr, rexpr)
-                codes, _ = T.factorize_joint([kl, kr])
-                per_term.append(codes)
-            rule_keys.append(T.combine_codes(per_term))
+            terms = [self._term(r, i, lexpr, rexpr, lexpr == rexpr) for i, (lexpr, rexpr) in enumerate(spec.terms)]
+            self.ctx.key_build(r, terms)
             symmetric.append(1 if spec.symmetric else 0)
-        if rule_keys and self.cluster:
-            rule_keys = self._cluster(rule_keys)
-        for r, (key_l, key_r) in enumerate(rule_keys):
-            self.ctx.table_set_key(0, r, 0, key_l)
-            self.ctx.table_set_key(1 if self.link_type == "link_only" else 0, r, 1, key_r)
+        if rules and self.cluster:
+            # rows of a block become contiguous: the comparison pass reads a block's records from a few
+            # cache lines.  The pair set and its ordinal order do not change (blocking sorts by key, rank).
+            p0, p1 = self.ctx.cluster(n0, len(self.inputs[1]) if self.link_type == "link_only" else None)
+            self.perm = [p0] + ([p1] if p1 is not None else [])
+            self._views, self._host_cols, self._col_index, self._prog_cache = {}, {}, {}, {}
+        t_keys = time.perf_counter()
         self.n_pairs, self.n_candidates = self.ctx.block(N.LINK_TYPES[self.link_type], symmetric, self.shard,
                                                          self.n_shards)
+        self.timings["block_keys_s"] = t_keys - t_start
+        self.timings["block_pairs_s"] = time.perf_counter() - t_keys
         self._pairs_host = None
         self.codes_token = None
         return self.n_pairs

@@ -132,10 +132,10 @@ class _HostColumns:
         else:
             base, side = name[:-2], name[-2:]
             rows_l, rows_r = job.pair_rows()
-            t = job.tables[0] if side == "_l" else job.r_table()
-            if base not in t.columns:
+            s = 0 if side == "_l" else job.r_side()
+            if base not in job.inputs[s].columns:
                 raise KeyError(name)
-            v = t[base].to_numpy()[rows_l if side == "_l" else rows_r]
+            v = job.host_values(s, base)[rows_l if side == "_l" else rows_r]
         self._cache[name] = v
         return v
 

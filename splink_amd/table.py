@@ -102,6 +102,35 @@ def encode_utf8(series: pd.Series):
     return offsets, data, valid
 
 
+def arrow_utf8(series: pd.Series):
+    """(offsets int64[n+1], bytes uint8[], valid uint8[n]) of a string column.  Arrow-backed columns
+    (pd.ArrowDtype string / large_string, pandas' pyarrow strings) hand over their buffers without a
+    per-row pass; object columns of str / None go through pyarrow's converter; anything else is
+    rendered with Spark's cast-to-string rules (encode_utf8)."""
+    n = len(series)
+    if pa is not None:
+        arr = getattr(series.array, "_pa_array", None)
+        if arr is not None and (pa.types.is_large_string(arr.type) or pa.types.is_string(arr.type)):
+            arr = arr.combine_chunks() if isinstance(arr, pa.ChunkedArray) else arr
+            if pa.types.is_string(arr.type):
+                arr = arr.cast(pa.large_string())
+            return _arrow_buffers(arr, n)
+    return encode_utf8(series)
+
+
+def numeric_key_bits(series: pd.Series):
+    """(int64 values, valid) whose bit patterns are equal iff the numbers are: int64 columns as they
+    are, float columns as canonical float64 bits (-0.0 -> 0.0); NaN is NULL."""
+    if pd.api.types.is_integer_dtype(series.dtype) and not pd.api.types.is_bool_dtype(series.dtype):
+        valid = (~series.isna()).to_numpy()
+        vals = series.to_numpy(dtype=np.int64, na_value=0) if hasattr(series, "to_numpy") else series.values
+        return np.asarray(vals, dtype=np.int64), valid.astype(np.uint8)
+    f = pd.to_numeric(series, errors="coerce").astype(np.float64).to_numpy()
+    valid = ~np.isnan(f)
+    f = np.where(valid, f, 0.0) + 0.0  # -0.0 + 0.0 == +0.0
+    return f.view(np.int64).copy(), valid.astype(np.uint8)
+
+
 def _arrow_buffers(arr, n):
     arr = arr.combine_chunks() if hasattr(arr, "combine_chunks") else arr
     valid = np.asarray(arr.is_valid()).astype(np.uint8) if arr.null_count else np.ones(n, dtype=np.uint8)

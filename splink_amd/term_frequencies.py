@@ -73,9 +73,9 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
     one_minus = float(1 - params.params["λ"])
     ids0_list, ids1_list, tables = [], [], []
     for c in tf_cols:
-        t0, tr = job.tables[0], job.r_table()
-        vals = [pd.Series([None if T.is_null_scalar(v) else v for v in t[c].tolist()], dtype=object)
-                for t in ((t0, tr) if job.link_type == "link_only" else (t0,))]
+        sides = (0, 1) if job.link_type == "link_only" else (0,)
+        vals = [pd.Series([None if T.is_null_scalar(v) else v for v in job.host_values(s, c).tolist()], dtype=object)
+                for s in sides]
         codes, n_values = T.factorize_joint(vals)
         ids0 = codes[0]
         ids1 = codes[1] if len(codes) > 1 else codes[0]
