@@ -31,7 +31,7 @@ warnings.filterwarnings("ignore")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 # HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same command
 # (scripts_gpu_round.sh -> tools/traffic.py); the counters cannot be read inside a timed run.
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r1_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2_traffic.json")
 COLS = ["first_name", "surname", "dob", "city", "email"]
 WORKLOADS = {2: "cfg2: synthetic person-record dedupe, 1M x sqrt(N) records, blocking surname|dob, "
                 "5 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3)",
@@ -79,7 +79,9 @@ def main():
     n_records = int(round(args.records * math.sqrt(world)))
     t0 = time.time()
     cols = COLS + (["address"] if args.config == 5 else [])
-    df = make_records(n_records, surname_vocab=15000, with_address=args.config == 5)[["unique_id"] + cols]
+    # Arrow-backed string columns: the columnar form a Spark / Arrow source hands over (values identical
+    # to the object-column records; spk_raw_utf8 takes their buffers without a per-row pass)
+    df = make_records(n_records, surname_vocab=15000, with_address=args.config == 5, arrow=True)[["unique_id"] + cols]
     log(f"[rank {rank}] generated {n_records} records in {time.time() - t0:.1f}s")
 
     settings = cfg_settings(args.config, max_iterations=10)
@@ -94,7 +96,9 @@ def main():
     block_kernel_ms = job.ctx.kernel_ms()["block"]
     log(f"[rank {rank}] blocking: {job.n_pairs} local pairs of {job.n_candidates} candidates "
         f"({block_s:.2f}s wall incl. host key prep, {block_kernel_ms:.1f} ms device)")
-    job.gammas(st)  # uploads columns, first launch
+    t0 = time.time()
+    job.gammas(st)  # uploads columns (device decode through the clustering permutation), first launch
+    first_gammas_s = time.time() - t0
     names, nlev = job.code_meta
 
     host = {"gammas_call": [], "em_call": [], "m_step_host": []}
@@ -152,23 +156,41 @@ def main():
         return
 
     # ---- roofline of the dominant kernel (comparison-vector pass) -------------------------
+    # SURVEY §8(d) algorithmic bytes: 8 + K bytes per pair (read the int32 pair, write the γ vector)
+    # plus every record's field bytes once (UTF-8).  The pass writes a packed 2-byte code instead of
+    # K bytes of γ; both figures are reported.
+    from splink_amd.table import arrow_utf8
+    K = len(cols)
     code_bytes = 2 if job.ctx.n_patterns() <= 65536 else 4
     g_ms = float(np.mean(gamma_ms))
     h_ms = float(np.mean(hist_ms))
-    rec_bytes = 0
-    for c in cols:
-        s = df[c].dropna()
-        rec_bytes += int(s.str.len().sum()) * 2 + 8 * 3 * len(df)  # UTF-16 units + offset/len/hash per row
-    gamma_bytes = local_pairs * (8 + code_bytes) + rec_bytes
-    em_bytes = local_pairs * code_bytes
+    f_ms = float(np.mean(fin_ms))
+    rec_bytes = int(sum(arrow_utf8(df[c])[0][-1] for c in cols))
+    gamma_bytes = local_pairs * (8 + K) + rec_bytes
+    gamma_bytes_packed = local_pairs * (8 + code_bytes) + rec_bytes
     roofline = {"bound": "hbm", "kernel": "spk_gammas pass (k_gamma_simple + k_gamma_exact per undecided column)",
                 "achieved": gamma_bytes / (g_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gamma_bytes / (g_ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                "algorithmic_bytes_per_launch": gamma_bytes, "avg_launch_ms": g_ms,
+                "algorithmic_bytes_per_launch": gamma_bytes,
+                "algorithmic_bytes_note": f"SURVEY 8(d): pairs x (8 + K={K}) + UTF-8 field bytes {rec_bytes}",
+                "bytes_per_launch_packed_codes": gamma_bytes_packed, "avg_launch_ms": g_ms,
                 "note": "comparison pass is VALU / gather-latency bound (string work), not HBM-bound; its HBM fraction is shown per the contract"}
-    em_roofline = {"bound": "hbm", "kernel": "k_hist", "achieved": em_bytes / (h_ms / 1e3) / 1e9,
-                   "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": em_bytes / (h_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
-                   "algorithmic_bytes_per_launch": em_bytes, "avg_launch_ms": h_ms}
+    # E/M: the contract counts K bytes of γ per pair per iteration; the kernel streams the packed
+    # 2-byte code (an exact re-encoding of the same γ vector), so both are reported.
+    em_bytes = local_pairs * code_bytes
+    em_bytes_contract = local_pairs * K
+    em_roofline = {"bound": "hbm", "kernel": "k_hist", "avg_launch_ms": h_ms, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "algorithmic_bytes_per_launch": em_bytes, "bytes_per_pair": code_bytes,
+                   "achieved": em_bytes / (h_ms / 1e3) / 1e9, "frac": em_bytes / (h_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                   "contract_bytes_per_pair": K, "achieved_contract": em_bytes_contract / (h_ms / 1e3) / 1e9,
+                   "frac_contract": em_bytes_contract / (h_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                   "note": "frac: the packed code the kernel streams; frac_contract: SURVEY 8(d)'s K bytes/pair "
+                           "(> 1 is possible because the code packs the K levels into 2 bytes)"}
+    # SURVEY 8(d) headline: %HBM = (P x K x iterations + P x (K + 8)) / t_EM / 8e12, t_EM = 10 E+M
+    # iterations (histogram + finalize, device time) + the final scoring pass
+    t_em = 10 * (h_ms + f_ms) / 1e3 + score_ms / 1e3
+    headline = {"formula": "(P*K*iters + P*(K+8)) / t_EM / 8e12, iters=10, t_EM = 10*(k_hist+finalize) + k_score",
+                "value": (local_pairs * K * 10 + local_pairs * (K + 8)) / t_em / 8e12, "t_em_ms": t_em * 1e3}
 
     traffic = None
     if os.path.exists(TRAFFIC_FILE):
@@ -207,9 +229,13 @@ def main():
                    "parallelism": f"pair-ordinal shards x{world}, RCCL all-reduce of pattern histogram"},
         "roofline": roofline,
         "roofline_em": em_roofline,
-        "breakdown_ms": {"gamma": g_ms, "em_hist": h_ms, "em_final": float(np.mean(fin_ms)), "score": score_ms,
-                         "block_device": block_kernel_ms, "block_wall_incl_host_prep": block_s * 1e3,
+        "hbm_headline_contract": headline,
+        "breakdown_ms": {"gamma": g_ms, "em_hist": h_ms, "em_final": f_ms, "score": score_ms,
+                         "block_device": block_kernel_ms, "block_wall": block_s * 1e3,
+                         "block_keys_wall": job.timings.get("block_keys_s", 0.0) * 1e3,
+                         "first_gammas_call_incl_column_decode": first_gammas_s * 1e3,
                          **{f"host_wall_{k}": float(np.mean(v)) for k, v in host.items()}},
+        "input": "Arrow-backed string columns (pd.ArrowDtype(large_string)); keys, ids, ranks, clustering on the device",
         "deferred_pairs": job.ctx.gammas_deferred(),
         "exact_cells_per_column": dict(zip(names, job.ctx.gammas_exact_counts(len(names)))),
         "cpu_baseline": cpu,

@@ -81,8 +81,12 @@ def _sprinkle(rng: np.random.Generator, s: str, alphabet) -> str:
 
 
 def make_records(n: int, seed: int = SEED, surname_vocab: int = 15000, surname_s: float = 0.3,
-                 first_vocab: int = 5000, city_vocab: int = 2000, with_address: bool = False) -> pd.DataFrame:
-    """Return `n` synthetic person records as a pandas DataFrame (deterministic in `seed`)."""
+                 first_vocab: int = 5000, city_vocab: int = 2000, with_address: bool = False,
+                 arrow: bool = False) -> pd.DataFrame:
+    """Return `n` synthetic person records as a pandas DataFrame (deterministic in `seed`).
+
+    arrow=True gives Arrow-backed string columns (pd.ArrowDtype(large_string)), the columnar form a
+    Spark / Arrow source hands over; the values are identical."""
     rng = np.random.Generator(np.random.PCG64(seed))
     firsts = _vocab(rng, first_vocab, 3, 12)
     surnames = _vocab(rng, surname_vocab, 3, 14)
@@ -168,6 +172,11 @@ def make_records(n: int, seed: int = SEED, surname_vocab: int = 15000, surname_s
     for name, arr in cols.items():
         df[name] = arr[perm]
     df["cluster"] = cluster[perm]
+    if arrow:
+        import pyarrow as pa
+        for name in cols:
+            df[name] = pd.Series(pa.array(df[name].tolist(), type=pa.large_string()),
+                                 dtype=pd.ArrowDtype(pa.large_string()))
     return df
 
 

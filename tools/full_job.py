@@ -1,0 +1,148 @@
+"""One complete linkage job on one GPU, timed end to end, with parity checks (a separately labelled row,
+never bench.py's headline).
+
+    python tools/full_job.py --records 20000000 --shard 0/8 [--iters 10] [--sample 2000000] [--out FILE]
+
+The job is BASELINE configs[3]'s per-GPU share: a 20M-record synthetic dedupe (blocking surname | dob,
+the five cfg2 comparison columns) whose candidate-pair ordinals are split over 8 GPUs; this process is
+rank `shard` and generates only its slice of the ordinal space (spk_block shard / n_shards), exactly as
+each rank of an 8-GPU run does.  Without a process group the EM statistics are this shard's (the RCCL
+all-reduce of the 8-rank job is a 4.6 KB histogram per iteration).
+
+Timed stages (wall clock, inputs in host memory as Arrow-backed columns, generation excluded):
+blocking (raw column upload + device keys + clustering + pair generation), the comparison-vector
+pass (first call: column upload + device decode), 10 EM iterations (histogram + finalize + the host
+M-step), the final scoring pass.  Parity: every comparison vector of a strided sample of pairs against
+oracle.template_gammas, and the 10 EM iterations of λ / m / u plus the final match probabilities of
+all of this shard's pairs against oracle.em_iterate (1e-9).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+COLS = ["first_name", "surname", "dob", "city", "email"]
+SPECS = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=20_000_000)
+    ap.add_argument("--surname-vocab", type=int, default=300_000)
+    ap.add_argument("--shard", default="0/8")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--sample", type=int, default=2_000_000, help="pairs in the strided gamma parity sample")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    shard, n_shards = (int(x) for x in a.shard.split("/"))
+
+    import torch
+    torch.cuda.set_device(0)
+    from splink_amd.engine import Job, m_step_rows
+    from splink_amd.params import Params
+    from splink_amd.session import AmdSession
+    from splink_amd.synthetic import cfg_settings, make_records
+
+    t0 = time.time()
+    df = make_records(a.records, surname_vocab=a.surname_vocab, arrow=True)[["unique_id"] + COLS]
+    gen_s = time.time() - t0
+    log(f"generated {a.records} records in {gen_s:.1f}s")
+    params = Params(cfg_settings(4, max_iterations=a.iters), AmdSession(0))
+    st = params.settings
+
+    wall = {}
+    t_job = time.perf_counter()
+    t = time.perf_counter()
+    job = Job("dedupe_only", [df], "unique_id", 0, shard=(shard, n_shards))
+    job.ctx.enable_timing(True)
+    wall["job_setup_incl_uid_rank"] = time.perf_counter() - t
+    t = time.perf_counter()
+    job.block(st["blocking_rules"])
+    wall["block"] = time.perf_counter() - t
+    wall["block_keys_and_cluster"] = job.timings["block_keys_s"]
+    block_dev = job.ctx.kernel_ms()["block"]
+    log(f"shard {shard}/{n_shards}: {job.n_pairs} pairs of {job.n_candidates} candidates, block {wall['block']:.2f}s")
+    t = time.perf_counter()
+    job.gammas(st)
+    wall["gammas_first_call_incl_column_decode"] = time.perf_counter() - t
+    gamma_dev = job.ctx.kernel_ms()["gamma"]
+    names, nlev = job.code_meta
+    lam0, lp0 = params.params["λ"], params._level_probabilities()
+    t = time.perf_counter()
+    em_dev = []
+    for _ in range(a.iters):
+        stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        ms = job.ctx.kernel_ms()
+        em_dev.append(ms["em_hist"] + ms["em_final"])
+        lam, rows = m_step_rows(stats, names, nlev)
+        params._update_params(lam, rows)
+    wall["em_iterations"] = time.perf_counter() - t
+    t = time.perf_counter()
+    mp = job.score(params.params["λ"], params._level_probabilities(), want_host=False)
+    torch.cuda.synchronize()
+    wall["score"] = time.perf_counter() - t
+    score_dev = job.ctx.kernel_ms()["score"]
+    total = time.perf_counter() - t_job
+    P = job.n_pairs
+    row = {
+        "row": "full job, one GPU (separately labelled; never the headline)",
+        "workload": f"cfg4 per-GPU share: {a.records} records, blocking surname|dob, 5 columns, "
+                    f"pair-ordinal shard {shard}/{n_shards}",
+        "records": a.records, "candidates_total": int(job.n_candidates), "pairs_this_gpu": int(P),
+        "iterations": a.iters, "wall_s": wall, "job_wall_s": total,
+        "device_ms": {"block": block_dev, "gamma_pass": gamma_dev, "em_per_iter_mean": float(np.mean(em_dev)),
+                      "score": score_dev},
+        "pairs_per_s_job": P / total,
+        "pairs_per_s_gamma_plus_em_iter": P / ((gamma_dev + float(np.mean(em_dev))) / 1e3),
+        "generation_s_excluded": gen_s,
+        "lambda_final": params.params["λ"],
+    }
+    if not a.no_parity:
+        import oracle as orc
+        t = time.perf_counter()
+        l, r = job.pair_rows()
+        step = max(1, P // a.sample)
+        idx = np.arange(0, P, step)
+        sl, sr = l[idx], r[idx]
+        rows_used, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
+        table = job.tables[0]
+        sub = table.take(rows_used)
+        ocols = [orc.StrCol(sub[c].tolist()) for c in COLS]
+        ref = orc.template_gammas(SPECS, ocols, ocols, inv[:len(sl)].astype(np.int32), inv[len(sl):].astype(np.int32))
+        gam = job.gammas_host()
+        bad = int((gam[idx] != ref).any(axis=1).sum())
+        row["parity_gamma"] = {"sampled_pairs": int(len(idx)), "stride": int(step), "mismatches": bad}
+        hist_o, mp_o = orc.em_iterate(gam, nlev, lam0, [m for m, _ in lp0], [u for _, u in lp0], a.iters, 1e-300)
+        lam_o, m_o, u_o = hist_o[-1]
+        rel = lambda x, y: abs(x - y) <= 1e-9 * max(abs(x), abs(y), 1e-300)  # noqa: E731
+        ok = rel(params.params["λ"], lam_o) and all(
+            rel(x, y) for k, (m, u) in enumerate(params._level_probabilities())
+            for x, y in zip(list(m) + list(u), list(m_o[k]) + list(u_o[k])))
+        mp_dev = job.score(params.params["λ"], params._level_probabilities())
+        mp_ok = bool(np.allclose(mp_dev, mp_o, rtol=1e-9, atol=0, equal_nan=True))
+        row["parity_em"] = {"iterations": len(hist_o), "lambda_m_u_1e-9": bool(ok), "match_probability_1e-9": mp_ok,
+                            "pairs": int(P)}
+        row["parity_check_s"] = time.perf_counter() - t
+    out = json.dumps(row)
+    print(out, flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(out + "\n")
+
+
+if __name__ == "__main__":
+    main()
