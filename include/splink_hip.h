@@ -202,7 +202,9 @@ int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
  * on the same two plain operands) are filtered from a packed per-row image of their fields; every
  * other column by the general interpreter.  on = 1 (default): template columns through the
  * column-batched filter; on = 2: through the register-resident row filter when the image row is
- * short (<= 128 bytes); on = 0: every column through the interpreter.  All
+ * short (<= 128 bytes); on = 0: every column through the interpreter; on + 10: the same, with
+ * the pairs of later blocking rules reading the table-ordered row image instead of their rule's
+ * view-ordered copy.  All
  * modes give identical results (for testing and measurement).  spk_gammas_simple_count: how many
  * columns the last spk_gammas took as template columns. */
 int spk_gammas_set_simple(spk_ctx *ctx, int on);

@@ -100,6 +100,7 @@ struct EnumArgs {
     int64_t *chunk_count;       // count pass output
     const int64_t *chunk_off;   // emit pass input
     int32_t *out_l, *out_r;
+    int32_t *out_vl, *out_vr;   // emit pass: view positions (rules with a view), or null
 };
 
 __device__ inline int64_t tri_s(int64_t a, int64_t n) { return a * (2 * n - a - 1) / 2; }
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_enum(EnumArgs A) {
     __shared__ int64_t s_scan[EN_THREADS];
     const int64_t chunk = blockIdx.x;
     const int64_t base = A.q0 + chunk * EN_CHUNK + (int64_t)threadIdx.x * EN_PER_THREAD;
-    int32_t xs[EN_PER_THREAD], ys[EN_PER_THREAD];
+    int32_t xs[EN_PER_THREAD], ys[EN_PER_THREAD], vx[EN_PER_THREAD], vy[EN_PER_THREAD];
     unsigned keep = 0;
     if (base < A.q1) {
         // block containing `base`: last b with cand_off[b] <= base
@@ -163,8 +164,11 @@ __global__ __launch_bounds__(EN_THREADS) void k_enum(EnumArgs A) {
                     }
                 }
             }
-            int32_t x = A.rowsL[A.bstart[b] + a];
-            int32_t y = A.tri ? A.rowsL[A.bstart[b] + c] : A.rowsR[A.bstartR[b] + c];
+            const int64_t pa = A.bstart[b] + a, pc = A.tri ? A.bstart[b] + c : A.bstartR[b] + c;
+            int32_t x = A.rowsL[pa];
+            int32_t y = A.tri ? A.rowsL[pc] : A.rowsR[pc];
+            vx[i] = (int32_t)pa;
+            vy[i] = (int32_t)pc;
             bool ok = true;
             if (A.rank_filter) {
                 int64_t rx = A.rankL[x], ry = A.rankR[y];
@@ -208,6 +212,10 @@ __global__ __launch_bounds__(EN_THREADS) void k_enum(EnumArgs A) {
         if (keep & (1u << i)) {
             A.out_l[pos] = xs[i];
             A.out_r[pos] = ys[i];
+            if (A.out_vl) {
+                A.out_vl[pos] = vx[i];
+                A.out_vr[pos] = vy[i];
+            }
             ++pos;
         }
     }
@@ -413,6 +421,15 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
     SPK_REQUIRE(n_out < (int64_t)1 << 40, SPK_E_LIMIT, "spk_block: pair count too large");
     SPK_TRY(ctx->pl.alloc((size_t)n_out + 1));
     SPK_TRY(ctx->pr.alloc((size_t)n_out + 1));
+    // rules 1 .. MAX_VIEWS-1 keep their row order (view) and emit their pairs' view positions
+    const int n_views = std::min(n_rules, MAX_VIEWS) - 1;
+    const int64_t pv_base = n_views > 0 ? rule_base[1] : n_out;
+    ctx->n_views = 0;
+    ctx->pv_base = pv_base;
+    if (n_views > 0 && n_out > pv_base) {
+        SPK_TRY(ctx->pvl.alloc((size_t)(n_out - pv_base) + 1));
+        SPK_TRY(ctx->pvr.alloc((size_t)(n_out - pv_base) + 1));
+    }
     for (int r = 0; r < n_rules; ++r) {
         if (!n_chunks[r]) continue;
         RulePlan &P = *plans[r];
@@ -435,13 +452,30 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         A.chunk_off = offs[r]->p;
         A.out_l = ctx->pl.p + rule_base[r];
         A.out_r = ctx->pr.p + rule_base[r];
+        const bool view = r >= 1 && r <= n_views;
+        A.out_vl = view ? ctx->pvl.p + (rule_base[r] - pv_base) : nullptr;
+        A.out_vr = view ? ctx->pvr.p + (rule_base[r] - pv_base) : nullptr;
         k_enum<true><<<(unsigned)n_chunks[r], EN_THREADS, 0, ctx->stream>>>(A);
         SPK_HIP(hipGetLastError());
     }
     SPK_TRY(ctx->end(K_BLOCK));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    for (int r = 1; r <= n_views; ++r) {
+        RuleView &v = ctx->views[r];
+        RulePlan &P = *plans[r];
+        take_buf(v.rowsL, P.L.rows);
+        v.nL = P.L.n_valid;
+        v.tri = P.tri != 0;
+        if (!v.tri) take_buf(v.rowsR, P.R.rows);
+        else v.rowsR.release();
+        v.nR = v.tri ? v.nL : P.R.n_valid;
+        v.pair_lo = rule_base[r];
+        v.pair_hi = r + 1 < n_rules ? rule_base[r + 1] : n_out;
+    }
+    ctx->n_views = n_views;
     ctx->n_pairs = n_out;
     ctx->pairs_valid = true;
+    ctx->pairs_epoch++;
     ctx->codes_valid = false;
     if (out_n_pairs) *out_n_pairs = n_out;
     if (out_n_candidates_total) *out_n_candidates_total = total;

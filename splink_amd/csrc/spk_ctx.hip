@@ -422,6 +422,9 @@ int spk_pairs_load(spk_ctx *ctx, int64_t n, const int32_t *rows_l, const int32_t
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     ctx->n_pairs = n;
     ctx->pairs_valid = true;
+    ctx->pairs_epoch++;
+    ctx->n_views = 0;
+    ctx->pv_base = n;
     ctx->codes_valid = false;
     return SPK_OK;
 }

@@ -87,6 +87,7 @@ constexpr int32_t TF_EQ = 16;      // `=` (else `<>`)
 //   SC_NUM 16 B {value f64, valid u32, pad}
 // lens = UTF-16 length | code points << 16, each saturating at LEN_SAT; LENS_NULL = NULL.
 constexpr int IMG_MAX = 256;
+constexpr int64_t VIEW_MIN_IMAGE_BYTES = (int64_t)192 << 20;  // rule-view images only past this size
 constexpr uint32_t LENS_NULL = 0xFFFFFFFFu;
 constexpr int LEN_SAT = 0xFFFE;
 // The comparison programs are read-only for the whole launch: reading them through the constant
@@ -132,6 +133,10 @@ struct GammaArgs {
     int64_t img_stride;          // bytes of one row's fields (a multiple of 16)
     int64_t img_rows0, img_rows1;  // rows of each image (chunk-major layout: chunk c of row r at (c * rows + r) * 16)
     int32_t slot_beg[17];        // k_gamma_rows: simple[slot_beg[s] .. slot_beg[s+1]) start at image byte 8 s
+    // per filter launch: regions [region_base, region_base + gridDim.x); a view launch (rule 1's pairs)
+    // reads pl / pr = their view positions and img0 / img1 = view-ordered images
+    int region_base;
+    int all_img;  // every simple column reads the row image (no SC_GEN / SC_NUMRAW): views allowed
 };
 
 // Codes are written in place: the filter pass sets each pair's code, the exact / slow passes of
@@ -491,7 +496,7 @@ struct Region {
 };
 
 __device__ inline Region my_region(const GammaArgs &A) {
-    const int64_t r0 = (int64_t)blockIdx.x * A.region_len;
+    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
     const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
     return Region{r0, r1};
 }
@@ -786,8 +791,10 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     constexpr int64_t SPAN = 64 * FP;
     constexpr int64_t STEP = (int64_t)(F_THREADS / 64) * SPAN;
     int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN;
-    // the pair rows of the next iteration are loaded while this one's columns are evaluated, so the
-    // image gathers do not wait behind the pair-array load
+    // the image rows of the next iteration are loaded while this one's columns are evaluated, so the
+    // image gathers do not wait behind the pair-array load.  In a view launch (pairs of rule 1) pl / pr
+    // are the pairs' view positions and img0 / img1 the view-ordered images (only when every column
+    // reads the image, so no column needs the table row).
     int32_t nx[FP], ny[FP];
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
@@ -870,7 +877,7 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                                             bits_to_double(vb[u].x, vb[u].y));
                     break;
                 }
-                case SC_NUMRAW: {
+                case SC_NUMRAW: {  // the columns' own records, by table row
                     const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
                     for (int u = 0; u < FP; ++u)
                         lev[u] = simple_num(sc, c0.valid[x[u]] != 0, c0.val[x[u]], c1.valid[y[u]] != 0, c1.val[y[u]]);
@@ -894,7 +901,7 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     }
     __syncthreads();
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
-        A.region_count[(int64_t)simple[i].k * A.n_regions + blockIdx.x] = s_cnt[i];
+        A.region_count[(int64_t)simple[i].k * A.n_regions + A.region_base + blockIdx.x] = s_cnt[i];
 }
 
 // Filter pass over rows held in registers: when the image row is at most ROW_MAXQ x 16 bytes,
@@ -1056,7 +1063,7 @@ __global__ __launch_bounds__(F_THREADS) void k_gamma_rows(GammaArgs A) {
     }
     __syncthreads();
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
-        A.region_count[(int64_t)simple[i].k * A.n_regions + blockIdx.x] = s_cnt[i];
+        A.region_count[(int64_t)simple[i].k * A.n_regions + A.region_base + blockIdx.x] = s_cnt[i];
 }
 
 // Filter pass, every other column through the interpreter: adds to code[p].
@@ -1090,7 +1097,7 @@ __global__ __launch_bounds__(F_THREADS) void k_gamma_filter(GammaArgs A) {
     }
     __syncthreads();
     for (int i = threadIdx.x; i < A.n_complex; i += F_THREADS)
-        A.region_count[(int64_t)A.complex_k[i] * A.n_regions + blockIdx.x] = s_cnt[i];
+        A.region_count[(int64_t)A.complex_k[i] * A.n_regions + A.region_base + blockIdx.x] = s_cnt[i];
 }
 
 // The exact passes run over column k's compacted work list -- every region's undecided pairs back
@@ -1782,6 +1789,60 @@ static int64_t layout_image(std::vector<SimpleCol> &simple) {
     return (end + 15) & ~(int64_t)15;
 }
 
+// Row image in a rule's view order: chunk c of view position v = chunk c of table row rows[v]; the
+// same chunk stride (row capacity) as the table's image.
+__global__ void k_view_image(int64_t nv, const int32_t *__restrict__ rows, int nq, const uint4 *__restrict__ src,
+                             uint4 *__restrict__ dst, int64_t cap) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nv * nq) return;
+    const int64_t v = i % nv, c = i / nv;
+    dst[c * cap + v] = src[c * cap + rows[v]];
+}
+
+// View-ordered copies of the row images for rule 1's pairs (RuleView), rebuilt when the image or the
+// pair set changes.  Returns false when there is no view to use.
+struct ViewLaunch {
+    const uint8_t *img0, *img1;
+    const int32_t *rows0, *rows1;  // view position -> table row
+    int64_t lo, hi;                // rule 1's pair ordinals
+};
+
+static int build_view_images(spk_ctx *ctx, const GammaArgs &A, int64_t stride, ViewLaunch *out, bool *ok) {
+    *ok = false;
+    if (stride <= 0 || A.n_simple == 0 || ctx->n_views < 1 || !A.img0 || !A.all_img) return SPK_OK;
+    const int nq = (int)(stride / 16);
+    const int r = 1;
+    RuleView &v = ctx->views[r];
+    for (int s = 0; s < 2; ++s) {
+        const int64_t nv = (s == 0 || v.tri) ? v.nL : v.nR;
+        const int32_t *rows = (s == 0 || v.tri) ? v.rowsL.p : v.rowsR.p;
+        if (s == 1 && v.tri) {  // symmetric self-join: both sides index the same view
+            out->img1 = out->img0;
+            out->rows1 = out->rows0;
+            continue;
+        }
+        const int64_t cap = s == 0 ? A.img_rows0 : A.img_rows1;
+        const uint8_t *src = s == 0 ? A.img0 : A.img1;
+        std::vector<int64_t> key = ctx->img_key[(s == 1 && A.img1 != A.img0) ? 1 : 0];
+        key.push_back((int64_t)ctx->pairs_epoch);
+        key.push_back(s);
+        const bool fresh = ctx->vimg[r][s].p && ctx->vimg_key[r][s] == key;
+        SPK_TRY(ctx->vimg[r][s].alloc((size_t)cap * (size_t)stride));
+        if (!fresh && nv > 0) {
+            k_view_image<<<(unsigned)((nv * nq + 255) / 256), 256, 0, ctx->stream>>>(
+                nv, rows, nq, reinterpret_cast<const uint4 *>(src), reinterpret_cast<uint4 *>(ctx->vimg[r][s].p), cap);
+            SPK_HIP(hipGetLastError());
+        }
+        ctx->vimg_key[r][s] = key;
+        (s == 0 ? out->img0 : out->img1) = ctx->vimg[r][s].p;
+        (s == 0 ? out->rows0 : out->rows1) = rows;
+    }
+    out->lo = v.pair_lo;
+    out->hi = v.pair_hi;
+    *ok = true;
+    return SPK_OK;
+}
+
 // The image is a re-layout of the resident records for the current set of simple columns: it is
 // rebuilt only when a table (or one of its columns) was replaced or the column layout changed.
 static int build_images(spk_ctx *ctx, Table &t0, Table &t1, GammaArgs &A, int64_t stride,
@@ -2035,6 +2096,8 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.n_regions = n_regions;
     A.slow_count = ctx->work_count.p;
     A.n_simple = (int)simple.size();
+    A.all_img = 1;
+    for (const SimpleCol &sc : simple) A.all_img &= (sc.cls != SC_GEN && sc.cls != SC_NUMRAW) ? 1 : 0;
     A.n_complex = (int)complex_k.size();
     for (int t = 0; t <= 16; ++t) A.slot_beg[t] = slot_beg[t];
     ctx->last_simple = (int)simple.size();
@@ -2055,16 +2118,48 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 default: k_gamma_rows<8><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
             }
         } else {
-            switch (ctx->filter_waves) {  // (waves per SIMD the filter is compiled for, pairs per lane)
-                case 1: k_gamma_simple<1, 4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 2: k_gamma_simple<6, 4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 3: k_gamma_simple<5, 4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 4: k_gamma_simple<8, 2><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 5: k_gamma_simple<5, 3><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
-                // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
-                default: k_gamma_simple<6, 3><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
+            // regions wholly inside rule 1's pairs read its view-ordered image (view launch); the others,
+            // and a region straddling a rule boundary, the table image (table launches)
+            // Only when the image outgrows the caches: at 1M rows (80 MB, held by the 256 MB Infinity
+            // Cache) the second launch's tail cost 4 % (1.41 vs 1.34 ms, cfg2); at 20M rows (1.6 GB) the
+            // view launch takes the pass from 31.1 to 22.8 ms (profiles/r2_ab_views.log).
+            ViewLaunch V{};
+            bool have_view = false;
+            const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
+            if (ctx->use_views && big) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
+            int64_t va = n_regions, vb = n_regions;  // view regions [va, vb)
+            if (have_view) {  // regions [i L, min((i + 1) L, P)) inside [V.lo, V.hi)
+                va = std::min<int64_t>(n_regions, (V.lo + region_len - 1) / region_len);
+                vb = V.hi >= P ? n_regions : std::min<int64_t>(n_regions, V.hi / region_len);
+                vb = std::max<int64_t>(va, vb);
             }
+            auto launch = [&](const GammaArgs &LA, int64_t r_lo, int64_t r_hi) {
+                if (r_hi <= r_lo) return;
+                GammaArgs B = LA;
+                B.region_base = (int)r_lo;
+                const unsigned g = (unsigned)(r_hi - r_lo);
+                switch (ctx->filter_waves) {  // (waves per SIMD the filter is compiled for, pairs per lane)
+                    case 1: k_gamma_simple<1, 4><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 2: k_gamma_simple<6, 4><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 3: k_gamma_simple<5, 4><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 4: k_gamma_simple<8, 2><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 5: k_gamma_simple<5, 3><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
+                    // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
+                    default: k_gamma_simple<6, 3><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                }
+            };
+            launch(A, 0, va);
+            if (vb > va) {
+                GammaArgs VA = A;
+                VA.pl = ctx->pvl.p - ctx->pv_base;  // pl[p] = view position of pair p (p >= pv_base)
+                VA.pr = ctx->pvr.p - ctx->pv_base;
+                VA.img0 = V.img0;
+                VA.img1 = V.img1;
+                launch(VA, va, vb);
+            }
+            launch(A, vb, n_regions);
+            ctx->last_view_regions = vb - va;
         }
         SPK_HIP(hipGetLastError());
         if (A.n_complex) {
@@ -2319,6 +2414,8 @@ extern "C" int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n) {
 
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->use_views = on < 10;  // + 10: later rules' pairs read the table image (A/B of the rule views)
+    on %= 10;
     ctx->simple_columns = on != 0;
     ctx->row_filter = on == 2;
     ctx->filter_waves = on >= 3 ? on - 2 : 0;  // A/B variants of the filter (tools/ab_gamma.py)

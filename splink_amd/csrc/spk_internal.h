@@ -169,6 +169,28 @@ struct Table {
     ~Table();
 };
 
+template <typename T>
+inline void take_buf(DevBuf<T> &dst, DevBuf<T> &src) {  // move src's allocation into dst
+    dst.release();
+    dst.p = src.p;
+    dst.n = src.n;
+    src.p = nullptr;
+    src.n = 0;
+}
+
+// Blocking rule r >= 1 as its own row order ("view"): the rows with a non-NULL key r sorted by
+// (key r, rank), so a block of rule r is contiguous in it.  Pairs of rule r also carry their view
+// positions (spk_ctx::pvl / pvr), and the comparison filter reads a copy of the row image laid out
+// in view order: the pairs of a later rule then touch a block's rows in a few cache lines, as the
+// first rule's pairs do in the table (clustered by rule 0) itself.
+constexpr int MAX_VIEWS = 2;  // rules 1 .. MAX_VIEWS - 1 get views (one: registers of the filter)
+struct RuleView {
+    DevBuf<int32_t> rowsL, rowsR;  // view position -> table row (l side; r side unless tri)
+    int64_t nL = 0, nR = 0;
+    bool tri = true;               // symmetric self-join: both sides index rowsL
+    int64_t pair_lo = 0, pair_hi = 0;  // this rule's pair ordinals (local shard)
+};
+
 enum Kern { K_BLOCK = 0, K_GAMMA = 1, K_EMHIST = 2, K_EMFIN = 3, K_SCORE = 4, K_COUNT = 5 };
 
 }  // namespace spk
@@ -184,6 +206,11 @@ struct spk_ctx {
     spk::DevBuf<int32_t> pl, pr;
     int64_t n_pairs = 0;
     bool pairs_valid = false;
+    uint64_t pairs_epoch = 0;          // bumped whenever the pair set is replaced
+    spk::RuleView views[spk::MAX_VIEWS];  // views[r] for rules 1 .. n_views
+    int n_views = 0;
+    spk::DevBuf<int32_t> pvl, pvr;     // view positions of pairs [pv_base, n_pairs)
+    int64_t pv_base = 0;
 
     // packed comparison-vector codes
     spk::DevBuf<uint8_t> codes;
@@ -198,6 +225,8 @@ struct spk_ctx {
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
     int filter_waves = 0;             // k_gamma_simple variant (waves per SIMD, pairs per lane): 0 = <6,3>; 1..5 A/B
+    bool use_views = true;            // rule 1's pairs read a view-ordered row image (A/B switch)
+    int64_t last_view_regions = 0;    // filter regions the last spk_gammas ran as a view launch
     int last_simple = 0;
 
     // comparison-vector work buffers (reused across calls)
@@ -223,6 +252,8 @@ struct spk_ctx {
     }
     spk::DevBuf<uint8_t> img[2];      // filter row images of table 0 / table 1
     std::vector<int64_t> img_key[2];  // what img[s] was built from: table version, rows, column layout
+    spk::DevBuf<uint8_t> vimg[spk::MAX_VIEWS][2];  // row images in rule-view order (views[r])
+    std::vector<int64_t> vimg_key[spk::MAX_VIEWS][2];
     uint64_t table_epoch = 0;
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)
     spk::DevBuf<unsigned int> work_count;    // [2K] slow-pass list lengths, then slow-Levenshtein rest lists

@@ -10,9 +10,10 @@ from splink_amd.session import AmdSession
 from splink_amd.synthetic import cfg_settings, make_records
 COLS = ["first_name", "surname", "dob", "city", "email"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-df = make_records(n, surname_vocab=15000)[["unique_id"] + COLS]
+df = make_records(n, surname_vocab=int(os.environ.get("AB_VOCAB", "15000")), arrow=True)[["unique_id"] + COLS]
 st = Params(cfg_settings(2), AmdSession(0)).settings
-job = Job("dedupe_only", [df], "unique_id", 0)
+shard = tuple(int(x) for x in os.environ.get("AB_SHARD", "0/1").split("/"))
+job = Job("dedupe_only", [df], "unique_id", 0, shard=shard)
 job.ctx.enable_timing(True)
 job.block(st["blocking_rules"])
 ref = None
