@@ -203,12 +203,14 @@ int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
  * other column by the general interpreter.  on = 1 (default): template columns through the
  * column-batched filter; on = 2: through the register-resident row filter when the image row is
  * short (<= 128 bytes); on = 0: every column through the interpreter; on + 10: the same, with
- * the pairs of later blocking rules reading the table-ordered row image instead of their rule's
- * view-ordered copy.  All
+ * the second blocking rule's pairs always reading the table-ordered row image, on + 20: always their
+ * rule's view-ordered copy (default: the copy once the image outgrows the caches).  All
  * modes give identical results (for testing and measurement).  spk_gammas_simple_count: how many
  * columns the last spk_gammas took as template columns. */
 int spk_gammas_set_simple(spk_ctx *ctx, int on);
 int spk_gammas_simple_count(spk_ctx *ctx, int *out);
+/* Filter regions (workgroups) the last spk_gammas ran over the second rule's view-ordered image. */
+int spk_gammas_view_regions(spk_ctx *ctx, int64_t *out);
 
 /* ---- the jar's similarity UDFs as bulk device functions ---------------------------------
  * spk_jaro_winkler_sim replaces uk.gov.moj.dash.linkage.JaroWinklerSimilarity.call(String, String)

@@ -2125,8 +2125,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             // view launch takes the pass from 31.1 to 22.8 ms (profiles/r2_ab_views.log).
             ViewLaunch V{};
             bool have_view = false;
+            ctx->last_view_regions = 0;
             const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
-            if (ctx->use_views && big) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
+            if ((ctx->use_views == 1 && big) || ctx->use_views == 2)
+                SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
             int64_t va = n_regions, vb = n_regions;  // view regions [va, vb)
             if (have_view) {  // regions [i L, min((i + 1) L, P)) inside [V.lo, V.hi)
                 va = std::min<int64_t>(n_regions, (V.lo + region_len - 1) / region_len);
@@ -2414,11 +2416,17 @@ extern "C" int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n) {
 
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
-    ctx->use_views = on < 10;  // + 10: later rules' pairs read the table image (A/B of the rule views)
+    ctx->use_views = on >= 20 ? 2 : (on >= 10 ? 0 : 1);  // + 10: never view launches, + 20: always (A/B, tests)
     on %= 10;
     ctx->simple_columns = on != 0;
     ctx->row_filter = on == 2;
     ctx->filter_waves = on >= 3 ? on - 2 : 0;  // A/B variants of the filter (tools/ab_gamma.py)
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_view_regions(spk_ctx *ctx, int64_t *out) {
+    SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
+    *out = ctx->last_view_regions;
     return SPK_OK;
 }
 

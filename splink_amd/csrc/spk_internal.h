@@ -225,7 +225,8 @@ struct spk_ctx {
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
     int filter_waves = 0;             // k_gamma_simple variant (waves per SIMD, pairs per lane): 0 = <6,3>; 1..5 A/B
-    bool use_views = true;            // rule 1's pairs read a view-ordered row image (A/B switch)
+    int use_views = 1;                // rule 1's pairs read a view-ordered row image: 0 never, 1 when the
+                                      // image outgrows the caches, 2 always (A/B and tests)
     int64_t last_view_regions = 0;    // filter regions the last spk_gammas ran as a view launch
     int last_simple = 0;
 

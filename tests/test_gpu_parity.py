@@ -262,6 +262,34 @@ def test_simple_columns_match_interpreter(amd):
     assert (fast == slow).all()
 
 
+@pytest.mark.parametrize("rules,big_rule1", [
+    (["l.surname = r.surname", "l.dob = r.dob"], True),
+    (["l.dob = r.dob", "l.first_name = r.first_name AND l.city = r.city", "l.surname = r.surname"], True),
+    (["l.surname = r.surname", "l.first_name = r.surname"], False)])  # few rule-1 pairs: no whole view region
+def test_rule_view_launch_matches_table_launch(amd, rules, big_rule1):
+    """The second rule's pairs through its view-ordered image (forced, + 20) and through the table image
+    (+ 10) give the oracle's comparison vectors -- symmetric, multi-term and asymmetric rules."""
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import cfg_settings
+    df = _synthetic(12000, seed=29, surname_vocab=300, first_vocab=200, city_vocab=40)
+    st = complete_settings_dict(cfg_settings(2), amd)
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(rules)
+    out = []
+    for mode in (21, 11, 21):
+        job.ctx.gammas_set_simple(mode)
+        job.gammas(st)
+        assert (job.ctx.gammas_view_regions() > 0) == (mode == 21 and big_rule1)
+        out.append(job.gammas_host())
+    assert (out[0] == out[1]).all() and (out[2] == out[1]).all()
+    table = job.tables[0]
+    l, r = job.pair_rows()
+    cols = [orc.StrCol(table[c].tolist()) for c in ["first_name", "surname", "dob", "city", "email"]]
+    specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
+    assert (out[0] == orc.template_gammas(specs, cols, cols, l, r)).all()
+
+
 def test_em_at_scale_matches_oracle(amd):
     from splink_amd.engine import Job, m_step_rows
     from splink_amd.params import Params
