@@ -1,17 +1,23 @@
 """HBM traffic per launch from rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE in separate runs).
 
-    python tools/traffic.py --fetch DIR --write DIR [--em-bytes B] [--out profiles/rN_traffic.json]
+    python tools/traffic.py --fetch DIR --write DIR [--calib DIR] [--head-em N] [--out profiles/rN_traffic.json]
 
-FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters (KiB per dispatch, from the L2's
-memory-side request counters).  The correction follows MI355X_MICROARCH.md "HBM [CDNA4]": on gfx950
-FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so fetched bytes =
-2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 is taken as is.  The calibration kernel is k_hist_lanes:
-it streams exactly P x 2 bytes of comparison codes with 16-byte loads, so its corrected
-fetch / algorithmic ratio (--em-bytes) is reported next to the figures.
+FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters (KiB per dispatch, from the L2's memory-side
+request counters).  Corrections, per access shape:
+  * streams (16-byte lanes, coalesced): FETCH_SIZE reports half the bytes on gfx950
+    (MI355X_MICROARCH.md "HBM [CDNA4]"), confirmed by tools/calib_fetch's k_stream16 (ratio 0.500);
+  * scattered loads (one load per 128-byte line, 4 / 8 / 16 bytes): FETCH_SIZE reports 64 bytes per
+    line (tools/calib_fetch k_gather*, 66.0 B per gather with the index stream), and their kernel time
+    (16M lines in 354 us vs 2 GiB streamed in 403 us) matches 64-byte sectors, not 128-byte lines,
+    so the counter is taken as is (factor 1).
+The comparison pass (gamma group) is gather-bound: its traffic is FETCH_SIZE x 1 (+ WRITE_SIZE), with
+the x 2 stream reading as an upper bound; the E/M kernels stream: x 2.
 
 Kernel groups, per call of the C-ABI entry point (one "launch" of bench.py's roofline):
-  gamma : every kernel spk_gammas launches (k_build_image, k_gamma_*), summed per call
-  em    : k_hist_lanes / k_hist + k_hist_reduce, per spk_em_histogram call
+  gamma : every kernel spk_gammas launches (k_build_image, k_view_image, k_gamma_*), per call
+          (calls = k_prefix dispatches)
+  em    : k_hist_lanes / k_hist + k_hist_reduce, per spk_em_histogram call; the first --head-em calls
+          (bench.py's warmup + timed steps at the headline size), the rest reported as em_at_scale
 """
 from __future__ import annotations
 
@@ -23,59 +29,79 @@ import json
 import os
 import re
 
-GROUPS = {"gamma": re.compile(r"k_build_image|k_gamma_"), "em": re.compile(r"k_hist")}
+GAMMA = re.compile(r"k_build_image|k_view_image|k_gamma_|k_compact|k_prefix")
+EM = re.compile(r"k_hist")
 
 
 def read_counter(d, name):
-    """{kernel name: [value per dispatch]}"""
-    out = collections.defaultdict(list)
+    """[(dispatch id, kernel name, value)] in dispatch order."""
+    out = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == name:
-                out[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return out
+                out.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    return sorted(out)
 
 
-def group_total(per_kernel, pat):
-    tot, n = 0.0, 0
-    for k, vs in per_kernel.items():
-        if pat.search(k):
-            tot += sum(vs)
-            n += len(vs)
-    return tot, n
+def calls_of(rows, pat):
+    return [i for i, (d, k, v) in enumerate(rows) if re.search(pat, k)]
+
+
+def split_em(rows, head):
+    """EM dispatches grouped per spk_em_histogram call (k_hist_lanes/k_hist + k_hist_reduce)."""
+    calls, cur = [], []
+    for d, k, v in rows:
+        if not EM.search(k):
+            continue
+        cur.append(v)
+        if "k_hist_reduce" in k or ("k_hist<" in k):
+            calls.append(sum(cur))
+            cur = []
+    return calls[:head], calls[head:]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
-    ap.add_argument("--em-bytes", type=float, default=None, help="algorithmic bytes of one k_hist launch")
+    ap.add_argument("--calib")
+    ap.add_argument("--head-em", type=int, default=3)
     ap.add_argument("--out")
     a = ap.parse_args()
-    fetch = read_counter(a.fetch, "FETCH_SIZE")
-    write = read_counter(a.write, "WRITE_SIZE")
-    # calls = dispatches of the kernel each entry point launches exactly once per call
-    calls = {"gamma": len([v for k, vs in fetch.items() if re.search(r"k_gamma_simple|k_gamma_rows", k) for v in vs]),
-             "em": len([v for k, vs in fetch.items() if re.search(r"k_hist_lanes|k_hist<", k) for v in vs])}
-    res = {"source": {"fetch_pass": a.fetch, "write_pass": a.write, "calls": calls},
-           "correction": "bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (MI355X_MICROARCH.md HBM [CDNA4])"}
-    for g, pat in GROUPS.items():
-        f, nf = group_total(fetch, pat)
-        w, nw = group_total(write, pat)
-        fb = 2.0 * f * 1024.0 / max(1, calls[g])
-        wb = w * 1024.0 / max(1, calls[g])
-        res[g] = {"fetch_bytes_per_call": fb, "write_bytes_per_call": wb, "traffic_bytes_per_call": fb + wb,
-                  "dispatches": [nf, nw]}
-    if a.em_bytes:
-        res["em"]["calibration_fetch_over_algorithmic"] = res["em"]["fetch_bytes_per_call"] / a.em_bytes
-    per_kernel = {}
-    for k in sorted(set(fetch) | set(write)):
-        short = re.sub(r"\(.*", "", k)[:80]
-        fs, ws = fetch.get(k, []), write.get(k, [])
-        per_kernel[short] = {"dispatches": max(len(fs), len(ws)),
-                             "fetch_bytes_avg": 2048.0 * sum(fs) / max(1, len(fs)),
-                             "write_bytes_avg": 1024.0 * sum(ws) / max(1, len(ws))}
-    res["per_kernel"] = per_kernel
+    fetch, write = read_counter(a.fetch, "FETCH_SIZE"), read_counter(a.write, "WRITE_SIZE")
+    res = {"source": {"fetch_pass": a.fetch, "write_pass": a.write}}
+    n_calls = max(1, len(calls_of(fetch, r"k_prefix")))
+    fg = sum(v for d, k, v in fetch if GAMMA.search(k)) * 1024.0 / n_calls
+    wg = sum(v for d, k, v in write if GAMMA.search(k)) * 1024.0 / n_calls
+    res["gamma"] = {"calls": n_calls, "fetch_bytes_per_call": fg, "fetch_bytes_per_call_x2": 2 * fg,
+                    "write_bytes_per_call": wg, "traffic_bytes_per_call": fg + wg,
+                    "traffic_bytes_per_call_upper": 2 * fg + wg,
+                    "correction": "FETCH_SIZE x 1 (scattered line gathers, calibrated); x 2 = stream upper bound"}
+    fh, ft = split_em(fetch, a.head_em)
+    wh, wt = split_em(write, a.head_em)
+    for name, fs, ws in (("em", fh, wh), ("em_at_scale", ft, wt)):
+        if fs:
+            fb = 2.0 * 1024.0 * sum(fs) / len(fs)
+            wb = 1024.0 * sum(ws) / max(1, len(ws))
+            res[name] = {"calls": len(fs), "fetch_bytes_per_call": fb, "write_bytes_per_call": wb,
+                         "traffic_bytes_per_call": fb + wb, "correction": "2 x FETCH_SIZE (streams) + WRITE_SIZE"}
+    if a.calib:
+        cal = collections.defaultdict(list)
+        for d, k, v in read_counter(a.calib, "FETCH_SIZE"):
+            cal[re.sub(r"\(.*", "", k)[:40]].append(v)
+        res["calibration"] = {k: {"fetch_kib_avg": sum(v) / len(v), "dispatches": len(v)} for k, v in cal.items()}
+        res["calibration"]["note"] = ("tools/calib_fetch: k_stream16 reads 2 GiB (2097152 KiB); k_gather* read one "
+                                      "4/8/16-byte word from each of 16M distinct 128-byte lines")
+    per_kernel = collections.defaultdict(lambda: {"dispatches": 0, "fetch_kib": 0.0, "write_kib": 0.0})
+    for d, k, v in fetch:
+        s = re.sub(r"\(.*", "", k)[:80]
+        per_kernel[s]["dispatches"] += 1
+        per_kernel[s]["fetch_kib"] += v
+    for d, k, v in write:
+        per_kernel[re.sub(r"\(.*", "", k)[:80]]["write_kib"] += v
+    res["per_kernel_avg_kib"] = {k: {"dispatches": x["dispatches"], "fetch_kib": x["fetch_kib"] / max(1, x["dispatches"]),
+                                     "write_kib": x["write_kib"] / max(1, x["dispatches"])}
+                                 for k, x in per_kernel.items()}
     print(json.dumps(res, indent=1))
     if a.out:
         with open(a.out, "w") as f:
