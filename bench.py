@@ -235,6 +235,7 @@ def main():
                          "block_keys_wall": job.timings.get("block_keys_s", 0.0) * 1e3,
                          "first_gammas_call_incl_column_decode": first_gammas_s * 1e3,
                          **{f"host_wall_{k}": float(np.mean(v)) for k, v in host.items()}},
+        "device_lds_per_block": job.ctx.lds_per_block(),
         "input": "Arrow-backed string columns (pd.ArrowDtype(large_string)); keys, ids, ranks, clustering on the device",
         "deferred_pairs": job.ctx.gammas_deferred(),
         "exact_cells_per_column": dict(zip(names, job.ctx.gammas_exact_counts(len(names)))),

@@ -56,6 +56,8 @@ int spk_ctx_set_link_type(spk_ctx *ctx, int link_type);
  * on the context stream: [0] block, [1] gamma, [2] em_hist, [3] em_final, [4] score. */
 int spk_ctx_kernel_ms(spk_ctx *ctx, double *out5);
 int spk_ctx_enable_timing(spk_ctx *ctx, int on);
+/* LDS bytes one workgroup may allocate on the context's device (sizes the E/M histogram copies). */
+int spk_ctx_lds_per_block(spk_ctx *ctx, int *out);
 
 /* ---- record tables (replaces createOrReplaceTempView of df / df_l / df_r,
  *      blocking.py:209-222, and the vertical concatenation of :70-93) ------------ */

@@ -47,7 +47,7 @@ EXPORTS = [
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
     "spk_gammas_set_simple", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
-    "spk_gammas_view_regions", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
+    "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
 ]
 
 
@@ -305,6 +305,11 @@ class Context:
     def gammas_set_simple(self, mode):
         """1 / True: template-column filters (column-batched), 2: register-row filter when short, 0: interpreter."""
         check(self._lib.spk_gammas_set_simple(self._h, ctypes.c_int(int(mode))), "spk_gammas_set_simple")
+
+    def lds_per_block(self) -> int:
+        n = ctypes.c_int(0)
+        check(self._lib.spk_ctx_lds_per_block(self._h, ctypes.byref(n)), "spk_ctx_lds_per_block")
+        return n.value
 
     def gammas_view_regions(self) -> int:
         n = ctypes.c_int64(0)

@@ -1,4 +1,5 @@
 // Context, record-table upload (UTF-8 -> UTF-16 on the device) and pair buffers.
+#include <algorithm>
 #include <cstring>
 
 #include "spk_internal.h"
@@ -198,6 +199,11 @@ int spk_ctx_create(int device, spk_ctx **out) {
     spk_ctx *c = new spk_ctx();
     c->device = device;
     c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    // LDS one workgroup may allocate (the lane-private E/M histogram sizes its copies to it)
+    int lds = 0, lds_optin = 0;
+    (void)hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+    (void)hipDeviceGetAttribute(&lds_optin, hipDeviceAttributeSharedMemPerBlockOptin, device);
+    c->lds_per_block = std::max(std::max(lds, lds_optin), 64 * 1024);
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;

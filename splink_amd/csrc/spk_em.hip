@@ -7,6 +7,7 @@
 // k_hist_lanes; wave-level aggregation of equal codes for large pattern spaces, k_hist), then evaluates mp per pattern with the reference's literal
 // arithmetic and reduces the per-(column, level) sums in a fixed order (deterministic, and
 // identical for any sharding of pairs over GPUs since the histogram is an exact integer sum).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(H_THREADS) void k_hist(const CodeT *__restrict__ co
 // 64 / R lanes per bank.  Waves of a workgroup share the copies (atomics; different instructions
 // never bank-conflict).  Codes are streamed as 16-byte vectors, four loads in flight per lane.
 constexpr int HL_THREADS = 1024;
-constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS
+constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS (gfx950), capped by the device attribute
 constexpr int HL_UNROLL = 4;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -467,7 +468,8 @@ extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     const int64_t P = ctx->n_pairs;
     const int vec = 16 / ctx->code_bytes;
     int R = 64;
-    while (R >= 4 && n_pat * R * 4 > HL_LDS_BYTES) R >>= 1;
+    const int64_t lds_budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block);
+    while (R >= 4 && n_pat * R * 4 > lds_budget) R >>= 1;
     SPK_TRY(ctx->begin(K_EMHIST));
     if (R >= 4 && ctx->hist_lanes) {
         // one 1024-thread workgroup per CU, per-workgroup partial counts, fixed-order reduction

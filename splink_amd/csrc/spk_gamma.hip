@@ -156,6 +156,18 @@ __device__ inline void code_add(const GammaArgs &A, int64_t p, uint32_t d) {
     }
 }
 
+// Exact passes of several columns in one launch (ExactCols) may update one pair's code concurrently:
+// an atomic add on the aligned dword (a 16-bit code never carries into its neighbour -- a code stays
+// below the pattern count, <= 65536).
+__device__ inline void code_add_atomic(const GammaArgs &A, int64_t p, uint32_t d) {
+    if (A.code16) {
+        uint32_t *w = reinterpret_cast<uint32_t *>(static_cast<uint16_t *>(A.codes) + (p & ~(int64_t)1));
+        atomicAdd(w, d << (16 * (uint32_t)(p & 1)));
+    } else {
+        atomicAdd(static_cast<uint32_t *>(A.codes) + p, d);
+    }
+}
+
 enum : int { KF = 0, KT = 1, KN = 2, KU = 3 };  // false, true, NULL, undecided (filter pass)
 
 __device__ inline int k_and(int a, int b) {
@@ -1418,12 +1430,26 @@ constexpr int LEV_WAVES = 5;
 // The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD): capped at
 // 4 waves (128 VGPRs, 40 B of spills) it measured the same on MI355X (52.1 vs 52.3 us per call).
 constexpr int JW_WAVES = 1;
+// Columns of one exact launch: blocks [c g, (c + 1) g) work through column si[c]'s list, so the
+// short Jaro-Winkler lists of several columns share one launch (and its tail).
+struct ExactCols {
+    int n;
+    int g;  // blocks per column
+    int si[4];
+};
+
 template <bool LEV>
-__global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma_exact_simple(GammaArgs A, int si, const int32_t *xlist,
-                                                                   const int64_t *xinfo) {
+__global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma_exact_simple(GammaArgs A, ExactCols C,
+                                                                   const int32_t *xlist, const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
+    const int col_slot = (int)(blockIdx.x / (unsigned)C.g);  // block-uniform
+    const int64_t bid = (int64_t)blockIdx.x - (int64_t)col_slot * C.g;
     if (threadIdx.x == 0) {
+        int si = C.si[0];
+#pragma unroll
+        for (int c = 1; c < 4; ++c)
+            if (c == col_slot) si = C.si[c];
         s_sc = A.simple[si];
         s_c0 = A.cols0[s_sc.col];
         s_c1 = A.cols1[s_sc.col];
@@ -1433,10 +1459,10 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
     const int k = sc.k;
     const int64_t n = exact_count(A, xinfo, k);
     const int32_t *items = xlist + xinfo[k];
-    const int64_t stride = (int64_t)gridDim.x * X_THREADS;
+    const int64_t stride = (int64_t)C.g * X_THREADS;
     // software pipeline: the next item's pair rows (and, for Levenshtein, the rows' lengths) are in
     // flight while this one is evaluated
-    int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x;
+    int64_t i = bid * X_THREADS + threadIdx.x;
     // Regroup by work bin only in free-text columns (rows past 64 units, so planes_hi exists): there the
     // trip counts spread widely (cfg5 addresses: 2.98 -> 2.67 ms per call).  In short-string columns
     // the sort's barriers cost more than it saves (cfg2 email: 475 -> 505 us), so they keep the old order.
@@ -1448,7 +1474,7 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
         y = A.pr[p];
         if (regroup) key = lev_work_bin(s_c0.meta[x].len16, s_c1.meta[y].len16);
     }
-    for (int64_t base = (int64_t)blockIdx.x * X_THREADS; base < n; base += stride) {  // block-uniform
+    for (int64_t base = bid * X_THREADS; base < n; base += stride) {  // block-uniform
         bool have = i < n;
         const int64_t i2 = i + stride;
         int32_t p2 = 0, x2 = 0, y2 = 0, key2 = LEV_BINS - 1;
@@ -1463,10 +1489,12 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
         if (have) {
             int level = 0;
             const int st = LEV ? lev_cell(sc, s_c0, s_c1, x, y, level) : simple_exact(A, sc, s_c0, s_c1, x, y, level);
-            if (st == ST_DONE)
-                code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
-            else
+            if (st != ST_DONE)
                 to_slow = true;
+            else if (C.n > 1)
+                code_add_atomic(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
+            else
+                code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
         }
         wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
         i = i2;
@@ -2190,19 +2218,47 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         if (P > 0) {
             k_prefix<<<1, PFX_THREADS, 0, ctx->stream>>>(ctx->region_count.p, K, n_regions, cap, ctx->xpref.p,
                                                         ctx->xinfo.p);
+            // Jaro-Winkler template columns: compact every list, then one exact launch over all of them
+            ExactCols jw{};
+            jw.g = (int)g_exact;
             for (int k = 0; k < K; ++k) {
-                if (!may_exact[k]) continue;
+                if (!may_exact[k] || simple_of[k] < 0) continue;
+                const SimpleCol &sc = simple[simple_of[k]];
+                if (sc.cls == SC_LEV || sc.kind != SK_STR || jw.n == 4) continue;
                 k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1),
                                                                        ctx->xlist.p, ctx->xinfo.p);
-                if (simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV)
-                    k_gamma_exact_simple<true><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
-                        A, simple_of[k], ctx->xlist.p, ctx->xinfo.p);
-                else if (simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR)
-                    k_gamma_exact_simple<false><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
-                        A, simple_of[k], ctx->xlist.p, ctx->xinfo.p);
-                else
+                jw.si[jw.n++] = simple_of[k];
+            }
+            if (jw.n)
+                k_gamma_exact_simple<false><<<(unsigned)(g_exact * jw.n), X_THREADS, 0, ctx->stream>>>(
+                    A, jw, ctx->xlist.p, ctx->xinfo.p);
+            for (int k = 0; k < K; ++k) {
+                if (!may_exact[k]) continue;
+                const bool simple_str = simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR;
+                const bool lev = simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV;
+                bool fused = false;
+                for (int c = 0; c < jw.n; ++c) fused = fused || jw.si[c] == simple_of[k];
+                if (!fused)
+                    k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1),
+                                                                           ctx->xlist.p, ctx->xinfo.p);
+                if (lev) {
+                    ExactCols one{};
+                    one.n = 1;
+                    one.g = (int)g_exact;
+                    one.si[0] = simple_of[k];
+                    k_gamma_exact_simple<true><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
+                                                                                                ctx->xinfo.p);
+                } else if (!fused && simple_str) {
+                    ExactCols one{};
+                    one.n = 1;
+                    one.g = (int)g_exact;
+                    one.si[0] = simple_of[k];
+                    k_gamma_exact_simple<false><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
+                                                                                                 ctx->xinfo.p);
+                } else if (!fused) {
                     k_gamma_exact<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
-                if (simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV) {
+                }
+                if (lev) {
                     k_gamma_slow_lev<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], ctx->xlist.p,
                                                                                          ctx->xinfo.p);
                     k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
@@ -2421,6 +2477,12 @@ extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     ctx->simple_columns = on != 0;
     ctx->row_filter = on == 2;
     ctx->filter_waves = on >= 3 ? on - 2 : 0;  // A/B variants of the filter (tools/ab_gamma.py)
+    return SPK_OK;
+}
+
+extern "C" int spk_ctx_lds_per_block(spk_ctx *ctx, int *out) {
+    SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
+    *out = ctx->lds_per_block;
     return SPK_OK;
 }
 

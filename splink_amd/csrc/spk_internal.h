@@ -267,6 +267,7 @@ struct spk_ctx {
     double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;
     int n_cu = 256;                   // compute units of the device (grid sizing)
+    int lds_per_block = 64 * 1024;    // LDS a workgroup may allocate (device attribute)
     int pinned_stats(size_t n) {
         if (n <= h_stats_n) return SPK_OK;
         if (h_stats) (void)hipHostFree(h_stats);
