@@ -96,6 +96,24 @@ constexpr int LEN_SAT = 0xFFFE;
 typedef const __attribute__((address_space(4))) SimpleCol ConstSimpleCol;
 __device__ inline ConstSimpleCol *const_simple(const SimpleCol *p) { return (ConstSimpleCol *)p; }
 
+// A chunk plane of the image as a buffer resource: gathers then take a 32-bit per-lane byte offset
+// (row x 16) against a wave-uniform descriptor -- no 64-bit address arithmetic per load
+// (cdna_hip_programming.md T8).  Used when every plane fits the descriptor's 31-bit range.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+__device__ inline __amdgpu_buffer_rsrc_t image_rsrc(const uint8_t *base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)bytes, 0x00020000);
+}
+// field at scalar byte offset `soff` (the chunk plane and in-chunk offset of a column) of the row at `off`
+__device__ inline uint4 buf16(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff) {
+    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ inline uint2 buf8(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff) {
+    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0);
+    return make_uint2(v.x, v.y);
+}
+
 // Chunk-major image: the 16-byte chunk c of every row is contiguous, so the lanes of a wave that
 // read the same field of consecutive rows (a block's pairs) share a few cache lines.
 __host__ __device__ inline int64_t img_at(int64_t rows, int64_t row, int off) {
@@ -792,7 +810,7 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
 // evaluating any: the pass is bound by the latency of those gathers, so every round trip is
 // shared by F_PAIRS pairs.  The column loop is uniform across the wave, so the class dispatch and
 // the test parameters are scalar.
-template <int MINW, int FP>
+template <int MINW, int FP, bool BUF>
 __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     __shared__ unsigned int s_cnt[MAX_SIMPLE];
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
@@ -802,6 +820,10 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     ConstSimpleCol *simple = const_simple(A.simple);
     constexpr int64_t SPAN = 64 * FP;
     constexpr int64_t STEP = (int64_t)(F_THREADS / 64) * SPAN;
+    // one buffer descriptor per side's whole image (BUF: the launch checked it fits 31 bits); a
+    // column's field is the scalar offset of its chunk plane
+    const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0, A.img_rows0 * A.img_stride);
+    const __amdgpu_buffer_rsrc_t r1 = image_rsrc(A.img1, A.img_rows1 * A.img_stride);
     int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN;
     // the image rows of the next iteration are loaded while this one's columns are evaluated, so the
     // image gathers do not wait behind the pair-array load.  In a view launch (pairs of rule 1) pl / pr
@@ -817,14 +839,18 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     for (; base < R.r1; base += STEP) {  // wave-uniform
         int64_t p[FP];
         bool act[FP];
-        int32_t x[FP], y[FP];
         uint32_t acc[FP];
+        // Byte offset of each pair's rows within one 16-byte chunk plane of the image (rows < 2^28): the
+        // gathers below address a wave-uniform chunk base plus this 32-bit offset (buffer descriptor +
+        // VGPR offset), so a load costs no per-lane 64-bit address arithmetic.  The row itself is
+        // ox >> 4 for the columns that read their own records.
+        uint32_t ox[FP], oy[FP];
 #pragma unroll
         for (int u = 0; u < FP; ++u) {
             p[u] = base + u * 64 + lane;
             act[u] = p[u] < R.r1;
-            x[u] = nx[u];
-            y[u] = ny[u];
+            ox[u] = (uint32_t)nx[u] << 4;
+            oy[u] = (uint32_t)ny[u] << 4;
             acc[u] = 0;
             const int64_t q = p[u] + STEP;
             nx[u] = q < R.r1 ? A.pl[q] : 0;
@@ -834,6 +860,11 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
             ConstSimpleCol &sc = simple[j];
             bool und[FP];
             int lev[FP];
+            // wave-uniform chunk bases of this column's fields (img_at with row 0)
+            const uint8_t *b0 = A.img0 + img_at(A.img_rows0, 0, sc.off), *b1 = A.img1 + img_at(A.img_rows1, 0, sc.off);
+            const uint8_t *h0 = A.img0 + img_at(A.img_rows0, 0, sc.off2), *h1 = A.img1 + img_at(A.img_rows1, 0, sc.off2);
+            const int s0 = (int)img_at(A.img_rows0, 0, sc.off), s1 = (int)img_at(A.img_rows1, 0, sc.off);
+            const int t0 = (int)img_at(A.img_rows0, 0, sc.off2), t1 = (int)img_at(A.img_rows1, 0, sc.off2);
 #pragma unroll
             for (int u = 0; u < FP; ++u) {
                 und[u] = false;
@@ -844,8 +875,8 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                     uint2 va[FP], vb[FP];
 #pragma unroll
                     for (int u = 0; u < FP; ++u) {
-                        va[u] = *reinterpret_cast<const uint2 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
-                        vb[u] = *reinterpret_cast<const uint2 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
+                        va[u] = BUF ? buf8(r0, ox[u], s0) : *reinterpret_cast<const uint2 *>(b0 + ox[u]);
+                        vb[u] = BUF ? buf8(r1, oy[u], s1) : *reinterpret_cast<const uint2 *>(b1 + oy[u]);
                     }
 #pragma unroll
                     for (int u = 0; u < FP; ++u) und[u] = img_eq(sc, va[u], vb[u], lev[u]) != ST_DONE;
@@ -856,10 +887,16 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                     uint64_t ha[FP], hb[FP];
 #pragma unroll
                     for (int u = 0; u < FP; ++u) {
-                        va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
-                        vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
-                        ha[u] = *reinterpret_cast<const uint64_t *>(A.img0 + img_at(A.img_rows0, x[u], sc.off2));
-                        hb[u] = *reinterpret_cast<const uint64_t *>(A.img1 + img_at(A.img_rows1, y[u], sc.off2));
+                        va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
+                        vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
+                        if (BUF) {
+                            const uint2 a2 = buf8(r0, ox[u], t0), b2 = buf8(r1, oy[u], t1);
+                            ha[u] = ((uint64_t)a2.y << 32) | a2.x;
+                            hb[u] = ((uint64_t)b2.y << 32) | b2.x;
+                        } else {
+                            ha[u] = *reinterpret_cast<const uint64_t *>(h0 + ox[u]);
+                            hb[u] = *reinterpret_cast<const uint64_t *>(h1 + oy[u]);
+                        }
                     }
 #pragma unroll
                     for (int u = 0; u < FP; ++u) und[u] = img_jw(sc, va[u], vb[u], ha[u], hb[u], lev[u]) != ST_DONE;
@@ -869,8 +906,8 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                     uint4 va[FP], vb[FP];
 #pragma unroll
                     for (int u = 0; u < FP; ++u) {
-                        va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
-                        vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
+                        va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
+                        vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
                     }
 #pragma unroll
                     for (int u = 0; u < FP; ++u) und[u] = img_lev(sc, va[u], vb[u], lev[u]) != ST_DONE;
@@ -880,8 +917,8 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                     uint4 va[FP], vb[FP];
 #pragma unroll
                     for (int u = 0; u < FP; ++u) {
-                        va[u] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], sc.off));
-                        vb[u] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], sc.off));
+                        va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
+                        vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
                     }
 #pragma unroll
                     for (int u = 0; u < FP; ++u)
@@ -891,13 +928,15 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                 }
                 case SC_NUMRAW: {  // the columns' own records, by table row
                     const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
-                    for (int u = 0; u < FP; ++u)
-                        lev[u] = simple_num(sc, c0.valid[x[u]] != 0, c0.val[x[u]], c1.valid[y[u]] != 0, c1.val[y[u]]);
+                    for (int u = 0; u < FP; ++u) {
+                        const uint32_t x = ox[u] >> 4, y = oy[u] >> 4;
+                        lev[u] = simple_num(sc, c0.valid[x] != 0, c0.val[x], c1.valid[y] != 0, c1.val[y]);
+                    }
                     break;
                 }
                 default: {  // SC_GEN: the full row records, one pair at a time (few registers)
                     const RecMeta *m0 = A.cols0[sc.col].meta, *m1 = A.cols1[sc.col].meta;
-                    for (int u = 0; u < FP; ++u) und[u] = simple_str(sc, m0[x[u]], m1[y[u]], lev[u]) != ST_DONE;
+                    for (int u = 0; u < FP; ++u) und[u] = simple_str(sc, m0[ox[u] >> 4], m1[oy[u] >> 4], lev[u]) != ST_DONE;
                 }
             }
 #pragma unroll
@@ -2168,15 +2207,19 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 GammaArgs B = LA;
                 B.region_base = (int)r_lo;
                 const unsigned g = (unsigned)(r_hi - r_lo);
-                switch (ctx->filter_waves) {  // (waves per SIMD the filter is compiled for, pairs per lane)
-                    case 1: k_gamma_simple<1, 4><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 2: k_gamma_simple<6, 4><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 3: k_gamma_simple<5, 4><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 4: k_gamma_simple<8, 2><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 5: k_gamma_simple<5, 3><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                // buffer-descriptor gathers while every chunk plane fits the 31-bit descriptor range
+                const bool buf = std::max(B.img_rows0, B.img_rows1) * B.img_stride < (int64_t)INT32_MAX;
+                switch (buf ? ctx->filter_waves : -1) {  // (waves per SIMD the filter is compiled for, pairs per lane)
+                    case -1: k_gamma_simple<6, 3, false><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 1: k_gamma_simple<1, 4, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 2: k_gamma_simple<6, 4, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 3: k_gamma_simple<5, 4, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 4: k_gamma_simple<8, 2, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 5: k_gamma_simple<5, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 6: k_gamma_simple<6, 3, false><<<g, F_THREADS, 0, ctx->stream>>>(B); break;  // A/B: flat loads
                     // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
                     // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
-                    default: k_gamma_simple<6, 3><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    default: k_gamma_simple<6, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
                 }
             };
             launch(A, 0, va);
@@ -2476,7 +2519,7 @@ extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     on %= 10;
     ctx->simple_columns = on != 0;
     ctx->row_filter = on == 2;
-    ctx->filter_waves = on >= 3 ? on - 2 : 0;  // A/B variants of the filter (tools/ab_gamma.py)
+    ctx->filter_waves = on >= 3 ? on - 2 : 0;  // A/B variants of the filter (tools/ab_gamma.py; 8 = flat loads)
     return SPK_OK;
 }
 
