@@ -312,8 +312,10 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
     SPK_TRY(c->meta.alloc((size_t)n + 1));
     SPK_TRY(c->planes.alloc((size_t)(n + 1) * N_PLANES));
     // two-word planes only for columns that can have rows of more than 64 units (> 64 bytes)
-    bool long_rows = false;
-    for (int64_t i = 0; i < n && !long_rows; ++i) long_rows = offsets[i + 1] - offsets[i] > 64;
+    int64_t max_bytes = 0;
+    for (int64_t i = 0; i < n; ++i) max_bytes = std::max<int64_t>(max_bytes, offsets[i + 1] - offsets[i]);
+    c->max_bytes = max_bytes;
+    const bool long_rows = max_bytes > 64;
     if (long_rows) SPK_TRY(c->planes_hi.alloc((size_t)(n + 1) * N_PLANES));
     else c->planes_hi.release();
     DevBuf<int64_t> d_off8, d_ids;

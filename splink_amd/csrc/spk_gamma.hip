@@ -35,7 +35,7 @@ constexpr int F_THREADS = 256;  // filter pass
 constexpr int X_THREADS = 256;  // exact pass
 constexpr int U_THREADS = 128;  // UDF kernel: 2 x 64 x 128 x 2 B = 32 KiB of LDS per block
 
-enum Mode { M_FILTER = 0, M_EXACT = 1, M_SLOW = 2 };
+enum Mode { M_FILTER = 0, M_EXACT = 1, M_SLOW = 2, M_HUGE = 3 };
 enum Status { ST_DONE = 0, ST_UNDECIDED = 1, ST_NEEDS_SLOW = 2 };
 
 // A "simple" comparison column: the shape every case_statements.py template has --
@@ -141,7 +141,7 @@ struct GammaArgs {
     int n_regions;
     int32_t *slow;             // slow-pass lists, column k at slow_off[k]
     const int64_t *slow_off;
-    unsigned int *slow_count;  // [K]
+    unsigned int *slow_count;  // [3K]: slow lists, k_gamma_slow_lev's rest lists, huge lists
     int *err;
     const SimpleCol *simple;   // filter pass: simple columns ...
     int n_simple;
@@ -353,7 +353,7 @@ struct Memo {
 // One WHEN predicate.  Sets *slow when the exact pass needs the global-memory pass.
 template <int MODE>
 __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, int32_t y, uint16_t *slot_a,
-                         uint16_t *slot_b, Memo &mm, bool *slow) {
+                         uint16_t *slot_b, Memo &mm, bool *slow, const Scratch &S) {
     uint32_t st = 0;  // stack of truth values, 2 bits per entry
     for (int k = 0; k < count; ++k) {
         const spk_instr in = A.instr[first + k];
@@ -434,8 +434,10 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
                             r = decide(0.0, hi + 1e-12, in.cmp, in.t);  // margin >> rounding of either side
                             break;
                         }
+                    } else if (MODE == M_HUGE) {
+                        v = jw_long(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n, S.at<uint64_t>(0), S.at<uint64_t>(S.words));
                     } else if (MODE == M_SLOW) {
-                        if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) { atomicOr(A.err, 1); v = 0.0; }
+                        if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) { *slow = true; return KN; }  // huge pass
                         else if (a.n <= 64 && b.n <= 64) v = jw_small(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n);
                         else v = jw_long(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n);
                     } else {
@@ -465,8 +467,10 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
                         if (in.op == SPK_OP_LEV) r = decide((double)lo, (double)hi, in.cmp, in.t);
                         else r = decide((double)lo / den, (double)hi / den, in.cmp, in.t);
                         break;
+                    } else if (MODE == M_HUGE) {
+                        v = lev_long(a, b, S.at<uint32_t>(0), S.at<int32_t>(S.units));
                     } else if (MODE == M_SLOW) {
-                        if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) { atomicOr(A.err, 1); v = 0; }
+                        if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) { *slow = true; return KN; }  // huge pass
                         else v = lev_long(a, b);
                     } else {
                         if (a.n > 64 || b.n > 64 || a.ncp != a.n || b.ncp != b.n) { *slow = true; return KN; }
@@ -487,13 +491,13 @@ __device__ int eval_pred(const GammaArgs &A, int first, int count, int32_t x, in
 
 template <int MODE>
 __device__ int eval_column(const GammaArgs &A, int k, int32_t x, int32_t y, uint16_t *slot_a, uint16_t *slot_b,
-                           int &level) {
+                           int &level, const Scratch &S = Scratch{}) {
     const spk_column_program prog = A.progs[k];
     Memo mm{-1, -1, 0.0, 0, -1, -1};
     for (int w = 0; w < prog.n_when; ++w) {
         const int wi = prog.first_when + w;
         bool slow = false;
-        const int r = eval_pred<MODE>(A, A.when_first[wi], A.when_n[wi], x, y, slot_a, slot_b, mm, &slow);
+        const int r = eval_pred<MODE>(A, A.when_first[wi], A.when_n[wi], x, y, slot_a, slot_b, mm, &slow, S);
         if (slow) return ST_NEEDS_SLOW;
         if (r == KU) return ST_UNDECIDED;
         if (r == KT) {
@@ -1544,14 +1548,30 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
     }
 }
 
-// Global-memory pass over column k's slow list (length on the device; usually empty).
-__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k) {
+// Global-memory pass over column k's slow list (length on the device; usually empty).  Cells with a
+// string past SLOW_LIMIT units go on to the huge pass: their list (counter slow_count[2K + k]) takes
+// column k's exact-list region, free once the exact pass ran and at least as long as the slow list.
+__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k, int32_t *xlist, const int64_t *xinfo) {
     const int64_t n = A.slow_count[k];
     const int32_t *items = A.slow + A.slow_off[k];
+    int32_t *huge = xlist + xinfo[k];
     for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 64) {
         const int32_t p = items[i];
         int level = 0;
-        eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level);
+        const bool done = eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level) == ST_DONE;
+        if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        wave_append(huge, A.slow_count + 2 * A.K + k, !done, p);
+    }
+}
+
+// Huge pass: cells with a string longer than SLOW_LIMIT units, one lane per cell, DP rows and flag
+// words in device scratch sized by the host to the longest string the column's program can meet.
+__global__ __launch_bounds__(64) void k_gamma_huge(GammaArgs A, int k, const int32_t *items, int64_t n, Scratch S) {
+    S.slot = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    for (int64_t i = S.slot; i < n; i += S.n_slots) {
+        const int32_t p = items[i];
+        int level = 0;
+        eval_column<M_HUGE>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level, S);
         code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
     }
 }
@@ -1656,15 +1676,18 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int s
     }
 }
 
-// The rest list of k_gamma_slow_lev through the global-memory evaluation.
+// The rest list of k_gamma_slow_lev through the global-memory evaluation; cells past SLOW_LIMIT
+// units go to the huge list, in column k's slow-list region (free once k_gamma_slow_lev ran).
 __global__ __launch_bounds__(64) void k_gamma_rest(GammaArgs A, int k, const int32_t *xlist, const int64_t *xinfo) {
     const int64_t n = A.slow_count[A.K + k];
     const int32_t *items = xlist + xinfo[k];
+    int32_t *huge = A.slow + A.slow_off[k];
     for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 64) {
         const int32_t p = items[i];
         int level = 0;
-        eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level);
-        code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        const bool done = eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level) == ST_DONE;
+        if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        wave_append(huge, A.slow_count + 2 * A.K + k, !done, p);
     }
 }
 
@@ -1990,6 +2013,21 @@ static bool classify_simple(int k, const spk_column_program &prog, const int32_t
     return true;
 }
 
+// Device scratch of a huge pass over `cells` cells whose strings have at most `units` UTF-16 units: a
+// slot per lane (JW: two flag-word arrays; Levenshtein: code points + one DP row), lanes = one per
+// cell, at most ~1 GiB of slots, at least one wave.
+static int huge_scratch(int64_t units, int64_t cells, DevBuf<uint8_t> &buf, Scratch &S) {
+    SPK_REQUIRE(units < INT32_MAX / 2, SPK_E_LIMIT, "a compared string is longer than 2^30 UTF-16 units");
+    S.units = (int32_t)units;
+    S.words = (int32_t)((units + 63) / 64);
+    const int64_t slot_bytes = std::max<int64_t>(16 * (int64_t)S.words, 4 * (2 * units + 1));
+    const int64_t budget = std::max<int64_t>(64, ((int64_t)1 << 30) / slot_bytes / 64 * 64);
+    S.n_slots = std::min<int64_t>(budget, (cells + 63) / 64 * 64);
+    SPK_TRY(buf.alloc((size_t)(S.n_slots * slot_bytes)));
+    S.base = buf.p;
+    return SPK_OK;
+}
+
 extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *cols, int n_when,
                           const int32_t *when_first_instr, const int32_t *when_n_instr, const int32_t *when_level,
                           int n_instr, const spk_instr *instr, int n_operands, const spk_operand *operands, int n_lits,
@@ -2121,7 +2159,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_REQUIRE(P <= (int64_t)INT32_MAX, SPK_E_LIMIT,
                 "spk_gammas: more than 2^31-1 pairs in one context (shard the pair set over more ranks)");
     SPK_TRY(ctx->work.alloc((size_t)K * (size_t)P + 1));
-    SPK_TRY(ctx->work_count.alloc((size_t)(2 * K)));  // slow-list lengths, then k_gamma_slow_lev's rest lists
+    SPK_TRY(ctx->work_count.alloc((size_t)(3 * K)));  // slow-list lengths, k_gamma_slow_lev's rest lists, huge lists
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
     // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
     // 20 regions (256-thread workgroups) per CU: four rounds of the 5 resident workgroups a CU holds
@@ -2132,7 +2170,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     const int64_t region_len = ((P + n_regions - 1) / n_regions + 63) / 64 * 64;
     SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions));
     SPK_HIP(hipMemsetAsync(ctx->region_count.p, 0, sizeof(unsigned int) * K * n_regions, ctx->stream));
-    SPK_HIP(hipMemsetAsync(ctx->work_count.p, 0, sizeof(unsigned int) * 2 * K, ctx->stream));
+    SPK_HIP(hipMemsetAsync(ctx->work_count.p, 0, sizeof(unsigned int) * 3 * K, ctx->stream));
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -2250,9 +2288,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     const int n_info = 2 * K + 2;
     SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions + 1)));
     SPK_TRY(ctx->xinfo.alloc((size_t)n_info));
-    SPK_TRY(ctx->pinned_info((size_t)n_info + K + 1));  // + slow counts (uint32) + err word
+    SPK_TRY(ctx->pinned_info((size_t)n_info + 2 * K + 1));  // + slow / rest / huge counts (3K uint32) + err word
     int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(P, 1 << 16));
     const int64_t g_exact = std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ctx->n_cu, (P + X_THREADS - 1) / X_THREADS));
+    std::vector<char> huge_in_slow(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
     for (int attempt = 0; attempt < 2; ++attempt) {
         SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));
         A.slow = ctx->xlist.p + cap;
@@ -2301,12 +2340,13 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 } else if (!fused) {
                     k_gamma_exact<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
                 }
+                huge_in_slow[k] = lev ? 1 : 0;
                 if (lev) {
                     k_gamma_slow_lev<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], ctx->xlist.p,
                                                                                          ctx->xinfo.p);
                     k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
                 } else
-                    k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k);
+                    k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
             }
             SPK_HIP(hipGetLastError());
         } else {
@@ -2314,9 +2354,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         }
         SPK_TRY(ctx->end(K_GAMMA));
         SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_info * 8, hipMemcpyDeviceToHost, ctx->stream));
-        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info, ctx->work_count.p, sizeof(unsigned int) * K, hipMemcpyDeviceToHost,
-                               ctx->stream));
-        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info + K, A.err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info, ctx->work_count.p, sizeof(unsigned int) * 3 * K,
+                               hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info + 2 * K, A.err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         SPK_HIP(hipStreamSynchronize(ctx->stream));
         if (!ctx->h_info[2 * K]) break;
         cap = ctx->h_info[2 * K + 1];  // exact lists did not fit: nothing ran, grow and redo the phase
@@ -2331,9 +2371,36 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         n_slow += h_slow[k];
     }
     int err = 0;
-    std::memcpy(&err, ctx->h_info + n_info + K, sizeof(err));
-    SPK_REQUIRE(!(err & 1), SPK_E_LIMIT, "spk_gammas: a compared string exceeds 1024 UTF-16 units");
+    std::memcpy(&err, ctx->h_info + n_info + 2 * K, sizeof(err));
     SPK_REQUIRE(!(err & 2), SPK_E_INVALID, "spk_gammas: unknown instruction");
+    // ---- huge pass: cells with a string longer than SLOW_LIMIT units (none in the benchmark configs)
+    int64_t n_huge = 0, max_huge = 0;
+    for (int k = 0; k < K; ++k) {
+        n_huge += h_slow[2 * K + k];
+        max_huge = std::max<int64_t>(max_huge, h_slow[2 * K + k]);
+    }
+    if (n_huge) {
+        // every string a program can meet is a row of a loaded string column (UTF-8 bytes bound its
+        // UTF-16 units), a substring of one, or a literal
+        int64_t units = 1;
+        for (const Table *t : {&t0, &t1})
+            for (const Column *c : t->cols)
+                if (c && c->kind == COL_STR) units = std::max<int64_t>(units, c->max_bytes);
+        for (int i = 0; i < n_lits; ++i) units = std::max<int64_t>(units, llen[i]);
+        Scratch S;
+        DevBuf<uint8_t> scratch;
+        SPK_TRY(huge_scratch(units, max_huge, scratch, S));
+        SPK_TRY(ctx->begin(K_GAMMA));
+        for (int k = 0; k < K; ++k) {
+            const int64_t nk = h_slow[2 * K + k];
+            if (!nk) continue;
+            const int32_t *items = (huge_in_slow[k] ? A.slow : ctx->xlist.p) + ctx->h_info[k];  // + xinfo[k]
+            k_gamma_huge<<<(unsigned)(S.n_slots / 64), 64, 0, ctx->stream>>>(A, k, items, nk, S);
+            SPK_HIP(hipGetLastError());
+        }
+        SPK_TRY(ctx->end(K_GAMMA));
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+    }
     ctx->codes_valid = true;
     ctx->mpat_valid = false;
     ctx->last_deferred = n_slow;
@@ -2391,7 +2458,8 @@ extern "C" int spk_gammas_copy(spk_ctx *ctx, int64_t start, int64_t count, int8_
 
 // ---- the jar's UDFs as bulk device functions (JaroWinklerSimilarity.call, Spark levenshtein) -----
 // Same device code as the comparison passes: LDS-staged jw_small / lev_myers for short strings,
-// the global-memory jw_long / lev_long for the rest.
+// the global-memory jw_long / lev_long for the rest, and pairs with a string past SLOW_LIMIT units
+// through the huge pass (device scratch sized to the longest string).
 struct UdfArgs {
     int64_t n;
     const uint16_t *u16;
@@ -2399,8 +2467,13 @@ struct UdfArgs {
     const int32_t *cp;   // code points per string
     int op;              // 0 JW, 1 Levenshtein
     double *out;
-    int *err;
+    int32_t *huge;              // pairs for k_udf_huge
+    unsigned int *n_huge;
 };
+
+__device__ inline StrView udf_view(const UdfArgs &U, int64_t s) {
+    return plain_view(U.u16 + U.off[s], (int32_t)(U.off[s + 1] - U.off[s]), U.cp[s]);
+}
 
 __global__ __launch_bounds__(U_THREADS) void k_udf(UdfArgs U) {
     __shared__ uint16_t lds[2][MAXU][U_THREADS];
@@ -2408,12 +2481,9 @@ __global__ __launch_bounds__(U_THREADS) void k_udf(UdfArgs U) {
     uint16_t *slot_b = &lds[1][0][threadIdx.x];
     int64_t p = (int64_t)blockIdx.x * U_THREADS + threadIdx.x;
     if (p >= U.n) return;
-    const StrView a = plain_view(U.u16 + U.off[2 * p], (int32_t)(U.off[2 * p + 1] - U.off[2 * p]), U.cp[2 * p]);
-    const StrView b =
-        plain_view(U.u16 + U.off[2 * p + 1], (int32_t)(U.off[2 * p + 2] - U.off[2 * p + 1]), U.cp[2 * p + 1]);
+    const StrView a = udf_view(U, 2 * p), b = udf_view(U, 2 * p + 1);
     if (a.n > SLOW_LIMIT || b.n > SLOW_LIMIT) {
-        atomicOr(U.err, 1);
-        U.out[p] = NAN;
+        U.huge[atomicAdd(U.n_huge, 1u)] = (int32_t)p;
         return;
     }
     if (U.op == 0) {
@@ -2436,6 +2506,16 @@ __global__ __launch_bounds__(U_THREADS) void k_udf(UdfArgs U) {
             v = lev_long(a, b);
         }
         U.out[p] = (double)v;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_udf_huge(UdfArgs U, int64_t n, Scratch S) {
+    S.slot = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    for (int64_t i = S.slot; i < n; i += S.n_slots) {
+        const int64_t p = U.huge[i];
+        const StrView a = udf_view(U, 2 * p), b = udf_view(U, 2 * p + 1);
+        U.out[p] = U.op == 0 ? jw_long(GlbAcc{a.p}, a.n, GlbAcc{b.p}, b.n, S.at<uint64_t>(0), S.at<uint64_t>(S.words))
+                             : (double)lev_long(a, b, S.at<uint32_t>(0), S.at<int32_t>(S.units));
     }
 }
 
@@ -2462,26 +2542,36 @@ static int run_udf(spk_ctx *ctx, int op, int64_t n, const int64_t *l_off, const 
     DevBuf<int64_t> d_off;
     DevBuf<int32_t> d_cp;
     DevBuf<double> d_out;
-    DevBuf<int> d_err;
+    DevBuf<int32_t> d_huge;
+    DevBuf<unsigned int> d_nhuge;
     SPK_TRY(d_u.alloc(u.size()));
     SPK_TRY(d_off.alloc(off.size()));
     SPK_TRY(d_cp.alloc(cp.size() + 1));
     SPK_TRY(d_out.alloc((size_t)n + 1));
-    SPK_TRY(d_err.alloc(1));
-    SPK_HIP(hipMemsetAsync(d_err.p, 0, sizeof(int), ctx->stream));  // hipMalloc does not zero
+    SPK_TRY(d_huge.alloc((size_t)n + 1));
+    SPK_TRY(d_nhuge.alloc(1));
+    SPK_HIP(hipMemsetAsync(d_nhuge.p, 0, sizeof(unsigned int), ctx->stream));  // hipMalloc does not zero
     SPK_HIP(hipMemcpyAsync(d_u.p, u.data(), u.size() * 2, hipMemcpyHostToDevice, ctx->stream));
     SPK_HIP(hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     if (!cp.empty()) SPK_HIP(hipMemcpyAsync(d_cp.p, cp.data(), cp.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    if (n) {
-        UdfArgs U{n, d_u.p, d_off.p, d_cp.p, op, d_out.p, d_err.p};
-        k_udf<<<(unsigned)((n + U_THREADS - 1) / U_THREADS), U_THREADS, 0, ctx->stream>>>(U);
-        SPK_HIP(hipGetLastError());
-        SPK_HIP(hipMemcpyAsync(out, d_out.p, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    int err = 0;
-    SPK_HIP(hipMemcpyAsync(&err, d_err.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (!n) return SPK_OK;
+    UdfArgs U{n, d_u.p, d_off.p, d_cp.p, op, d_out.p, d_huge.p, d_nhuge.p};
+    k_udf<<<(unsigned)((n + U_THREADS - 1) / U_THREADS), U_THREADS, 0, ctx->stream>>>(U);
+    SPK_HIP(hipGetLastError());
+    unsigned int n_huge = 0;
+    SPK_HIP(hipMemcpyAsync(&n_huge, d_nhuge.p, sizeof(n_huge), hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
-    SPK_REQUIRE(!err, SPK_E_LIMIT, "spk udf: a string exceeds 1024 UTF-16 units");
+    DevBuf<uint8_t> scratch;
+    if (n_huge) {
+        int64_t units = 1;
+        for (size_t i = 0; i + 1 < off.size(); ++i) units = std::max<int64_t>(units, off[i + 1] - off[i]);
+        Scratch S;
+        SPK_TRY(huge_scratch(units, n_huge, scratch, S));
+        k_udf_huge<<<(unsigned)(S.n_slots / 64), 64, 0, ctx->stream>>>(U, (int64_t)n_huge, S);
+        SPK_HIP(hipGetLastError());
+    }
+    SPK_HIP(hipMemcpyAsync(out, d_out.p, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
     return SPK_OK;
 }
 

@@ -557,6 +557,7 @@ int spk_table_add_raw_utf8(spk_ctx *ctx, int col, int raw0, int raw1) {
         SPK_REQUIRE(nbytes + 3 * n + 16 < ((int64_t)1 << 34), SPK_E_LIMIT,
                     "a string column is limited to 2^34 UTF-16 units (16 GiB of text)");
         const bool long_rows = r->max_len > 64;
+        c->max_bytes = r->max_len;
         SPK_TRY(c->units.alloc((size_t)(nbytes + 3 * n + 16)));
         SPK_TRY(c->meta.alloc((size_t)n + 1));
         SPK_TRY(c->planes.alloc((size_t)(n + 1) * N_PLANES));

@@ -141,6 +141,7 @@ struct Column {
     DevBuf<double> val;
     DevBuf<uint8_t> valid;
     bool has_ids = false;  // COL_STR: RecMeta.key is a dictionary id
+    int64_t max_bytes = 0; // COL_STR: longest row in UTF-8 bytes (>= its UTF-16 units)
 };
 
 // An input column as handed over (Arrow buffers), kept on the device in input row order: the source

@@ -14,7 +14,8 @@
 namespace spk {
 
 constexpr int MAXU = 64;          // LDS staging capacity per string (UTF-16 units), exact pass
-constexpr int SLOW_LIMIT = 1024;  // global-memory pass capacity per string
+constexpr int SLOW_LIMIT = 1024;  // slow pass: per-lane scratch arrays up to this many units per string;
+                                  // longer strings go to the huge pass (device scratch sized to the data)
 
 struct StrView {
     const uint16_t *p = nullptr;
@@ -46,6 +47,29 @@ struct LdsAcc {
 struct GlbAcc {
     const uint16_t *p;
     __device__ uint16_t operator[](int i) const { return p[i]; }
+};
+
+// Element i of one lane's array in a device scratch buffer shared by `s` lanes, interleaved so that
+// lanes stepping through the same index touch consecutive words.
+template <typename T>
+struct Strided {
+    T *p;
+    int64_t s;
+    __device__ T &operator[](int i) const { return p[(int64_t)i * s]; }
+};
+
+// Device scratch of the huge pass (strings longer than SLOW_LIMIT units): n_slots lanes, lane `slot`
+// owns elements slot, slot + n_slots, ... of each typed view of `base`.  `units` bounds every string
+// the pass can meet (the longest row of any string column, in UTF-8 bytes >= UTF-16 units, and the
+// longest literal); `words` = ceil(units / 64).
+struct Scratch {
+    uint8_t *base = nullptr;
+    int64_t n_slots = 0, slot = 0;
+    int32_t units = 0, words = 0;
+    template <typename T>
+    __device__ Strided<T> at(int64_t elem0) const {
+        return Strided<T>{reinterpret_cast<T *>(base) + elem0 * n_slots + slot, n_slots};
+    }
 };
 
 template <int STRIDE>
@@ -167,15 +191,17 @@ __device__ double jw_small(Acc first, int lf, Acc second, int ls) {
     return jw_finish(m, t, prefix, lf, ls, lmx);
 }
 
-// Same algorithm for any length up to SLOW_LIMIT (flag words in scratch).
-__device__ inline double jw_long(GlbAcc first, int lf, GlbAcc second, int ls) {
+// Same algorithm for any length: flag words in caller storage (a lane's scratch array up to
+// SLOW_LIMIT units, or the huge pass's device scratch); ceil(lmx / 64) + ceil(lmn / 64) words.
+template <class Words>
+__device__ inline double jw_long(GlbAcc first, int lf, GlbAcc second, int ls, Words flags, Words matched) {
     const bool fmax = lf > ls;
     const GlbAcc mx = fmax ? first : second;
     const GlbAcc mn = fmax ? second : first;
     const int lmx = fmax ? lf : ls, lmn = fmax ? ls : lf;
     const int range = lmx / 2 - 1 > 0 ? lmx / 2 - 1 : 0;
-    uint64_t flags[SLOW_LIMIT / 64], matched[SLOW_LIMIT / 64];
-    for (int i = 0; i < SLOW_LIMIT / 64; ++i) flags[i] = matched[i] = 0;
+    for (int i = 0; i < (lmx + 63) / 64; ++i) flags[i] = 0;
+    for (int i = 0; i < (lmn + 63) / 64; ++i) matched[i] = 0;
     int m = 0;
     for (int mi = 0; mi < lmn; ++mi) {
         const uint16_t c = mn[mi];
@@ -206,6 +232,11 @@ __device__ inline double jw_long(GlbAcc first, int lf, GlbAcc second, int ls) {
     return jw_finish(m, t, prefix, lf, ls, lmx);
 }
 
+__device__ inline double jw_long(GlbAcc first, int lf, GlbAcc second, int ls) {  // <= SLOW_LIMIT units
+    uint64_t flags[SLOW_LIMIT / 64], matched[SLOW_LIMIT / 64];
+    return jw_long(first, lf, second, ls, flags, matched);
+}
+
 // ---- Levenshtein (exact) -----------------------------------------------------------------------
 // Myers 1999 bit-parallel, pattern <= 64 symbols.
 template <class Acc>
@@ -233,10 +264,10 @@ __device__ int lev_myers(Acc pat, int m, Acc txt, int n) {
     return dist;
 }
 
-// Code points, any length up to SLOW_LIMIT (two-row DP in scratch).
-__device__ inline int lev_long(const StrView &a, const StrView &b) {
-    uint32_t cb[SLOW_LIMIT];
-    int32_t row[SLOW_LIMIT + 1];
+// Code points, any length: two-row DP with b's code points and the row in caller storage (nb and
+// nb + 1 elements).
+template <class U32, class I32>
+__device__ inline int lev_long(const StrView &a, const StrView &b, U32 cb, I32 row) {
     int nb = 0;
     for (int j = 0; j < b.n; ++j) {
         uint32_t w = b.p[j];
@@ -257,16 +288,24 @@ __device__ inline int lev_long(const StrView &a, const StrView &b) {
         ++i;
         int diag = row[0];
         row[0] = i;
+        int left = i;
         for (int j = 1; j <= nb; ++j) {
-            int up = row[j];
+            const int up = row[j];
             int best = diag + (w != cb[j - 1] ? 1 : 0);
             if (up + 1 < best) best = up + 1;
-            if (row[j - 1] + 1 < best) best = row[j - 1] + 1;
+            if (left + 1 < best) best = left + 1;
             row[j] = best;
+            left = best;
             diag = up;
         }
     }
     return row[nb];
+}
+
+__device__ inline int lev_long(const StrView &a, const StrView &b) {  // <= SLOW_LIMIT units
+    uint32_t cb[SLOW_LIMIT];
+    int32_t row[SLOW_LIMIT + 1];
+    return lev_long(a, b, cb, row);
 }
 
 // ---- bounds for the filter pass ---------------------------------------------------------------

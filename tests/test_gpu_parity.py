@@ -175,6 +175,60 @@ def test_udf_long_and_surrogate_strings(amd):
         assert lev[i] == orc.levenshtein(left[i], right[i])
 
 
+def _long_pairs(seed, lengths, reps):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    alpha = list("abcdefgh") + ["é", "\U0001F600"]
+    left, right = [], []
+    for n in lengths:
+        for r in range(reps):
+            a = "".join(rng.choice(alpha, size=n))
+            b = _mutate(rng, a, int(rng.integers(0, 12)), alpha) if r % 2 == 0 else "".join(rng.choice(alpha, size=n))
+            left.append(a)
+            right.append(b)
+    return left, right
+
+
+def test_strings_past_slow_limit(amd):
+    """Strings longer than the slow pass's 1024-unit scratch arrays (up to 6000 UTF-16 units, with
+    surrogate pairs) go through the huge pass (device scratch sized to the longest row): the bulk UDFs
+    and the comparison levels of template Jaro-Winkler / Levenshtein columns and of a general program
+    agree with the oracle.  Spark compares strings of any length; there is no limit to hit."""
+    from splink_amd import _native as N
+    from splink_amd.gammas import add_gammas
+    left, right = _long_pairs(41, [700, 1023, 1024, 1025, 1600, 3000], 4)
+    left += ["x" * 5000, "ab" * 3000, "short"]
+    right += ["x" * 4990 + "y", "ab" * 2990, "é" * 2000]
+    ctx = N.Context(0)
+    jw, lev = ctx.jaro_winkler_sim(left, right), ctx.levenshtein(left, right)
+    ref_jw = [orc.jaro_winkler(a, b) for a, b in zip(left, right)]
+    ref_lev = [orc.levenshtein(a, b) for a, b in zip(left, right)]
+    for i in range(len(left)):
+        assert jw[i] == ref_jw[i], (len(left[i]), len(right[i]), jw[i], ref_jw[i])
+        assert lev[i] == ref_lev[i], (len(left[i]), len(right[i]))
+    df = pd.DataFrame({"a_l": left + [None], "a_r": right + ["x"]})
+    lev_lv = ("case when a_l is null or a_r is null then -1 "
+              + " ".join(f"when levenshtein(a_l, a_r) <= {d} then {5 - k}" for k, d in enumerate((0, 5, 20, 200, 1000)))
+              + " else 0 end")
+    jw_lv = ("case when a_l is null or a_r is null then -1 when jaro_winkler_sim(a_l, a_r) >= 0.97 then 3 "
+             "when jaro_winkler_sim(a_l, a_r) >= 0.9 then 2 when jaro_winkler_sim(a_l, a_r) >= 0.7 then 1 else 0 end")
+    mixed = ("case when a_l is null or a_r is null then -1 "
+             "when jaro_winkler_sim(a_l, a_r) >= 0.9 and levenshtein(a_l, a_r) <= 300 then 2 "
+             "when length(a_l) > 1024 or levenshtein(a_l, a_r) <= 1000 then 1 else 0 end")
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "lv", "custom_columns_used": ["a"], "num_levels": 6, "case_expression": lev_lv,
+         "m_probabilities": [0.1, 0.1, 0.1, 0.1, 0.2, 0.4], "u_probabilities": [0.5, 0.2, 0.1, 0.1, 0.05, 0.05]},
+        {"custom_name": "jw", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": jw_lv},
+        {"custom_name": "mx", "custom_columns_used": ["a"], "num_levels": 3, "case_expression": mixed}]}
+    got = add_gammas(df, st, amd).gamma_matrix()
+    for i, (a, b) in enumerate(zip(left, right)):
+        d, j = ref_lev[i], ref_jw[i]
+        want_lv = next((5 - k for k, t in enumerate((0, 5, 20, 200, 1000)) if d <= t), 0)
+        want_jw = 3 if j >= 0.97 else 2 if j >= 0.9 else 1 if j >= 0.7 else 0
+        want_mx = 2 if (j >= 0.9 and d <= 300) else 1 if (len(a) > 1024 or d <= 1000) else 0
+        assert list(got[i]) == [want_lv, want_jw, want_mx], (i, len(a), len(b), d, j, list(got[i]))
+    assert list(got[-1]) == [-1, -1, -1]
+
+
 def _synthetic(n, seed, **kw):
     from splink_amd.synthetic import make_records
     return make_records(n, seed=seed, **kw)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
