@@ -503,6 +503,81 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
     return dist > cut ? cut + 1 : dist;
 }
 
+// Patterns of 33..64 units: the upper word starts late (Ukkonen's cutoff).  D[i][j] >= |i - j|, so a
+// cell of a row i >= 33 at text unit j <= 31 - cut is > cut, and a path through it ends > cut.  Rows
+// 1..32 never depend on the rows above them, so the scan runs one 32-bit word (pattern rows 1..32,
+// the score tracked at row 32) up to text unit J0 <= 31 - cut, then takes the rows above as D[32][J0]
+// + (i - 32) (vertical deltas +1, an upper bound of the true values, and > cut where they differ) and
+// continues with 64-bit words.  Every distance <= cut comes out exact and every larger one > cut, as
+// the callers need; the early exit is taken on the computed scores, which obey the same delta
+// bounds.  J0 is the wave's minimum (one switch point for all lanes); lanes with m <= 32 run the
+// same loops with their one word.  cfg2 emails: most waves hold a cell of 33+ units, cut ~ 10.
+__device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
+                                            int cut) {
+    const bool wide = m > 32;
+    const int mine = wide ? (cut < 31 ? 31 - cut : 0) : 32;
+    int lo = 0, hi = 32;  // wave minimum of `mine` (active lanes) by bisection over ballots
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (__ballot(mine <= mid)) hi = mid;
+        else lo = mid + 1;
+    }
+    const int J0 = lo;
+    uint32_t pl[N_PLANES], tw[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) {
+        pl[b] = (uint32_t)P[b];
+        tw[b] = (uint32_t)T[b];
+    }
+    uint32_t vp = ~0u, vn = 0;
+    const int tb = wide ? 31 : m - 1;
+    const uint32_t hib = 1u << tb;
+    int dist = tb + 1;
+    const int j1 = n < J0 ? n : J0;
+    for (int j = 0; j < j1; ++j) {
+        uint32_t eq = ~0u;
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], j, 1), pl[b]);
+        const uint32_t x = eq | vn;
+        const uint32_t d0 = (((x & vp) + vp) ^ vp) | x;
+        uint32_t hp = vn | ~(d0 | vp);
+        const uint32_t hn = d0 & vp;
+        dist += (hp & hib) ? 1 : 0;
+        dist -= (hn & hib) ? 1 : 0;
+        if (!wide && (j & 3) == 3 && dist - (n - 1 - j) > cut) return cut + 1;
+        hp = (hp << 1) | 1u;
+        vp = (hn << 1) | ~(d0 | hp);
+        vn = hp & d0;
+    }
+    if (wide) dist += m - 32;
+    if (n <= J0) return dist > cut ? cut + 1 : dist;
+    uint64_t VP = (uint64_t)vp | 0xFFFFFFFF00000000ull, VN = vn;
+    const uint64_t HIB = 1ull << (m - 1);
+    for (int h = J0 >> 5; h < 2 && 32 * h < n; ++h) {
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
+        const int jb = 32 * h < J0 ? J0 - 32 * h : 0;
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        for (int jj = jb; jj < jn; ++jj) {
+            uint64_t eq = ~0ull;
+#pragma unroll
+            for (int b = 0; b < N_PLANES; ++b)
+                eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), P[b]);
+            const uint64_t x = eq | VN;
+            const uint64_t d0 = (((x & VP) + VP) ^ VP) | x;
+            uint64_t hp = VN | ~(d0 | VP);
+            const uint64_t hn = d0 & VP;
+            dist += (hp & HIB) ? 1 : 0;
+            dist -= (hn & HIB) ? 1 : 0;
+            if ((jj & 3) == 3 && dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
+            hp = (hp << 1) | 1ull;
+            VP = (hn << 1) | ~(d0 | hp);
+            VN = hp & d0;
+        }
+    }
+    return dist > cut ? cut + 1 : dist;
+}
+
 // Code-point Levenshtein of two unequal rows that both carry bit-planes (<= 64 units, all < 256, so
 // units are code points), from the planes alone: the common prefix is the lowest set bit of
 // OR_b(a_b ^ b_b), the common suffix the highest of the same with both strings' ends aligned at bit
@@ -536,7 +611,7 @@ __device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, co
     }
     // one word width for all active lanes: a wave that mixed both would run both loops
     if (!__any(m > 32)) return myers_plane_text<uint32_t>(P, m, T, n, cut);
-    return myers_plane_text<uint64_t>(P, m, T, n, cut);
+    return myers_plane_text_lazy(P, m, T, n, cut);
 }
 
 // ---- rows of 65..128 units (CPF_PLANES2): the same scan over 128-bit plane words ----------------
@@ -626,7 +701,7 @@ __device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, con
             T64[b] = (uint64_t)T[b];
         }
         if (!__any(m > 32)) return myers_plane_text<uint32_t>(P64, m, T64, n, cut);
-        return myers_plane_text<uint64_t>(P64, m, T64, n, cut);
+        return myers_plane_text_lazy(P64, m, T64, n, cut);
     }
     return myers_plane_text128(P, m, T, n, cut);
 }
