@@ -200,6 +200,12 @@ int spk_gammas_deferred(spk_ctx *ctx, int64_t *out);
 /* Per comparison column: pairs the last spk_gammas could not decide from bounds in the filter pass
  * and evaluated with the exact similarity (out[n], n >= number of columns). */
 int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
+/* Per comparison column: pairs of the last spk_gammas whose level the filter took from the blocking
+ * key instead of the rows -- a rule built by spk_key_build whose key includes the plain term
+ * `l.c = r.c` on the raw columns the column was decoded from (spk_table_add_raw_utf8) emits only
+ * pairs with equal, non-NULL values of c (the longest such run of the pair order; 0 when the
+ * column holds an empty string, or was not built from raw columns). */
+int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n);
 /* Columns in the shape of the case_statements.py templates (NULL branch, then single-leaf tests
  * on the same two plain operands) are filtered from a packed per-row image of their fields; every
  * other column by the general interpreter.  on = 1 (default): template columns through the

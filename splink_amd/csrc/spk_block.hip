@@ -473,6 +473,10 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         v.pair_hi = r + 1 < n_rules ? rule_base[r + 1] : n_out;
     }
     ctx->n_views = n_views;
+    ctx->pair_terms.assign(ctx->rule_terms, ctx->rule_terms + n_rules);
+    ctx->pair_rule_lo.assign(rule_base.begin(), rule_base.end());
+    ctx->pair_rule_hi.resize(n_rules);
+    for (int r = 0; r < n_rules; ++r) ctx->pair_rule_hi[r] = r + 1 < n_rules ? rule_base[r + 1] : n_out;
     ctx->n_pairs = n_out;
     ctx->pairs_valid = true;
     ctx->pairs_epoch++;

@@ -278,6 +278,7 @@ int spk_table_create(spk_ctx *ctx, int side, int64_t n_rows, int n_cols) {
     t.rank.release();
     t.perm.release();
     t.null_div = 0;
+    for (auto &v : ctx->rule_terms) v.clear();
     t.n = n_rows;
     t.desc_dirty = true;
     t.version = ++ctx->table_epoch;
@@ -388,6 +389,7 @@ int spk_table_set_key(spk_ctx *ctx, int side, int rule, int which, const int64_t
         SPK_REQUIRE(keys[i] >= -1 && keys[i] < (int64_t)INT32_MAX, SPK_E_LIMIT, "key ids must be in [-1, 2^31)");
     while ((int)t.key[which].size() <= rule) t.key[which].push_back(new DevBuf<int64_t>());
     SPK_TRY(t.key[which][rule]->alloc((size_t)t.n + 1));
+    if (rule < 32) ctx->rule_terms[rule].clear();  // a host-computed key: no term is known
     if (t.n)
         SPK_HIP(hipMemcpyAsync(t.key[which][rule]->p, keys, (size_t)t.n * sizeof(int64_t), hipMemcpyHostToDevice,
                                ctx->stream));
@@ -433,6 +435,9 @@ int spk_pairs_load(spk_ctx *ctx, int64_t n, const int32_t *rows_l, const int32_t
     ctx->pairs_epoch++;
     ctx->n_views = 0;
     ctx->pv_base = n;
+    ctx->pair_terms.clear();
+    ctx->pair_rule_lo.clear();
+    ctx->pair_rule_hi.clear();
     ctx->codes_valid = false;
     return SPK_OK;
 }

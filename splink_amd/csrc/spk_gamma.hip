@@ -69,6 +69,11 @@ struct SimpleCol {
     int32_t tflag[MAX_TESTS];  // TF_* bits
     int32_t lev_a[MAX_TESTS];  // LEV (absolute): integer bound of the equivalent integer test
     float jw_cf[MAX_TESTS];    // JW: an upper bound hi < jw_cf proves the test false
+    // Pairs [imp_lo, imp_hi) come from a blocking rule whose key includes `l.c = r.c` on this
+    // column's own raw columns: their strings are equal, non-NULL (and non-empty: no empty value
+    // in the column), so their level is eq_level and the filter reads nothing for them.
+    int64_t imp_lo, imp_hi;
+    int32_t eq_level;
 };
 constexpr int32_t TF_ZERO = 1;     // the value 0.0 passes the test (JW of strings without a common unit; lev ratio 0)
 constexpr int32_t TF_ONE = 2;      // JW: the value 1.0 passes (equal non-empty strings)
@@ -206,7 +211,8 @@ __device__ inline int k_not(int a) { return (a == KN || a == KU) ? a : (a == KT 
 // state stays in integer registers (VALU bit ops) instead of per-lane condition masks, and the
 // lanes of a wave never diverge over which test decided them.
 struct Chain {
-    int open = 1, und = 0, lvl;
+    int open = 1, und = 0, lvl = 0;
+    Chain() = default;
     __device__ explicit Chain(int else_level) : lvl(else_level) {}
     __device__ __attribute__((always_inline)) void fold(int r, int lvl_i) {
         const int hit = r & open;  // bit 0: TRUE / UNDECIDED while open
@@ -686,15 +692,32 @@ __device__ __attribute__((always_inline)) inline int sketch_inter_ub_bf(uint64_t
     return inter < lmn ? inter : lmn;
 }
 
+// The image tests of FP pairs at once: each pair's bounds first, then the column's tests in order
+// with every test's parameters read once for all FP pairs (scalar loads outside the pair loop).
+// und[u]: pair u needs the exact pass; level[u]: its level otherwise.
+
 // `=` / `<>` tests.  Equal keys prove equality with dictionary ids; without them only the units can tell.
-template <class SC>
-__device__ inline int img_eq(const SC &sc, uint2 a, uint2 b, int &level) {
-    const bool nul = a.y == LENS_NULL || b.y == LENS_NULL;
-    const int same = (a.x == b.x) & (a.y == b.y);
-    Chain c(sc.else_level);
-    for (int i = 0; i < sc.n_tests; ++i) c.fold(same ^ ((sc.tflag[i] & TF_EQ) ? 0 : 1), sc.level[i]);
-    level = nul ? sc.null_level : c.lvl;
-    return (!nul && same && !sc.has_ids) ? ST_UNDECIDED : ST_DONE;
+template <int FP, class SC>
+__device__ __attribute__((always_inline)) inline void img_eq(const SC &sc, const uint2 (&a)[FP], const uint2 (&b)[FP],
+                                                             int (&level)[FP], bool (&und)[FP]) {
+    int same[FP];
+    Chain c[FP];
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        same[u] = (a[u].x == b[u].x) & (a[u].y == b[u].y);
+        c[u] = Chain(sc.else_level);
+    }
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int f = (sc.tflag[i] & TF_EQ) ? 0 : 1, lv = sc.level[i];
+#pragma unroll
+        for (int u = 0; u < FP; ++u) c[u].fold(same[u] ^ f, lv);
+    }
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        const bool nul = a[u].y == LENS_NULL || b[u].y == LENS_NULL;
+        level[u] = nul ? sc.null_level : c[u].lvl;
+        und[u] = !nul && same[u] && !sc.has_ids;
+    }
 }
 
 // jaro_winkler_sim(l, r) > / >= t tests.  Equal strings and strings without a common unit have
@@ -704,79 +727,134 @@ __device__ inline int img_eq(const SC &sc, uint2 a, uint2 b, int &level) {
 // float thresholds jw_cf are the doubles' exact float images (prepare_tests).  The bound is only
 // computed when some lane of the wave needs it (in the first rule's blocks every pair shares
 // the blocking key, so a wave of such pairs skips it for that column).
-template <class SC>
-__device__ inline int img_jw(const SC &sc, uint4 a, uint4 b, uint64_t ha, uint64_t hb, int &level) {
-    const bool nul = a.y == LENS_NULL || b.y == LENS_NULL;
-    const bool same = a.x == b.x && a.y == b.y;
-    const int lf = lens_u16(a.y), ls = lens_u16(b.y);
-    const bool und0 = (same && !sc.has_ids) || lf >= LEN_SAT || ls >= LEN_SAT;
-    const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
-    bool exact = same || lmn == 0;
-    float hi = 0.f;
-    if (__ballot(!exact) != 0ull) {  // wave-uniform
-        const int M = sketch_inter_ub_bf(img_sketch(a), img_sketch(b), lf, ls);
-        exact = exact || M == 0;
-        // v_rcp_f32 (1 ulp) instead of IEEE divisions: the error (< 1e-6 on j) sits far inside the
-        // 1e-5 margin, so hi stays an upper bound (the exact cases never read it)
-        const float j = ((float)M * (float)(lf + ls) * __builtin_amdgcn_rcpf((float)lf * (float)ls) + 1.0f) *
-                        (1.0f / 3.0f);
-        const uint64_t d = ha ^ hb;
-        const int cp = d ? (__ffsll((unsigned long long)d) - 1) >> 4 : 4;
-        const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
-        const float pw = (lmx > 10 ? __builtin_amdgcn_rcpf((float)lmx) : 0.1f) * (float)prefix;
-        hi = (j >= 0.7f - 1e-4f ? j + pw * (1.0f - j) : j) + 1e-5f;
+template <int FP, class SC>
+__device__ __attribute__((always_inline)) inline void img_jw(const SC &sc, const uint4 (&a)[FP], const uint4 (&b)[FP],
+                                                             const uint64_t (&ha)[FP], const uint64_t (&hb)[FP],
+                                                             int (&level)[FP], bool (&und)[FP]) {
+    bool exact[FP], one[FP], und0[FP];
+    float hi[FP];
+    bool need = false;
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        const bool same = a[u].x == b[u].x && a[u].y == b[u].y;
+        const int lf = lens_u16(a[u].y), ls = lens_u16(b[u].y);
+        und0[u] = (same && !sc.has_ids) || lf >= LEN_SAT || ls >= LEN_SAT;
+        exact[u] = same || (lf < ls ? lf : ls) == 0;
+        one[u] = same && lf > 0;
+        hi[u] = 0.f;
+        need = need || !exact[u];
     }
-    const bool one = same && lf > 0;
-    Chain c(sc.else_level);
+    if (__ballot(need) != 0ull) {  // wave-uniform
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            const int lf = lens_u16(a[u].y), ls = lens_u16(b[u].y);
+            const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
+            const int M = sketch_inter_ub_bf(img_sketch(a[u]), img_sketch(b[u]), lf, ls);
+            exact[u] = exact[u] || M == 0;
+            // v_rcp_f32 (1 ulp) instead of IEEE divisions: the error (< 1e-6 on j) sits far inside the
+            // 1e-5 margin, so hi stays an upper bound (the exact cases never read it)
+            const float j = ((float)M * (float)(lf + ls) * __builtin_amdgcn_rcpf((float)lf * (float)ls) + 1.0f) *
+                            (1.0f / 3.0f);
+            const uint64_t d = ha[u] ^ hb[u];
+            const int cp = d ? (__ffsll((unsigned long long)d) - 1) >> 4 : 4;
+            const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
+            const float pw = (lmx > 10 ? __builtin_amdgcn_rcpf((float)lmx) : 0.1f) * (float)prefix;
+            hi[u] = (j >= 0.7f - 1e-4f ? j + pw * (1.0f - j) : j) + 1e-5f;
+        }
+    }
+    Chain c[FP];
+#pragma unroll
+    for (int u = 0; u < FP; ++u) c[u] = Chain(sc.else_level);
     for (int i = 0; i < sc.n_tests; ++i) {
-        const int f = sc.tflag[i];
-        const int r_exact = one ? ((f >> 1) & 1) : (f & TF_ZERO);   // TF_ONE / TF_ZERO -> KT / KF
-        const int r_bound = hi < sc.jw_cf[i] ? KF : ((f & TF_ZERO) ? KT : KU);
-        c.fold(exact ? r_exact : r_bound, sc.level[i]);
+        const int f = sc.tflag[i], lv = sc.level[i];
+        const float cf = sc.jw_cf[i];
+        const int r_one = (f >> 1) & 1, r_zero = f & TF_ZERO, r_pass = (f & TF_ZERO) ? KT : KU;  // TF_ONE / TF_ZERO -> KT / KF
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            const int r_exact = one[u] ? r_one : r_zero;
+            const int r_bound = hi[u] < cf ? KF : r_pass;
+            c[u].fold(exact[u] ? r_exact : r_bound, lv);
+        }
     }
-    level = nul ? sc.null_level : c.lvl;
-    return (!nul && (und0 || c.und)) ? ST_UNDECIDED : ST_DONE;
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        const bool nul = a[u].y == LENS_NULL || b[u].y == LENS_NULL;
+        level[u] = nul ? sc.null_level : c[u].lvl;
+        und[u] = !nul && (und0[u] || c[u].und);
+    }
 }
 
 // `=` / `<>` and levenshtein [ratio] tests: the distance lies in [max(length gap, bag distance),
 // max(length)].  Absolute tests compare integer bounds (lev_a); the ratio test `lev / den <= t`
 // (or `<`) is decided against t * den with one part in 1e12 of margin instead of a division per
 // pair; exact ties are left to the exact pass.
-template <class SC>
-__device__ inline int img_lev(const SC &sc, uint4 a, uint4 b, int &level) {
-    const bool nul = a.y == LENS_NULL || b.y == LENS_NULL;
-    const bool same = a.x == b.x && a.y == b.y;
-    const int la = lens_u16(a.y), lb = lens_u16(b.y), na = lens_cp(a.y), nb = lens_cp(b.y);
-    const bool und0 = (same && !sc.has_ids) || la >= LEN_SAT || lb >= LEN_SAT || na >= LEN_SAT || nb >= LEN_SAT;
-    const int gap = na > nb ? na - nb : nb - na, mx = na > nb ? na : nb;
-    // BMP rows: units are code points, so the bag bound holds
-    const bool bmp = na == la && nb == lb && !same;
-    int bag = 0;
-    if (__ballot(bmp) != 0ull) bag = bmp ? mx - sketch_inter_ub_bf(img_sketch(a), img_sketch(b), na, nb) : 0;
-    const int lo = same ? 0 : (bag > gap ? bag : gap), hi = same ? 0 : mx;
-    const double den = (double)(na + nb) * 0.5;
-    Chain c(sc.else_level);
+template <int FP, class SC>
+__device__ __attribute__((always_inline)) inline void img_lev(const SC &sc, const uint4 (&a)[FP], const uint4 (&b)[FP],
+                                                              int (&level)[FP], bool (&und)[FP]) {
+    bool same[FP], bmp[FP], und0[FP];
+    int lo[FP], hi[FP];
+    bool need = false;
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        same[u] = a[u].x == b[u].x && a[u].y == b[u].y;
+        const int la = lens_u16(a[u].y), lb = lens_u16(b[u].y), na = lens_cp(a[u].y), nb = lens_cp(b[u].y);
+        und0[u] = (same[u] && !sc.has_ids) || la >= LEN_SAT || lb >= LEN_SAT || na >= LEN_SAT || nb >= LEN_SAT;
+        // BMP rows: units are code points, so the bag bound holds
+        bmp[u] = na == la && nb == lb && !same[u];
+        need = need || bmp[u];
+        const int gap = na > nb ? na - nb : nb - na;
+        lo[u] = same[u] ? 0 : gap;
+        hi[u] = same[u] ? 0 : (na > nb ? na : nb);
+    }
+    if (__ballot(need) != 0ull) {  // wave-uniform
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            const int na = lens_cp(a[u].y), nb = lens_cp(b[u].y);
+            const int bag = bmp[u] ? (na > nb ? na : nb) - sketch_inter_ub_bf(img_sketch(a[u]), img_sketch(b[u]), na, nb) : 0;
+            lo[u] = bag > lo[u] ? bag : lo[u];
+        }
+    }
+    Chain c[FP];
+#pragma unroll
+    for (int u = 0; u < FP; ++u) c[u] = Chain(sc.else_level);
     for (int i = 0; i < sc.n_tests; ++i) {
-        const int op = sc.op[i], f = sc.tflag[i];
-        int r;
+        const int op = sc.op[i], f = sc.tflag[i], lv = sc.level[i];
         if (op == SPK_OP_STR_CMP) {  // wave-uniform branches on the test kind
-            r = (int)same ^ ((f & TF_EQ) ? 0 : 1);
+            const int x = (f & TF_EQ) ? 0 : 1;
+#pragma unroll
+            for (int u = 0; u < FP; ++u) c[u].fold((int)same[u] ^ x, lv);
         } else if (op == SPK_OP_LEV) {
             const int A = sc.lev_a[i];
-            if (f & TF_EXACT) r = lo == hi ? cmpd((double)lo, sc.t[i], sc.cmp[i]) : KU;
-            else if (f & TF_GE) r = lo >= A ? KT : (hi < A ? KF : KU);
-            else r = hi <= A ? KT : (lo > A ? KF : KU);
+            const double t = sc.t[i];
+            const int cmp = sc.cmp[i];
+#pragma unroll
+            for (int u = 0; u < FP; ++u) {
+                int r;
+                if (f & TF_EXACT) r = lo[u] == hi[u] ? cmpd((double)lo[u], t, cmp) : KU;
+                else if (f & TF_GE) r = lo[u] >= A ? KT : (hi[u] < A ? KF : KU);
+                else r = hi[u] <= A ? KT : (lo[u] > A ? KF : KU);
+                c[u].fold(r, lv);
+            }
         } else {
-            const double tl = sc.t[i] * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
-            const double tl_hi = up > dn ? up : dn, tl_lo = up > dn ? dn : up;
-            const int rr = sc.cmp[i] == SPK_CMP_LE ? ((double)hi <= tl_lo ? KT : ((double)lo > tl_hi ? KF : KU))
-                                                   : ((double)hi < tl_lo ? KT : ((double)lo >= tl_hi ? KF : KU));
-            r = den == 0.0 ? KN : (same ? (f & TF_ZERO) : rr);
+            const double t = sc.t[i];
+            const bool le = sc.cmp[i] == SPK_CMP_LE;
+#pragma unroll
+            for (int u = 0; u < FP; ++u) {
+                const double den = (double)(lens_cp(a[u].y) + lens_cp(b[u].y)) * 0.5;
+                const double tl = t * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
+                const double tl_hi = up > dn ? up : dn, tl_lo = up > dn ? dn : up;
+                const int rr = le ? ((double)hi[u] <= tl_lo ? KT : ((double)lo[u] > tl_hi ? KF : KU))
+                                  : ((double)hi[u] < tl_lo ? KT : ((double)lo[u] >= tl_hi ? KF : KU));
+                c[u].fold(den == 0.0 ? KN : (same[u] ? (f & TF_ZERO) : rr), lv);
+            }
         }
-        c.fold(r, sc.level[i]);
     }
-    level = nul ? sc.null_level : c.lvl;
-    return (!nul && (und0 || c.und)) ? ST_UNDECIDED : ST_DONE;
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        const bool nul = a[u].y == LENS_NULL || b[u].y == LENS_NULL;
+        level[u] = nul ? sc.null_level : c[u].lvl;
+        und[u] = !nul && (und0[u] || c[u].und);
+    }
 }
 
 __device__ inline double bits_to_double(uint32_t lo, uint32_t hi) {
@@ -869,6 +947,12 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
             const uint8_t *h0 = A.img0 + img_at(A.img_rows0, 0, sc.off2), *h1 = A.img1 + img_at(A.img_rows1, 0, sc.off2);
             const int s0 = (int)img_at(A.img_rows0, 0, sc.off), s1 = (int)img_at(A.img_rows1, 0, sc.off);
             const int t0 = (int)img_at(A.img_rows0, 0, sc.off2), t1 = (int)img_at(A.img_rows1, 0, sc.off2);
+            if (base >= sc.imp_lo && base + SPAN <= sc.imp_hi) {  // wave-uniform: the blocking key implies equality
+                const uint32_t add = (uint32_t)(sc.eq_level + 1) * (uint32_t)sc.stride;
+#pragma unroll
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? add : 0u;
+                continue;
+            }
 #pragma unroll
             for (int u = 0; u < FP; ++u) {
                 und[u] = false;
@@ -882,8 +966,7 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                         va[u] = BUF ? buf8(r0, ox[u], s0) : *reinterpret_cast<const uint2 *>(b0 + ox[u]);
                         vb[u] = BUF ? buf8(r1, oy[u], s1) : *reinterpret_cast<const uint2 *>(b1 + oy[u]);
                     }
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) und[u] = img_eq(sc, va[u], vb[u], lev[u]) != ST_DONE;
+                    img_eq<FP>(sc, va, vb, lev, und);
                     break;
                 }
                 case SC_JW: {
@@ -902,8 +985,7 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                             hb[u] = *reinterpret_cast<const uint64_t *>(h1 + oy[u]);
                         }
                     }
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) und[u] = img_jw(sc, va[u], vb[u], ha[u], hb[u], lev[u]) != ST_DONE;
+                    img_jw<FP>(sc, va, vb, ha, hb, lev, und);
                     break;
                 }
                 case SC_LEV: {
@@ -913,8 +995,7 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                         va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
                         vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
                     }
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) und[u] = img_lev(sc, va[u], vb[u], lev[u]) != ST_DONE;
+                    img_lev<FP>(sc, va, vb, lev, und);
                     break;
                 }
                 case SC_NUM: {
@@ -989,28 +1070,44 @@ __device__ __attribute__((always_inline)) inline void slot_cols(const GammaArgs 
                 und[u] = false;
                 lev[u] = 0;
             }
-            if constexpr (S % 2 == 1) {  // only 8-byte EQ fields start at an odd slot
+            uint4 va[RP], vb[RP];
 #pragma unroll
-                for (int u = 0; u < RP; ++u)
-                    und[u] = img_eq(sc, make_uint2(ra[u][CQ].z, ra[u][CQ].w), make_uint2(rb[u][CQ].z, rb[u][CQ].w),
-                                    lev[u]) != ST_DONE;
+            for (int u = 0; u < RP; ++u) {
+                va[u] = ra[u][CQ];
+                vb[u] = rb[u][CQ];
+            }
+            if constexpr (S % 2 == 1) {  // only 8-byte EQ fields start at an odd slot
+                uint2 ea[RP], eb[RP];
+#pragma unroll
+                for (int u = 0; u < RP; ++u) {
+                    ea[u] = make_uint2(va[u].z, va[u].w);
+                    eb[u] = make_uint2(vb[u].z, vb[u].w);
+                }
+                img_eq<RP>(sc, ea, eb, lev, und);
             } else {
                 switch (sc.cls) {
-                    case SC_EQ:
+                    case SC_EQ: {
+                        uint2 ea[RP], eb[RP];
 #pragma unroll
-                        for (int u = 0; u < RP; ++u)
-                            und[u] = img_eq(sc, make_uint2(ra[u][CQ].x, ra[u][CQ].y),
-                                            make_uint2(rb[u][CQ].x, rb[u][CQ].y), lev[u]) != ST_DONE;
+                        for (int u = 0; u < RP; ++u) {
+                            ea[u] = make_uint2(va[u].x, va[u].y);
+                            eb[u] = make_uint2(vb[u].x, vb[u].y);
+                        }
+                        img_eq<RP>(sc, ea, eb, lev, und);
                         break;
-                    case SC_JW:
+                    }
+                    case SC_JW: {
+                        uint64_t ha[RP], hb[RP];
 #pragma unroll
-                        for (int u = 0; u < RP; ++u)
-                            und[u] = img_jw(sc, ra[u][CQ], rb[u][CQ], ((uint64_t)ra[u][HQ].y << 32) | ra[u][HQ].x,
-                                            ((uint64_t)rb[u][HQ].y << 32) | rb[u][HQ].x, lev[u]) != ST_DONE;
+                        for (int u = 0; u < RP; ++u) {
+                            ha[u] = ((uint64_t)ra[u][HQ].y << 32) | ra[u][HQ].x;
+                            hb[u] = ((uint64_t)rb[u][HQ].y << 32) | rb[u][HQ].x;
+                        }
+                        img_jw<RP>(sc, va, vb, ha, hb, lev, und);
                         break;
+                    }
                     case SC_LEV:
-#pragma unroll
-                        for (int u = 0; u < RP; ++u) und[u] = img_lev(sc, ra[u][CQ], rb[u][CQ], lev[u]) != ST_DONE;
+                        img_lev<RP>(sc, va, vb, lev, und);
                         break;
                     default:  // SC_NUM
 #pragma unroll
@@ -1809,6 +1906,42 @@ static void prepare_tests(SimpleCol &s) {
     }
 }
 
+// Level of a simple string column for two equal, non-NULL, non-empty strings: `=` holds, jw = 1.0,
+// levenshtein = 0 and its ratio 0.0 (den > 0); the first test that holds decides.
+static int32_t equal_level(const SimpleCol &s) {
+    for (int i = 0; i < s.n_tests; ++i) {
+        const int op = s.op[i], cmp = s.cmp[i];
+        bool r;
+        if (op == SPK_OP_STR_CMP) r = cmp == SPK_CMP_EQ;
+        else if (op == SPK_OP_JW) r = host_cmp(1.0, s.t[i], cmp);
+        else r = host_cmp(0.0, s.t[i], cmp);  // SPK_OP_LEV / SPK_OP_LEVRATIO
+        if (r) return s.level[i];
+    }
+    return s.else_level;
+}
+
+// The pairs of one blocking rule are contiguous in the pair order; a rule whose key includes the
+// plain term `l.c = r.c` on the raw columns column c was decoded from puts equal, non-NULL strings
+// of c in every pair it emits (keys are byte-verified dense ids; NULL keys emit nothing).  The
+// longest run of such pairs becomes the column's implied range (SimpleCol.imp_lo / imp_hi).
+static void implied_equal(const spk_ctx *ctx, const Table &t0, const Table &t1, SimpleCol &sc) {
+    sc.imp_lo = sc.imp_hi = 0;
+    sc.eq_level = 0;
+    if (sc.kind != SK_STR || !(sc.cls == SC_EQ || sc.cls == SC_JW || sc.cls == SC_LEV)) return;
+    const Column *c0 = t0.cols[sc.col], *c1 = t1.cols[sc.col];
+    if (!c0 || !c1 || !c0->src[0] || !c1->src[1] || c0->has_empty || c1->has_empty) return;
+    int64_t lo = -1, hi = -1;
+    for (size_t r = 0; r < ctx->pair_terms.size(); ++r) {
+        bool imp = false;
+        for (const KeyTerm &k : ctx->pair_terms[r]) imp = imp || (k.plain && k.src_l == c0->src[0] && k.src_r == c1->src[1]);
+        if (!imp) continue;
+        if (lo >= 0 && ctx->pair_rule_lo[r] == hi) hi = ctx->pair_rule_hi[r];  // adjacent rules merge
+        else lo = ctx->pair_rule_lo[r], hi = ctx->pair_rule_hi[r];
+        if (hi - lo > sc.imp_hi - sc.imp_lo) sc.imp_lo = lo, sc.imp_hi = hi;
+    }
+    sc.eq_level = equal_level(sc);
+}
+
 // Recognise a simple column (see SimpleCol); false leaves it to the interpreter.
 static int32_t simple_class(const SimpleCol &s) {
     if (s.kind == SK_NUM) return SC_NUM;
@@ -2112,6 +2245,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         sc.cls = simple_class(sc);
         prepare_tests(sc);
         sc.has_ids = (t0.cols[sc.col]->has_ids && t1.cols[sc.col]->has_ids) ? 1 : 0;
+        implied_equal(ctx, t0, t1, sc);
     }
     const int64_t img_stride = layout_image(simple);
     // image columns first, by field offset (the row filter walks the chunks in order), then the rest
@@ -2257,7 +2391,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                     case 6: k_gamma_simple<6, 3, false><<<g, F_THREADS, 0, ctx->stream>>>(B); break;  // A/B: flat loads
                     // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
                     // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
-                    default: k_gamma_simple<6, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 7: k_gamma_simple<6, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    // measured on MI355X after the per-test parameter hoist (cfg2 pass, tools/ab_gamma.py):
+                    // <5,3> 1.236 ms, <8,2> 1.260, <6,3> (VGPR spills) 1.306
+                    default: k_gamma_simple<5, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
                 }
             };
             launch(A, 0, va);
@@ -2405,6 +2542,8 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     ctx->mpat_valid = false;
     ctx->last_deferred = n_slow;
     ctx->last_exact.assign(counts.begin(), counts.begin() + K);
+    ctx->last_implied.assign((size_t)K, 0);
+    for (const SimpleCol &sc : simple) ctx->last_implied[sc.k] = sc.imp_hi - sc.imp_lo;
     return SPK_OK;
 }
 
@@ -2600,6 +2739,12 @@ extern "C" int spk_gammas_deferred(spk_ctx *ctx, int64_t *out) {
 extern "C" int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n) {
     SPK_REQUIRE(ctx && out && n >= (int)ctx->last_exact.size(), SPK_E_INVALID, "spk_gammas_exact_counts: bad args");
     for (size_t k = 0; k < ctx->last_exact.size(); ++k) out[k] = ctx->last_exact[k];
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n) {
+    SPK_REQUIRE(ctx && out && n >= (int)ctx->last_implied.size(), SPK_E_INVALID, "spk_gammas_implied_pairs: bad args");
+    for (size_t k = 0; k < ctx->last_implied.size(); ++k) out[k] = ctx->last_implied[k];
     return SPK_OK;
 }
 

@@ -311,6 +311,7 @@ static int new_raw(spk_ctx *ctx, int raw, RawCol **out) {
     if (raw >= (int)ctx->raw.size()) ctx->raw.resize((size_t)raw + 1, nullptr);
     delete ctx->raw[raw];
     ctx->raw[raw] = new RawCol();
+    ctx->raw[raw]->serial = ++ctx->raw_serial;
     *out = ctx->raw[raw];
     return SPK_OK;
 }
@@ -338,8 +339,13 @@ int spk_raw_utf8(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const
     r->n = n;
     const int64_t nbytes = offsets[n];
     int64_t mx = 0;
-    for (int64_t i = 0; i < n; ++i) mx = std::max(mx, offsets[i + 1] - offsets[i]);
+    bool empty = false;
+    for (int64_t i = 0; i < n; ++i) {
+        mx = std::max(mx, offsets[i + 1] - offsets[i]);
+        empty = empty || (valid[i] && offsets[i + 1] == offsets[i]);
+    }
     r->max_len = mx;
+    r->has_empty = empty;
     SPK_TRY(r->off.alloc((size_t)n + 1));
     SPK_TRY(r->bytes.alloc((size_t)nbytes + 1));
     SPK_TRY(r->valid.alloc((size_t)n + 1));
@@ -406,6 +412,17 @@ int spk_key_build(spk_ctx *ctx, int rule, int n_terms, const spk_key_term *terms
     SPK_TRY(set_key(ctx, t0, 0, rule, acc.p, n0));
     SPK_TRY(set_key(ctx, tr, 1, rule, any_r ? acc.p + n0 : acc.p, n1));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<KeyTerm> rec;
+    for (int i = 0; i < n_terms; ++i) {
+        const spk_key_term &tm = terms[i];
+        const int rr = tm.raw_r >= 0 ? tm.raw_r : tm.raw_l;
+        KeyTerm k;
+        k.src_l = ctx->raw[tm.raw_l]->serial;
+        k.src_r = ctx->raw[rr]->serial;
+        k.plain = tm.l_substr_len < 0 && (tm.raw_r >= 0 ? tm.r_substr_len : tm.l_substr_len) < 0;
+        rec.push_back(k);
+    }
+    ctx->rule_terms[rule] = rec;
     return SPK_OK;
 }
 
@@ -539,6 +556,9 @@ int spk_table_add_raw_utf8(spk_ctx *ctx, int col, int raw0, int raw1) {
         SPK_TRY(new_column(ctx, side, col, &c));
         c->kind = COL_STR;
         c->has_ids = true;
+        c->src[0] = ctx->raw[raw0]->serial;
+        c->src[1] = ctx->raw[two ? raw1 : raw0]->serial;
+        c->has_empty = ctx->raw[raw0]->has_empty || (two && ctx->raw[raw1]->has_empty);
         DevBuf<int64_t> len, off8;
         SPK_TRY(len.alloc((size_t)n + 1));
         SPK_TRY(off8.alloc((size_t)n + 1));

@@ -142,6 +142,16 @@ struct Column {
     DevBuf<uint8_t> valid;
     bool has_ids = false;  // COL_STR: RecMeta.key is a dictionary id
     int64_t max_bytes = 0; // COL_STR: longest row in UTF-8 bytes (>= its UTF-16 units)
+    uint64_t src[2] = {0, 0};  // spk_table_add_raw_utf8: serials of the raw columns of the l / r side (0: other)
+    bool has_empty = false;    // some non-NULL row is the empty string
+};
+
+// A blocking-key term as spk_key_build saw it, by raw-column serial: the comparison filter skips a
+// string column for the pairs of a rule whose key includes `l.c = r.c` on that column's own raw
+// columns (the strings are then equal and non-NULL; see spk_gammas).
+struct KeyTerm {
+    uint64_t src_l = 0, src_r = 0;
+    bool plain = false;  // no substr on either side
 };
 
 // An input column as handed over (Arrow buffers), kept on the device in input row order: the source
@@ -149,6 +159,8 @@ struct Column {
 enum RawKind : int32_t { RAW_UTF8 = 1, RAW_I64 = 2 };
 struct RawCol {
     RawKind kind = RAW_UTF8;
+    uint64_t serial = 0;     // ctx-wide upload counter (a replaced raw column gets a new one)
+    bool has_empty = false;  // RAW_UTF8: some non-NULL value is the empty string
     int64_t n = 0;
     int64_t max_len = 0;     // longest value in bytes (UTF-8)
     DevBuf<int64_t> off;     // RAW_UTF8: n + 1 byte offsets
@@ -208,6 +220,10 @@ struct spk_ctx {
     int64_t n_pairs = 0;
     bool pairs_valid = false;
     uint64_t pairs_epoch = 0;          // bumped whenever the pair set is replaced
+    std::vector<spk::KeyTerm> rule_terms[32];   // spk_key_build terms per rule (cleared by spk_table_set_key)
+    std::vector<std::vector<spk::KeyTerm>> pair_terms;  // the terms of each rule of the current pair set
+    std::vector<int64_t> pair_rule_lo, pair_rule_hi;   // local pair ordinals of each rule (spk_block)
+    uint64_t raw_serial = 0;
     spk::RuleView views[spk::MAX_VIEWS];  // views[r] for rules 1 .. n_views
     int n_views = 0;
     spk::DevBuf<int32_t> pvl, pvr;     // view positions of pairs [pv_base, n_pairs)
@@ -223,6 +239,7 @@ struct spk_ctx {
     bool codes_valid = false;
     int64_t last_deferred = 0;
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
+    std::vector<int64_t> last_implied;  // per column: pairs whose level the blocking key implied
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
     int filter_waves = 0;             // k_gamma_simple variant (waves per SIMD, pairs per lane): 0 = <6,3>; 1..5 A/B

@@ -284,6 +284,49 @@ def test_blocking_and_gammas_at_scale(amd, shards):
     assert (gam == ref).all()
 
 
+@pytest.mark.parametrize("link_type", ["dedupe_only", "link_only", "link_and_dedupe"])
+def test_blocking_key_implied_levels(amd, link_type):
+    """Pairs of a rule whose key includes the plain term `l.c = r.c` take column c's equal-strings
+    level from the key (the filter reads no rows for them).  Against the oracle on every pair, with
+    rules that must NOT imply equality next to ones that do: substr terms, an asymmetric term, a
+    column holding the empty string, and a multi-term rule."""
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    df = _synthetic(6000, seed=17, surname_vocab=150, first_vocab=100, city_vocab=30)
+    rng = np.random.Generator(np.random.PCG64(17))
+    df.loc[rng.random(len(df)) < 0.05, "city"] = ""  # empty strings: city is never implied
+    rules = ["l.surname = r.surname", "l.dob = r.dob and l.city = r.city",
+             "substr(l.email, 1, 4) = substr(r.email, 1, 4)", "l.first_name = r.surname"]
+    from splink_amd.synthetic import cfg_settings
+    st = cfg_settings(2)  # first_name / surname JW-3, dob / city exact-2, email Lev-3
+    st["link_type"] = link_type
+    st["blocking_rules"] = rules
+    st = complete_settings_dict(st, amd)
+    inputs = [df] if link_type == "dedupe_only" else [df.iloc[:3000].reset_index(drop=True),
+                                                       df.iloc[3000:].reset_index(drop=True)]
+    if link_type == "link_and_dedupe":
+        inputs = [pd.concat(inputs, ignore_index=True)]
+        inputs[0]["_source_table"] = ["left"] * 3000 + ["right"] * 3000
+    job = Job(link_type, inputs, "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    imp = job.ctx.gammas_implied_pairs(5)
+    l, r = job.pair_rows()
+    tl, tr = job.tables[0], job.r_table()
+    cols = ["first_name", "surname", "dob", "city", "email"]
+    specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
+    ref = orc.template_gammas(specs, [orc.StrCol(tl[c].tolist()) for c in cols],
+                              [orc.StrCol(tr[c].tolist()) for c in cols], l, r)
+    got = job.gammas_host()
+    assert (got == ref).all(), np.nonzero((got != ref).any(axis=1))[0][:10]
+    assert imp[1] > 0 and imp[2] > 0, imp       # surname (rule 0), dob (rule 1)
+    assert imp[0] == 0 and imp[3] == 0 and imp[4] == 0, imp  # asymmetric, has "", substr
+    # the interpreter path (no filter shortcut) agrees
+    job.ctx.gammas_set_simple(0)
+    job.gammas(st)
+    assert (job.gammas_host() == ref).all()
+
+
 def test_simple_columns_match_interpreter(amd):
     """The record-only filter for template-shaped columns and the general interpreter agree."""
     from splink_amd.engine import Job
