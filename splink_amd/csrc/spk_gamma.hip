@@ -162,27 +162,18 @@ struct GammaArgs {
     int all_img;  // every simple column reads the row image (no SC_GEN / SC_NUMRAW): views allowed
 };
 
-// Codes are written in place: the filter pass sets each pair's code, the exact / slow passes of
-// column k add to it.  A pair occurs at most once in column k's lists and the passes are ordered
-// launches on one stream, so the read-modify-write needs no atomic -- and a 2-byte store leaves
-// the neighbouring pair's code alone.
+// Codes are written in place: the filter pass sets each pair's code (a 2-byte store leaves the
+// neighbouring pair's code alone), the exact / slow passes of column k add to it (a pair occurs at
+// most once in column k's lists).
 __device__ inline void code_set(const GammaArgs &A, int64_t p, uint32_t v) {
     if (A.code16) static_cast<uint16_t *>(A.codes)[p] = (uint16_t)v;
     else static_cast<uint32_t *>(A.codes)[p] = v;
 }
+// The exact and slow passes add their column's digit to the code the filter set.  Passes of different
+// columns may run concurrently (several columns in one launch, ExactCols), so the add is atomic, on the aligned dword (a 16-bit code never carries
+// into its neighbour -- a code stays below the pattern count, <= 65536); no value is returned, so
+// the lane does not wait for it.
 __device__ inline void code_add(const GammaArgs &A, int64_t p, uint32_t d) {
-    if (A.code16) {
-        uint16_t *c = static_cast<uint16_t *>(A.codes) + p;
-        *c = (uint16_t)(*c + d);
-    } else {
-        static_cast<uint32_t *>(A.codes)[p] += d;
-    }
-}
-
-// Exact passes of several columns in one launch (ExactCols) may update one pair's code concurrently:
-// an atomic add on the aligned dword (a 16-bit code never carries into its neighbour -- a code stays
-// below the pattern count, <= 65536).
-__device__ inline void code_add_atomic(const GammaArgs &A, int64_t p, uint32_t d) {
     if (A.code16) {
         uint32_t *w = reinterpret_cast<uint32_t *>(static_cast<uint16_t *>(A.codes) + (p & ~(int64_t)1));
         atomicAdd(w, d << (16 * (uint32_t)(p & 1)));
@@ -1629,12 +1620,8 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
         if (have) {
             int level = 0;
             const int st = LEV ? lev_cell(sc, s_c0, s_c1, x, y, level) : simple_exact(A, sc, s_c0, s_c1, x, y, level);
-            if (st != ST_DONE)
-                to_slow = true;
-            else if (C.n > 1)
-                code_add_atomic(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
-            else
-                code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
+            if (st != ST_DONE) to_slow = true;
+            else code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
         }
         wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
         i = i2;
@@ -2448,9 +2435,15 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                                                                        ctx->xlist.p, ctx->xinfo.p);
                 jw.si[jw.n++] = simple_of[k];
             }
-            if (jw.n)
+            // (running this launch on a second stream beside the Levenshtein pass measured no faster:
+            // 1.198-1.205 ms per cfg2 pass either way)
+            if (jw.n) {
                 k_gamma_exact_simple<false><<<(unsigned)(g_exact * jw.n), X_THREADS, 0, ctx->stream>>>(
                     A, jw, ctx->xlist.p, ctx->xinfo.p);
+                for (int c = 0; c < jw.n; ++c)
+                    k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, simple[jw.si[c]].k, ctx->xlist.p,
+                                                                                   ctx->xinfo.p);
+            }
             for (int k = 0; k < K; ++k) {
                 if (!may_exact[k]) continue;
                 const bool simple_str = simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR;
@@ -2482,8 +2475,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                     k_gamma_slow_lev<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], ctx->xlist.p,
                                                                                          ctx->xinfo.p);
                     k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
-                } else
+                } else if (!fused) {
                     k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+                }
             }
             SPK_HIP(hipGetLastError());
         } else {
