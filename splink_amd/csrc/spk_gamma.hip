@@ -169,11 +169,23 @@ __device__ inline void code_set(const GammaArgs &A, int64_t p, uint32_t v) {
     if (A.code16) static_cast<uint16_t *>(A.codes)[p] = (uint16_t)v;
     else static_cast<uint32_t *>(A.codes)[p] = v;
 }
-// The exact and slow passes add their column's digit to the code the filter set.  Passes of different
-// columns may run concurrently (several columns in one launch, ExactCols), so the add is atomic, on the aligned dword (a 16-bit code never carries
-// into its neighbour -- a code stays below the pattern count, <= 65536); no value is returned, so
-// the lane does not wait for it.
+// The exact and slow passes add their column's digit to the code the filter set.  Launches of one
+// column run in stream order and a pair occurs once in a column's lists: a plain read-modify-write
+// (an atomic add measured 2.4x the HBM writes of the Levenshtein pass at the same kernel time,
+// profiles/r2b_traffic.json).
 __device__ inline void code_add(const GammaArgs &A, int64_t p, uint32_t d) {
+    if (A.code16) {
+        uint16_t *c = static_cast<uint16_t *>(A.codes) + p;
+        *c = (uint16_t)(*c + d);
+    } else {
+        static_cast<uint32_t *>(A.codes)[p] += d;
+    }
+}
+
+// Several columns in one launch (ExactCols) may update one pair's code at once: an atomic add on
+// the aligned dword (a 16-bit code never carries into its neighbour -- a code stays below the
+// pattern count, <= 65536).
+__device__ inline void code_add_atomic(const GammaArgs &A, int64_t p, uint32_t d) {
     if (A.code16) {
         uint32_t *w = reinterpret_cast<uint32_t *>(static_cast<uint16_t *>(A.codes) + (p & ~(int64_t)1));
         atomicAdd(w, d << (16 * (uint32_t)(p & 1)));
@@ -1621,6 +1633,7 @@ __global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma
             int level = 0;
             const int st = LEV ? lev_cell(sc, s_c0, s_c1, x, y, level) : simple_exact(A, sc, s_c0, s_c1, x, y, level);
             if (st != ST_DONE) to_slow = true;
+            else if (C.n > 1) code_add_atomic(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
             else code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
         }
         wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
