@@ -32,7 +32,7 @@ extern "C" {
 #define SPK_E_HIP (-2)     /* HIP runtime failure */
 #define SPK_E_OOM (-3)     /* device allocation failed */
 #define SPK_E_STATE (-4)   /* call out of order (e.g. gammas before pairs) */
-#define SPK_E_LIMIT (-5)   /* input beyond a supported limit (e.g. string length) */
+#define SPK_E_LIMIT (-5)   /* input beyond a supported limit (e.g. 2^31 pairs in one context) */
 
 #define SPK_LINK_DEDUPE 0        /* "dedupe_only"     */
 #define SPK_LINK_ONLY 1          /* "link_only"       */
