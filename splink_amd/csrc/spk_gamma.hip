@@ -74,7 +74,12 @@ struct SimpleCol {
     // in the column), so their level is eq_level and the filter reads nothing for them.
     int64_t imp_lo, imp_hi;
     int32_t eq_level;
+    // LEVRATIO tests: offset of the test's threshold table in GammaArgs.thr (-1: none).  Entry S is
+    // the largest distance v with `v / (S / 2.0) cmp t` true in fp64 (Spark's division), for
+    // S = len_l + len_r (code points) < THR_S: the filter decides the test with integer compares.
+    int32_t thr_off[MAX_TESTS];
 };
+constexpr int THR_S = 256;
 constexpr int32_t TF_ZERO = 1;     // the value 0.0 passes the test (JW of strings without a common unit; lev ratio 0)
 constexpr int32_t TF_ONE = 2;      // JW: the value 1.0 passes (equal non-empty strings)
 constexpr int32_t TF_GE = 4;       // LEV: the test is `lev >= lev_a` (else `lev <= lev_a`)
@@ -160,6 +165,8 @@ struct GammaArgs {
     // reads pl / pr = their view positions and img0 / img1 = view-ordered images
     int region_base;
     int all_img;  // every simple column reads the row image (no SC_GEN / SC_NUMRAW): views allowed
+    const int16_t *thr;  // LEVRATIO threshold tables (SimpleCol.thr_off), n_thr entries
+    int n_thr;
 };
 
 // Codes are written in place: the filter pass sets each pair's code (a 2-byte store leaves the
@@ -793,7 +800,7 @@ __device__ __attribute__((always_inline)) inline void img_jw(const SC &sc, const
 // pair; exact ties are left to the exact pass.
 template <int FP, class SC>
 __device__ __attribute__((always_inline)) inline void img_lev(const SC &sc, const uint4 (&a)[FP], const uint4 (&b)[FP],
-                                                              int (&level)[FP], bool (&und)[FP]) {
+                                                              int (&level)[FP], bool (&und)[FP], const int16_t *thr) {
     bool same[FP], bmp[FP], und0[FP];
     int lo[FP], hi[FP];
     bool need = false;
@@ -839,16 +846,26 @@ __device__ __attribute__((always_inline)) inline void img_lev(const SC &sc, cons
                 c[u].fold(r, lv);
             }
         } else {
-            const double t = sc.t[i];
-            const bool le = sc.cmp[i] == SPK_CMP_LE;
+            // integer thresholds from the table when len_l + len_r < THR_S, else the fp64 bound
+            // with one part in 1e12 of margin (exact ties left to the exact pass)
+            const int off = thr ? sc.thr_off[i] : -1;
 #pragma unroll
             for (int u = 0; u < FP; ++u) {
-                const double den = (double)(lens_cp(a[u].y) + lens_cp(b[u].y)) * 0.5;
-                const double tl = t * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
-                const double tl_hi = up > dn ? up : dn, tl_lo = up > dn ? dn : up;
-                const int rr = le ? ((double)hi[u] <= tl_lo ? KT : ((double)lo[u] > tl_hi ? KF : KU))
-                                  : ((double)hi[u] < tl_lo ? KT : ((double)lo[u] >= tl_hi ? KF : KU));
-                c[u].fold(den == 0.0 ? KN : (same[u] ? (f & TF_ZERO) : rr), lv);
+                const int S = lens_cp(a[u].y) + lens_cp(b[u].y);
+                const bool tab = off >= 0 && S < THR_S;
+                int rr = KU;
+                if (tab) {
+                    const int th = thr[off + S];
+                    rr = hi[u] <= th ? KT : (lo[u] > th ? KF : KU);
+                }
+                if (__ballot(!tab) != 0ull && !tab) {
+                    const double t = sc.t[i], den = (double)S * 0.5;
+                    const double tl = t * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
+                    const double tl_hi = up > dn ? up : dn, tl_lo = up > dn ? dn : up;
+                    rr = sc.cmp[i] == SPK_CMP_LE ? ((double)hi[u] <= tl_lo ? KT : ((double)lo[u] > tl_hi ? KF : KU))
+                                                 : ((double)hi[u] < tl_lo ? KT : ((double)lo[u] >= tl_hi ? KF : KU));
+                }
+                c[u].fold(S == 0 ? KN : (same[u] ? (f & TF_ZERO) : rr), lv);
             }
         }
     }
@@ -898,7 +915,9 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
 template <int MINW, int FP, bool BUF>
 __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     __shared__ unsigned int s_cnt[MAX_SIMPLE];
+    extern __shared__ int16_t s_thr[];  // A.thr (dynamic LDS: n_thr entries)
     for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
+    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const Region R = my_region(A);
@@ -998,7 +1017,7 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
                         va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
                         vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
                     }
-                    img_lev<FP>(sc, va, vb, lev, und);
+                    img_lev<FP>(sc, va, vb, lev, und, s_thr);
                     break;
                 }
                 case SC_NUM: {
@@ -1110,7 +1129,7 @@ __device__ __attribute__((always_inline)) inline void slot_cols(const GammaArgs 
                         break;
                     }
                     case SC_LEV:
-                        img_lev<RP>(sc, va, vb, lev, und);
+                        img_lev<RP>(sc, va, vb, lev, und, nullptr);
                         break;
                     default:  // SC_NUM
 #pragma unroll
@@ -2247,6 +2266,25 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         sc.has_ids = (t0.cols[sc.col]->has_ids && t1.cols[sc.col]->has_ids) ? 1 : 0;
         implied_equal(ctx, t0, t1, sc);
     }
+    // threshold tables of the Levenshtein-ratio tests (SimpleCol.thr_off)
+    std::vector<int16_t> thr_tab;
+    for (SimpleCol &sc : simple) {
+        for (int i = 0; i < MAX_TESTS; ++i) sc.thr_off[i] = -1;
+        if (sc.cls != SC_LEV) continue;
+        for (int i = 0; i < sc.n_tests; ++i) {
+            if (sc.op[i] != SPK_OP_LEVRATIO || (sc.cmp[i] != SPK_CMP_LE && sc.cmp[i] != SPK_CMP_LT)) continue;
+            sc.thr_off[i] = (int32_t)thr_tab.size();
+            for (int S = 0; S < THR_S; ++S) {
+                // `v / den cmp t` holds for v <= the entry (monotone in v); S = 0 is NULL (den = 0)
+                int th = -1;
+                const double den = (double)S / 2.0;
+                for (int v = 0; v < THR_S && S > 0; ++v)
+                    if (host_cmp((double)v / den, sc.t[i], sc.cmp[i])) th = v;
+                    else break;
+                thr_tab.push_back((int16_t)th);
+            }
+        }
+    }
     const int64_t img_stride = layout_image(simple);
     // image columns first, by field offset (the row filter walks the chunks in order), then the rest
     std::stable_sort(simple.begin(), simple.end(), [](const SimpleCol &a, const SimpleCol &b) {
@@ -2281,7 +2319,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                  o_lu = put(lu.data(), lu.size()), o_loff = put(loff.data(), loff.size()),
                  o_llen = put(llen.data(), llen.size()), o_lcp = put(lcp.data(), lcp.size()),
                  o_stride = put(ctx->stride.data(), ctx->stride.size()), o_simple = put(simple.data(), simple.size()),
-                 o_complex = put(complex_k.data(), complex_k.size());
+                 o_complex = put(complex_k.data(), complex_k.size()), o_thr = put(thr_tab.data(), thr_tab.size());
     const int32_t zero = 0;
     const size_t o_err = put(&zero, 1);
     SPK_TRY(ctx->prog_blob.alloc(blob.size()));
@@ -2326,6 +2364,8 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     at(A.stride, o_stride);
     at(A.simple, o_simple);
     at(A.complex_k, o_complex);
+    at(A.thr, o_thr);
+    A.n_thr = (int)thr_tab.size();
     at(A.err, o_err);
     A.codes = ctx->codes.p;
     A.code16 = ctx->code_bytes == 2;
@@ -2381,20 +2421,21 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 const unsigned g = (unsigned)(r_hi - r_lo);
                 // buffer-descriptor gathers while every chunk plane fits the 31-bit descriptor range
                 const bool buf = std::max(B.img_rows0, B.img_rows1) * B.img_stride < (int64_t)INT32_MAX;
+                const size_t shm = (size_t)B.n_thr * sizeof(int16_t);
                 switch (buf ? ctx->filter_waves : -1) {  // (waves per SIMD the filter is compiled for, pairs per lane)
-                    case -1: k_gamma_simple<6, 3, false><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 1: k_gamma_simple<1, 4, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 2: k_gamma_simple<6, 4, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 3: k_gamma_simple<5, 4, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 4: k_gamma_simple<8, 2, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 5: k_gamma_simple<5, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
-                    case 6: k_gamma_simple<6, 3, false><<<g, F_THREADS, 0, ctx->stream>>>(B); break;  // A/B: flat loads
+                    case -1: k_gamma_simple<6, 3, false><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    case 1: k_gamma_simple<1, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    case 2: k_gamma_simple<6, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    case 3: k_gamma_simple<5, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    case 4: k_gamma_simple<8, 2, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    case 5: k_gamma_simple<5, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    case 6: k_gamma_simple<6, 3, false><<<g, F_THREADS, shm, ctx->stream>>>(B); break;  // A/B: flat loads
                     // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
                     // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
-                    case 7: k_gamma_simple<6, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    case 7: k_gamma_simple<6, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
                     // measured on MI355X after the per-test parameter hoist (cfg2 pass, tools/ab_gamma.py):
                     // <5,3> 1.236 ms, <8,2> 1.260, <6,3> (VGPR spills) 1.306
-                    default: k_gamma_simple<5, 3, true><<<g, F_THREADS, 0, ctx->stream>>>(B); break;
+                    default: k_gamma_simple<5, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
                 }
             };
             launch(A, 0, va);
