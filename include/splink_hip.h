@@ -200,6 +200,8 @@ int spk_gammas_deferred(spk_ctx *ctx, int64_t *out);
 /* Per comparison column: pairs the last spk_gammas could not decide from bounds in the filter pass
  * and evaluated with the exact similarity (out[n], n >= number of columns). */
 int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
+/* Diagnostics: the first n pair ordinals of column k's exact list of the last spk_gammas (host). */
+int spk_gammas_exact_list(spk_ctx *ctx, int k, int32_t *out, int64_t n);
 /* Per comparison column: pairs of the last spk_gammas whose level the filter took from the blocking
  * key instead of the rows -- a rule built by spk_key_build whose key includes the plain term
  * `l.c = r.c` on the raw columns the column was decoded from (spk_table_add_raw_utf8) emits only

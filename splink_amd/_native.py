@@ -46,7 +46,7 @@ EXPORTS = [
     "spk_pairs_count", "spk_pairs_copy", "spk_pairs_load", "spk_gammas", "spk_gammas_copy", "spk_gammas_load",
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
-    "spk_gammas_set_simple", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
+    "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs",
 ]
@@ -302,6 +302,12 @@ class Context:
         out = np.zeros(max(K, 1), dtype=np.int64)
         check(self._lib.spk_gammas_exact_counts(self._h, _ptr(out), ctypes.c_int(len(out))), "spk_gammas_exact_counts")
         return out[:K].tolist()
+
+    def gammas_exact_list(self, k: int, n: int):
+        out = np.empty(int(n), dtype=np.int32)
+        check(self._lib.spk_gammas_exact_list(self._h, ctypes.c_int(k), _ptr(out), ctypes.c_int64(int(n))),
+              "spk_gammas_exact_list")
+        return out
 
     def gammas_implied_pairs(self, K: int):
         out = np.zeros(max(K, 1), dtype=np.int64)

@@ -2424,7 +2424,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 const size_t shm = (size_t)B.n_thr * sizeof(int16_t);
                 switch (buf ? ctx->filter_waves : -1) {  // (waves per SIMD the filter is compiled for, pairs per lane)
                     case -1: k_gamma_simple<6, 3, false><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    case 1: k_gamma_simple<1, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    case 1: k_gamma_simple<4, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
                     case 2: k_gamma_simple<6, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
                     case 3: k_gamma_simple<5, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
                     case 4: k_gamma_simple<8, 2, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
@@ -2590,6 +2590,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     ctx->mpat_valid = false;
     ctx->last_deferred = n_slow;
     ctx->last_exact.assign(counts.begin(), counts.begin() + K);
+    ctx->last_xbase.assign(ctx->h_info, ctx->h_info + K);
     ctx->last_implied.assign((size_t)K, 0);
     for (const SimpleCol &sc : simple) ctx->last_implied[sc.k] = sc.imp_hi - sc.imp_lo;
     return SPK_OK;
@@ -2781,6 +2782,15 @@ extern "C" int spk_n_patterns(spk_ctx *ctx, int64_t *out) {
 extern "C" int spk_gammas_deferred(spk_ctx *ctx, int64_t *out) {
     SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
     *out = ctx->last_deferred;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_exact_list(spk_ctx *ctx, int k, int32_t *out, int64_t n) {
+    SPK_REQUIRE(ctx && out && k >= 0 && k < (int)ctx->last_exact.size() && n >= 0, SPK_E_INVALID,
+                "spk_gammas_exact_list: bad args");
+    const int64_t m = std::min<int64_t>(n, ctx->last_exact[k]);
+    if (m > 0)
+        SPK_HIP(hipMemcpy(out, ctx->xlist.p + ctx->last_xbase[k], (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost));
     return SPK_OK;
 }
 

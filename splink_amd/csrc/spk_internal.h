@@ -239,6 +239,7 @@ struct spk_ctx {
     bool codes_valid = false;
     int64_t last_deferred = 0;
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
+    std::vector<int64_t> last_xbase;  // per column: start of its exact list in xlist (diagnostics)
     std::vector<int64_t> last_implied;  // per column: pairs whose level the blocking key implied
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)

@@ -465,6 +465,18 @@ __device__ inline uint64_t eq_plane(uint64_t eq, uint32_t mb, uint64_t pl) {
            eq_plane((uint32_t)eq, mb, (uint32_t)pl);
 }
 
+// The score D[m][j+1] is not carried through the scan: after text unit j the vertical deltas give
+// it as (j + 1) + popc(VP & M) - popc(VN & M) (row 0 is D[0][j+1] = j + 1, M the pattern's m rows),
+// so it is computed only where the cut is tested (every fourth unit) and once at the end.
+template <typename W>
+__device__ inline int popc_w(W x) {
+    return sizeof(W) == 4 ? __builtin_popcount((uint32_t)x) : __builtin_popcountll((unsigned long long)x);
+}
+template <typename W>
+__device__ inline W low_mask(int m) {  // bits [0, m), 1 <= m <= bits of W
+    return m >= (int)(8 * sizeof(W)) ? ~(W)0 : (((W)1 << m) - 1);
+}
+
 template <typename W>
 __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
                                        int cut) {
@@ -472,8 +484,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
     W vp = ~(W)0, vn = 0;
-    const W hib = (W)1 << (m - 1);
-    int dist = m;
+    const W M = low_mask<W>(m);
     for (int h = 0; h < 2 && 32 * h < n; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -486,20 +497,21 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
                 eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), pl[b]);
             const W x = eq | vn;
             const W d0 = (((x & vp) + vp) ^ vp) | x;
-            W hp = vn | ~(d0 | vp);
-            W hn = d0 & vp;
-            dist += (hp & hib) ? 1 : 0;
-            dist -= (hn & hib) ? 1 : 0;
+            const W hp = (vn | ~(d0 | vp)) << 1 | (W)1;
+            const W hn = (d0 & vp) << 1;
+            vp = hn | ~(d0 | hp);
+            vn = hp & d0;
             // The bound dist - (units left) never decreases and ends at dist, so testing it every
             // fourth unit plus clamping at the end returns cut + 1 for exactly the cells a per-unit
             // test cuts.
-            if ((jj & 3) == 3 && dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
-            hp = (hp << 1) | (W)1;
-            hn = hn << 1;
-            vp = hn | ~(d0 | hp);
-            vn = hp & d0;
+            if ((jj & 3) == 3) {
+                const int j = 32 * h + jj;
+                const int dist = j + 1 + popc_w(vp & M) - popc_w(vn & M);
+                if (dist - (n - 1 - j) > cut) return cut + 1;
+            }
         }
     }
+    const int dist = n + popc_w(vp & M) - popc_w(vn & M);
     return dist > cut ? cut + 1 : dist;
 }
 
@@ -530,9 +542,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
         tw[b] = (uint32_t)T[b];
     }
     uint32_t vp = ~0u, vn = 0;
-    const int tb = wide ? 31 : m - 1;
-    const uint32_t hib = 1u << tb;
-    int dist = tb + 1;
+    const uint32_t M1 = low_mask<uint32_t>(wide ? 32 : m);  // the rows the first phase scores
     const int j1 = n < J0 ? n : J0;
     for (int j = 0; j < j1; ++j) {
         uint32_t eq = ~0u;
@@ -540,19 +550,22 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
         for (int b = 0; b < N_PLANES; ++b) eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], j, 1), pl[b]);
         const uint32_t x = eq | vn;
         const uint32_t d0 = (((x & vp) + vp) ^ vp) | x;
-        uint32_t hp = vn | ~(d0 | vp);
-        const uint32_t hn = d0 & vp;
-        dist += (hp & hib) ? 1 : 0;
-        dist -= (hn & hib) ? 1 : 0;
-        if (!wide && (j & 3) == 3 && dist - (n - 1 - j) > cut) return cut + 1;
-        hp = (hp << 1) | 1u;
-        vp = (hn << 1) | ~(d0 | hp);
+        const uint32_t hp = (vn | ~(d0 | vp)) << 1 | 1u;
+        const uint32_t hn = (d0 & vp) << 1;
+        vp = hn | ~(d0 | hp);
         vn = hp & d0;
+        if (!wide && (j & 3) == 3) {
+            const int dist = j + 1 + popc_w(vp & M1) - popc_w(vn & M1);
+            if (dist - (n - 1 - j) > cut) return cut + 1;
+        }
     }
-    if (wide) dist += m - 32;
-    if (n <= J0) return dist > cut ? cut + 1 : dist;
+    if (n <= J0) {
+        const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 32 : 0);
+        return dist > cut ? cut + 1 : dist;
+    }
+    // rows 33..m enter with vertical deltas +1 (D[32][J0] + (i - 32))
     uint64_t VP = (uint64_t)vp | 0xFFFFFFFF00000000ull, VN = vn;
-    const uint64_t HIB = 1ull << (m - 1);
+    const uint64_t M2 = low_mask<uint64_t>(m);
     for (int h = J0 >> 5; h < 2 && 32 * h < n; ++h) {
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
@@ -565,16 +578,18 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
                 eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), P[b]);
             const uint64_t x = eq | VN;
             const uint64_t d0 = (((x & VP) + VP) ^ VP) | x;
-            uint64_t hp = VN | ~(d0 | VP);
-            const uint64_t hn = d0 & VP;
-            dist += (hp & HIB) ? 1 : 0;
-            dist -= (hn & HIB) ? 1 : 0;
-            if ((jj & 3) == 3 && dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;
-            hp = (hp << 1) | 1ull;
-            VP = (hn << 1) | ~(d0 | hp);
+            const uint64_t hp = (VN | ~(d0 | VP)) << 1 | 1ull;
+            const uint64_t hn = (d0 & VP) << 1;
+            VP = hn | ~(d0 | hp);
             VN = hp & d0;
+            if ((jj & 3) == 3) {
+                const int j = 32 * h + jj;
+                const int dist = j + 1 + popc_w(VP & M2) - popc_w(VN & M2);
+                if (dist - (n - 1 - j) > cut) return cut + 1;
+            }
         }
     }
+    const int dist = n + popc_w(VP & M2) - popc_w(VN & M2);
     return dist > cut ? cut + 1 : dist;
 }
 
@@ -630,11 +645,14 @@ __device__ inline int clz128(u128 v) {
     return hi ? __clzll((long long)hi) : (lo ? 64 + __clzll((long long)lo) : 128);
 }
 
+__device__ inline int popc128(u128 x) {
+    return __builtin_popcountll((unsigned long long)x) + __builtin_popcountll((unsigned long long)(x >> 64));
+}
+
 __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
                                           int cut) {
     u128 vp = ~(u128)0, vn = 0;
-    const u128 hib = (u128)1 << (m - 1);
-    int dist = m;
+    const u128 M = m >= 128 ? ~(u128)0 : (((u128)1 << m) - 1);  // score from the deltas, as in myers_plane_text
     for (int h = 0; h < 4 && 32 * h < n; ++h) {  // text units [32h, 32h + 32)
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -650,17 +668,18 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
             }
             const u128 x = (((u128)e1 << 64) | e0) | vn;
             const u128 d0 = (((x & vp) + vp) ^ vp) | x;
-            u128 hp = vn | ~(d0 | vp);
-            u128 hn = d0 & vp;
-            dist += (hp & hib) ? 1 : 0;
-            dist -= (hn & hib) ? 1 : 0;
-            if ((jj & 3) == 3 && dist - (n - 1 - (32 * h + jj)) > cut) return cut + 1;  // as in myers_plane_text
-            hp = (hp << 1) | (u128)1;
-            hn = hn << 1;
+            const u128 hp = (vn | ~(d0 | vp)) << 1 | (u128)1;
+            const u128 hn = (d0 & vp) << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
+            if ((jj & 3) == 3) {  // as in myers_plane_text
+                const int j = 32 * h + jj;
+                const int dist = j + 1 + popc128(vp & M) - popc128(vn & M);
+                if (dist - (n - 1 - j) > cut) return cut + 1;
+            }
         }
     }
+    const int dist = n + popc128(vp & M) - popc128(vn & M);
     return dist > cut ? cut + 1 : dist;
 }
 

@@ -28,4 +28,6 @@ for mode in MODES:
     g = job.gammas_host()
     if ref is None:
         ref = g
-    print(f"mode {mode}: gamma pass {np.median(ts):.3f} ms (min {min(ts):.3f}), same as first: {(g == ref).all()}", flush=True)
+    cells = job.ctx.gammas_exact_counts(len(COLS))
+    print(f"mode {mode}: gamma pass {np.median(ts):.3f} ms (min {min(ts):.3f}), same as first: {(g == ref).all()}, "
+          f"exact cells {cells}", flush=True)
