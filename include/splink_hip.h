@@ -258,6 +258,15 @@ int spk_score(spk_ctx *ctx, double lambda, double one_minus, const double *m, co
  * pairs with equal non-null values, Σ mp and count(mp) per value id (n_values slots). */
 int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
                       double *out_sum, int64_t *out_count);
+/* The same with the value ids taken on the device from a string column's dictionary ids (columns
+ * added with spk_table_add_raw_utf8: dense in [0, n_values), one id space for both sides, NULL
+ * rows excluded), so no host-side factorisation of the tf column is needed.  spk_tf_column_values
+ * gives n_values (SPK_E_STATE for a column without device ids). */
+int spk_tf_column_values(spk_ctx *ctx, int col, int64_t *out_n_values);
+int spk_tf_accumulate_column(spk_ctx *ctx, int col, int64_t n_values, double *out_sum, int64_t *out_count);
+int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *cols, const double *const *adj_tables,
+                         const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
+                         double *out_adj /* [count x n_tf_cols] or NULL */);
 /* tf_adjusted_match_prob = bayes(mp, adj_1, ..., adj_n) (:98-117) with adj_c = table_c[id] for pairs
  * with equal non-null values and 0.5 otherwise.  out (host) [start, start+count). */
 int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0, const int64_t *const *ids_side1,

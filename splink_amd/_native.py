@@ -48,7 +48,7 @@ EXPORTS = [
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
     "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
-    "spk_gammas_implied_pairs",
+    "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
 ]
 
 
@@ -382,6 +382,31 @@ class Context:
         check(self._lib.spk_tf_accumulate(self._h, ctypes.c_int64(n_values), _ptr(ids0), _ptr(ids1), _ptr(s), _ptr(c)),
               "spk_tf_accumulate")
         return s[:n_values], c[:n_values]
+
+    def tf_column_values(self, col: int) -> int:
+        n = ctypes.c_int64(0)
+        check(self._lib.spk_tf_column_values(self._h, ctypes.c_int(col), ctypes.byref(n)), "spk_tf_column_values")
+        return n.value
+
+    def tf_accumulate_column(self, col: int, n_values: int):
+        s = np.zeros(max(n_values, 1), dtype=np.float64)
+        c = np.zeros(max(n_values, 1), dtype=np.int64)
+        check(self._lib.spk_tf_accumulate_column(self._h, ctypes.c_int(col), ctypes.c_int64(n_values), _ptr(s), _ptr(c)),
+              "spk_tf_accumulate_column")
+        return s[:n_values], c[:n_values]
+
+    def tf_apply_columns(self, cols, tables, start, count, want_adj=True):
+        n = len(tables)
+        keep = [np.ascontiguousarray(t, dtype=np.float64) if len(t) else np.zeros(1) for t in tables]
+        tabs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in keep])
+        sizes = np.array([len(t) for t in tables], dtype=np.int64)
+        cols = np.ascontiguousarray(cols, dtype=np.int32)
+        out = np.empty(count, dtype=np.float64)
+        adj = np.empty((count, n), dtype=np.float64) if want_adj else None
+        check(self._lib.spk_tf_apply_columns(self._h, ctypes.c_int(n), _ptr(cols), tabs, _ptr(sizes),
+                                             ctypes.c_int64(start), ctypes.c_int64(count), _ptr(out), _ptr(adj)),
+              "spk_tf_apply_columns")
+        return out, adj
 
     def tf_apply(self, ids0_list, ids1_list, tables, start, count, want_adj=True):
         n = len(tables)

@@ -621,6 +621,113 @@ extern "C" int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *
     return SPK_OK;
 }
 
+// Term-frequency value ids straight from a string column's dictionary ids (spk_table_add_raw_utf8:
+// dense, one id space for both sides, equal iff the strings are): NULL rows get -1.  No host-side
+// factorisation of the column's values.
+__global__ void k_ids_from_meta(int64_t n, const RecMeta *__restrict__ meta, int64_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = meta[i].len16 < 0 ? -1 : (int64_t)meta[i].key;
+}
+
+static int column_ids(spk_ctx *ctx, Table &t, int col, DevBuf<int64_t> &out, int64_t *n_ids) {
+    SPK_REQUIRE(col >= 0 && col < (int)t.cols.size() && t.cols[col] && t.cols[col]->kind == COL_STR &&
+                    t.cols[col]->n_ids >= 0,
+                SPK_E_STATE, "tf: the column carries no device dictionary ids (spk_table_add_raw_utf8)");
+    *n_ids = t.cols[col]->n_ids;
+    SPK_TRY(out.alloc((size_t)t.n + 1));
+    if (t.n) k_ids_from_meta<<<(unsigned)((t.n + 255) / 256), 256, 0, ctx->stream>>>(t.n, t.cols[col]->meta.p, out.p);
+    SPK_HIP(hipGetLastError());
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_column_values(spk_ctx *ctx, int col, int64_t *out_n_values) {
+    SPK_REQUIRE(ctx && out_n_values, SPK_E_INVALID, "spk_tf_column_values: null arg");
+    Table &t = ctx->table[0];
+    SPK_REQUIRE(col >= 0 && col < (int)t.cols.size() && t.cols[col] && t.cols[col]->kind == COL_STR &&
+                    t.cols[col]->n_ids >= 0,
+                SPK_E_STATE, "spk_tf_column_values: the column carries no device dictionary ids");
+    *out_n_values = t.cols[col]->n_ids;
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_accumulate_column(spk_ctx *ctx, int col, int64_t n_values, double *out_sum, int64_t *out_count) {
+    SPK_REQUIRE(ctx && out_sum && out_count && n_values >= 0, SPK_E_INVALID, "spk_tf_accumulate_column: bad args");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_accumulate_column: run spk_score over all pairs first");
+    SPK_HIP(hipSetDevice(ctx->device));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0, d1;
+    int64_t n0 = 0, n1 = 0;
+    SPK_TRY(column_ids(ctx, t0, col, d0, &n0));
+    if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, col, d1, &n1));
+    SPK_REQUIRE(n_values == n0, SPK_E_INVALID, "spk_tf_accumulate_column: n_values is not the column's value count");
+    DevBuf<double> ds;
+    DevBuf<unsigned long long> dc;
+    SPK_TRY(ds.alloc((size_t)n_values + 1));
+    SPK_TRY(dc.alloc((size_t)n_values + 1));
+    SPK_HIP(hipMemsetAsync(ds.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
+    SPK_HIP(hipMemsetAsync(dc.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
+    const int64_t P = ctx->n_pairs;
+    if (P)
+        k_tf_accumulate<<<(unsigned)((P + 255) / 256), 256, 0, ctx->stream>>>(
+            P, ctx->pl.p, ctx->pr.p, d0.p, &t1 != &t0 ? d1.p : d0.p, ctx->mp.p, n_values, ds.p, dc.p);
+    SPK_HIP(hipGetLastError());
+    if (n_values) {
+        SPK_HIP(hipMemcpyAsync(out_sum, ds.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(out_count, dc.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+static int tf_apply_dev(spk_ctx *ctx, TfApply &T, const double *const *adj_tables, const int64_t *table_sizes,
+                        int64_t start, int64_t count, double *out_tf_mp, double *out_adj) {
+    DevBuf<double> dt[8], dout, dadj;
+    for (int c = 0; c < T.n; ++c) {
+        SPK_TRY(dt[c].alloc((size_t)table_sizes[c] + 1));
+        if (table_sizes[c])
+            SPK_HIP(hipMemcpyAsync(dt[c].p, adj_tables[c], (size_t)table_sizes[c] * 8, hipMemcpyHostToDevice,
+                                   ctx->stream));
+        T.tab[c] = dt[c].p;
+        T.tab_n[c] = table_sizes[c];
+    }
+    SPK_TRY(dout.alloc((size_t)count + 1));
+    if (out_adj) SPK_TRY(dadj.alloc((size_t)count * T.n + 1));
+    if (count)
+        k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
+                                                                         ctx->mp.p, dout.p,
+                                                                         out_adj ? dadj.p : nullptr);
+    SPK_HIP(hipGetLastError());
+    if (count) {
+        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (out_adj)
+            SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * T.n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *cols, const double *const *adj_tables,
+                                    const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
+                                    double *out_adj) {
+    SPK_REQUIRE(ctx && cols && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID,
+                "spk_tf_apply_columns: 1..8 columns");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply_columns: run spk_score first");
+    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply_columns: range");
+    SPK_HIP(hipSetDevice(ctx->device));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0[8], d1[8];
+    TfApply T{};
+    T.n = n_tf_cols;
+    for (int c = 0; c < n_tf_cols; ++c) {
+        int64_t n0 = 0, n1 = 0;
+        SPK_TRY(column_ids(ctx, t0, cols[c], d0[c], &n0));
+        if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, cols[c], d1[c], &n1));
+        T.ids0[c] = d0[c].p;
+        T.ids1[c] = &t1 != &t0 ? d1[c].p : d0[c].p;
+    }
+    return tf_apply_dev(ctx, T, adj_tables, table_sizes, start, count, out_tf_mp, out_adj);
+}
+
 extern "C" int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0,
                             const int64_t *const *ids_side1, const double *const *adj_tables,
                             const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,

@@ -912,7 +912,7 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
 // evaluating any: the pass is bound by the latency of those gathers, so every round trip is
 // shared by F_PAIRS pairs.  The column loop is uniform across the wave, so the class dispatch and
 // the test parameters are scalar.
-template <int MINW, int FP, bool BUF>
+template <int MINW, int FP, bool BUF, bool LOCAL = false>
 __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
     __shared__ unsigned int s_cnt[MAX_SIMPLE];
     extern __shared__ int16_t s_thr[];  // A.thr (dynamic LDS: n_thr entries)
@@ -953,8 +953,8 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
         for (int u = 0; u < FP; ++u) {
             p[u] = base + u * 64 + lane;
             act[u] = p[u] < R.r1;
-            ox[u] = (uint32_t)nx[u] << 4;
-            oy[u] = (uint32_t)ny[u] << 4;
+            ox[u] = LOCAL ? (uint32_t)(nx[u] & 255) << 4 : (uint32_t)nx[u] << 4;  // LOCAL: timing experiment only
+            oy[u] = LOCAL ? (uint32_t)(ny[u] & 255) << 4 : (uint32_t)ny[u] << 4;
             acc[u] = 0;
             const int64_t q = p[u] + STEP;
             nx[u] = q < R.r1 ? A.pl[q] : 0;
@@ -2433,6 +2433,8 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                     // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
                     // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
                     case 7: k_gamma_simple<6, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
+                    // timing experiment (wrong results): every gather hits the image's first 256 rows
+                    case 9: k_gamma_simple<5, 3, true, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
                     // measured on MI355X after the per-test parameter hoist (cfg2 pass, tools/ab_gamma.py):
                     // <5,3> 1.236 ms, <8,2> 1.260, <6,3> (VGPR spills) 1.306
                     default: k_gamma_simple<5, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
@@ -2808,11 +2810,13 @@ extern "C" int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n) {
 
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    const bool local = on >= 1000;  // + 1000: timing experiment, gathers kept local (wrong results)
+    on %= 1000;
     ctx->use_views = on >= 20 ? 2 : (on >= 10 ? 0 : 1);  // + 10: never view launches, + 20: always (A/B, tests)
     on %= 10;
     ctx->simple_columns = on != 0;
     ctx->row_filter = on == 2;
-    ctx->filter_waves = on >= 3 ? on - 2 : 0;  // A/B variants of the filter (tools/ab_gamma.py; 8 = flat loads)
+    ctx->filter_waves = local ? 9 : (on >= 3 ? on - 2 : 0);  // A/B variants of the filter (tools/ab_gamma.py)
     return SPK_OK;
 }
 

@@ -556,6 +556,7 @@ int spk_table_add_raw_utf8(spk_ctx *ctx, int col, int raw0, int raw1) {
         SPK_TRY(new_column(ctx, side, col, &c));
         c->kind = COL_STR;
         c->has_ids = true;
+        c->n_ids = n_ids;
         c->src[0] = ctx->raw[raw0]->serial;
         c->src[1] = ctx->raw[two ? raw1 : raw0]->serial;
         c->has_empty = ctx->raw[raw0]->has_empty || (two && ctx->raw[raw1]->has_empty);

@@ -144,6 +144,7 @@ struct Column {
     int64_t max_bytes = 0; // COL_STR: longest row in UTF-8 bytes (>= its UTF-16 units)
     uint64_t src[2] = {0, 0};  // spk_table_add_raw_utf8: serials of the raw columns of the l / r side (0: other)
     bool has_empty = false;    // some non-NULL row is the empty string
+    int64_t n_ids = -1;        // spk_table_add_raw_utf8: distinct non-NULL values (ids are dense in [0, n_ids))
 };
 
 // A blocking-key term as spk_key_build saw it, by raw-column serial: the comparison filter skips a

@@ -71,15 +71,25 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
     df_e.gammas.ensure_codes()
     job.score(df_e.lam, df_e.level_probs, want_host=False)  # device mp for exactly this df_e
     one_minus = float(1 - params.params["λ"])
+    # value ids: the device dictionary ids of the string column when the job decoded it on the device
+    # (no host pass over the values), else a joint host factorisation
+    dev_cols = [job._col_index.get((c, "str")) for c in tf_cols]
+    on_device = all(i is not None for i in dev_cols)
     ids0_list, ids1_list, tables = [], [], []
-    for c in tf_cols:
-        sides = (0, 1) if job.link_type == "link_only" else (0,)
-        vals = [pd.Series([None if T.is_null_scalar(v) else v for v in job.host_values(s, c).tolist()], dtype=object)
-                for s in sides]
-        codes, n_values = T.factorize_joint(vals)
-        ids0 = codes[0]
-        ids1 = codes[1] if len(codes) > 1 else codes[0]
-        sums, counts = job.ctx.tf_accumulate(n_values, ids0, ids1)
+    for c, col in zip(tf_cols, dev_cols):
+        if on_device:
+            n_values = job.ctx.tf_column_values(col)
+            sums, counts = job.ctx.tf_accumulate_column(col, n_values)
+        else:
+            sides = (0, 1) if job.link_type == "link_only" else (0,)
+            vals = [pd.Series([None if T.is_null_scalar(v) else v for v in job.host_values(s, c).tolist()],
+                              dtype=object) for s in sides]
+            codes, n_values = T.factorize_joint(vals)
+            ids0 = codes[0]
+            ids1 = codes[1] if len(codes) > 1 else codes[0]
+            sums, counts = job.ctx.tf_accumulate(n_values, ids0, ids1)
+            ids0_list.append(ids0)
+            ids1_list.append(ids1)
         if job.reduces_across_ranks():
             # the reference groups over ALL pairs (:49-65); each rank holds one shard of them
             D.allreduce_host_(sums)
@@ -87,7 +97,8 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
         with np.errstate(invalid="ignore", divide="ignore"):
             adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
         tables.append(_bayes_pair(adj_lambda, one_minus))
-        ids0_list.append(ids0)
-        ids1_list.append(ids1)
-    tf_mp, adj = job.ctx.tf_apply(ids0_list, ids1_list, tables, 0, job.n_pairs, want_adj=True)
+    if on_device:
+        tf_mp, adj = job.ctx.tf_apply_columns(dev_cols, tables, 0, job.n_pairs, want_adj=True)
+    else:
+        tf_mp, adj = job.ctx.tf_apply(ids0_list, ids1_list, tables, 0, job.n_pairs, want_adj=True)
     return TermFrequencyFrame(df_e, settings, tf_cols, tf_mp, adj, retain_adjustment_columns)

@@ -2,6 +2,7 @@
 never bench.py's headline).
 
     python tools/full_job.py --records 20000000 --shard 0/8 [--iters 10] [--sample 2000000] [--out FILE]
+    python tools/full_job.py --config 3 --records 10000000 --shard 0/8 ...   (link_only 2 x 10M + tf)
 
 The job is BASELINE configs[3]'s per-GPU share: a 20M-record synthetic dedupe (blocking surname | dob,
 the five cfg2 comparison columns) whose candidate-pair ordinals are split over 8 GPUs; this process is
@@ -15,6 +16,13 @@ pass (first call: column upload + device decode), 10 EM iterations (histogram + 
 M-step), the final scoring pass.  Parity: every comparison vector of a strided sample of pairs against
 oracle.template_gammas, and the 10 EM iterations of λ / m / u plus the final match probabilities of
 all of this shard's pairs against oracle.em_iterate (1e-9).
+
+--config 3 is BASELINE configs[2]'s per-GPU share: link_only between two synthetic tables of
+`--records` rows each (one 2 x records population split in halves, so duplicates straddle them),
+rules surname | dob | email, the five cfg2 columns, and the term-frequency
+adjustment on surname after EM (device dictionary ids as tf value ids; timed as `tf_adjust`).  Its
+parity adds every pair's tf_adjusted_match_prob against a numpy restatement of
+term_frequencies.py:49-117 over host-factorised values (1e-9).
 """
 from __future__ import annotations
 
@@ -47,6 +55,7 @@ def main():
     ap.add_argument("--sample", type=int, default=2_000_000, help="pairs in the strided gamma parity sample")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--out")
+    ap.add_argument("--config", type=int, default=4, choices=[3, 4])
     a = ap.parse_args()
     shard, n_shards = (int(x) for x in a.shard.split("/"))
 
@@ -58,16 +67,26 @@ def main():
     from splink_amd.synthetic import cfg_settings, make_records
 
     t0 = time.time()
-    df = make_records(a.records, surname_vocab=a.surname_vocab, arrow=True)[["unique_id"] + COLS]
+    link = a.config == 3
+    df = make_records(a.records * (2 if link else 1), surname_vocab=a.surname_vocab, arrow=True)[["unique_id"] + COLS]
+    inputs = [df.iloc[:a.records].reset_index(drop=True), df.iloc[a.records:].reset_index(drop=True)] if link else [df]
+    del df
     gen_s = time.time() - t0
-    log(f"generated {a.records} records in {gen_s:.1f}s")
-    params = Params(cfg_settings(4, max_iterations=a.iters), AmdSession(0))
+    log(f"generated {a.records} records x {len(inputs)} in {gen_s:.1f}s")
+    settings = cfg_settings(4, max_iterations=a.iters)
+    if link:
+        settings["link_type"] = "link_only"
+        settings["blocking_rules"] = ["l.surname = r.surname", "l.dob = r.dob", "l.email = r.email"]
+        for c in settings["comparison_columns"]:
+            if c["col_name"] == "surname":
+                c["term_frequency_adjustments"] = True
+    params = Params(settings, AmdSession(0))
     st = params.settings
 
     wall = {}
     t_job = time.perf_counter()
     t = time.perf_counter()
-    job = Job("dedupe_only", [df], "unique_id", 0, shard=(shard, n_shards))
+    job = Job(st["link_type"], inputs, "unique_id", 0, shard=(shard, n_shards))
     job.ctx.enable_timing(True)
     wall["job_setup_incl_uid_rank"] = time.perf_counter() - t
     t = time.perf_counter()
@@ -81,6 +100,9 @@ def main():
     wall["gammas_first_call_incl_column_decode"] = time.perf_counter() - t
     gamma_dev = job.ctx.kernel_ms()["gamma"]
     names, nlev = job.code_meta
+    exact_cells = dict(zip(names, job.ctx.gammas_exact_counts(len(names))))
+    job.gammas(st)  # a second pass (row images built, lists sized): the per-pass device time
+    gamma_warm = job.ctx.kernel_ms()["gamma"]
     lam0, lp0 = params.params["λ"], params._level_probabilities()
     t = time.perf_counter()
     em_dev = []
@@ -96,18 +118,33 @@ def main():
     torch.cuda.synchronize()
     wall["score"] = time.perf_counter() - t
     score_dev = job.ctx.kernel_ms()["score"]
+    tf_mp = None
+    if link:  # term-frequency adjustment on surname (term_frequencies.py:122-168), device value ids
+        from splink_amd.term_frequencies import _bayes_pair
+        t = time.perf_counter()
+        col = job._col_index[("surname", "str")]
+        n_values = job.ctx.tf_column_values(col)
+        sums, counts = job.ctx.tf_accumulate_column(col, n_values)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
+        table = _bayes_pair(adj_lambda, float(1 - params.params["λ"]))
+        tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
+        wall["tf_adjust"] = time.perf_counter() - t
     total = time.perf_counter() - t_job
     P = job.n_pairs
     row = {
         "row": "full job, one GPU (separately labelled; never the headline)",
-        "workload": f"cfg4 per-GPU share: {a.records} records, blocking surname|dob, 5 columns, "
-                    f"pair-ordinal shard {shard}/{n_shards}",
+        "workload": (f"cfg3 per-GPU share: link_only {a.records} x {a.records} records, blocking surname|dob|email, "
+                     f"5 columns, tf on surname, pair-ordinal shard {shard}/{n_shards}") if link else
+                    (f"cfg4 per-GPU share: {a.records} records, blocking surname|dob, 5 columns, "
+                     f"pair-ordinal shard {shard}/{n_shards}"),
         "records": a.records, "candidates_total": int(job.n_candidates), "pairs_this_gpu": int(P),
         "iterations": a.iters, "wall_s": wall, "job_wall_s": total,
-        "device_ms": {"block": block_dev, "gamma_pass": gamma_dev, "em_per_iter_mean": float(np.mean(em_dev)),
-                      "score": score_dev},
+        "device_ms": {"block": block_dev, "gamma_pass_first": gamma_dev, "gamma_pass": gamma_warm,
+                      "em_per_iter_mean": float(np.mean(em_dev)), "score": score_dev},
+        "exact_cells_per_column": exact_cells,
         "pairs_per_s_job": P / total,
-        "pairs_per_s_gamma_plus_em_iter": P / ((gamma_dev + float(np.mean(em_dev))) / 1e3),
+        "pairs_per_s_gamma_plus_em_iter": P / ((gamma_warm + float(np.mean(em_dev))) / 1e3),
         "generation_s_excluded": gen_s,
         "lambda_final": params.params["λ"],
     }
@@ -119,10 +156,19 @@ def main():
         idx = np.arange(0, P, step)
         sl, sr = l[idx], r[idx]
         rows_used, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
-        table = job.tables[0]
-        sub = table.take(rows_used)
-        ocols = [orc.StrCol(sub[c].tolist()) for c in COLS]
-        ref = orc.template_gammas(SPECS, ocols, ocols, inv[:len(sl)].astype(np.int32), inv[len(sl):].astype(np.int32))
+        if link:  # rows index the two tables separately
+            tl, tr = job.tables[0], job.r_table()
+            ul, il = np.unique(sl, return_inverse=True)
+            ur, ir = np.unique(sr, return_inverse=True)
+            ocl = [orc.StrCol(tl.take(ul)[c].tolist()) for c in COLS]
+            ocr = [orc.StrCol(tr.take(ur)[c].tolist()) for c in COLS]
+            ref = orc.template_gammas(SPECS, ocl, ocr, il.astype(np.int32), ir.astype(np.int32))
+        else:
+            table = job.tables[0]
+            sub = table.take(rows_used)
+            ocols = [orc.StrCol(sub[c].tolist()) for c in COLS]
+            ref = orc.template_gammas(SPECS, ocols, ocols, inv[:len(sl)].astype(np.int32),
+                                      inv[len(sl):].astype(np.int32))
         gam = job.gammas_host()
         bad = int((gam[idx] != ref).any(axis=1).sum())
         row["parity_gamma"] = {"sampled_pairs": int(len(idx)), "stride": int(step), "mismatches": bad}
@@ -136,12 +182,48 @@ def main():
         mp_ok = bool(np.allclose(mp_dev, mp_o, rtol=1e-9, atol=0, equal_nan=True))
         row["parity_em"] = {"iterations": len(hist_o), "lambda_m_u_1e-9": bool(ok), "match_probability_1e-9": mp_ok,
                             "pairs": int(P)}
+        if link:
+            row["parity_tf"] = tf_parity(job, l, r, mp_dev, params.params["λ"], tf_mp)
         row["parity_check_s"] = time.perf_counter() - t
     out = json.dumps(row)
     print(out, flush=True)
     if a.out:
         with open(a.out, "w") as f:
             f.write(out + "\n")
+
+
+def tf_parity(job, l, r, mp, lam, tf_mp):
+    """term_frequencies.py:49-117 restated with numpy over host-factorised surname values (not the
+    device's dictionary ids): per value v, adj_lambda = mean mp over pairs with surname_l = surname_r
+    = v (NULL mp excluded from sum and count), adj = bayes(adj_lambda, 1 - λ), 0.5 without a lookup,
+    tf_adjusted_match_prob = bayes(mp, adj)."""
+    import pandas as pd
+    vl = job.tables[0]["surname"]
+    vr = job.r_table()["surname"]
+    codes, uniq = pd.factorize(pd.concat([vl, vr], ignore_index=True), use_na_sentinel=True)
+    cl, cr = codes[:len(vl)], codes[len(vl):]
+    a, b = cl[l], cr[r]
+    ok = (a >= 0) & (a == b)
+    good = ok & ~np.isnan(mp)
+    n_v = len(uniq)
+    s = np.bincount(a[good], weights=mp[good], minlength=n_v)
+    c = np.bincount(a[good], minlength=n_v)
+    one_minus = float(repr(1 - lam))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        adj_lambda = np.where(c > 0, s / np.maximum(c, 1), np.nan)
+        tnum = adj_lambda * one_minus
+        tden = tnum + (1 - adj_lambda) * (1 - one_minus)
+        tab = np.where(tden == 0, np.nan, tnum / tden)
+        adj = np.full(len(mp), 0.5)
+        look = tab[np.where(ok, a, 0)]
+        sel = ok & ~np.isnan(look)
+        adj[sel] = look[sel]
+        num = mp * adj
+        den = num + (1 - mp) * (1 - adj)
+        want = np.where(den == 0, np.nan, num / den)
+    same = np.isclose(tf_mp, want, rtol=1e-9, atol=0, equal_nan=True)
+    return {"pairs": int(len(mp)), "pairs_with_equal_surname": int(ok.sum()), "tf_adjusted_match_prob_1e-9": bool(same.all()),
+            "mismatches": int((~same).sum())}
 
 
 if __name__ == "__main__":
