@@ -1600,8 +1600,8 @@ struct ExactCols {
     int si[4];
 };
 
-template <bool LEV>
-__global__ __launch_bounds__(X_THREADS, LEV ? LEV_WAVES : JW_WAVES) void k_gamma_exact_simple(GammaArgs A, ExactCols C,
+template <bool LEV, int XW = (LEV ? LEV_WAVES : JW_WAVES)>
+__global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs A, ExactCols C,
                                                                    const int32_t *xlist, const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
@@ -2320,10 +2320,13 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                  o_llen = put(llen.data(), llen.size()), o_lcp = put(lcp.data(), lcp.size()),
                  o_stride = put(ctx->stride.data(), ctx->stride.size()), o_simple = put(simple.data(), simple.size()),
                  o_complex = put(complex_k.data(), complex_k.size()), o_thr = put(thr_tab.data(), thr_tab.size());
-    const int32_t zero = 0;
-    const size_t o_err = put(&zero, 1);
-    SPK_TRY(ctx->prog_blob.alloc(blob.size()));
-    SPK_HIP(hipMemcpyAsync(ctx->prog_blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, ctx->stream));
+    // the device keeps the last blob: an unchanged program (every call of an EM run) is not re-sent
+    const bool fresh_blob = ctx->prog_blob.p && ctx->prog_blob.n >= blob.size() && ctx->last_blob == blob;
+    if (!fresh_blob) {
+        SPK_TRY(ctx->prog_blob.alloc(blob.size()));
+        SPK_HIP(hipMemcpyAsync(ctx->prog_blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, ctx->stream));
+        ctx->last_blob = blob;
+    }
     uint8_t *base = ctx->prog_blob.p;
     auto at = [&](auto *&dst, size_t off) { dst = reinterpret_cast<std::remove_reference_t<decltype(dst)>>(base + off); };
     const int64_t P = ctx->n_pairs;
@@ -2331,7 +2334,6 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_REQUIRE(P <= (int64_t)INT32_MAX, SPK_E_LIMIT,
                 "spk_gammas: more than 2^31-1 pairs in one context (shard the pair set over more ranks)");
     SPK_TRY(ctx->work.alloc((size_t)K * (size_t)P + 1));
-    SPK_TRY(ctx->work_count.alloc((size_t)(3 * K)));  // slow-list lengths, k_gamma_slow_lev's rest lists, huge lists
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
     // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
     // 20 regions (256-thread workgroups) per CU: four rounds of the 5 resident workgroups a CU holds
@@ -2340,9 +2342,16 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     const int64_t max_regions = 20 * (int64_t)ctx->n_cu;
     const int n_regions = (int)std::max<int64_t>(1, std::min<int64_t>(max_regions, (P + F_THREADS - 1) / F_THREADS));
     const int64_t region_len = ((P + n_regions - 1) / n_regions + 63) / 64 * 64;
+    // every (column, region) count is written by the filter launch that covers the region: no memset
     SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions));
-    SPK_HIP(hipMemsetAsync(ctx->region_count.p, 0, sizeof(unsigned int) * K * n_regions, ctx->stream));
-    SPK_HIP(hipMemsetAsync(ctx->work_count.p, 0, sizeof(unsigned int) * 3 * K, ctx->stream));
+    // One device info block, read back with one copy: xinfo (k_prefix: list bases and counts, overflow,
+    // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed here.
+    const int n_info = 2 * K + 2;
+    const int n_cnt = (3 * K + 1) / 2;  // int64 slots of the 3K uint32 list lengths
+    const int n_all = n_info + n_cnt + 1;
+    SPK_TRY(ctx->xinfo.alloc((size_t)n_all));
+    SPK_TRY(ctx->pinned_info((size_t)n_all));
+    SPK_HIP(hipMemsetAsync(ctx->xinfo.p + n_info, 0, (size_t)(n_cnt + 1) * 8, ctx->stream));
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -2366,14 +2375,14 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     at(A.complex_k, o_complex);
     at(A.thr, o_thr);
     A.n_thr = (int)thr_tab.size();
-    at(A.err, o_err);
+    A.err = reinterpret_cast<int *>(ctx->xinfo.p + n_info + n_cnt);
     A.codes = ctx->codes.p;
     A.code16 = ctx->code_bytes == 2;
     A.work = ctx->work.p;
     A.region_count = ctx->region_count.p;
     A.region_len = region_len;
     A.n_regions = n_regions;
-    A.slow_count = ctx->work_count.p;
+    A.slow_count = reinterpret_cast<unsigned int *>(ctx->xinfo.p + n_info);
     A.n_simple = (int)simple.size();
     A.all_img = 1;
     for (const SimpleCol &sc : simple) A.all_img &= (sc.cls != SC_GEN && sc.cls != SC_NUMRAW) ? 1 : 0;
@@ -2465,10 +2474,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     for (const SimpleCol &sc : simple)
         if (sc.kind == SK_NUM || sc.cls == SC_NUM || sc.cls == SC_NUMRAW || (sc.cls == SC_EQ && sc.has_ids))
             may_exact[sc.k] = 0;
-    const int n_info = 2 * K + 2;
     SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions + 1)));
-    SPK_TRY(ctx->xinfo.alloc((size_t)n_info));
-    SPK_TRY(ctx->pinned_info((size_t)n_info + 2 * K + 1));  // + slow / rest / huge counts (3K uint32) + err word
     int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(P, 1 << 16));
     const int64_t g_exact = std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ctx->n_cu, (P + X_THREADS - 1) / X_THREADS));
     std::vector<char> huge_in_slow(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
@@ -2482,7 +2488,11 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                                                         ctx->xinfo.p);
             // Jaro-Winkler template columns: compact every list, then one exact launch over all of them
             ExactCols jw{};
-            jw.g = (int)g_exact;
+            // JW lists are short (cfg2: 0.1-0.3 M cells): fewer blocks give each lane several cells, so
+            // the next cell's loads overlap the current one's work (the pass is load-latency bound)
+            const int64_t g_jw = ctx->jw_grid > 0
+                ? std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->jw_grid * ctx->n_cu, g_exact)) : g_exact;
+            jw.g = (int)g_jw;
             for (int k = 0; k < K; ++k) {
                 if (!may_exact[k] || simple_of[k] < 0) continue;
                 const SimpleCol &sc = simple[simple_of[k]];
@@ -2494,7 +2504,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             // (running this launch on a second stream beside the Levenshtein pass measured no faster:
             // 1.198-1.205 ms per cfg2 pass either way)
             if (jw.n) {
-                k_gamma_exact_simple<false><<<(unsigned)(g_exact * jw.n), X_THREADS, 0, ctx->stream>>>(
+                k_gamma_exact_simple<false><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
                     A, jw, ctx->xlist.p, ctx->xinfo.p);
                 for (int c = 0; c < jw.n; ++c)
                     k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, simple[jw.si[c]].k, ctx->xlist.p,
@@ -2514,8 +2524,14 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                     one.n = 1;
                     one.g = (int)g_exact;
                     one.si[0] = simple_of[k];
-                    k_gamma_exact_simple<true><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
-                                                                                                ctx->xinfo.p);
+                    switch (ctx->lev_waves) {  // A/B: waves per SIMD the Levenshtein pass is compiled for
+                        case 4: k_gamma_exact_simple<true, 4><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
+                                    A, one, ctx->xlist.p, ctx->xinfo.p); break;
+                        case 6: k_gamma_exact_simple<true, 6><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
+                                    A, one, ctx->xlist.p, ctx->xinfo.p); break;
+                        default: k_gamma_exact_simple<true><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
+                                     A, one, ctx->xlist.p, ctx->xinfo.p); break;
+                    }
                 } else if (!fused && simple_str) {
                     ExactCols one{};
                     one.n = 1;
@@ -2540,10 +2556,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             SPK_HIP(hipMemsetAsync(ctx->xinfo.p, 0, (size_t)n_info * 8, ctx->stream));
         }
         SPK_TRY(ctx->end(K_GAMMA));
-        SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_info * 8, hipMemcpyDeviceToHost, ctx->stream));
-        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info, ctx->work_count.p, sizeof(unsigned int) * 3 * K,
-                               hipMemcpyDeviceToHost, ctx->stream));
-        SPK_HIP(hipMemcpyAsync(ctx->h_info + n_info + 2 * K, A.err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
         SPK_HIP(hipStreamSynchronize(ctx->stream));
         if (!ctx->h_info[2 * K]) break;
         cap = ctx->h_info[2 * K + 1];  // exact lists did not fit: nothing ran, grow and redo the phase
@@ -2558,7 +2571,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         n_slow += h_slow[k];
     }
     int err = 0;
-    std::memcpy(&err, ctx->h_info + n_info + 2 * K, sizeof(err));
+    std::memcpy(&err, ctx->h_info + n_info + n_cnt, sizeof(err));
     SPK_REQUIRE(!(err & 2), SPK_E_INVALID, "spk_gammas: unknown instruction");
     // ---- huge pass: cells with a string longer than SLOW_LIMIT units (none in the benchmark configs)
     int64_t n_huge = 0, max_huge = 0;
@@ -2810,6 +2823,9 @@ extern "C" int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n) {
 
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->jw_grid = on / 100000;  // + G x 100000: the JW exact launch at G blocks per CU and column (A/B)
+    ctx->lev_waves = (on / 10000) % 10;  // + W x 10000: Levenshtein pass at W waves per SIMD (A/B)
+    on %= 10000;
     const bool local = on >= 1000;  // + 1000: timing experiment, gathers kept local (wrong results)
     on %= 1000;
     ctx->use_views = on >= 20 ? 2 : (on >= 10 ? 0 : 1);  // + 10: never view launches, + 20: always (A/B, tests)

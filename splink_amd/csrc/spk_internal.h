@@ -244,6 +244,8 @@ struct spk_ctx {
     std::vector<int64_t> last_implied;  // per column: pairs whose level the blocking key implied
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
+    int lev_waves = 0;                // Levenshtein exact pass variant (waves per SIMD; 0 = LEV_WAVES), A/B
+    int jw_grid = 0;                  // JW exact launch: blocks per CU and column (0 = the exact passes' 8), A/B
     int filter_waves = 0;             // k_gamma_simple variant (waves per SIMD, pairs per lane): 0 = <6,3>; 1..5 A/B
     int use_views = 1;                // rule 1's pairs read a view-ordered row image: 0 never, 1 when the
                                       // image outgrows the caches, 2 always (A/B and tests)
@@ -276,8 +278,8 @@ struct spk_ctx {
     spk::DevBuf<uint8_t> vimg[spk::MAX_VIEWS][2];  // row images in rule-view order (views[r])
     std::vector<int64_t> vimg_key[spk::MAX_VIEWS][2];
     uint64_t table_epoch = 0;
-    spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (one upload per call)
-    spk::DevBuf<unsigned int> work_count;    // [2K] slow-pass list lengths, then slow-Levenshtein rest lists
+    spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (uploaded when they change)
+    std::vector<uint8_t> last_blob;   // host copy of what prog_blob holds
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
     // EM state

@@ -106,6 +106,22 @@ def test_pipeline_matches_reference(name, amd):
         compare_frames(tf, g["df_tf"], g["df_tf_columns"])
 
 
+def test_tf_host_value_ids_match_device_ids(amd):
+    """The tf adjustment keyed by the device dictionary ids (default) and by host-factorised values
+    (the path for columns the job did not decode on the device) give the reference golden."""
+    g = load_golden("link_tf")
+    for host_ids in (False, True):
+        linker = run_linker(g, amd)
+        df_e = linker.get_scored_comparisons()
+        job, saved = df_e.job, df_e.job._col_index
+        if host_ids:  # hide the device-decoded columns from the tf stage only
+            job._col_index = {k: v for k, v in saved.items() if k[1] != "str"}
+        tf_frame = linker.make_term_frequency_adjustments(df_e)
+        job._col_index = saved
+        tf = tf_frame.toPandas()
+        compare_frames(tf, g["df_tf"], g["df_tf_columns"])
+
+
 @pytest.mark.parametrize("case", LINK_CASES)
 def test_link_options_match_reference(case, amd):
     g = load_golden("link_options")[case]

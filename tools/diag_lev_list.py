@@ -96,3 +96,31 @@ for p in sample:
 print(dict(stats))
 for e in ex:
     print(e)
+
+# shape of the exact pass's work: pattern / text lengths after the common prefix / suffix strip,
+# and the longest text of each wave of 64 consecutive list entries (what a wave's scan runs)
+first = lst[: min(len(lst), 64 * 4000)]
+ms, ns = [], []
+for p in first:
+    a, b = em[l[p]], em[r[p]]
+    if a is None or b is None or a == b:
+        ms.append(0)
+        ns.append(0)
+        continue
+    pre = 0
+    while pre < min(len(a), len(b)) and a[pre] == b[pre]:
+        pre += 1
+    suf = 0
+    while suf < min(len(a), len(b)) - pre and a[-1 - suf] == b[-1 - suf]:
+        suf += 1
+    ra, rb = len(a) - pre - suf, len(b) - pre - suf
+    ms.append(max(ra, rb))
+    ns.append(min(ra, rb))
+ms, ns = np.array(ms), np.array(ns)
+wn = ns[: len(ns) // 64 * 64].reshape(-1, 64)
+print("stripped pattern m: mean %.1f p50 %d p90 %d max %d; text n: mean %.1f p50 %d p90 %d" % (
+    ms.mean(), np.median(ms), np.percentile(ms, 90), ms.max(), ns.mean(), np.median(ns), np.percentile(ns, 90)))
+print("wave max n: mean %.1f; sum n / sum wave-max n = %.2f; m > 32: %.3f" % (
+    wn.max(axis=1).mean(), wn.sum() / (wn.max(axis=1).sum() * 64), (ms > 32).mean()))
+lens = np.array([len(em[l[p]]) for p in first if em[l[p]] is not None])
+print("email length mean %.1f" % lens.mean())
