@@ -131,6 +131,59 @@ __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const
     meta[row] = m;
 }
 
+// OR / AND over the units of every plane row of a column (bits 0..7, from the planes: bit b of the
+// OR is set when some unit has bit b, of the AND when every unit has it).  spk_gammas drops the top
+// planes whose bit is the same for every unit of both sides (SimpleCol.np).
+__global__ void k_unit_bits(int64_t n, const RecMeta *__restrict__ meta, const uint64_t *__restrict__ planes,
+                            const uint64_t *__restrict__ planes_hi, unsigned int *__restrict__ out) {
+    __shared__ unsigned int s_or, s_and;
+    if (threadIdx.x == 0) {
+        s_or = 0;
+        s_and = 0xFFu;
+    }
+    __syncthreads();
+    unsigned int o = 0, a = 0xFFu;
+    for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < n; row += (int64_t)gridDim.x * blockDim.x) {
+        const RecMeta m = meta[row];
+        const bool two = (m.cpf & CPF_PLANES2) != 0, one = (m.cpf & CPF_PLANES) != 0;
+        if (m.len16 <= 0 || !(one || two)) continue;
+        const int nu = m.len16;
+        const uint64_t lo_mask = nu >= 64 ? ~0ull : ((1ull << nu) - 1);
+        const uint64_t hi_mask = two ? (nu - 64 >= 64 ? ~0ull : ((1ull << (nu - 64)) - 1)) : 0ull;
+        for (int b = 0; b < N_PLANES; ++b) {
+            const uint64_t p = planes[row * N_PLANES + b], q = two ? planes_hi[row * N_PLANES + b] : 0ull;
+            if (p | q) o |= 1u << b;
+            if ((p & lo_mask) != lo_mask || (q & hi_mask) != hi_mask) a &= ~(1u << b);
+        }
+    }
+    atomicOr(&s_or, o);
+    atomicAnd(&s_and, a);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicOr(&out[0], s_or);
+        atomicAnd(&out[1], s_and);
+    }
+}
+
+int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c) {
+    c->unit_bits = false;
+    if (n <= 0) return SPK_OK;
+    DevBuf<unsigned int> d;
+    SPK_TRY(d.alloc(2));
+    const unsigned int init[2] = {0u, 0xFFu};
+    SPK_HIP(hipMemcpyAsync(d.p, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4 * (int64_t)ctx->n_cu);
+    k_unit_bits<<<(unsigned)blocks, 256, 0, ctx->stream>>>(n, c->meta.p, c->planes.p, c->planes_hi.p, d.p);
+    SPK_HIP(hipGetLastError());
+    unsigned int h[2];
+    SPK_HIP(hipMemcpyAsync(h, d.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    c->unit_or = h[0];
+    c->unit_and = h[1];
+    c->unit_bits = true;
+    return SPK_OK;
+}
+
 int launch_utf8_decode(spk_ctx *ctx, int64_t n, const int64_t *off8, const int64_t *src_off, const int32_t *perm,
                        const uint8_t *bytes, const uint8_t *valid, Column *c, bool long_rows, const int64_t *ids) {
     if (n <= 0) return SPK_OK;
@@ -338,6 +391,7 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
         SPK_HIP(hipGetLastError());
     }
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    SPK_TRY(launch_unit_bits(ctx, n, c));
     ctx->codes_valid = false;
     return SPK_OK;
 }

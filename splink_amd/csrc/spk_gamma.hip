@@ -78,6 +78,9 @@ struct SimpleCol {
     // the largest distance v with `v / (S / 2.0) cmp t` true in fp64 (Spark's division), for
     // S = len_l + len_r (code points) < THR_S: the filter decides the test with integer compares.
     int32_t thr_off[MAX_TESTS];
+    // Bit-planes the Levenshtein scans need: bits np..7 of every plane-row unit of the column (both
+    // sides) are the same (Column.unit_or / unit_and), so those planes' match-mask terms are no-ops.
+    int32_t np;
 };
 constexpr int THR_S = 256;
 constexpr int32_t TF_ZERO = 1;     // the value 0.0 passes the test (JW of strings without a common unit; lev ratio 0)
@@ -1463,7 +1466,7 @@ __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDe
                             pa[q] = a.planes[q];
                             pb[q] = b.planes[q];
                         }
-                        lev = lev_rows_planes(pa, a.n, pb, b.n, simple_lev_cut(sc, a.ncp, b.ncp));
+                        lev = lev_rows_planes(pa, a.n, pb, b.n, simple_lev_cut(sc, a.ncp, b.ncp), sc.np);
                     } else {
                         lev = lev_exact(a, b, simple_lev_cut(sc, a.ncp, b.ncp));
                     }
@@ -1522,7 +1525,7 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
                 if (lev < 0) {
                     if (eq == 1) lev = 0;
                     else if (!planes) return ST_NEEDS_SLOW;
-                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb));
+                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
                 }
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
@@ -1751,7 +1754,8 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
             if (op == SPK_OP_LEVRATIO && den == 0.0) {
                 r = KN;
             } else {
-                if (lev < 0) lev = eq == 1 ? 0 : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb));
+                if (lev < 0)
+                    lev = eq == 1 ? 0 : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
         }
@@ -2263,6 +2267,12 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     for (SimpleCol &sc : simple) {
         sc.cls = simple_class(sc);
         prepare_tests(sc);
+        sc.np = N_PLANES;
+        if (sc.kind == SK_STR && t0.cols[sc.col]->unit_bits && t1.cols[sc.col]->unit_bits) {
+            const uint32_t any = t0.cols[sc.col]->unit_or | t1.cols[sc.col]->unit_or;
+            const uint32_t all = t0.cols[sc.col]->unit_and & t1.cols[sc.col]->unit_and;
+            while (sc.np > 5 && (((any ^ all) >> (sc.np - 1)) & 1u) == 0) --sc.np;  // top bit constant
+        }
         sc.has_ids = (t0.cols[sc.col]->has_ids && t1.cols[sc.col]->has_ids) ? 1 : 0;
         implied_equal(ctx, t0, t1, sc);
     }

@@ -588,6 +588,7 @@ int spk_table_add_raw_utf8(spk_ctx *ctx, int col, int raw0, int raw1) {
         SPK_TRY(launch_utf8_decode(ctx, n, off8.p, r->off.p, perm, r->bytes.p, r->valid.p, c, long_rows,
                                    ids.p + (side == 0 ? 0 : s0.n)));
         SPK_HIP(hipStreamSynchronize(ctx->stream));
+        SPK_TRY(launch_unit_bits(ctx, n, c));
     }
     ctx->codes_valid = false;
     return SPK_OK;

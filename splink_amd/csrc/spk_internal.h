@@ -145,6 +145,9 @@ struct Column {
     uint64_t src[2] = {0, 0};  // spk_table_add_raw_utf8: serials of the raw columns of the l / r side (0: other)
     bool has_empty = false;    // some non-NULL row is the empty string
     int64_t n_ids = -1;        // spk_table_add_raw_utf8: distinct non-NULL values (ids are dense in [0, n_ids))
+    // OR / AND of the units of every row that has bit-planes (bits 0..7), set by launch_unit_bits
+    bool unit_bits = false;
+    uint32_t unit_or = 0, unit_and = 0xFFu;
 };
 
 // A blocking-key term as spk_key_build saw it, by raw-column serial: the comparison filter skips a
@@ -324,6 +327,7 @@ struct spk_ctx {
 namespace spk {
 int ensure_desc(spk_ctx *ctx, Table &t);
 int new_column(spk_ctx *ctx, int side, int col, Column **out);
+int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c);
 int launch_utf8_decode(spk_ctx *ctx, int64_t n, const int64_t *off8, const int64_t *src_off, const int32_t *perm,
                        const uint8_t *bytes, const uint8_t *valid, Column *c, bool long_rows, const int64_t *ids);
 }

@@ -477,7 +477,10 @@ __device__ inline W low_mask(int m) {  // bits [0, m), 1 <= m <= bits of W
     return m >= (int)(8 * sizeof(W)) ? ~(W)0 : (((W)1 << m) - 1);
 }
 
-template <typename W>
+// NP: the scans read planes 0..NP-1 only.  A caller passes NP < 8 when every unit of the column
+// (both sides) has the same bits NP..7 (e.g. 7 for ASCII text): those planes' terms then only touch
+// mask bits above the pattern, which never reach the rows below (carries and shifts move upward).
+template <typename W, int NP = N_PLANES>
 __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
                                        int cut) {
     W pl[N_PLANES];
@@ -493,7 +496,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
         for (int jj = 0; jj < jn; ++jj) {
             W eq = ~(W)0;
 #pragma unroll
-            for (int b = 0; b < N_PLANES; ++b)
+            for (int b = 0; b < NP; ++b)
                 eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), pl[b]);
             const W x = eq | vn;
             const W d0 = (((x & vp) + vp) ^ vp) | x;
@@ -524,6 +527,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
 // the callers need; the early exit is taken on the computed scores, which obey the same delta
 // bounds.  J0 is the wave's minimum (one switch point for all lanes); lanes with m <= 32 run the
 // same loops with their one word.  cfg2 emails: most waves hold a cell of 33+ units, cut ~ 10.
+template <int NP = N_PLANES>
 __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
                                             int cut) {
     const bool wide = m > 32;
@@ -547,7 +551,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
     for (int j = 0; j < j1; ++j) {
         uint32_t eq = ~0u;
 #pragma unroll
-        for (int b = 0; b < N_PLANES; ++b) eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], j, 1), pl[b]);
+        for (int b = 0; b < NP; ++b) eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], j, 1), pl[b]);
         const uint32_t x = eq | vn;
         const uint32_t d0 = (((x & vp) + vp) ^ vp) | x;
         const uint32_t hp = (vn | ~(d0 | vp)) << 1 | 1u;
@@ -574,7 +578,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
         for (int jj = jb; jj < jn; ++jj) {
             uint64_t eq = ~0ull;
 #pragma unroll
-            for (int b = 0; b < N_PLANES; ++b)
+            for (int b = 0; b < NP; ++b)
                 eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), P[b]);
             const uint64_t x = eq | VN;
             const uint64_t d0 = (((x & VP) + VP) ^ VP) | x;
@@ -598,8 +602,9 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
 // OR_b(a_b ^ b_b), the common suffix the highest of the same with both strings' ends aligned at bit
 // 63; both strips are exact for unit-cost edit distance.  The longer remainder is the pattern, so
 // the scan runs over the shorter one.  `cut` as in lev_planes.
-__device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
-                                      int cut) {
+template <int NP>
+__device__ inline int lev_rows_planes_np(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
+                                         int cut) {
     if (la == 0) return lb;
     if (lb == 0) return la;
     const int mn = la < lb ? la : lb;
@@ -625,8 +630,19 @@ __device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, co
         T[b] = (a_pat ? pb[b] : pa[b]) >> pre;
     }
     // one word width for all active lanes: a wave that mixed both would run both loops
-    if (!__any(m > 32)) return myers_plane_text<uint32_t>(P, m, T, n, cut);
-    return myers_plane_text_lazy(P, m, T, n, cut);
+    if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P, m, T, n, cut);
+    return myers_plane_text_lazy<NP>(P, m, T, n, cut);
+}
+
+// np: planes the scans need (wave-uniform; see myers_plane_text), 8 when unknown.
+__device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
+                                      int cut, int np = N_PLANES) {
+    switch (np) {
+        case 5: return lev_rows_planes_np<5>(pa, la, pb, lb, cut);
+        case 6: return lev_rows_planes_np<6>(pa, la, pb, lb, cut);
+        case 7: return lev_rows_planes_np<7>(pa, la, pb, lb, cut);
+        default: return lev_rows_planes_np<N_PLANES>(pa, la, pb, lb, cut);
+    }
 }
 
 // ---- rows of 65..128 units (CPF_PLANES2): the same scan over 128-bit plane words ----------------
@@ -649,6 +665,7 @@ __device__ inline int popc128(u128 x) {
     return __builtin_popcountll((unsigned long long)x) + __builtin_popcountll((unsigned long long)(x >> 64));
 }
 
+template <int NP = N_PLANES>
 __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
                                           int cut) {
     u128 vp = ~(u128)0, vn = 0;
@@ -661,7 +678,7 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
         for (int jj = 0; jj < jn; ++jj) {
             uint64_t e0 = ~0ull, e1 = ~0ull;
 #pragma unroll
-            for (int b = 0; b < N_PLANES; ++b) {
+            for (int b = 0; b < NP; ++b) {
                 const uint32_t m32 = (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1);
                 e0 = eq_plane(e0, m32, (uint64_t)P[b]);
                 e1 = eq_plane(e1, m32, (uint64_t)(P[b] >> 64));
@@ -686,8 +703,9 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
 // lev_rows_planes for rows of up to 128 units held as 128-bit planes (bits past a row's length are
 // zero).  After the common prefix and suffix are stripped, a pattern of <= 64 units runs the
 // one-word scan (the same word width for the whole wave), else the 128-bit one.
-__device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
-                                         int cut) {
+template <int NP>
+__device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
+                                            int cut) {
     if (la == 0) return lb;
     if (lb == 0) return la;
     const int mn = la < lb ? la : lb;
@@ -719,10 +737,20 @@ __device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, con
             P64[b] = (uint64_t)P[b];
             T64[b] = (uint64_t)T[b];
         }
-        if (!__any(m > 32)) return myers_plane_text<uint32_t>(P64, m, T64, n, cut);
-        return myers_plane_text_lazy(P64, m, T64, n, cut);
+        if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P64, m, T64, n, cut);
+        return myers_plane_text_lazy<NP>(P64, m, T64, n, cut);
     }
-    return myers_plane_text128(P, m, T, n, cut);
+    return myers_plane_text128<NP>(P, m, T, n, cut);
+}
+
+__device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
+                                         int cut, int np = N_PLANES) {
+    switch (np) {
+        case 5: return lev_rows_planes128_np<5>(pa, la, pb, lb, cut);
+        case 6: return lev_rows_planes128_np<6>(pa, la, pb, lb, cut);
+        case 7: return lev_rows_planes128_np<7>(pa, la, pb, lb, cut);
+        default: return lev_rows_planes128_np<N_PLANES>(pa, la, pb, lb, cut);
+    }
 }
 
 // Exact Jaro-Winkler for unequal strings of <= 64 units, without LDS.

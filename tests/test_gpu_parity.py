@@ -573,6 +573,50 @@ def test_levenshtein_levels_exact(amd):
         assert got[i, 1] == want, (a, b, d, got[i, 1])
 
 
+@pytest.mark.parametrize("alpha,planes", [
+    (list("0123456789-"), 5),          # bits 7, 6, 5 the same for every unit: 5 planes
+    (list("abcdefghijklmnopqrstuvwxyz"), 5),
+    (list("abcxyz.@_-0123"), 7),       # ASCII: plane 7 dropped
+    (list("abcde") + ["é", "ü"], 8)])  # Latin-1: all 8 planes
+def test_levenshtein_reduced_planes(amd, alpha, planes):
+    """Levenshtein template levels when the scans skip the top bit-planes a column's units all share
+    (SimpleCol.np): distances up to 5 and the ratio levels against the oracle, rows of 0-128 units
+    (one- and two-word planes), shared prefixes / suffixes and NULLs."""
+    from splink_amd import case_statements as cs
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(len(alpha)))
+    left, right = [], []
+    for n in [0, 1, 3, 12, 31, 32, 33, 47, 64, 65, 90, 128]:
+        for k in [0, 1, 2, 4, 7]:
+            for rep in range(4):
+                a = "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), n))
+                b = _mutate(rng, a, k, alpha)[:128]
+                if rep == 3:
+                    b = "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), len(b)))
+                left.append(a)
+                right.append(b)
+    left += [None, alpha[0]]
+    right += [alpha[0], None]
+    df = pd.DataFrame({"a_l": left, "a_r": right})
+    exact = ("case when a_l is null or a_r is null then -1 "
+             + " ".join(f"when levenshtein(a_l, a_r) <= {d} then {6 - d}" for d in range(6)) + " else 0 end")
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "lv", "custom_columns_used": ["a"], "num_levels": 7, "case_expression": exact,
+         "m_probabilities": [0.1, 0.1, 0.1, 0.1, 0.1, 0.2, 0.3], "u_probabilities": [0.4, 0.2, 0.1, 0.1, 0.1, 0.05, 0.05]},
+        {"custom_name": "lr", "custom_columns_used": ["a"], "num_levels": 4,
+         "case_expression": cs.sql_gen_case_stmt_levenshtein_4("a")}]}
+    got = add_gammas(df, st, amd).gamma_matrix()
+    for i, (a, b) in enumerate(zip(left, right)):
+        if a is None or b is None:
+            assert got[i, 0] == -1 and got[i, 1] == -1
+            continue
+        d = orc.levenshtein(a, b)
+        assert got[i, 0] == (6 - d if d <= 5 else 0), (a, b, d, got[i, 0])
+        den = (len(a) + len(b)) / 2.0
+        want = 3 if a == b else (2 if den and d / den <= 0.2 else (1 if den and d / den <= 0.4 else 0))
+        assert got[i, 1] == want, (a, b, d, got[i, 1])
+
+
 def test_exact_work_lists_grow(amd):
     """More undecided cells than the exact-pass lists hold on the first try (3 columns x 40k pairs of
     anagrams, which no length / letter-count bound decides): the lists are re-sized on the device
