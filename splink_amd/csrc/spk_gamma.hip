@@ -2514,8 +2514,14 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             // (running this launch on a second stream beside the Levenshtein pass measured no faster:
             // 1.198-1.205 ms per cfg2 pass either way)
             if (jw.n) {
-                k_gamma_exact_simple<false><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
-                    A, jw, ctx->xlist.p, ctx->xinfo.p);
+                switch (ctx->jw_waves) {  // A/B: waves per SIMD the JW pass is compiled for
+                    case 3: k_gamma_exact_simple<false, 3><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
+                                A, jw, ctx->xlist.p, ctx->xinfo.p); break;
+                    case 4: k_gamma_exact_simple<false, 4><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
+                                A, jw, ctx->xlist.p, ctx->xinfo.p); break;
+                    default: k_gamma_exact_simple<false><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
+                                 A, jw, ctx->xlist.p, ctx->xinfo.p); break;
+                }
                 for (int c = 0; c < jw.n; ++c)
                     k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, simple[jw.si[c]].k, ctx->xlist.p,
                                                                                    ctx->xinfo.p);
@@ -2833,6 +2839,8 @@ extern "C" int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n) {
 
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->jw_waves = on / 1000000;  // + W x 1000000: the JW exact pass at W waves per SIMD (A/B)
+    on %= 1000000;
     ctx->jw_grid = on / 100000;  // + G x 100000: the JW exact launch at G blocks per CU and column (A/B)
     ctx->lev_waves = (on / 10000) % 10;  // + W x 10000: Levenshtein pass at W waves per SIMD (A/B)
     on %= 10000;

@@ -248,6 +248,7 @@ struct spk_ctx {
     bool simple_columns = true;       // template-shaped columns take the record-only filter
     bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
     int lev_waves = 0;                // Levenshtein exact pass variant (waves per SIMD; 0 = LEV_WAVES), A/B
+    int jw_waves = 0;                 // JW exact pass variant (waves per SIMD; 0 = JW_WAVES), A/B
     int jw_grid = 0;                  // JW exact launch: blocks per CU and column (0 = the exact passes' 8), A/B
     int filter_waves = 0;             // k_gamma_simple variant (waves per SIMD, pairs per lane): 0 = <6,3>; 1..5 A/B
     int use_views = 1;                // rule 1's pairs read a view-ordered row image: 0 never, 1 when the

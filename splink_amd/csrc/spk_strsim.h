@@ -753,11 +753,78 @@ __device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, con
     }
 }
 
+// matches() with BOTH strings as bit-planes (<= 64 units each, all < 256): the greedy matching,
+// the transpositions and the common prefix come from register planes, with no unit loads (the
+// unit-reading form waits on a dependent load per four units and per match).  The k-th matched
+// unit of the shorter string is recorded as bit k of A_b (its bit b), the k-th flagged unit of the
+// longer string as bit k of B_b, so transpositions = popc(OR_b (A_b ^ B_b)).  The prefix is the
+// first position where the planes differ (zero past a row's end), capped at the shorter length.
+template <typename W>
+__device__ double jw_planes2(const uint64_t *mxq, int lmx, const uint64_t *mnq, int lmn, int lf, int ls) {
+    uint64_t px[N_PLANES], pn[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) {
+        px[b] = mxq[b];
+        pn[b] = mnq[b];
+    }
+    W pl[N_PLANES], A[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) {
+        pl[b] = (W)px[b];
+        A[b] = 0;
+    }
+    const int range = lmx / 2 - 1 > 0 ? lmx / 2 - 1 : 0;
+    W flags = 0;
+    int m = 0;
+    for (int h = 0; h < 2 && 32 * h < lmn; ++h) {
+        uint32_t tw[N_PLANES];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(pn[b] >> (32 * h));
+        const int jn = lmn - 32 * h < 32 ? lmn - 32 * h : 32;
+        for (int jj = 0; jj < jn; ++jj) {
+            const int mi = 32 * h + jj;
+            const int lo = mi - range > 0 ? mi - range : 0;
+            const int hi = mi + range + 1 < lmx ? mi + range + 1 : lmx;
+            W eq = ~(W)0;
+#pragma unroll
+            for (int b = 0; b < N_PLANES; ++b) eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), pl[b]);
+            const W cand = eq & mask_below<W>(hi) & ~mask_below<W>(lo) & ~flags;
+            if (cand) {
+                flags |= cand & (~cand + (W)1);  // lowest set bit: the first free match in the window
+#pragma unroll
+                for (int b = 0; b < N_PLANES; ++b) A[b] |= (W)((tw[b] >> jj) & 1u) << m;
+                ++m;
+            }
+        }
+    }
+    if (m == 0) return 0.0;
+    W diff = 0, fm = flags;
+    for (int k = 0; k < m; ++k) {  // the longer string's flagged units, in order
+        const int x = sizeof(W) == 4 ? __builtin_ctz((uint32_t)fm) : __builtin_ctzll((unsigned long long)fm);
+        fm &= fm - (W)1;
+        W d = 0;
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) d |= (W)(((px[b] >> x) & 1u) ^ ((A[b] >> k) & 1u));
+        diff |= d << k;
+    }
+    const int t = sizeof(W) == 4 ? __builtin_popcount((uint32_t)diff) : __builtin_popcountll((unsigned long long)diff);
+    uint64_t d = 0;
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) d |= px[b] ^ pn[b];
+    int prefix = d ? __ffsll((unsigned long long)d) - 1 : 64;
+    if (prefix > lmn) prefix = lmn;
+    return jw_finish(m, t, prefix, lf, ls, lmx);
+}
+
 // Exact Jaro-Winkler for unequal strings of <= 64 units, without LDS.
 __device__ inline double jw_exact(const StrView &a, const StrView &b) {
     const bool fmax = a.n > b.n;  // commons-text: max = first only if strictly longer
     const StrView &mx = fmax ? a : b;
     const StrView &mn = fmax ? b : a;
+    if (mx.planes && mn.planes) {
+        if (mx.n <= 32) return jw_planes2<uint32_t>(mx.planes, mx.n, mn.planes, mn.n, a.n, b.n);
+        return jw_planes2<uint64_t>(mx.planes, mx.n, mn.planes, mn.n, a.n, b.n);
+    }
     if (mx.planes) {
         if (mx.n <= 32) return jw_planes<uint32_t>(mx.planes, mx.p, mx.n, mn.p, mn.n, a.p, a.n, b.p, b.n);
         return jw_planes<uint64_t>(mx.planes, mx.p, mx.n, mn.p, mn.n, a.p, a.n, b.p, b.n);
