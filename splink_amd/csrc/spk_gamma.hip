@@ -1370,9 +1370,18 @@ __global__ __launch_bounds__(PFX_THREADS) void k_prefix(const unsigned int *__re
     }
 }
 
-__global__ void k_compact(GammaArgs A, int k, const int64_t *__restrict__ pref, int32_t *__restrict__ xlist,
+// Up to four columns per launch (blockIdx.y picks the column): the JW template columns' lists are
+// compacted, their slow lists evaluated, in one launch each instead of one per column.
+struct ColSet {
+    int n;
+    int k[4];
+};
+
+__global__ void k_compact(GammaArgs A, ColSet cs, const int64_t *__restrict__ xpref, int32_t *__restrict__ xlist,
                           const int64_t *__restrict__ xinfo) {
     if (xinfo[2 * A.K]) return;  // overflow: the host re-runs the phase
+    const int k = cs.k[blockIdx.y];
+    const int64_t *pref = xpref + (int64_t)k * (A.n_regions + 1);
     const Region R = my_region(A);
     const int32_t *src = region_list(A, k, R);
     const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
@@ -1670,7 +1679,8 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
 // Global-memory pass over column k's slow list (length on the device; usually empty).  Cells with a
 // string past SLOW_LIMIT units go on to the huge pass: their list (counter slow_count[2K + k]) takes
 // column k's exact-list region, free once the exact pass ran and at least as long as the slow list.
-__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, int k, int32_t *xlist, const int64_t *xinfo) {
+__global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, ColSet cs, int32_t *xlist, const int64_t *xinfo) {
+    const int k = cs.k[blockIdx.y];
     const int64_t n = A.slow_count[k];
     const int32_t *items = A.slow + A.slow_off[k];
     int32_t *huge = xlist + xinfo[k];
@@ -2503,14 +2513,17 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             const int64_t g_jw = ctx->jw_grid > 0
                 ? std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->jw_grid * ctx->n_cu, g_exact)) : g_exact;
             jw.g = (int)g_jw;
+            ColSet jk{};
             for (int k = 0; k < K; ++k) {
                 if (!may_exact[k] || simple_of[k] < 0) continue;
                 const SimpleCol &sc = simple[simple_of[k]];
                 if (sc.cls == SC_LEV || sc.kind != SK_STR || jw.n == 4) continue;
-                k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1),
-                                                                       ctx->xlist.p, ctx->xinfo.p);
+                jk.k[jk.n++] = k;
                 jw.si[jw.n++] = simple_of[k];
             }
+            if (jk.n)
+                k_compact<<<dim3((unsigned)n_regions, (unsigned)jk.n), 256, 0, ctx->stream>>>(A, jk, ctx->xpref.p,
+                                                                                           ctx->xlist.p, ctx->xinfo.p);
             // (running this launch on a second stream beside the Levenshtein pass measured no faster:
             // 1.198-1.205 ms per cfg2 pass either way)
             if (jw.n) {
@@ -2522,9 +2535,8 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                     default: k_gamma_exact_simple<false><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
                                  A, jw, ctx->xlist.p, ctx->xinfo.p); break;
                 }
-                for (int c = 0; c < jw.n; ++c)
-                    k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, simple[jw.si[c]].k, ctx->xlist.p,
-                                                                                   ctx->xinfo.p);
+                k_gamma_slow<<<dim3((unsigned)(4 * ctx->n_cu), (unsigned)jk.n), 64, 0, ctx->stream>>>(A, jk, ctx->xlist.p,
+                                                                                                     ctx->xinfo.p);
             }
             for (int k = 0; k < K; ++k) {
                 if (!may_exact[k]) continue;
@@ -2532,9 +2544,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                 const bool lev = simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV;
                 bool fused = false;
                 for (int c = 0; c < jw.n; ++c) fused = fused || jw.si[c] == simple_of[k];
+                const ColSet one_k{1, {k, 0, 0, 0}};
                 if (!fused)
-                    k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, k, ctx->xpref.p + (size_t)k * (n_regions + 1),
-                                                                           ctx->xlist.p, ctx->xinfo.p);
+                    k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p,
+                                                                           ctx->xinfo.p);
                 if (lev) {
                     ExactCols one{};
                     one.n = 1;
@@ -2564,7 +2577,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                                                                                          ctx->xinfo.p);
                     k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
                 } else if (!fused) {
-                    k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+                    k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
                 }
             }
             SPK_HIP(hipGetLastError());
