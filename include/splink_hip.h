@@ -214,7 +214,10 @@ int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n);
  * column-batched filter; on = 2: through the register-resident row filter when the image row is
  * short (<= 128 bytes); on = 0: every column through the interpreter; on + 10: the same, with
  * the second blocking rule's pairs always reading the table-ordered row image, on + 20: always their
- * rule's view-ordered copy (default: the copy once the image outgrows the caches).  All
+ * rule's view-ordered copy (default: the copy once the image outgrows the caches).  Further
+ * A/B digits (splink_amd/csrc/spk_gamma.hip, spk_gammas_set_simple): + 1000 a timing-only filter
+ * variant, + W x 10000 / + W x 1000000 the Levenshtein / JW exact passes at W waves per SIMD,
+ * + G x 100000 the JW launch at G blocks per CU, + 10000000 the pass replayed as a HIP graph.  All
  * modes give identical results (for testing and measurement).  spk_gammas_simple_count: how many
  * columns the last spk_gammas took as template columns. */
 int spk_gammas_set_simple(spk_ctx *ctx, int on);

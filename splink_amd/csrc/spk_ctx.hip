@@ -282,6 +282,7 @@ void spk_ctx_destroy(spk_ctx *ctx) {
     }
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->h_info) (void)hipHostFree(ctx->h_info);
+    ctx->drop_graph();
     hipStream_t own = ctx->own_stream;
     delete ctx;
     if (own) (void)hipStreamDestroy(own);

@@ -284,6 +284,19 @@ struct spk_ctx {
     uint64_t table_epoch = 0;
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (uploaded when they change)
     std::vector<uint8_t> last_blob;   // host copy of what prog_blob holds
+    // spk_gammas launch sequence as a HIP graph: captured the second time a key (GammaArgs, list
+    // capacity, variants, program blob) repeats, replayed while it does
+    bool graphs = false;
+    std::vector<uint8_t> graph_key, graph_seen;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    void drop_graph() {
+        if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+        if (graph) (void)hipGraphDestroy(graph);
+        graph_exec = nullptr;
+        graph = nullptr;
+        graph_key.clear();
+    }
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
     // EM state
