@@ -32,6 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level
 # HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same command
 # (scripts_gpu_round.sh -> tools/traffic.py); the counters cannot be read inside a timed run.
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r2c_traffic.json")
+# per-kernel issue counters of the same command (rocprofv3 --pmc passes, tools/pmc_summary.py)
+PMC_FILE = os.path.join(ROOT, "profiles", "r2c_pmc_kernels.json")
 COLS = ["first_name", "surname", "dob", "city", "email"]
 WORKLOADS = {2: "cfg2: synthetic person-record dedupe, 1M x sqrt(N) records, blocking surname|dob, "
                 "5 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3)",
@@ -201,6 +203,22 @@ def main():
         roofline["traffic_source"] = em_roofline["traffic_source"] = (
             os.path.relpath(TRAFFIC_FILE, ROOT) + ": rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command")
 
+    # The γ kernels are issue-bound, not HBM-bound: their VALU / SALU issue against the SIMD peaks and
+    # the share of wave time stalled, from the committed counter passes of this command
+    issue = None
+    if os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+        issue = {"source": os.path.relpath(PMC_FILE, ROOT) + ": rocprofv3 --pmc SQ_* passes of this command",
+                 "peak_note": "valu_util = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles at 2.4 GHz)"}
+        for name, key in (("filter", "k_gamma_simple"), ("levenshtein_exact", "k_gamma_exact_simple<true"),
+                          ("jw_exact", "k_gamma_exact_simple<false")):
+            for k, v in pmc.items():
+                if key in k:
+                    issue[name] = {x: round(float(v[x]), 4) for x in ("valu_util", "salu_util", "wait_frac", "l2_hit")
+                                   if x in v}
+                    break
+
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(job, df, st, args.cpu_seconds, cols)
@@ -229,6 +247,7 @@ def main():
                    "parallelism": f"pair-ordinal shards x{world}, RCCL all-reduce of pattern histogram"},
         "roofline": roofline,
         "roofline_em": em_roofline,
+        "issue_gamma_kernels": issue,
         "hbm_headline_contract": headline,
         "breakdown_ms": {"gamma": g_ms, "em_hist": h_ms, "em_final": f_ms, "score": score_ms,
                          "block_device": block_kernel_ms, "block_wall": block_s * 1e3,
