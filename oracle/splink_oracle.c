@@ -18,6 +18,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 /* ------------------------------------------------------------------------- */
 /* Jaro-Winkler: commons-text 1.4 JaroWinklerDistance.apply / matches, as     */
@@ -229,6 +232,18 @@ static inline int mp_one(int K, const int8_t *g, const int *lvl_off, double lamb
 }
 
 /* lvl_off[k] = Σ_{j<k} (L_j + 1): slot of (k, -1); m/u are flattened [Σ L_k] so m index = lvl_off[k]-k+v */
+/* Sums over up to billions of pairs: each thread keeps Neumaier-compensated partial sums and the
+ * partials are combined in thread order, so the statistics are accurate to a few ulps whatever P and
+ * the thread count (a plain running sum drifts by ~1e-9 relative past 1e9 terms, enough to move a
+ * float32-cast m / u by an ulp and fail a 1e-9 comparison against an exact evaluation). */
+static inline void neu_add(double *s, double *c, double x)
+{
+    double t = *s + x;
+    if (fabs(*s) >= fabs(x)) *c += (*s - t) + x;
+    else *c += (x - t) + *s;
+    *s = t;
+}
+
 int orc_em_stats(int K, const int *nlev, int64_t P, const int8_t *gam, double lambda, double one_minus,
                  const double *m, const double *u, double *stats, int n_threads_hint)
 {
@@ -238,26 +253,46 @@ int orc_em_stats(int K, const int *nlev, int64_t P, const int8_t *gam, double la
     for (int k = 0; k < K; k++) { lvl_off[k] = n_slots; n_slots += nlev[k] + 1; }
     int n_stats = 3 + 4 * n_slots;
     memset(stats, 0, sizeof(double) * (size_t)n_stats);
+    int nt = 1;
+#ifdef _OPENMP
+    nt = omp_get_max_threads();
+#endif
+    double *part = (double *)calloc((size_t)nt * 2 * (size_t)n_stats, sizeof(double));  /* [thread][sum | comp] */
 #pragma omp parallel
     {
-        double *loc = (double *)calloc((size_t)n_stats, sizeof(double));
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        double *loc = part + (size_t)tid * 2 * (size_t)n_stats, *cmp = loc + n_stats;
 #pragma omp for schedule(static)
         for (int64_t p = 0; p < P; p++) {
             const int8_t *g = gam + p * K;
             double mp = 0.0;
             int ok = mp_one(K, g, lvl_off, lambda, one_minus, m, u, &mp);
-            loc[1] += 1.0;
-            if (ok) { loc[0] += mp; loc[2] += 1.0; }
+            loc[1] += 1.0;  /* counts stay exact in doubles (< 2^53) */
+            if (ok) { neu_add(&loc[0], &cmp[0], mp); loc[2] += 1.0; }
             for (int k = 0; k < K; k++) {
-                double *s = loc + 3 + 4 * (lvl_off[k] + g[k] + 1);
-                s[0] += 1.0;
-                if (ok) { s[1] += 1.0; s[2] += mp; s[3] += 1.0 - mp; }
+                const int o = 3 + 4 * (lvl_off[k] + g[k] + 1);
+                loc[o] += 1.0;
+                if (ok) {
+                    loc[o + 1] += 1.0;
+                    neu_add(&loc[o + 2], &cmp[o + 2], mp);
+                    neu_add(&loc[o + 3], &cmp[o + 3], 1.0 - mp);
+                }
             }
         }
-#pragma omp critical
-        for (int i = 0; i < n_stats; i++) stats[i] += loc[i];
-        free(loc);
     }
+    for (int i = 0; i < n_stats; i++) {
+        double s = 0.0, c = 0.0;
+        for (int t = 0; t < nt; t++) {
+            const double *loc = part + (size_t)t * 2 * (size_t)n_stats;
+            neu_add(&s, &c, loc[i]);
+            neu_add(&s, &c, loc[n_stats + i]);
+        }
+        stats[i] = s + c;
+    }
+    free(part);
     return n_stats;
 }
 
@@ -270,17 +305,36 @@ void orc_log_likelihood(int K, const int *nlev, int64_t P, const int8_t *gam, do
     int lvl_off[64];
     int n_slots = 0;
     for (int k = 0; k < K; k++) { lvl_off[k] = n_slots; n_slots += nlev[k] + 1; }
-    double sum = 0.0, cnt = 0.0;
-#pragma omp parallel for schedule(static) reduction(+ : sum, cnt)
-    for (int64_t p = 0; p < P; p++) {
-        const int8_t *g = gam + p * K;
-        double num = lambda, den = one_minus;
-        for (int k = 0; k < K; k++) num = num * (g[k] < 0 ? 1.0 : m[lvl_off[k] - k + g[k]]);
-        for (int k = 0; k < K; k++) den = den * (g[k] < 0 ? 1.0 : u[lvl_off[k] - k + g[k]]);
-        const double d = num + den;
-        if (d > 0.0) { sum += log(d); cnt += 1.0; }
+    int nt = 1;
+#ifdef _OPENMP
+    nt = omp_get_max_threads();
+#endif
+    double *part = (double *)calloc((size_t)nt * 3, sizeof(double));  /* [thread][sum, comp, count] */
+#pragma omp parallel
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        double *q = part + 3 * (size_t)tid;
+#pragma omp for schedule(static)
+        for (int64_t p = 0; p < P; p++) {
+            const int8_t *g = gam + p * K;
+            double num = lambda, den = one_minus;
+            for (int k = 0; k < K; k++) num = num * (g[k] < 0 ? 1.0 : m[lvl_off[k] - k + g[k]]);
+            for (int k = 0; k < K; k++) den = den * (g[k] < 0 ? 1.0 : u[lvl_off[k] - k + g[k]]);
+            const double d = num + den;
+            if (d > 0.0) { neu_add(&q[0], &q[1], log(d)); q[2] += 1.0; }
+        }
     }
-    out[0] = sum;
+    double s = 0.0, c = 0.0, cnt = 0.0;  /* compensated, in thread order */
+    for (int t = 0; t < nt; t++) {
+        neu_add(&s, &c, part[3 * t]);
+        neu_add(&s, &c, part[3 * t + 1]);
+        cnt += part[3 * t + 2];
+    }
+    free(part);
+    out[0] = s + c;
     out[1] = cnt;
 }
 

@@ -17,6 +17,10 @@ M-step), the final scoring pass.  Parity: every comparison vector of a strided s
 oracle.template_gammas, and the 10 EM iterations of λ / m / u plus the final match probabilities of
 all of this shard's pairs against oracle.em_iterate (1e-9).
 
+--config 5 adds cfg5's free-text address column (30-128 characters, Levenshtein-4) to the five cfg2
+columns; with --records 20000000 --shard 0/5 one GPU holds ~1.2B pairs, cfg5's per-GPU pair count
+(100M records, ~10B pairs over 8 GPUs).
+
 --config 3 is BASELINE configs[2]'s per-GPU share: link_only between two synthetic tables of
 `--records` rows each (one 2 x records population split in halves, so duplicates straddle them),
 rules surname | dob | email, the five cfg2 columns, and the term-frequency
@@ -55,8 +59,12 @@ def main():
     ap.add_argument("--sample", type=int, default=2_000_000, help="pairs in the strided gamma parity sample")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--out")
-    ap.add_argument("--config", type=int, default=4, choices=[3, 4])
+    ap.add_argument("--config", type=int, default=4, choices=[3, 4, 5])
     a = ap.parse_args()
+    global COLS, SPECS
+    if a.config == 5:  # + the free-text address column, Levenshtein-4 (cfg5's columns)
+        COLS = COLS + ["address"]
+        SPECS = SPECS + [("lev", 4, [0.2, 0.4])]
     shard, n_shards = (int(x) for x in a.shard.split("/"))
 
     import torch
@@ -68,12 +76,13 @@ def main():
 
     t0 = time.time()
     link = a.config == 3
-    df = make_records(a.records * (2 if link else 1), surname_vocab=a.surname_vocab, arrow=True)[["unique_id"] + COLS]
+    df = make_records(a.records * (2 if link else 1), surname_vocab=a.surname_vocab, arrow=True,
+                      with_address=a.config == 5)[["unique_id"] + COLS]
     inputs = [df.iloc[:a.records].reset_index(drop=True), df.iloc[a.records:].reset_index(drop=True)] if link else [df]
     del df
     gen_s = time.time() - t0
     log(f"generated {a.records} records x {len(inputs)} in {gen_s:.1f}s")
-    settings = cfg_settings(4, max_iterations=a.iters)
+    settings = cfg_settings(5 if a.config == 5 else 4, max_iterations=a.iters)
     if link:
         settings["link_type"] = "link_only"
         settings["blocking_rules"] = ["l.surname = r.surname", "l.dob = r.dob", "l.email = r.email"]
@@ -136,7 +145,7 @@ def main():
         "row": "full job, one GPU (separately labelled; never the headline)",
         "workload": (f"cfg3 per-GPU share: link_only {a.records} x {a.records} records, blocking surname|dob|email, "
                      f"5 columns, tf on surname, pair-ordinal shard {shard}/{n_shards}") if link else
-                    (f"cfg4 per-GPU share: {a.records} records, blocking surname|dob, 5 columns, "
+                    (f"cfg{a.config} columns at {a.records} records: blocking surname|dob, {len(COLS)} columns, "
                      f"pair-ordinal shard {shard}/{n_shards}"),
         "records": a.records, "candidates_total": int(job.n_candidates), "pairs_this_gpu": int(P),
         "iterations": a.iters, "wall_s": wall, "job_wall_s": total,
