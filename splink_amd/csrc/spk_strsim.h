@@ -700,6 +700,90 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
     return dist > cut ? cut + 1 : dist;
 }
 
+// Patterns of 65..128 units: the upper 64 rows start late, the 64-bit analogue of
+// myers_plane_text_lazy (same argument: D[i][j] >= |i - j|, so rows >= 65 cannot hold a distance
+// <= cut before text unit 63 - cut).  The scan runs 64-bit words (score tracked at row 64) up to the
+// wave's minimum switch point J0, takes rows 65..m as D[64][J0] + (i - 64), and continues with
+// 128-bit words.  Free-text columns (cfg5 addresses, cut ~ 0.4 x length) spend about a third of
+// their text in the cheaper first phase.
+template <int NP = N_PLANES>
+__device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
+                                               int cut) {
+    const bool wide = m > 64;
+    const int mine = wide ? (cut < 63 ? 63 - cut : 0) : 128;
+    int lo = 0, hi = 128;  // wave minimum of `mine` (active lanes) by bisection over ballots
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (__ballot(mine <= mid)) hi = mid;
+        else lo = mid + 1;
+    }
+    const int J0 = lo;
+    uint64_t pl[N_PLANES];
+#pragma unroll
+    for (int b = 0; b < N_PLANES; ++b) pl[b] = (uint64_t)P[b];
+    uint64_t vp = ~0ull, vn = 0;
+    const uint64_t M1 = low_mask<uint64_t>(wide ? 64 : m);  // the rows the first phase scores
+    const int j1 = n < J0 ? n : J0;
+    for (int h = 0; h < 4 && 32 * h < j1; ++h) {
+        uint32_t tw[N_PLANES];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
+        const int jn = j1 - 32 * h < 32 ? j1 - 32 * h : 32;
+        for (int jj = 0; jj < jn; ++jj) {
+            uint64_t eq = ~0ull;
+#pragma unroll
+            for (int b = 0; b < NP; ++b) eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), pl[b]);
+            const uint64_t x = eq | vn;
+            const uint64_t d0 = (((x & vp) + vp) ^ vp) | x;
+            const uint64_t hp = (vn | ~(d0 | vp)) << 1 | 1ull;
+            const uint64_t hn = (d0 & vp) << 1;
+            vp = hn | ~(d0 | hp);
+            vn = hp & d0;
+            if (!wide && (jj & 3) == 3) {
+                const int j = 32 * h + jj;
+                const int dist = j + 1 + popc_w(vp & M1) - popc_w(vn & M1);
+                if (dist - (n - 1 - j) > cut) return cut + 1;
+            }
+        }
+    }
+    if (n <= J0) {
+        const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 64 : 0);
+        return dist > cut ? cut + 1 : dist;
+    }
+    // rows 65..m enter with vertical deltas +1 (D[64][J0] + (i - 64))
+    u128 VP = (u128)vp | ((u128)~0ull << 64), VN = vn;
+    const u128 M2 = m >= 128 ? ~(u128)0 : (((u128)1 << m) - 1);
+    for (int h = J0 >> 5; h < 4 && 32 * h < n; ++h) {
+        uint32_t tw[N_PLANES];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
+        const int jb = 32 * h < J0 ? J0 - 32 * h : 0;
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        for (int jj = jb; jj < jn; ++jj) {
+            uint64_t e0 = ~0ull, e1 = ~0ull;
+#pragma unroll
+            for (int b = 0; b < NP; ++b) {
+                const uint32_t m32 = (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1);
+                e0 = eq_plane(e0, m32, (uint64_t)P[b]);
+                e1 = eq_plane(e1, m32, (uint64_t)(P[b] >> 64));
+            }
+            const u128 x = (((u128)e1 << 64) | e0) | VN;
+            const u128 d0 = (((x & VP) + VP) ^ VP) | x;
+            const u128 hp = (VN | ~(d0 | VP)) << 1 | (u128)1;
+            const u128 hn = (d0 & VP) << 1;
+            VP = hn | ~(d0 | hp);
+            VN = hp & d0;
+            if ((jj & 3) == 3) {
+                const int j = 32 * h + jj;
+                const int dist = j + 1 + popc128(VP & M2) - popc128(VN & M2);
+                if (dist - (n - 1 - j) > cut) return cut + 1;
+            }
+        }
+    }
+    const int dist = n + popc128(VP & M2) - popc128(VN & M2);
+    return dist > cut ? cut + 1 : dist;
+}
+
 // lev_rows_planes for rows of up to 128 units held as 128-bit planes (bits past a row's length are
 // zero).  After the common prefix and suffix are stripped, a pattern of <= 64 units runs the
 // one-word scan (the same word width for the whole wave), else the 128-bit one.
@@ -740,7 +824,7 @@ __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, 
         if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P64, m, T64, n, cut);
         return myers_plane_text_lazy<NP>(P64, m, T64, n, cut);
     }
-    return myers_plane_text128<NP>(P, m, T, n, cut);
+    return myers_plane_text128_lazy<NP>(P, m, T, n, cut);
 }
 
 __device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
