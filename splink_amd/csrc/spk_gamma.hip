@@ -1292,81 +1292,81 @@ constexpr int PFX_THREADS = 1024;
 constexpr int PFX_PER = 8;  // region counts a k_prefix thread keeps in registers
 __global__ __launch_bounds__(PFX_THREADS) void k_prefix(const unsigned int *__restrict__ region_count, int K,
                                                         int n_regions, int64_t cap, int64_t *__restrict__ xpref,
-                                                        int64_t *__restrict__ xinfo) {
-    // Per column: wave-level inclusive scans (shuffles) and one scan of the 16 wave totals, two
-    // barriers per column instead of a Hillis-Steele ladder of 20.  A thread's counts (<= PFX_PER of
-    // them, 5 at 20 regions per CU) stay in registers, and the next column's are loaded before this
-    // column's scan, so the K columns pay about one load latency instead of 2K.
+                                                        int64_t *__restrict__ xinfo, unsigned long long *__restrict__ done) {
+    // One workgroup per column (blockIdx.x): wave-level inclusive scans (shuffles) and one scan of the
+    // 16 wave totals, two barriers.  A thread's counts (<= PFX_PER of them, 5 at 20 regions per CU)
+    // stay in registers.  The last workgroup to finish (device-scope counter) lays the columns' lists
+    // out one after another and flags an overflow of `cap`.
     constexpr int NW = PFX_THREADS / 64;
     __shared__ int64_t wsum[NW];
+    __shared__ bool s_last;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int per = (n_regions + PFX_THREADS - 1) / PFX_THREADS;
     const int b0 = threadIdx.x * per;
     const bool in_regs = per <= PFX_PER;  // block-uniform
-    auto load = [&](int k, unsigned int (&c)[PFX_PER]) {
-        const unsigned int *rc = region_count + (int64_t)k * n_regions;
+    const int k = blockIdx.x;
+    const unsigned int *rc = region_count + (int64_t)k * n_regions;
+    unsigned int cur[PFX_PER];
+    int64_t mine = 0;
+    if (in_regs) {
 #pragma unroll
-        for (int q = 0; q < PFX_PER; ++q) c[q] = (q < per && b0 + q < n_regions) ? rc[b0 + q] : 0u;
-    };
-    unsigned int cur[PFX_PER], nxt[PFX_PER];
-    if (in_regs && K > 0) load(0, cur);
-    int64_t base = 0;
-    for (int k = 0; k < K; ++k) {
-        const unsigned int *rc = region_count + (int64_t)k * n_regions;
-        int64_t mine = 0;
-        if (in_regs) {
-            if (k + 1 < K) load(k + 1, nxt);
-#pragma unroll
-            for (int q = 0; q < PFX_PER; ++q) mine += cur[q];
-        } else {
-            for (int b = b0; b < b0 + per && b < n_regions; ++b) mine += rc[b];
+        for (int q = 0; q < PFX_PER; ++q) {
+            cur[q] = (q < per && b0 + q < n_regions) ? rc[b0 + q] : 0u;
+            mine += cur[q];
         }
-        int64_t v = mine;
+    } else {
+        for (int b = b0; b < b0 + per && b < n_regions; ++b) mine += rc[b];
+    }
+    int64_t v = mine;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int64_t t = __shfl_up(v, off, 64);
-            if (lane >= off) v += t;
-        }
-        if (lane == 63) wsum[wave] = v;
-        __syncthreads();
-        if (wave == 0) {
-            int64_t w = lane < NW ? wsum[lane] : 0;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    if (wave == 0) {
+        int64_t w = lane < NW ? wsum[lane] : 0;
 #pragma unroll
-            for (int off = 1; off < NW; off <<= 1) {
-                const int64_t t = __shfl_up(w, off, 64);
-                if (lane >= off) w += t;
-            }
-            if (lane < NW) wsum[lane] = w;
+        for (int off = 1; off < NW; off <<= 1) {
+            const int64_t t = __shfl_up(w, off, 64);
+            if (lane >= off) w += t;
         }
-        __syncthreads();
-        int64_t acc = v - mine + (wave > 0 ? wsum[wave - 1] : 0);  // exclusive
-        int64_t *pf = xpref + (int64_t)k * (n_regions + 1);
-        if (in_regs) {
+        if (lane < NW) wsum[lane] = w;
+    }
+    __syncthreads();
+    int64_t acc = v - mine + (wave > 0 ? wsum[wave - 1] : 0);  // exclusive
+    int64_t *pf = xpref + (int64_t)k * (n_regions + 1);
+    if (in_regs) {
 #pragma unroll
-            for (int q = 0; q < PFX_PER; ++q) {
-                if (q < per && b0 + q < n_regions) pf[b0 + q] = acc;
-                acc += cur[q];
-            }
-#pragma unroll
-            for (int q = 0; q < PFX_PER; ++q) cur[q] = nxt[q];
-        } else {
-            for (int b = b0; b < b0 + per && b < n_regions; ++b) {
-                pf[b] = acc;
-                acc += rc[b];
-            }
+        for (int q = 0; q < PFX_PER; ++q) {
+            if (q < per && b0 + q < n_regions) pf[b0 + q] = acc;
+            acc += cur[q];
         }
-        const int64_t tot = wsum[NW - 1];
-        if (threadIdx.x == 0) {
-            pf[n_regions] = tot;
-            xinfo[k] = base;
-            xinfo[K + k] = tot;
+    } else {
+        for (int b = b0; b < b0 + per && b < n_regions; ++b) {
+            pf[b] = acc;
+            acc += rc[b];
         }
-        base += tot;
-        __syncthreads();  // wsum is rewritten by the next column
     }
     if (threadIdx.x == 0) {
+        const int64_t tot = wsum[NW - 1];
+        pf[n_regions] = tot;
+        xinfo[K + k] = tot;
+        __threadfence();
+        s_last = atomicAdd(done, 1ull) == (unsigned long long)(K - 1);
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x == 0) {
+        __threadfence();
+        int64_t base = 0;
+        for (int c = 0; c < K; ++c) {
+            xinfo[c] = base;
+            base += (int64_t)atomicAdd(reinterpret_cast<unsigned long long *>(&xinfo[K + c]), 0ull);  // from L2
+        }
         xinfo[2 * K] = base > cap ? 1 : 0;
         xinfo[2 * K + 1] = base;
+        *done = 0;  // ready for a re-run of the phase
     }
 }
 
@@ -2368,10 +2368,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed here.
     const int n_info = 2 * K + 2;
     const int n_cnt = (3 * K + 1) / 2;  // int64 slots of the 3K uint32 list lengths
-    const int n_all = n_info + n_cnt + 1;
+    const int n_all = n_info + n_cnt + 2;  // + the error word and k_prefix's completion counter
     SPK_TRY(ctx->xinfo.alloc((size_t)n_all));
     SPK_TRY(ctx->pinned_info((size_t)n_all));
-    SPK_HIP(hipMemsetAsync(ctx->xinfo.p + n_info, 0, (size_t)(n_cnt + 1) * 8, ctx->stream));
+    SPK_HIP(hipMemsetAsync(ctx->xinfo.p + n_info, 0, (size_t)(n_cnt + 2) * 8, ctx->stream));
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -2515,8 +2515,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         A.slow_off = ctx->xinfo.p;
         ctx->xcap = cap;
         if (P > 0) {
-        k_prefix<<<1, PFX_THREADS, 0, ctx->stream>>>(ctx->region_count.p, K, n_regions, cap, ctx->xpref.p,
-                                                    ctx->xinfo.p);
+        k_prefix<<<(unsigned)K, PFX_THREADS, 0, ctx->stream>>>(
+            ctx->region_count.p, K, n_regions, cap, ctx->xpref.p, ctx->xinfo.p,
+            reinterpret_cast<unsigned long long *>(ctx->xinfo.p + n_info + n_cnt + 1));
         // Jaro-Winkler template columns: compact every list, then one exact launch over all of them
         ExactCols jw{};
         // JW lists are short (cfg2: 0.1-0.3 M cells): fewer blocks give each lane several cells, so
