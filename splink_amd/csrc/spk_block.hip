@@ -25,9 +25,17 @@ static constexpr int64_t EN_CHUNK = (int64_t)EN_THREADS * EN_PER_THREAD;
 static constexpr int MAX_RULES = 32;
 
 struct RuleKeys {
-    const int64_t *keyL[MAX_RULES];  // key of the l-side row (table 0)
-    const int64_t *keyR[MAX_RULES];  // key of the r-side row (table of the r side)
+    const int64_t *keyL[MAX_RULES];  // key of rule j at each l-view position (position-ordered copy)
+    const int64_t *keyR[MAX_RULES];  // key of rule j at each r-view position
 };
+
+// dst[i] = src[rows[i]]: a table array in a rule's view order, so k_enum reads it by view position
+// (contiguous within a block) instead of gathering it by row for every candidate pair.
+__global__ void k_by_position(int64_t n, const int32_t *__restrict__ rows, const int64_t *__restrict__ src,
+                              int64_t *__restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[rows[i]];
+}
 
 __global__ void k_make_sort_keys(int64_t n, const int64_t *__restrict__ key, const int64_t *__restrict__ rank,
                                  uint64_t *__restrict__ out_keys, int32_t *__restrict__ out_rows,
@@ -91,7 +99,7 @@ struct EnumArgs {
     const int64_t *bstartR;     // [B] r-view starts (bipartite)
     const int64_t *bnR;         // [B] r-view sizes (bipartite)
     const int32_t *rowsL, *rowsR;
-    const int64_t *rankL, *rankR;
+    const int64_t *rankL, *rankR;  // rank at each l- / r-view position (position-ordered copies)
     int tri;
     int rank_filter;            // 1: keep rank(l) < rank(r) (dedupe / link_and_dedupe)
     int64_t null_div;           // > 0: rank = src * null_div + r, r == null_div - 1 for a NULL unique id
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(EN_THREADS) void k_enum(EnumArgs A) {
             vy[i] = (int32_t)pc;
             bool ok = true;
             if (A.rank_filter) {
-                int64_t rx = A.rankL[x], ry = A.rankR[y];
+                int64_t rx = A.rankL[pa], ry = A.rankR[pc];
                 if (A.tri) {
                     ok = rx != ry;  // sorted by rank inside the block: rx <= ry
                 } else {
@@ -184,8 +192,8 @@ __global__ __launch_bounds__(EN_THREADS) void k_enum(EnumArgs A) {
                     ok = false;
             }
             for (int j = 0; ok && j < A.rule; ++j) {
-                int64_t kl = A.keys.keyL[j][x];
-                if (kl >= 0 && kl == A.keys.keyR[j][y]) ok = false;
+                int64_t kl = A.keys.keyL[j][pa];
+                if (kl >= 0 && kl == A.keys.keyR[j][pc]) ok = false;
             }
             xs[i] = x;
             ys[i] = y;
@@ -270,6 +278,10 @@ static int exclusive_scan(spk_ctx *ctx, const T *in, T *out, int64_t n, DevBuf<u
 struct RulePlan {
     SortedView L, R;
     DevBuf<int64_t> bstart, bstartR, bnR, cand, cand_off;
+    // by view position: rank (l, r), then the keys of the earlier rules (l then r per rule)
+    DevBuf<int64_t> bypos;
+    const int64_t *rankL = nullptr, *rankR = nullptr;
+    const int64_t *keyL[MAX_RULES] = {}, *keyR[MAX_RULES] = {};
     int64_t B = 0, T = 0;
     int tri = 1;
 };
@@ -315,6 +327,29 @@ static int plan_rule(spk_ctx *ctx, int rule, bool symmetric, RulePlan &P, DevBuf
     SPK_HIP(hipMemcpyAsync(&lc[1], P.cand.p + B - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     P.T = lc[0] + lc[1];
+    if (P.T == 0) return SPK_OK;
+    // position-ordered copies of what k_enum reads per candidate pair: ranks (dedupe / link_and_dedupe)
+    // and the keys of rules 0 .. rule-1 (earlier-rule exclusion)
+    const int64_t nL = P.L.n_valid, nR = P.tri ? nL : P.R.n_valid;
+    const int32_t *rowsR = P.tri ? P.L.rows.p : P.R.rows.p;
+    const bool ranks = !link_only;
+    SPK_TRY(P.bypos.alloc((size_t)((ranks ? 1 : 0) + rule) * (size_t)(nL + nR) + 1));
+    int64_t *at = P.bypos.p;
+    auto by_pos = [&](int64_t m, const int32_t *rows, const int64_t *src) -> const int64_t * {
+        int64_t *dst = at;
+        at += m;
+        if (m > 0) k_by_position<<<(unsigned)((m + 255) / 256), 256, 0, ctx->stream>>>(m, rows, src, dst);
+        return dst;
+    };
+    if (ranks) {
+        P.rankL = by_pos(nL, P.L.rows.p, rankL);
+        P.rankR = by_pos(nR, rowsR, tr.rank.p);
+    }
+    for (int j = 0; j < rule; ++j) {
+        P.keyL[j] = by_pos(nL, P.L.rows.p, tl.key[0][j]->p);
+        P.keyR[j] = by_pos(nR, rowsR, tr.key[1][j]->p);
+    }
+    SPK_HIP(hipGetLastError());
     return SPK_OK;
 }
 
@@ -364,10 +399,6 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
     int64_t g_hi = (int64_t)((__int128)total * (shard + 1) / n_shards);
 
     EnumArgs base{};
-    for (int r = 0; r < n_rules; ++r) {
-        base.keys.keyL[r] = tl.key[0][r]->p;
-        base.keys.keyR[r] = tr.key[1][r]->p;
-    }
     // count pass
     std::vector<DevBuf<int64_t> *> counts(n_rules, nullptr), offs(n_rules, nullptr);
     struct G2 {
@@ -402,8 +433,12 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         A.bnR = P.bnR.p;
         A.rowsL = P.L.rows.p;
         A.rowsR = P.tri ? P.L.rows.p : P.R.rows.p;
-        A.rankL = tl.rank.p;
-        A.rankR = tr.rank.p;
+        A.rankL = P.rankL;
+        A.rankR = P.rankR;
+        for (int j = 0; j < r; ++j) {
+            A.keys.keyL[j] = P.keyL[j];
+            A.keys.keyR[j] = P.keyR[j];
+        }
         A.tri = P.tri;
         A.rank_filter = link_only ? 0 : 1;
         A.null_div = tl.null_div;
@@ -443,8 +478,12 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         A.bnR = P.bnR.p;
         A.rowsL = P.L.rows.p;
         A.rowsR = P.tri ? P.L.rows.p : P.R.rows.p;
-        A.rankL = tl.rank.p;
-        A.rankR = tr.rank.p;
+        A.rankL = P.rankL;
+        A.rankR = P.rankR;
+        for (int j = 0; j < r; ++j) {
+            A.keys.keyL[j] = P.keyL[j];
+            A.keys.keyR[j] = P.keyR[j];
+        }
         A.tri = P.tri;
         A.rank_filter = link_only ? 0 : 1;
         A.null_div = tl.null_div;
