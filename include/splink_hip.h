@@ -73,7 +73,9 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
                        const uint8_t *valid, const int64_t *value_ids);
 int spk_table_add_float64(spk_ctx *ctx, int side, int col, const double *values, const uint8_t *valid);
 /* Order rank per row for the link-type predicate: dedupe `l.uid < r.uid` (blocking.py:136),
- * link_and_dedupe `(l.src < r.src) or (l.uid < r.uid and same src)` (:139).  Equal rank = equal key. */
+ * link_and_dedupe `(l.src < r.src) or (l.uid < r.uid and same src)` (:139).  Equal rank = equal key.
+ * Per-row host arrays (rank, keys) are in INPUT row order; after spk_cluster they are taken through the
+ * table's permutation.  A new rank clears the NULL-id layout (declare it again with spk_table_set_rank_null). */
 int spk_table_set_rank(spk_ctx *ctx, int side, const int64_t *rank);
 /* NULL unique ids (blocking.py:136, :139: `l.uid < r.uid` is NULL, so the pair is dropped, unless
  * `l._source_table < r._source_table` holds).  divisor > 0 declares the rank layout
@@ -108,8 +110,9 @@ int spk_key_build(spk_ctx *ctx, int rule, int n_terms, const spk_key_term *terms
 int spk_rank_from_raw(spk_ctx *ctx, int raw_uid, int64_t right_from);
 /* Reorder the tables' rows by rule 0's key, then rank (NULL keys last), so a block's rows are
  * contiguous on the device.  Keys and ranks move with the rows; comparison columns must be added
- * after this (they are decoded through the permutation).  out_perm0 / out_perm1 (host, optional):
- * input row of each table row. */
+ * after this (they are decoded through the permutation); keys built and ranks set after it follow the
+ * table's row order too (calling it again composes the permutations).  out_perm0 / out_perm1 (host,
+ * optional): input row of each table row. */
 int spk_cluster(spk_ctx *ctx, int32_t *out_perm0, int32_t *out_perm1);
 /* String comparison column `col` from raw column raw0 (table 0) and, for link_only, raw1 (table 1):
  * decoded to UTF-16 through the tables' row permutations, with dictionary ids computed on the
@@ -185,7 +188,11 @@ typedef struct {
 } spk_column_program;
 
 /* Install the comparison programs and evaluate them over the current pairs, producing one
- * packed comparison-vector code per pair: code = Σ_k (γ_k + 1) · Π_{j<k} (L_j + 1). */
+ * packed comparison-vector code per pair: code = Σ_k (γ_k + 1) · Π_{j<k} (L_j + 1).
+ * Asynchronous: returns once the passes are queued on the context stream.  A work-list overflow
+ * or cells past the exact passes' string limit are completed at the next synchronising call that
+ * reads the codes (spk_em_iteration, spk_em_finalize, spk_em_histogram with a caller buffer,
+ * spk_score, spk_gammas_copy, the tf calls, spk_ctx_sync), so results are always complete. */
 int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *cols, int n_when,
                const int32_t *when_first_instr, const int32_t *when_n_instr, const int32_t *when_level,
                int n_instr, const spk_instr *instr, int n_operands, const spk_operand *operands,
@@ -209,17 +216,13 @@ int spk_gammas_exact_list(spk_ctx *ctx, int k, int32_t *out, int64_t n);
  * column holds an empty string, or was not built from raw columns). */
 int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n);
 /* Columns in the shape of the case_statements.py templates (NULL branch, then single-leaf tests
- * on the same two plain operands) are filtered from a packed per-row image of their fields; every
- * other column by the general interpreter.  on = 1 (default): template columns through the
- * column-batched filter; on = 2: through the register-resident row filter when the image row is
- * short (<= 128 bytes); on = 0: every column through the interpreter; on + 10: the same, with
- * the second blocking rule's pairs always reading the table-ordered row image, on + 20: always their
- * rule's view-ordered copy (default: the copy once the image outgrows the caches).  Further
- * A/B digits (splink_amd/csrc/spk_gamma.hip, spk_gammas_set_simple): + 1000 a timing-only filter
- * variant, + W x 10000 / + W x 1000000 the Levenshtein / JW exact passes at W waves per SIMD,
- * + G x 100000 the JW launch at G blocks per CU, + 10000000 the pass replayed as a HIP graph.  All
- * modes give identical results (for testing and measurement).  spk_gammas_simple_count: how many
- * columns the last spk_gammas took as template columns. */
+ * on the same two plain operands) are filtered from a packed per-row image of their fields
+ * (spk_filter.hip); every other column by the general interpreter.  on = 1 (default): template
+ * columns through the filter kernel; on = 0: every column through the interpreter; + 10: the second
+ * blocking rule's pairs always read the table-ordered row image, + 20: always their rule's
+ * view-ordered copy (default: the copy once the image outgrows the caches).  All modes give
+ * identical results (for testing).  spk_gammas_simple_count: how many columns the last spk_gammas
+ * took as template columns. */
 int spk_gammas_set_simple(spk_ctx *ctx, int on);
 int spk_gammas_simple_count(spk_ctx *ctx, int *out);
 /* Filter regions (workgroups) the last spk_gammas ran over the second rule's view-ordered image. */
@@ -237,9 +240,15 @@ int spk_levenshtein(spk_ctx *ctx, int64_t n, const int64_t *l_offsets, const uin
 
 /* ---- EM (replaces run_expectation_step + run_maximisation_step's aggregate,
  *      expectation_step.py:25-221, maximisation_step.py:41-90) ------------------ */
-/* Streams every pair's code once and writes the pattern histogram (uint64 [n_patterns]) to
- * d_hist, a DEVICE buffer (NULL = context-owned).  The histogram is the sufficient statistic of
- * the E+M step; callers sharding pairs over GPUs all-reduce it (exact integer sum). */
+/* One EM iteration over this context's pairs in ONE launch: streams every pair's code into the
+ * pattern histogram, and the workgroup that finishes last evaluates mp per pattern and the M-step
+ * sums.  out_stats / m / u / lambda as spk_em_finalize.  For a single GPU (no exchange). */
+int spk_em_iteration(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
+                     double *out_stats, int n_stats);
+/* Multi-GPU form of the same iteration: spk_em_histogram streams every pair's code once and writes
+ * the pattern histogram (uint64 [n_patterns]) to d_hist, a DEVICE buffer (NULL = context-owned);
+ * with a caller buffer it returns once the histogram is final.  Callers sharding pairs over GPUs
+ * all-reduce it (exact integer sum), then spk_em_finalize. */
 int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist);
 /* Histogram kernel choice (same result): 1 = lane-private LDS counters when the pattern space fits
  * (default), 0 = wave-ballot aggregation into one LDS histogram.  For testing and measurement. */

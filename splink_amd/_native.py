@@ -44,7 +44,7 @@ EXPORTS = [
     "spk_ctx_sync", "spk_ctx_set_link_type", "spk_ctx_kernel_ms", "spk_ctx_enable_timing", "spk_table_create",
     "spk_table_add_utf8", "spk_table_add_float64", "spk_table_set_rank", "spk_table_set_key", "spk_block",
     "spk_pairs_count", "spk_pairs_copy", "spk_pairs_load", "spk_gammas", "spk_gammas_copy", "spk_gammas_load",
-    "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_score",
+    "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_em_iteration", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
     "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
@@ -315,7 +315,8 @@ class Context:
         return out[:K].tolist()
 
     def gammas_set_simple(self, mode):
-        """1 / True: template-column filters (column-batched), 2: register-row filter when short, 0: interpreter."""
+        """1 / True: template-shaped columns through the filter kernel, 0: every column through the interpreter;
+        + 10: rule 1's pairs never read the view-ordered image, + 20: always (tests)."""
         check(self._lib.spk_gammas_set_simple(self._h, ctypes.c_int(int(mode))), "spk_gammas_set_simple")
 
     def lds_per_block(self) -> int:
@@ -347,6 +348,18 @@ class Context:
                                         ctypes.c_double(one_minus), _ptr(m), _ptr(u), _ptr(out),
                                         ctypes.c_int(n_stats)), "spk_em_finalize")
         return out
+
+    def em_iteration(self, lam, one_minus, m, u, n_stats):
+        """One E+M iteration on this GPU's pairs in one launch (histogram, E-step per pattern, M-step sums)."""
+        m = np.ascontiguousarray(m, dtype=np.float64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        out = self._stats_buf(n_stats)
+        check(self._lib.spk_em_iteration(self._h, ctypes.c_double(lam), ctypes.c_double(one_minus), _ptr(m), _ptr(u),
+                                         _ptr(out), ctypes.c_int(n_stats)), "spk_em_iteration")
+        return out
+
+    def _stats_buf(self, n_stats):
+        return np.zeros(n_stats, dtype=np.float64)
 
     def score(self, lam, one_minus, m, u, start=0, count=0, want_host=True):
         m = np.ascontiguousarray(m, dtype=np.float64)

@@ -215,16 +215,31 @@ __global__ __launch_bounds__(EN_THREADS) void k_enum(EnumArgs A) {
         if (threadIdx.x == EN_THREADS - 1) A.chunk_count[chunk] = incl;
         return;
     }
-    int64_t pos = A.chunk_off[chunk] + incl - cnt;
+    // the block's kept pairs are compacted in LDS, then written out with consecutive lanes on
+    // consecutive positions (a thread's own run of EN_PER_THREAD would give strided lane writes)
+    __shared__ int32_t s_out[4][EN_CHUNK];
+    const bool views = A.out_vl != nullptr;
+    int loc = (int)(incl - cnt);
     for (int i = 0; i < EN_PER_THREAD; ++i) {
         if (keep & (1u << i)) {
-            A.out_l[pos] = xs[i];
-            A.out_r[pos] = ys[i];
-            if (A.out_vl) {
-                A.out_vl[pos] = vx[i];
-                A.out_vr[pos] = vy[i];
+            s_out[0][loc] = xs[i];
+            s_out[1][loc] = ys[i];
+            if (views) {
+                s_out[2][loc] = vx[i];
+                s_out[3][loc] = vy[i];
             }
-            ++pos;
+            ++loc;
+        }
+    }
+    __syncthreads();
+    const int total = (int)s_scan[EN_THREADS - 1];
+    const int64_t out0 = A.chunk_off[chunk];
+    for (int k = threadIdx.x; k < total; k += EN_THREADS) {
+        A.out_l[out0 + k] = s_out[0][k];
+        A.out_r[out0 + k] = s_out[1][k];
+        if (views) {
+            A.out_vl[out0 + k] = s_out[2][k];
+            A.out_vr[out0 + k] = s_out[3][k];
         }
     }
 }
@@ -327,13 +342,21 @@ static int plan_rule(spk_ctx *ctx, int rule, bool symmetric, RulePlan &P, DevBuf
     SPK_HIP(hipMemcpyAsync(&lc[1], P.cand.p + B - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     P.T = lc[0] + lc[1];
-    if (P.T == 0) return SPK_OK;
-    // position-ordered copies of what k_enum reads per candidate pair: ranks (dedupe / link_and_dedupe)
-    // and the keys of rules 0 .. rule-1 (earlier-rule exclusion)
+    return SPK_OK;
+}
+
+// Position-ordered copies of what k_enum reads per candidate pair: ranks (dedupe / link_and_dedupe) and
+// the keys of rules 0 .. rule-1 (earlier-rule exclusion).  Built just before a pass over the rule and
+// released after it (release_by_position), so at most one rule's copies exist at a time; a symmetric
+// self-join (tri) reads the l-side rank copy for both sides.
+static int build_by_position(spk_ctx *ctx, int rule, RulePlan &P) {
+    Table &tl = ctx->table[0];
+    Table &tr = ctx->side_table(1);
+    const bool ranks = ctx->link_type != SPK_LINK_ONLY;
     const int64_t nL = P.L.n_valid, nR = P.tri ? nL : P.R.n_valid;
     const int32_t *rowsR = P.tri ? P.L.rows.p : P.R.rows.p;
-    const bool ranks = !link_only;
-    SPK_TRY(P.bypos.alloc((size_t)((ranks ? 1 : 0) + rule) * (size_t)(nL + nR) + 1));
+    const int64_t n_rank = ranks ? (P.tri ? nL : nL + nR) : 0;
+    SPK_TRY(P.bypos.alloc((size_t)(n_rank + (int64_t)rule * (nL + nR)) + 1));
     int64_t *at = P.bypos.p;
     auto by_pos = [&](int64_t m, const int32_t *rows, const int64_t *src) -> const int64_t * {
         int64_t *dst = at;
@@ -342,8 +365,8 @@ static int plan_rule(spk_ctx *ctx, int rule, bool symmetric, RulePlan &P, DevBuf
         return dst;
     };
     if (ranks) {
-        P.rankL = by_pos(nL, P.L.rows.p, rankL);
-        P.rankR = by_pos(nR, rowsR, tr.rank.p);
+        P.rankL = by_pos(nL, P.L.rows.p, tl.rank.p);
+        P.rankR = P.tri ? P.rankL : by_pos(nR, rowsR, tr.rank.p);
     }
     for (int j = 0; j < rule; ++j) {
         P.keyL[j] = by_pos(nL, P.L.rows.p, tl.key[0][j]->p);
@@ -351,6 +374,12 @@ static int plan_rule(spk_ctx *ctx, int rule, bool symmetric, RulePlan &P, DevBuf
     }
     SPK_HIP(hipGetLastError());
     return SPK_OK;
+}
+
+static void release_by_position(RulePlan &P) {
+    P.bypos.release();
+    P.rankL = P.rankR = nullptr;
+    for (int j = 0; j < MAX_RULES; ++j) P.keyL[j] = P.keyR[j] = nullptr;
 }
 
 }  // namespace spk
@@ -421,6 +450,7 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         if (!n_chunks[r]) continue;
         counts[r] = new DevBuf<int64_t>();
         offs[r] = new DevBuf<int64_t>();
+        SPK_TRY(build_by_position(ctx, r, P));
         SPK_TRY(counts[r]->alloc((size_t)n_chunks[r]));
         SPK_TRY(offs[r]->alloc((size_t)n_chunks[r]));
         EnumArgs A = base;
@@ -447,6 +477,8 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         k_enum<false><<<(unsigned)n_chunks[r], EN_THREADS, 0, ctx->stream>>>(A);
         SPK_HIP(hipGetLastError());
         SPK_TRY(exclusive_scan<int64_t>(ctx, counts[r]->p, offs[r]->p, n_chunks[r], tmp));
+        SPK_HIP(hipStreamSynchronize(ctx->stream));  // the copies are freed next: the pass must be done
+        release_by_position(P);
         int64_t lc[2];
         SPK_HIP(hipMemcpyAsync(&lc[0], offs[r]->p + n_chunks[r] - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
         SPK_HIP(hipMemcpyAsync(&lc[1], counts[r]->p + n_chunks[r] - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -468,6 +500,7 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
     for (int r = 0; r < n_rules; ++r) {
         if (!n_chunks[r]) continue;
         RulePlan &P = *plans[r];
+        SPK_TRY(build_by_position(ctx, r, P));
         EnumArgs A = base;
         A.q0 = rule_lo[r];
         A.q1 = rule_hi[r];
@@ -496,6 +529,8 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
         A.out_vr = view ? ctx->pvr.p + (rule_base[r] - pv_base) : nullptr;
         k_enum<true><<<(unsigned)n_chunks[r], EN_THREADS, 0, ctx->stream>>>(A);
         SPK_HIP(hipGetLastError());
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        release_by_position(P);
     }
     SPK_TRY(ctx->end(K_BLOCK));
     SPK_HIP(hipStreamSynchronize(ctx->stream));

@@ -282,7 +282,6 @@ void spk_ctx_destroy(spk_ctx *ctx) {
     }
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->h_info) (void)hipHostFree(ctx->h_info);
-    ctx->drop_graph();
     hipStream_t own = ctx->own_stream;
     delete ctx;
     if (own) (void)hipStreamDestroy(own);
@@ -297,6 +296,7 @@ int spk_ctx_set_stream(spk_ctx *ctx, void *hip_stream) {
 int spk_ctx_sync(spk_ctx *ctx) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     return SPK_OK;
 }
 
@@ -415,6 +415,34 @@ int spk_table_add_float64(spk_ctx *ctx, int side, int col, const double *values,
     return SPK_OK;
 }
 
+}  // extern "C"
+
+// Per-row host values (input row order) into a device array in table row order: a table reordered by
+// spk_cluster takes them through its permutation (table row i = input row perm[i]).
+__global__ void k_take_rows(int64_t n, const int64_t *__restrict__ src, const int32_t *__restrict__ perm,
+                            int64_t *__restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[perm[i]];
+}
+
+static int upload_rows(spk_ctx *ctx, const Table &t, const int64_t *host, int64_t *dev) {
+    if (t.n <= 0) return SPK_OK;
+    if (!t.perm.p) {
+        SPK_HIP(hipMemcpyAsync(dev, host, (size_t)t.n * 8, hipMemcpyHostToDevice, ctx->stream));
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        return SPK_OK;
+    }
+    DevBuf<int64_t> tmp;
+    SPK_TRY(tmp.alloc((size_t)t.n));
+    SPK_HIP(hipMemcpyAsync(tmp.p, host, (size_t)t.n * 8, hipMemcpyHostToDevice, ctx->stream));
+    k_take_rows<<<(unsigned)((t.n + 255) / 256), 256, 0, ctx->stream>>>(t.n, tmp.p, t.perm.p, dev);
+    SPK_HIP(hipGetLastError());
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+extern "C" {
+
 int spk_table_set_rank(spk_ctx *ctx, int side, const int64_t *rank) {
     SPK_REQUIRE(ctx && (side == 0 || side == 1) && rank, SPK_E_INVALID, "spk_table_set_rank: bad args");
     Table &t = ctx->table[side];
@@ -423,8 +451,9 @@ int spk_table_set_rank(spk_ctx *ctx, int side, const int64_t *rank) {
     for (int64_t i = 0; i < t.n; ++i)
         SPK_REQUIRE(rank[i] >= 0 && rank[i] < (int64_t)UINT32_MAX, SPK_E_LIMIT, "rank must be in [0, 2^32)");
     SPK_TRY(t.rank.alloc((size_t)t.n + 1));
-    if (t.n) SPK_HIP(hipMemcpyAsync(t.rank.p, rank, (size_t)t.n * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    SPK_TRY(upload_rows(ctx, t, rank, t.rank.p));
+    // a new rank has no NULL-id layout until spk_table_set_rank_null declares one again
+    t.null_div = 0;
     return SPK_OK;
 }
 
@@ -445,10 +474,7 @@ int spk_table_set_key(spk_ctx *ctx, int side, int rule, int which, const int64_t
     while ((int)t.key[which].size() <= rule) t.key[which].push_back(new DevBuf<int64_t>());
     SPK_TRY(t.key[which][rule]->alloc((size_t)t.n + 1));
     if (rule < 32) ctx->rule_terms[rule].clear();  // a host-computed key: no term is known
-    if (t.n)
-        SPK_HIP(hipMemcpyAsync(t.key[which][rule]->p, keys, (size_t)t.n * sizeof(int64_t), hipMemcpyHostToDevice,
-                               ctx->stream));
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    SPK_TRY(upload_rows(ctx, t, keys, t.key[which][rule]->p));
     return SPK_OK;
 }
 

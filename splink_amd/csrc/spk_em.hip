@@ -91,92 +91,6 @@ constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LD
 constexpr int HL_UNROLL = 4;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <typename CodeT, int R>
-__global__ __launch_bounds__(HL_THREADS) void k_hist_lanes(const CodeT *__restrict__ codes, int64_t P, int n_pat,
-                                                           uint32_t *__restrict__ part) {
-    extern __shared__ uint32_t sh[];
-    for (int b = threadIdx.x; b < n_pat * R; b += HL_THREADS) sh[b] = 0;
-    __syncthreads();
-    constexpr int VEC = 16 / sizeof(CodeT);
-    constexpr int BITS = 8 * sizeof(CodeT);
-    const uint32_t copy = threadIdx.x & (R - 1);
-    const u32x4 *cv = reinterpret_cast<const u32x4 *>(codes);
-    const int64_t n_vec = P / VEC;
-    const int64_t stride = (int64_t)gridDim.x * HL_THREADS;
-    int64_t v = (int64_t)blockIdx.x * HL_THREADS + threadIdx.x;
-    auto count_word = [&](uint32_t w) {
-#pragma unroll
-        for (int j = 0; j < 32 / BITS; ++j) {
-            const uint32_t c = BITS == 32 ? w : ((w >> (BITS * j)) & ((1u << BITS) - 1u));
-            atomicAdd(&sh[c * R + copy], 1u);
-        }
-    };
-    // Software-pipelined: the next group's HL_UNROLL loads are issued before the current group's
-    // LDS counts, so every lane keeps 2 x HL_UNROLL x 16 B in flight while it counts.  Nontemporal
-    // loads: 76 % of HBM peak over 368M pairs against 70 % with default-policy loads.
-    const int64_t step = HL_UNROLL * stride;
-    bool have = v + (HL_UNROLL - 1) * stride < n_vec;
-    u32x4 w[HL_UNROLL];
-    if (have) {
-#pragma unroll
-        for (int u = 0; u < HL_UNROLL; ++u) w[u] = __builtin_nontemporal_load(cv + v + u * stride);
-    }
-    while (have) {
-        const int64_t vn = v + step;
-        const bool hn = vn + (HL_UNROLL - 1) * stride < n_vec;
-        u32x4 x[HL_UNROLL];
-        if (hn) {
-#pragma unroll
-            for (int u = 0; u < HL_UNROLL; ++u) x[u] = __builtin_nontemporal_load(cv + vn + u * stride);
-        }
-#pragma unroll
-        for (int u = 0; u < HL_UNROLL; ++u) {
-            count_word(w[u].x);
-            count_word(w[u].y);
-            count_word(w[u].z);
-            count_word(w[u].w);
-        }
-#pragma unroll
-        for (int u = 0; u < HL_UNROLL; ++u) w[u] = x[u];
-        v = vn;
-        have = hn;
-    }
-    for (; v < n_vec; v += stride) {
-        const u32x4 w = cv[v];
-        count_word(w.x);
-        count_word(w.y);
-        count_word(w.z);
-        count_word(w.w);
-    }
-    if (blockIdx.x == 0)  // tail (P not a multiple of VEC)
-        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
-    __syncthreads();
-    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
-        uint32_t s = 0;
-#pragma unroll
-        for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
-        part[(int64_t)blockIdx.x * n_pat + b] = (uint32_t)s;
-    }
-}
-
-// hist[b] = Σ_w part[w][b]: one 256-thread block per bin, fixed-order tree -- deterministic, no
-// atomics, no memset (the loop over hundreds of partials is spread over the block's lanes).
-constexpr int HR_THREADS = 256;
-__global__ __launch_bounds__(HR_THREADS) void k_hist_reduce(const uint32_t *__restrict__ part, int n_part, int n_pat,
-                                                            unsigned long long *__restrict__ hist) {
-    __shared__ unsigned long long s[HR_THREADS];
-    const int b = blockIdx.x;
-    unsigned long long acc = 0;
-    for (int w = threadIdx.x; w < n_part; w += HR_THREADS) acc += part[(int64_t)w * n_pat + b];
-    s[threadIdx.x] = acc;
-    __syncthreads();
-    for (int off = HR_THREADS / 2; off > 0; off >>= 1) {
-        if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) hist[b] = s[0];
-}
-
 // Comparison-pattern arithmetic.  The pattern space description (mixed-radix strides, levels,
 // offsets into the flattened m / u) and -- for up to PA_INLINE_MU levels, every template setting --
 // the m / u tables themselves travel in the kernel arguments: no per-iteration uploads.
@@ -241,70 +155,235 @@ __global__ void k_pattern_mp(PatArgs A0, double *__restrict__ mpat, double *__re
     if (llpat) llpat[p] = ll;
 }
 
-constexpr int S_THREADS = 256;
 constexpr int N_HEAD = 5;  // [Σmp, rows, non-null rows, Σ ln(...), non-null ln rows]
 
-// E-step per pattern + the M-step sums, one block per statistics slot: slot 0 = totals, slot 1 + s =
-// (column k, level v) in (k, v) order.  Each thread sums a fixed strided subset of patterns; a fixed
-// LDS tree finishes: deterministic, and the same for any sharding of pairs (integer histogram).
-__global__ __launch_bounds__(S_THREADS) void k_em_stats(PatArgs A0, const unsigned long long *__restrict__ hist,
-                                                        const double *__restrict__ mpat,
-                                                        const double *__restrict__ llpat, double *__restrict__ out) {
-    __shared__ double s[6][S_THREADS];
-    __shared__ PatArgs sA;
-    const PatArgs &A = stage_args(A0, &sA);
-    const int slot = blockIdx.x;
-    int kk = -1, vv = 0;
-    if (slot > 0) {
-        int r = slot - 1;
-        for (kk = 0; kk < A.K && r > A.nlev[kk]; ++kk) r -= A.nlev[kk] + 1;
-        vv = r - 1;
+// ---- one EM iteration in one launch (single GPU) ----------------------------------------------------------
+// The E-step per pattern and the M-step sums of the whole pattern space, by ONE workgroup of
+// EF_THREADS: each thread evaluates its strided patterns (mp, ln, count) into LDS (global arrays past
+// EF_LDS_PAT patterns), then each wave takes statistics slots (slot 0 = totals, slot 1 + s = (column k,
+// level v)), sums its lanes' strided patterns and reduces with a fixed butterfly -- deterministic, and
+// the same for any sharding of the pairs (the histogram is an exact integer sum).  count(p) supplies
+// pattern p's count.  Pattern digits come from divisions by wave-uniform radices in fp64 (exact for
+// p < 2^31 after one correction step) instead of integer division sequences.
+constexpr int EF_THREADS = 1024;
+constexpr int EF_LDS_PAT = 4096;  // 3 doubles per pattern in LDS (96 KiB)
+
+__device__ __forceinline__ int udiv_uniform(int p, int d, double rd, int &rem) {
+    int q = (int)((double)p * rd);
+    int r = p - q * d;
+    if (r < 0) {
+        --q;
+        r += d;
+    } else if (r >= d) {
+        ++q;
+        r -= d;
     }
-    double rows = 0, nn = 0, sm = 0, s1 = 0, sll = 0, nll = 0;
-    for (int p = threadIdx.x; p < A.n_pat; p += S_THREADS) {
-        const unsigned long long c = hist[p];
-        if (!c) continue;
-        if (kk >= 0 && pa_gamma(A, p, kk) != vv) continue;
-        const double cd = (double)c;
-        const double mp = mpat[p], ll = llpat[p];
-        rows += cd;
-        if (!isnan(mp)) {
-            nn += cd;
-            sm += cd * mp;
-            s1 += cd * (1.0 - mp);
+    rem = r;
+    return q;
+}
+
+template <class Count>
+__device__ void em_finalize_block(const PatArgs &A, Count count, double *__restrict__ mpat, double *__restrict__ llpat,
+                                  double *__restrict__ cpat, double *__restrict__ out, double *s_tab) {
+    const bool lds = s_tab != nullptr && A.n_pat <= EF_LDS_PAT;  // block-uniform
+    double *tc = lds ? s_tab : cpat, *tm = lds ? s_tab + A.n_pat : mpat, *tl = lds ? s_tab + 2 * A.n_pat : llpat;
+    for (int p = threadIdx.x; p < A.n_pat; p += blockDim.x) {
+        const unsigned long long c = count(p);
+        // mixed-radix digits, then the reference's left-associative products (pattern_mp)
+        double num = A.lambda, den = A.one_minus;
+        int q = p;
+        for (int k = 0; k < A.K; ++k) {
+            const int radix = A.nlev[k] + 1;
+            int g;
+            q = udiv_uniform(q, radix, 1.0 / (double)radix, g);
+            --g;
+            num = num * (g < 0 ? 1.0 : pa_m(A, A.moff[k] + g));
         }
-        if (!isnan(ll)) {
-            nll += cd;
-            sll += cd * ll;
+        q = p;
+        for (int k = 0; k < A.K; ++k) {
+            const int radix = A.nlev[k] + 1;
+            int g;
+            q = udiv_uniform(q, radix, 1.0 / (double)radix, g);
+            --g;
+            den = den * (g < 0 ? 1.0 : pa_u(A, A.moff[k] + g));
+        }
+        const double d = num + den;
+        const double ll = d > 0.0 ? log(d) : NAN;
+        const double mp = d == 0.0 ? NAN : num / d;
+        mpat[p] = mp;
+        llpat[p] = ll;
+        cpat[p] = (double)c;
+        if (lds) {
+            tc[p] = (double)c;
+            tm[p] = mp;
+            tl[p] = ll;
         }
     }
-    s[0][threadIdx.x] = rows;
-    s[1][threadIdx.x] = nn;
-    s[2][threadIdx.x] = sm;
-    s[3][threadIdx.x] = s1;
-    s[4][threadIdx.x] = sll;
-    s[5][threadIdx.x] = nll;
+    __threadfence_block();
     __syncthreads();
-    for (int off = S_THREADS / 2; off > 0; off >>= 1) {
-        if (threadIdx.x < off)
-            for (int q = 0; q < 6; ++q) s[q][threadIdx.x] += s[q][threadIdx.x + off];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        if (slot == 0) {
-            out[0] = s[2][0];
-            out[1] = s[0][0];
-            out[2] = s[1][0];
-            out[3] = s[4][0];
-            out[4] = s[5][0];
-        } else {
-            double *o = out + N_HEAD + 4 * (slot - 1);
-            o[0] = s[0][0];
-            o[1] = s[1][0];
-            o[2] = s[2][0];
-            o[3] = s[3][0];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n_waves = blockDim.x >> 6;
+    for (int slot = wave; slot <= A.n_slots; slot += n_waves) {  // wave-uniform
+        int kk = -1, vv = 0;
+        if (slot > 0) {
+            int r = slot - 1;
+            for (kk = 0; kk < A.K && r > A.nlev[kk]; ++kk) r -= A.nlev[kk] + 1;
+            vv = r - 1;
+        }
+        const int st = kk >= 0 ? A.stride[kk] : 1, radix = kk >= 0 ? A.nlev[kk] + 1 : 1;
+        const double rst = 1.0 / (double)st, rrad = 1.0 / (double)radix;
+        double v[6] = {0, 0, 0, 0, 0, 0};  // rows, non-null rows, Σmp, Σ(1-mp), Σ ln, non-null ln rows
+        for (int p = lane; p < A.n_pat; p += 64) {
+            const double c = tc[p], mp = tm[p], ll = tl[p];
+            bool in = c != 0.0;
+            if (kk >= 0) {
+                int rem, g;
+                const int hi = udiv_uniform(p, st, rst, rem);
+                udiv_uniform(hi, radix, rrad, g);
+                in = in && g - 1 == vv;
+            }
+            if (!in) continue;
+            v[0] += c;
+            if (!isnan(mp)) {
+                v[1] += c;
+                v[2] += c * mp;
+                v[3] += c * (1.0 - mp);
+            }
+            if (!isnan(ll)) {
+                v[5] += c;
+                v[4] += c * ll;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) v[q] += __shfl_xor(v[q], off);
+        if (lane == 0) {
+            if (slot == 0) {
+                out[0] = v[2];
+                out[1] = v[0];
+                out[2] = v[1];
+                out[3] = v[4];
+                out[4] = v[5];
+            } else {
+                double *o = out + N_HEAD + 4 * (slot - 1);
+                o[0] = v[0];
+                o[1] = v[1];
+                o[2] = v[2];
+                o[3] = v[3];
+            }
         }
     }
+}
+
+// E-step + M-step sums from a complete histogram (after the ranks' all-reduce): one workgroup.
+__global__ __launch_bounds__(EF_THREADS) void k_em_finalize(PatArgs A0, const unsigned long long *__restrict__ hist,
+                                                            double *__restrict__ mpat, double *__restrict__ llpat,
+                                                            double *__restrict__ cpat, double *__restrict__ out) {
+    __shared__ PatArgs sA;
+    __shared__ double s_tab[3 * EF_LDS_PAT];
+    const PatArgs &A = stage_args(A0, &sA);
+    em_finalize_block(A, [&](int p) { return hist[p]; }, mpat, llpat, cpat, out, s_tab);
+}
+
+// Histogram of the codes with lane-private LDS counters (as k_hist_lanes), each workgroup's counts added
+// to the device accumulator `hist` (integer atomics: exact, order-free; one 128-byte line per bin, so the
+// workgroups' adds to different bins do not serialise on shared lines: 8 bins per line cost 40.6 us per
+// cfg2 iteration against the 20 us of streaming).  The workgroup that finishes last (device-scope
+// ticket) reads the accumulator back -- exchanging every bin with 0, so it is zero again for the next
+// launch -- and either (FIN) runs the E-step and M-step sums, one launch per EM iteration, or writes the
+// plain histogram to out_hist (multi-GPU: the caller all-reduces it).
+constexpr int HIST_PAD = 16;  // u64 per accumulator bin (one 128-byte line)
+template <typename CodeT, int R, bool FIN>
+__global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict__ codes, int64_t P, PatArgs A0,
+                                                        unsigned long long *__restrict__ hist,
+                                                        unsigned int *__restrict__ ticket, double *__restrict__ mpat,
+                                                        double *__restrict__ llpat, double *__restrict__ cpat,
+                                                        double *__restrict__ out, unsigned long long *__restrict__ out_hist) {
+    extern __shared__ uint32_t sh[];
+    __shared__ bool s_last;
+    const int n_pat = A0.n_pat;
+    for (int b = threadIdx.x; b < n_pat * R; b += HL_THREADS) sh[b] = 0;
+    __syncthreads();
+    constexpr int VEC = 16 / sizeof(CodeT);
+    constexpr int BITS = 8 * sizeof(CodeT);
+    const uint32_t copy = threadIdx.x & (R - 1);
+    const u32x4 *cv = reinterpret_cast<const u32x4 *>(codes);
+    const int64_t n_vec = P / VEC;
+    const int64_t stride = (int64_t)gridDim.x * HL_THREADS;
+    int64_t v = (int64_t)blockIdx.x * HL_THREADS + threadIdx.x;
+    auto count_word = [&](uint32_t w) {
+#pragma unroll
+        for (int j = 0; j < 32 / BITS; ++j) {
+            const uint32_t c = BITS == 32 ? w : ((w >> (BITS * j)) & ((1u << BITS) - 1u));
+            atomicAdd(&sh[c * R + copy], 1u);
+        }
+    };
+    // software-pipelined 16-byte nontemporal loads, 2 x HL_UNROLL in flight per lane (k_hist_lanes)
+    const int64_t step = HL_UNROLL * stride;
+    bool have = v + (HL_UNROLL - 1) * stride < n_vec;
+    u32x4 w[HL_UNROLL];
+    if (have) {
+#pragma unroll
+        for (int u = 0; u < HL_UNROLL; ++u) w[u] = __builtin_nontemporal_load(cv + v + u * stride);
+    }
+    while (have) {
+        const int64_t vn = v + step;
+        const bool hn = vn + (HL_UNROLL - 1) * stride < n_vec;
+        u32x4 x[HL_UNROLL];
+        if (hn) {
+#pragma unroll
+            for (int u = 0; u < HL_UNROLL; ++u) x[u] = __builtin_nontemporal_load(cv + vn + u * stride);
+        }
+#pragma unroll
+        for (int u = 0; u < HL_UNROLL; ++u) {
+            count_word(w[u].x);
+            count_word(w[u].y);
+            count_word(w[u].z);
+            count_word(w[u].w);
+        }
+#pragma unroll
+        for (int u = 0; u < HL_UNROLL; ++u) w[u] = x[u];
+        v = vn;
+        have = hn;
+    }
+    for (; v < n_vec; v += stride) {
+        const u32x4 x = cv[v];
+        count_word(x.x);
+        count_word(x.y);
+        count_word(x.z);
+        count_word(x.w);
+    }
+    if (blockIdx.x == 0)  // tail (P not a multiple of VEC)
+        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
+        if (s) atomicAdd(&hist[(int64_t)b * HIST_PAD], (unsigned long long)s);
+    }
+    // last-workgroup-done: every wave's atomics complete, then one release + ticket (k_prefix's pattern)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (FIN) {
+        // the counters are no longer needed: their LDS holds the staged arguments and the pattern table
+        PatArgs *sA = reinterpret_cast<PatArgs *>(sh);
+        const PatArgs &A = stage_args(A0, sA);
+        double *tab = reinterpret_cast<double *>(sh) + (sizeof(PatArgs) + 7) / 8;
+        const bool room = ((sizeof(PatArgs) + 7) / 8 + 3 * (size_t)n_pat) * 8 <= (size_t)n_pat * R * 4;
+        em_finalize_block(A, [&](int p) { return atomicExch(&hist[(int64_t)p * HIST_PAD], 0ull); }, mpat, llpat, cpat,
+                          out, room ? tab : nullptr);
+    } else {
+        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) out_hist[p] = atomicExch(&hist[(int64_t)p * HIST_PAD], 0ull);
+    }
+    if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
 // Final E-step: mp[i] = mpat[code[i]] for pairs [start, start + n).  Each lane turns two codes into
@@ -449,16 +528,50 @@ static int pat_args(spk_ctx *ctx, double lambda, double one_minus, const double 
 
 using namespace spk;
 
-extern "C" int spk_em_set_lane_histogram(spk_ctx *ctx, int on) {
-    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
-    ctx->hist_lanes = on != 0;
+
+// Lane-private copies of the counters that fit the LDS budget (R = 64 .. 4), 0 when none fits.
+static int lane_copies(spk_ctx *ctx) {
+    int R = 64;
+    const int64_t lds_budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block);
+    while (R >= 4 && ctx->n_patterns * R * 4 > lds_budget) R >>= 1;
+    return (R >= 4 && ctx->hist_lanes) ? R : 0;
+}
+
+// Grid of the lane-histogram launches: one 1024-thread workgroup per CU.
+static int64_t lane_grid(spk_ctx *ctx) {
+    const int64_t vecs = ctx->n_pairs / (16 / ctx->code_bytes);
+    return std::max<int64_t>(1, std::min<int64_t>(ctx->n_cu, (vecs + HL_THREADS - 1) / HL_THREADS));
+}
+
+#define SPK_EM_ITER(RR, FIN)                                                                                      \
+    case RR:                                                                                                     \
+        if (ctx->code_bytes == 2)                                                                                \
+            k_em_iter<uint16_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
+                reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h); \
+        else                                                                                                     \
+            k_em_iter<uint32_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
+                reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h); \
+        break;
+
+// The padded accumulation histogram and the ticket of k_em_iter: zero between launches (the last workgroup
+// resets them), zeroed here only when (re)allocated.
+static int em_accumulator(spk_ctx *ctx, unsigned long long **acc, unsigned int **ticket) {
+    const size_t need = (size_t)ctx->n_patterns * HIST_PAD;
+    if (ctx->hist_acc.n < need || !ctx->hist_acc.p) {
+        SPK_TRY(ctx->hist_acc.alloc(need));
+        SPK_HIP(hipMemsetAsync(ctx->hist_acc.p, 0, ctx->hist_acc.n * 8, ctx->stream));
+    }
+    if (!ctx->em_ticket.p) {
+        SPK_TRY(ctx->em_ticket.alloc(1));
+        SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, 4, ctx->stream));
+    }
+    *acc = reinterpret_cast<unsigned long long *>(ctx->hist_acc.p);
+    *ticket = ctx->em_ticket.p;
     return SPK_OK;
 }
 
-extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
-    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
-    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_histogram: no gammas");
-    SPK_HIP(hipSetDevice(ctx->device));
+// The pattern histogram into d_hist (NULL = the context's).
+static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     const int64_t n_pat = ctx->n_patterns;
     unsigned long long *h = reinterpret_cast<unsigned long long *>(d_hist);
     if (!h) {
@@ -467,39 +580,24 @@ extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     }
     const int64_t P = ctx->n_pairs;
     const int vec = 16 / ctx->code_bytes;
-    int R = 64;
-    const int64_t lds_budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block);
-    while (R >= 4 && n_pat * R * 4 > lds_budget) R >>= 1;
+    const int R = lane_copies(ctx);
     SPK_TRY(ctx->begin(K_EMHIST));
-    if (R >= 4 && ctx->hist_lanes) {
-        // one 1024-thread workgroup per CU, per-workgroup partial counts, fixed-order reduction
-        int64_t g = ctx->n_cu;
-        const int64_t vecs = P / vec;
-        if (g > (vecs + HL_THREADS - 1) / HL_THREADS) g = (vecs + HL_THREADS - 1) / HL_THREADS;
-        if (g < 1) g = 1;
-        while (P / g >= ((int64_t)1 << 31)) g *= 2;  // uint32 partial counts
-        SPK_TRY(ctx->hist_part.alloc((size_t)(g * n_pat)));
+    if (R) {
+        PatArgs A{};
+        A.n_pat = (int)n_pat;
+        const int64_t g = lane_grid(ctx);
         const size_t sh = (size_t)n_pat * R * 4;
-        const auto *c16 = reinterpret_cast<const uint16_t *>(ctx->codes.p);
-        const auto *c32 = reinterpret_cast<const uint32_t *>(ctx->codes.p);
-        uint32_t *part = ctx->hist_part.p;
-#define SPK_HL(RR)                                                                                           \
-    case RR:                                                                                                  \
-        if (ctx->code_bytes == 2)                                                                             \
-            k_hist_lanes<uint16_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c16, P, (int)n_pat, part); \
-        else                                                                                                  \
-            k_hist_lanes<uint32_t, RR><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(c32, P, (int)n_pat, part); \
-        break;
+        unsigned long long *acc = nullptr;
+        unsigned int *ticket = nullptr;
+        SPK_TRY(em_accumulator(ctx, &acc, &ticket));
+        double *mpat = nullptr, *llpat = nullptr, *cpat = nullptr, *out = nullptr;
         switch (R) {
-            SPK_HL(64)
-            SPK_HL(32)
-            SPK_HL(16)
-            SPK_HL(8)
-            SPK_HL(4)
+            SPK_EM_ITER(64, false)
+            SPK_EM_ITER(32, false)
+            SPK_EM_ITER(16, false)
+            SPK_EM_ITER(8, false)
+            SPK_EM_ITER(4, false)
         }
-#undef SPK_HL
-        SPK_HIP(hipGetLastError());
-        k_hist_reduce<<<(unsigned)n_pat, HR_THREADS, 0, ctx->stream>>>(part, (int)g, (int)n_pat, h);
     } else {
         SPK_HIP(hipMemsetAsync(h, 0, (size_t)n_pat * 8, ctx->stream));
         int64_t blocks = (P / vec + H_THREADS - 1) / H_THREADS;
@@ -521,7 +619,52 @@ extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     }
     SPK_HIP(hipGetLastError());
     SPK_TRY(ctx->end(K_EMHIST));
-    if (d_hist) SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+static int em_buffers(spk_ctx *ctx, int n_stats) {
+    SPK_TRY(ctx->stats.alloc((size_t)n_stats));
+    SPK_TRY(ctx->pinned_stats(n_stats));
+    SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
+    SPK_TRY(ctx->llpat.alloc((size_t)ctx->n_patterns));
+    SPK_TRY(ctx->cpat.alloc((size_t)ctx->n_patterns));
+    return SPK_OK;
+}
+
+// E-step + M-step sums from the histogram h (one workgroup), statistics copied to out_stats.
+static int finalize_from(spk_ctx *ctx, const unsigned long long *h, const PatArgs &A, double *out_stats, int n_stats) {
+    SPK_TRY(em_buffers(ctx, n_stats));
+    SPK_TRY(ctx->begin(K_EMFIN));
+    k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, h, ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p);
+    SPK_HIP(hipGetLastError());
+    SPK_TRY(ctx->end(K_EMFIN));
+    SPK_HIP(hipMemcpyAsync(ctx->h_stats, ctx->stats.p, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(out_stats, ctx->h_stats, (size_t)n_stats * 8);
+    return SPK_OK;
+}
+
+extern "C" int spk_em_set_lane_histogram(spk_ctx *ctx, int on) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->hist_lanes = on != 0;
+    return SPK_OK;
+}
+
+extern "C" int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_histogram: no gammas");
+    SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(enqueue_histogram(ctx, d_hist));
+    if (d_hist) {
+        // a caller-owned histogram is all-reduced over ranks next: it must be final when this returns
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        bool fixed = false;
+        SPK_TRY(settle_gammas(ctx, &fixed));
+        if (fixed) {
+            SPK_TRY(enqueue_histogram(ctx, d_hist));
+            SPK_HIP(hipStreamSynchronize(ctx->stream));
+        }
+    }
     return SPK_OK;
 }
 
@@ -535,28 +678,69 @@ extern "C" int spk_em_finalize(spk_ctx *ctx, const uint64_t *d_hist, double lamb
     SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_finalize: n_stats mismatch");
     const unsigned long long *h = reinterpret_cast<const unsigned long long *>(d_hist ? d_hist : ctx->hist.p);
     SPK_REQUIRE(h, SPK_E_STATE, "spk_em_finalize: no histogram");
-    SPK_TRY(ctx->stats.alloc((size_t)n_stats));
-    SPK_TRY(ctx->pinned_stats(n_stats));
-    SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
-    SPK_TRY(ctx->llpat.alloc((size_t)ctx->n_patterns));
-    SPK_TRY(ctx->begin(K_EMFIN));
-    k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat.p, ctx->llpat.p);
-    k_em_stats<<<(unsigned)(A.n_slots + 1), S_THREADS, 0, ctx->stream>>>(A, h, ctx->mpat.p, ctx->llpat.p,
-                                                                          ctx->stats.p);
-    SPK_HIP(hipGetLastError());
-    SPK_TRY(ctx->end(K_EMFIN));
-    SPK_HIP(hipMemcpyAsync(ctx->h_stats, ctx->stats.p, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    std::memcpy(out_stats, ctx->h_stats, (size_t)n_stats * 8);
+    SPK_TRY(finalize_from(ctx, h, A, out_stats, n_stats));
+    bool fixed = false;
+    SPK_TRY(settle_gammas(ctx, &fixed));
+    if (fixed && !d_hist) {  // the codes changed after the histogram was taken: take it again
+        SPK_TRY(enqueue_histogram(ctx, nullptr));
+        SPK_TRY(finalize_from(ctx, h, A, out_stats, n_stats));
+    }
     return SPK_OK;
 }
 
+extern "C" int spk_em_iteration(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
+                                double *out_stats, int n_stats) {
+    SPK_REQUIRE(ctx && m && u && out_stats, SPK_E_INVALID, "spk_em_iteration: null arg");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_iteration: no gammas");
+    SPK_HIP(hipSetDevice(ctx->device));
+    PatArgs A;
+    SPK_TRY(pat_args(ctx, lambda, one_minus, m, u, A));
+    SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_iteration: n_stats mismatch");
+    const int R = lane_copies(ctx);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if (!R) {  // pattern space past the lane-private counters: histogram, then finalize
+            SPK_TRY(enqueue_histogram(ctx, nullptr));
+            SPK_TRY(finalize_from(ctx, reinterpret_cast<const unsigned long long *>(ctx->hist.p), A, out_stats, n_stats));
+        } else {
+            const int64_t n_pat = ctx->n_patterns;
+            unsigned long long *acc = nullptr, *h = nullptr;
+            unsigned int *ticket = nullptr;
+            SPK_TRY(em_accumulator(ctx, &acc, &ticket));
+            SPK_TRY(em_buffers(ctx, n_stats));
+            const int64_t P = ctx->n_pairs;
+            const int64_t g = lane_grid(ctx);
+            const size_t sh = std::max<size_t>((size_t)n_pat * R * 4, sizeof(PatArgs));
+            double *mpat = ctx->mpat.p, *llpat = ctx->llpat.p, *cpat = ctx->cpat.p, *out = ctx->stats.p;
+            SPK_TRY(ctx->begin(K_EMHIST));
+            switch (R) {
+                SPK_EM_ITER(64, true)
+                SPK_EM_ITER(32, true)
+                SPK_EM_ITER(16, true)
+                SPK_EM_ITER(8, true)
+                SPK_EM_ITER(4, true)
+            }
+            SPK_HIP(hipGetLastError());
+            SPK_TRY(ctx->end(K_EMHIST));
+            ctx->ev_used[K_EMFIN] = false;  // one launch: the E-step is inside the histogram kernel
+            SPK_HIP(hipMemcpyAsync(ctx->h_stats, out, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
+            SPK_HIP(hipStreamSynchronize(ctx->stream));
+            std::memcpy(out_stats, ctx->h_stats, (size_t)n_stats * 8);
+        }
+        bool fixed = false;
+        SPK_TRY(settle_gammas(ctx, &fixed));
+        if (!fixed) break;  // else the codes changed after this iteration read them: run it again
+    }
+    return SPK_OK;
+}
+
+#undef SPK_EM_ITER
 extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
                          int64_t start, int64_t count, double *out_mp) {
     SPK_REQUIRE(ctx && m && u, SPK_E_INVALID, "spk_score: null arg");
     SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_score: no gammas");
     SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_score: range");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     PatArgs A;
     SPK_TRY(pat_args(ctx, lambda, one_minus, m, u, A));
     SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
@@ -596,6 +780,7 @@ extern "C" int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *
                 "spk_tf_accumulate: bad args");
     SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_accumulate: run spk_score over all pairs first");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
     DevBuf<int64_t> d0, d1;
     DevBuf<double> ds;
@@ -654,6 +839,7 @@ extern "C" int spk_tf_accumulate_column(spk_ctx *ctx, int col, int64_t n_values,
     SPK_REQUIRE(ctx && out_sum && out_count && n_values >= 0, SPK_E_INVALID, "spk_tf_accumulate_column: bad args");
     SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_accumulate_column: run spk_score over all pairs first");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
     DevBuf<int64_t> d0, d1;
     int64_t n0 = 0, n1 = 0;
@@ -714,6 +900,7 @@ extern "C" int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *
     SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply_columns: run spk_score first");
     SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply_columns: range");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
     DevBuf<int64_t> d0[8], d1[8];
     TfApply T{};
@@ -736,6 +923,7 @@ extern "C" int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *i
     SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply: run spk_score first");
     SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply: range");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
     DevBuf<int64_t> d0[8], d1[8];
     DevBuf<double> dt[8], dout, dadj;

@@ -27,240 +27,9 @@
 #include <type_traits>
 #include <cmath>
 
-#include "spk_strsim.h"
+#include "spk_gamma.h"
 
 namespace spk {
-
-constexpr int F_THREADS = 256;  // filter pass
-constexpr int X_THREADS = 256;  // exact pass
-constexpr int U_THREADS = 128;  // UDF kernel: 2 x 64 x 128 x 2 B = 32 KiB of LDS per block
-
-enum Mode { M_FILTER = 0, M_EXACT = 1, M_SLOW = 2, M_HUGE = 3 };
-enum Status { ST_DONE = 0, ST_UNDECIDED = 1, ST_NEEDS_SLOW = 2 };
-
-// A "simple" comparison column: the shape every case_statements.py template has --
-//   WHEN x_l IS NULL OR x_r IS NULL THEN null_level
-//   WHEN test_1(x_l, x_r) THEN level_1 ... WHEN test_n(x_l, x_r) THEN level_n ELSE else_level
-// with each test one leaf (=, <>, jaro_winkler_sim cmp t, levenshtein [ratio] cmp t, numeric
-// compare / abs diff / percent diff) over the same two plain operands.  The filter pass evaluates
-// these straight from the two rows' metadata records, loaded for several columns at once; every
-// other program runs through the general interpreter.  Both give identical levels.
-constexpr int MAX_TESTS = 6;
-constexpr int MAX_SIMPLE = 64;   // = the column limit of set_pattern_space
-enum SimpleKind : int32_t { SK_STR = 1, SK_NUM = 2 };
-// Filter class of a simple column, chosen on the host: which row-image fields the filter reads and
-// which bound logic decides the column.  SC_GEN (strings) and SC_NUMRAW (numbers) read the
-// columns' own records instead of the row image.
-enum SimpleClass : int32_t { SC_GEN = 0, SC_EQ = 1, SC_JW = 2, SC_LEV = 3, SC_NUM = 4, SC_NUMRAW = 5 };
-struct SimpleCol {
-    int32_t k;  // comparison column (position in the code)
-    int32_t kind;
-    int32_t col;  // table column, the same index on both sides
-    int32_t null_level, else_level, n_tests;
-    int32_t op[MAX_TESTS], cmp[MAX_TESTS], level[MAX_TESTS];
-    double t[MAX_TESTS];
-    int64_t stride;
-    int32_t cls;      // SimpleClass
-    int32_t off;      // byte offset of the column's fields in a row-image row
-    int32_t off2;     // SC_JW: offset of the four head units
-    int32_t has_ids;  // both sides carry dictionary ids (equal keys = equal strings)
-    // Per-test decision parameters, precomputed on the host (prepare_tests) so the filter decides
-    // every test with compares and selects only -- no divergent branches:
-    int32_t tflag[MAX_TESTS];  // TF_* bits
-    int32_t lev_a[MAX_TESTS];  // LEV (absolute): integer bound of the equivalent integer test
-    float jw_cf[MAX_TESTS];    // JW: an upper bound hi < jw_cf proves the test false
-    // Pairs [imp_lo, imp_hi) come from a blocking rule whose key includes `l.c = r.c` on this
-    // column's own raw columns: their strings are equal, non-NULL (and non-empty: no empty value
-    // in the column), so their level is eq_level and the filter reads nothing for them.
-    int64_t imp_lo, imp_hi;
-    int32_t eq_level;
-    // LEVRATIO tests: offset of the test's threshold table in GammaArgs.thr (-1: none).  Entry S is
-    // the largest distance v with `v / (S / 2.0) cmp t` true in fp64 (Spark's division), for
-    // S = len_l + len_r (code points) < THR_S: the filter decides the test with integer compares.
-    int32_t thr_off[MAX_TESTS];
-    // Bit-planes the Levenshtein scans need: bits np..7 of every plane-row unit of the column (both
-    // sides) are the same (Column.unit_or / unit_and), so those planes' match-mask terms are no-ops.
-    int32_t np;
-};
-constexpr int THR_S = 256;
-constexpr int32_t TF_ZERO = 1;     // the value 0.0 passes the test (JW of strings without a common unit; lev ratio 0)
-constexpr int32_t TF_ONE = 2;      // JW: the value 1.0 passes (equal non-empty strings)
-constexpr int32_t TF_GE = 4;       // LEV: the test is `lev >= lev_a` (else `lev <= lev_a`)
-constexpr int32_t TF_EXACT = 8;    // LEV `=` / `<>`: decided only when the bounds meet
-constexpr int32_t TF_EQ = 16;      // `=` (else `<>`)
-
-// ---- filter row image ----------------------------------------------------------------------------
-// The filter needs a few bytes per (row, column) -- equality key, lengths, unit sketch, head units --
-// but reading them from each column's own 32-byte records costs a cache line per row AND column,
-// and the pairs of a second blocking rule land on random rows.  So before the filter pass the
-// fields of every simple column are packed, per row, into one row of a row image (<= IMG_MAX
-// bytes, 16-byte aligned): a pair then reads two rows' lines whatever the number of columns.
-//   SC_EQ   8 B {key u32, lens u32}            SC_LEV 16 B {key, lens, sketch u64}
-//   SC_JW  16 B {key, lens, sketch} + 8 B head units at off2
-//   SC_NUM 16 B {value f64, valid u32, pad}
-// lens = UTF-16 length | code points << 16, each saturating at LEN_SAT; LENS_NULL = NULL.
-constexpr int IMG_MAX = 256;
-constexpr int64_t VIEW_MIN_IMAGE_BYTES = (int64_t)192 << 20;  // rule-view images only past this size
-constexpr uint32_t LENS_NULL = 0xFFFFFFFFu;
-constexpr int LEN_SAT = 0xFFFE;
-// The comparison programs are read-only for the whole launch: reading them through the constant
-// address space lets wave-uniform reads become scalar loads (s_load) instead of per-lane vector
-// loads, which would compete with the row gathers for the texture addresser.
-typedef const __attribute__((address_space(4))) SimpleCol ConstSimpleCol;
-__device__ inline ConstSimpleCol *const_simple(const SimpleCol *p) { return (ConstSimpleCol *)p; }
-
-// A chunk plane of the image as a buffer resource: gathers then take a 32-bit per-lane byte offset
-// (row x 16) against a wave-uniform descriptor -- no 64-bit address arithmetic per load
-// (cdna_hip_programming.md T8).  Used when every plane fits the descriptor's 31-bit range.
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-__device__ inline __amdgpu_buffer_rsrc_t image_rsrc(const uint8_t *base, int64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)bytes, 0x00020000);
-}
-// field at scalar byte offset `soff` (the chunk plane and in-chunk offset of a column) of the row at `off`
-__device__ inline uint4 buf16(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff) {
-    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ inline uint2 buf8(__amdgpu_buffer_rsrc_t r, uint32_t off, int soff) {
-    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0);
-    return make_uint2(v.x, v.y);
-}
-
-// Chunk-major image: the 16-byte chunk c of every row is contiguous, so the lanes of a wave that
-// read the same field of consecutive rows (a block's pairs) share a few cache lines.
-__host__ __device__ inline int64_t img_at(int64_t rows, int64_t row, int off) {
-    return ((int64_t)(off >> 4) * rows + row) * 16 + (off & 15);
-}
-
-struct GammaArgs {
-    const ColDesc *cols0, *cols1;  // tables for operand side 0 (`_l`) and 1 (`_r`)
-    const int32_t *pl, *pr;
-    int64_t P;
-    int K;
-    const spk_column_program *progs;
-    const int32_t *when_first, *when_n, *when_level;
-    const spk_instr *instr;
-    const spk_operand *ops;
-    const uint16_t *lit_units;
-    const int64_t *lit_off;
-    const int32_t *lit_len, *lit_cplen;
-    const int64_t *stride;
-    void *codes;                  // packed code per pair: uint16 (code16) or uint32
-    int code16;
-    int32_t *work;                // [K][P] pair indices per column needing the exact pass, by region
-    unsigned int *region_count;   // [K][n_regions] list length of each region
-    int64_t region_len;           // pair ordinals per region (one filter workgroup each)
-    int n_regions;
-    int32_t *slow;             // slow-pass lists, column k at slow_off[k]
-    const int64_t *slow_off;
-    unsigned int *slow_count;  // [3K]: slow lists, k_gamma_slow_lev's rest lists, huge lists
-    int *err;
-    const SimpleCol *simple;   // filter pass: simple columns ...
-    int n_simple;
-    const int32_t *complex_k;  // ... and the columns the interpreter evaluates
-    int n_complex;
-    const uint8_t *img0, *img1;  // filter row images of the l- and r-side tables (k_build_image)
-    int64_t img_stride;          // bytes of one row's fields (a multiple of 16)
-    int64_t img_rows0, img_rows1;  // rows of each image (chunk-major layout: chunk c of row r at (c * rows + r) * 16)
-    int32_t slot_beg[17];        // k_gamma_rows: simple[slot_beg[s] .. slot_beg[s+1]) start at image byte 8 s
-    // per filter launch: regions [region_base, region_base + gridDim.x); a view launch (rule 1's pairs)
-    // reads pl / pr = their view positions and img0 / img1 = view-ordered images
-    int region_base;
-    int all_img;  // every simple column reads the row image (no SC_GEN / SC_NUMRAW): views allowed
-    const int16_t *thr;  // LEVRATIO threshold tables (SimpleCol.thr_off), n_thr entries
-    int n_thr;
-};
-
-// Codes are written in place: the filter pass sets each pair's code (a 2-byte store leaves the
-// neighbouring pair's code alone), the exact / slow passes of column k add to it (a pair occurs at
-// most once in column k's lists).
-__device__ inline void code_set(const GammaArgs &A, int64_t p, uint32_t v) {
-    if (A.code16) static_cast<uint16_t *>(A.codes)[p] = (uint16_t)v;
-    else static_cast<uint32_t *>(A.codes)[p] = v;
-}
-// The exact and slow passes add their column's digit to the code the filter set.  Launches of one
-// column run in stream order and a pair occurs once in a column's lists: a plain read-modify-write
-// (an atomic add measured 2.4x the HBM writes of the Levenshtein pass at the same kernel time,
-// profiles/r2b_traffic.json).
-__device__ inline void code_add(const GammaArgs &A, int64_t p, uint32_t d) {
-    if (A.code16) {
-        uint16_t *c = static_cast<uint16_t *>(A.codes) + p;
-        *c = (uint16_t)(*c + d);
-    } else {
-        static_cast<uint32_t *>(A.codes)[p] += d;
-    }
-}
-
-// Several columns in one launch (ExactCols) may update one pair's code at once: an atomic add on
-// the aligned dword (a 16-bit code never carries into its neighbour -- a code stays below the
-// pattern count, <= 65536).
-__device__ inline void code_add_atomic(const GammaArgs &A, int64_t p, uint32_t d) {
-    if (A.code16) {
-        uint32_t *w = reinterpret_cast<uint32_t *>(static_cast<uint16_t *>(A.codes) + (p & ~(int64_t)1));
-        atomicAdd(w, d << (16 * (uint32_t)(p & 1)));
-    } else {
-        atomicAdd(static_cast<uint32_t *>(A.codes) + p, d);
-    }
-}
-
-enum : int { KF = 0, KT = 1, KN = 2, KU = 3 };  // false, true, NULL, undecided (filter pass)
-
-__device__ inline int k_and(int a, int b) {
-    if (a == KF || b == KF) return KF;
-    if (a == KU || b == KU) return KU;
-    return (a == KN || b == KN) ? KN : KT;
-}
-__device__ inline int k_or(int a, int b) {
-    if (a == KT || b == KT) return KT;
-    if (a == KU || b == KU) return KU;
-    return (a == KN || b == KN) ? KN : KF;
-}
-__device__ inline int k_not(int a) { return (a == KN || a == KU) ? a : (a == KT ? KF : KT); }
-
-// Fold one WHEN test into the branch chain: the first test that is TRUE (or UNDECIDED) ends it;
-// FALSE and NULL fall through to the next WHEN (a NULL predicate is a branch not taken).  r is
-// KF 0 / KT 1 / KN 2 / KU 3, so "ends the chain" is r & 1 and "undecided" r >> 1 on top: the chain
-// state stays in integer registers (VALU bit ops) instead of per-lane condition masks, and the
-// lanes of a wave never diverge over which test decided them.
-struct Chain {
-    int open = 1, und = 0, lvl = 0;
-    Chain() = default;
-    __device__ explicit Chain(int else_level) : lvl(else_level) {}
-    __device__ __attribute__((always_inline)) void fold(int r, int lvl_i) {
-        const int hit = r & open;  // bit 0: TRUE / UNDECIDED while open
-        und |= hit & (r >> 1);
-        lvl += hit * (lvl_i - lvl);
-        open &= ~hit;
-    }
-};
-
-
-__device__ inline int cmpd(double a, double b, int cmp) {
-    bool r;
-    switch (cmp) {
-        case SPK_CMP_EQ: r = a == b; break;
-        case SPK_CMP_NE: r = a != b; break;
-        case SPK_CMP_LT: r = a < b; break;
-        case SPK_CMP_LE: r = a <= b; break;
-        case SPK_CMP_GT: r = a > b; break;
-        default: r = a >= b; break;
-    }
-    return r ? KT : KF;
-}
-
-// `v cmp t` for an unknown v in [lo, hi]: decided only if every v in the interval agrees.
-__device__ inline int decide(double lo, double hi, int cmp, double t) {
-    if (lo == hi) return cmpd(lo, t, cmp);
-    switch (cmp) {
-        case SPK_CMP_GT: return lo > t ? KT : (hi <= t ? KF : KU);
-        case SPK_CMP_GE: return lo >= t ? KT : (hi < t ? KF : KU);
-        case SPK_CMP_LT: return hi < t ? KT : (lo >= t ? KF : KU);
-        case SPK_CMP_LE: return hi <= t ? KT : (lo > t ? KF : KU);
-        case SPK_CMP_EQ: return (t < lo || t > hi) ? KF : KU;
-        default: return (t < lo || t > hi) ? KT : KU;
-    }
-}
 
 // Spark UTF8String.substringSQL(pos, len) on a code-point range, mapped to UTF-16 units.
 __device__ inline void apply_substr(StrView &s, int pos, int len) {
@@ -528,36 +297,6 @@ __device__ int eval_column(const GammaArgs &A, int k, int32_t x, int32_t y, uint
     return ST_DONE;
 }
 
-// Append `val` for every lane with `want`; one atomic per wave.  Call with the whole wave converged.
-__device__ inline void wave_append(int32_t *list, unsigned int *count, bool want, int32_t val) {
-    const unsigned long long mask = __ballot(want);
-    if (!mask) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll(mask) - 1;
-    unsigned int base = 0;
-    if (lane == leader) base = atomicAdd(count, (unsigned int)__popcll(mask));
-    base = __shfl(base, leader);
-    if (want) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = val;
-}
-
-// Work lists of the filter pass.  Each workgroup owns one contiguous region of pair ordinals and
-// appends the region's undecided pairs of column k to work[k][region start ...] under a counter
-// in LDS: no device-scope atomic on a shared counter (those serialise at ~12 ns each across the
-// whole chip), deterministic list order, and a region's rows stay in one XCD's L2.
-struct Region {
-    int64_t r0, r1;  // pair ordinals [r0, r1)
-};
-
-__device__ inline Region my_region(const GammaArgs &A) {
-    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
-    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
-    return Region{r0, r1};
-}
-
-__device__ inline int32_t *region_list(const GammaArgs &A, int k, const Region &r) {
-    return A.work + (int64_t)k * A.P + r.r0;
-}
-
 // ---- simple columns in the filter pass ----------------------------------------------------------
 // Upper bound of jaro_winkler_sim(a, b) for unequal rows from their records alone (jw_upper with
 // the prefix bounded by the four head units: exact below 4, else by the shorter length).
@@ -643,21 +382,6 @@ __device__ __attribute__((always_inline)) inline int simple_str(const SC &sc, co
     return ST_DONE;
 }
 
-template <class SC>
-__device__ __attribute__((always_inline)) inline int simple_num(const SC &sc, bool va, double a, bool vb, double b) {
-    Chain c(sc.else_level);
-    const double diff = fabs(a - b), big = fabs(a > b ? a : b);
-    for (int i = 0; i < sc.n_tests; ++i) {
-        const int op = sc.op[i], cmp = sc.cmp[i];
-        int r;
-        if (op == SPK_OP_NUM_CMP) r = cmpd(a, b, cmp);
-        else if (op == SPK_OP_ABSDIFF) r = cmpd(diff, sc.t[i], cmp);
-        else r = big == 0.0 ? KN : cmpd(diff / big, sc.t[i], cmp);  // SPK_OP_PERCDIFF
-        c.fold(r, sc.level[i]);
-    }
-    return (!va || !vb) ? sc.null_level : c.lvl;
-}
-
 // rows_img: the image's row capacity (its chunk stride); rows [0, n) are filled.
 __global__ void k_build_image(int64_t n, const ColDesc *__restrict__ cols, const SimpleCol *__restrict__ simple,
                               int n_simple, uint8_t *__restrict__ img, int64_t rows_img) {
@@ -665,7 +389,6 @@ __global__ void k_build_image(int64_t n, const ColDesc *__restrict__ cols, const
     if (row >= n) return;
     for (int j = 0; j < n_simple; ++j) {
         const SimpleCol &sc = simple[j];
-        if (sc.cls == SC_GEN || sc.cls == SC_NUMRAW) continue;
         const ColDesc &c = cols[sc.col];
         if (sc.cls == SC_NUM) {
             const bool ok = c.valid[row] != 0;
@@ -684,563 +407,6 @@ __global__ void k_build_image(int64_t n, const ColDesc *__restrict__ cols, const
         if (sc.cls != SC_EQ) *reinterpret_cast<uint64_t *>(img + img_at(rows_img, row, sc.off + 8)) = m.sketch;
         if (sc.cls == SC_JW) *reinterpret_cast<uint64_t *>(img + img_at(rows_img, row, sc.off2)) = m.head;
     }
-}
-
-__device__ inline int lens_u16(uint32_t l) { return (int)(l & 0xFFFFu); }
-__device__ inline int lens_cp(uint32_t l) { return (int)(l >> 16); }
-__device__ inline uint64_t img_sketch(const uint4 &v) { return ((uint64_t)v.w << 32) | v.z; }
-
-// sketch_inter_ub without the data-dependent branch (both saturated buckets add min(rest_a, rest_b)).
-__device__ __attribute__((always_inline)) inline int sketch_inter_ub_bf(uint64_t sa, uint64_t sb, int la, int lb) {
-    const uint32_t aL = (uint32_t)sa, aH = (uint32_t)(sa >> 32);
-    const uint32_t bL = (uint32_t)sb, bH = (uint32_t)(sb >> 32);
-    const uint32_t gt = (aH & ~bH) | (~(aH ^ bH) & aL & ~bL);
-    const uint32_t mL = (aL & ~gt) | (bL & gt), mH = (aH & ~gt) | (bH & gt);
-    const uint32_t both_sat = aL & aH & bL & bH, rest = ~both_sat;
-    int inter = __builtin_popcount(mL & rest) + 2 * __builtin_popcount(mH & rest);
-    const int ra = la - (__builtin_popcount(aL & rest) + 2 * __builtin_popcount(aH & rest));
-    const int rb = lb - (__builtin_popcount(bL & rest) + 2 * __builtin_popcount(bH & rest));
-    inter += both_sat ? (ra < rb ? ra : rb) : 0;
-    const int lmn = la < lb ? la : lb;
-    return inter < lmn ? inter : lmn;
-}
-
-// The image tests of FP pairs at once: each pair's bounds first, then the column's tests in order
-// with every test's parameters read once for all FP pairs (scalar loads outside the pair loop).
-// und[u]: pair u needs the exact pass; level[u]: its level otherwise.
-
-// `=` / `<>` tests.  Equal keys prove equality with dictionary ids; without them only the units can tell.
-template <int FP, class SC>
-__device__ __attribute__((always_inline)) inline void img_eq(const SC &sc, const uint2 (&a)[FP], const uint2 (&b)[FP],
-                                                             int (&level)[FP], bool (&und)[FP]) {
-    int same[FP];
-    Chain c[FP];
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        same[u] = (a[u].x == b[u].x) & (a[u].y == b[u].y);
-        c[u] = Chain(sc.else_level);
-    }
-    for (int i = 0; i < sc.n_tests; ++i) {
-        const int f = (sc.tflag[i] & TF_EQ) ? 0 : 1, lv = sc.level[i];
-#pragma unroll
-        for (int u = 0; u < FP; ++u) c[u].fold(same[u] ^ f, lv);
-    }
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        const bool nul = a[u].y == LENS_NULL || b[u].y == LENS_NULL;
-        level[u] = nul ? sc.null_level : c[u].lvl;
-        und[u] = !nul && same[u] && !sc.has_ids;
-    }
-}
-
-// jaro_winkler_sim(l, r) > / >= t tests.  Equal strings and strings without a common unit have
-// exact values (1.0 / 0.0); otherwise the upper bound from the sketches (m <= M, (m - t)/m <= 1)
-// and the head units (Winkler prefix) is evaluated in fp32 with a 1e-5 margin, far above its
-// rounding; a bound can only prove a test false, every other cell goes to the exact pass.  The
-// float thresholds jw_cf are the doubles' exact float images (prepare_tests).  The bound is only
-// computed when some lane of the wave needs it (in the first rule's blocks every pair shares
-// the blocking key, so a wave of such pairs skips it for that column).
-template <int FP, class SC>
-__device__ __attribute__((always_inline)) inline void img_jw(const SC &sc, const uint4 (&a)[FP], const uint4 (&b)[FP],
-                                                             const uint64_t (&ha)[FP], const uint64_t (&hb)[FP],
-                                                             int (&level)[FP], bool (&und)[FP]) {
-    bool exact[FP], one[FP], und0[FP];
-    float hi[FP];
-    bool need = false;
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        const bool same = a[u].x == b[u].x && a[u].y == b[u].y;
-        const int lf = lens_u16(a[u].y), ls = lens_u16(b[u].y);
-        und0[u] = (same && !sc.has_ids) || lf >= LEN_SAT || ls >= LEN_SAT;
-        exact[u] = same || (lf < ls ? lf : ls) == 0;
-        one[u] = same && lf > 0;
-        hi[u] = 0.f;
-        need = need || !exact[u];
-    }
-    if (__ballot(need) != 0ull) {  // wave-uniform
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            const int lf = lens_u16(a[u].y), ls = lens_u16(b[u].y);
-            const int lmn = lf < ls ? lf : ls, lmx = lf < ls ? ls : lf;
-            const int M = sketch_inter_ub_bf(img_sketch(a[u]), img_sketch(b[u]), lf, ls);
-            exact[u] = exact[u] || M == 0;
-            // v_rcp_f32 (1 ulp) instead of IEEE divisions: the error (< 1e-6 on j) sits far inside the
-            // 1e-5 margin, so hi stays an upper bound (the exact cases never read it)
-            const float j = ((float)M * (float)(lf + ls) * __builtin_amdgcn_rcpf((float)lf * (float)ls) + 1.0f) *
-                            (1.0f / 3.0f);
-            const uint64_t d = ha[u] ^ hb[u];
-            const int cp = d ? (__ffsll((unsigned long long)d) - 1) >> 4 : 4;
-            const int prefix = cp < 4 ? (cp < lmn ? cp : lmn) : lmn;
-            const float pw = (lmx > 10 ? __builtin_amdgcn_rcpf((float)lmx) : 0.1f) * (float)prefix;
-            hi[u] = (j >= 0.7f - 1e-4f ? j + pw * (1.0f - j) : j) + 1e-5f;
-        }
-    }
-    Chain c[FP];
-#pragma unroll
-    for (int u = 0; u < FP; ++u) c[u] = Chain(sc.else_level);
-    for (int i = 0; i < sc.n_tests; ++i) {
-        const int f = sc.tflag[i], lv = sc.level[i];
-        const float cf = sc.jw_cf[i];
-        const int r_one = (f >> 1) & 1, r_zero = f & TF_ZERO, r_pass = (f & TF_ZERO) ? KT : KU;  // TF_ONE / TF_ZERO -> KT / KF
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            const int r_exact = one[u] ? r_one : r_zero;
-            const int r_bound = hi[u] < cf ? KF : r_pass;
-            c[u].fold(exact[u] ? r_exact : r_bound, lv);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        const bool nul = a[u].y == LENS_NULL || b[u].y == LENS_NULL;
-        level[u] = nul ? sc.null_level : c[u].lvl;
-        und[u] = !nul && (und0[u] || c[u].und);
-    }
-}
-
-// `=` / `<>` and levenshtein [ratio] tests: the distance lies in [max(length gap, bag distance),
-// max(length)].  Absolute tests compare integer bounds (lev_a); the ratio test `lev / den <= t`
-// (or `<`) is decided against t * den with one part in 1e12 of margin instead of a division per
-// pair; exact ties are left to the exact pass.
-template <int FP, class SC>
-__device__ __attribute__((always_inline)) inline void img_lev(const SC &sc, const uint4 (&a)[FP], const uint4 (&b)[FP],
-                                                              int (&level)[FP], bool (&und)[FP], const int16_t *thr) {
-    bool same[FP], bmp[FP], und0[FP];
-    int lo[FP], hi[FP];
-    bool need = false;
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        same[u] = a[u].x == b[u].x && a[u].y == b[u].y;
-        const int la = lens_u16(a[u].y), lb = lens_u16(b[u].y), na = lens_cp(a[u].y), nb = lens_cp(b[u].y);
-        und0[u] = (same[u] && !sc.has_ids) || la >= LEN_SAT || lb >= LEN_SAT || na >= LEN_SAT || nb >= LEN_SAT;
-        // BMP rows: units are code points, so the bag bound holds
-        bmp[u] = na == la && nb == lb && !same[u];
-        need = need || bmp[u];
-        const int gap = na > nb ? na - nb : nb - na;
-        lo[u] = same[u] ? 0 : gap;
-        hi[u] = same[u] ? 0 : (na > nb ? na : nb);
-    }
-    if (__ballot(need) != 0ull) {  // wave-uniform
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            const int na = lens_cp(a[u].y), nb = lens_cp(b[u].y);
-            const int bag = bmp[u] ? (na > nb ? na : nb) - sketch_inter_ub_bf(img_sketch(a[u]), img_sketch(b[u]), na, nb) : 0;
-            lo[u] = bag > lo[u] ? bag : lo[u];
-        }
-    }
-    Chain c[FP];
-#pragma unroll
-    for (int u = 0; u < FP; ++u) c[u] = Chain(sc.else_level);
-    for (int i = 0; i < sc.n_tests; ++i) {
-        const int op = sc.op[i], f = sc.tflag[i], lv = sc.level[i];
-        if (op == SPK_OP_STR_CMP) {  // wave-uniform branches on the test kind
-            const int x = (f & TF_EQ) ? 0 : 1;
-#pragma unroll
-            for (int u = 0; u < FP; ++u) c[u].fold((int)same[u] ^ x, lv);
-        } else if (op == SPK_OP_LEV) {
-            const int A = sc.lev_a[i];
-            const double t = sc.t[i];
-            const int cmp = sc.cmp[i];
-#pragma unroll
-            for (int u = 0; u < FP; ++u) {
-                int r;
-                if (f & TF_EXACT) r = lo[u] == hi[u] ? cmpd((double)lo[u], t, cmp) : KU;
-                else if (f & TF_GE) r = lo[u] >= A ? KT : (hi[u] < A ? KF : KU);
-                else r = hi[u] <= A ? KT : (lo[u] > A ? KF : KU);
-                c[u].fold(r, lv);
-            }
-        } else {
-            // integer thresholds from the table when len_l + len_r < THR_S, else the fp64 bound
-            // with one part in 1e12 of margin (exact ties left to the exact pass)
-            const int off = thr ? sc.thr_off[i] : -1;
-#pragma unroll
-            for (int u = 0; u < FP; ++u) {
-                const int S = lens_cp(a[u].y) + lens_cp(b[u].y);
-                const bool tab = off >= 0 && S < THR_S;
-                int rr = KU;
-                if (tab) {
-                    const int th = thr[off + S];
-                    rr = hi[u] <= th ? KT : (lo[u] > th ? KF : KU);
-                }
-                if (__ballot(!tab) != 0ull && !tab) {
-                    const double t = sc.t[i], den = (double)S * 0.5;
-                    const double tl = t * den, up = tl * (1.0 + 1e-12), dn = tl * (1.0 - 1e-12);
-                    const double tl_hi = up > dn ? up : dn, tl_lo = up > dn ? dn : up;
-                    rr = sc.cmp[i] == SPK_CMP_LE ? ((double)hi[u] <= tl_lo ? KT : ((double)lo[u] > tl_hi ? KF : KU))
-                                                 : ((double)hi[u] < tl_lo ? KT : ((double)lo[u] >= tl_hi ? KF : KU));
-                }
-                c[u].fold(S == 0 ? KN : (same[u] ? (f & TF_ZERO) : rr), lv);
-            }
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        const bool nul = a[u].y == LENS_NULL || b[u].y == LENS_NULL;
-        level[u] = nul ? sc.null_level : c[u].lvl;
-        und[u] = !nul && (und0[u] || c[u].und);
-    }
-}
-
-__device__ inline double bits_to_double(uint32_t lo, uint32_t hi) {
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// Append the lanes' wanted values of F_PAIRS ballots to a list: one LDS atomic per call.  The wave
-// must be converged (lane 0 active).
-constexpr int F_PAIRS = 4;  // pairs per lane per iteration of the general filter (k_gamma_simple: a template parameter)
-template <int FP>
-__device__ inline void wave_append_batch(int32_t *list, unsigned int *count, const bool (&want)[FP],
-                                         const int64_t (&val)[FP]) {
-    unsigned long long m[FP];
-    unsigned int total = 0;
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        m[u] = __ballot(want[u]);
-        total += (unsigned int)__popcll(m[u]);
-    }
-    if (!total) return;
-    const int lane = threadIdx.x & 63;
-    unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(count, total);
-    base = __shfl(base, 0);
-    const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        if (want[u]) list[base + __popcll(m[u] & below)] = (int32_t)val[u];
-        base += (unsigned int)__popcll(m[u]);
-    }
-}
-
-// Filter pass, simple columns: initialises code[p] with their levels.  Each lane takes F_PAIRS
-// pairs per iteration and, column by column, issues the image loads of all of them before
-// evaluating any: the pass is bound by the latency of those gathers, so every round trip is
-// shared by F_PAIRS pairs.  The column loop is uniform across the wave, so the class dispatch and
-// the test parameters are scalar.
-template <int MINW, int FP, bool BUF, bool LOCAL = false>
-__global__ __launch_bounds__(F_THREADS, MINW) void k_gamma_simple(GammaArgs A) {
-    __shared__ unsigned int s_cnt[MAX_SIMPLE];
-    extern __shared__ int16_t s_thr[];  // A.thr (dynamic LDS: n_thr entries)
-    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
-    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const Region R = my_region(A);
-    ConstSimpleCol *simple = const_simple(A.simple);
-    constexpr int64_t SPAN = 64 * FP;
-    constexpr int64_t STEP = (int64_t)(F_THREADS / 64) * SPAN;
-    // one buffer descriptor per side's whole image (BUF: the launch checked it fits 31 bits); a
-    // column's field is the scalar offset of its chunk plane
-    const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0, A.img_rows0 * A.img_stride);
-    const __amdgpu_buffer_rsrc_t r1 = image_rsrc(A.img1, A.img_rows1 * A.img_stride);
-    int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN;
-    // the image rows of the next iteration are loaded while this one's columns are evaluated, so the
-    // image gathers do not wait behind the pair-array load.  In a view launch (pairs of rule 1) pl / pr
-    // are the pairs' view positions and img0 / img1 the view-ordered images (only when every column
-    // reads the image, so no column needs the table row).
-    int32_t nx[FP], ny[FP];
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        const int64_t q = base + u * 64 + lane;
-        nx[u] = q < R.r1 ? A.pl[q] : 0;  // inactive lanes read row 0 harmlessly
-        ny[u] = q < R.r1 ? A.pr[q] : 0;
-    }
-    for (; base < R.r1; base += STEP) {  // wave-uniform
-        int64_t p[FP];
-        bool act[FP];
-        uint32_t acc[FP];
-        // Byte offset of each pair's rows within one 16-byte chunk plane of the image (rows < 2^28): the
-        // gathers below address a wave-uniform chunk base plus this 32-bit offset (buffer descriptor +
-        // VGPR offset), so a load costs no per-lane 64-bit address arithmetic.  The row itself is
-        // ox >> 4 for the columns that read their own records.
-        uint32_t ox[FP], oy[FP];
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            p[u] = base + u * 64 + lane;
-            act[u] = p[u] < R.r1;
-            ox[u] = LOCAL ? (uint32_t)(nx[u] & 255) << 4 : (uint32_t)nx[u] << 4;  // LOCAL: timing experiment only
-            oy[u] = LOCAL ? (uint32_t)(ny[u] & 255) << 4 : (uint32_t)ny[u] << 4;
-            acc[u] = 0;
-            const int64_t q = p[u] + STEP;
-            nx[u] = q < R.r1 ? A.pl[q] : 0;
-            ny[u] = q < R.r1 ? A.pr[q] : 0;
-        }
-        for (int j = 0; j < A.n_simple; ++j) {
-            ConstSimpleCol &sc = simple[j];
-            bool und[FP];
-            int lev[FP];
-            // wave-uniform chunk bases of this column's fields (img_at with row 0)
-            const uint8_t *b0 = A.img0 + img_at(A.img_rows0, 0, sc.off), *b1 = A.img1 + img_at(A.img_rows1, 0, sc.off);
-            const uint8_t *h0 = A.img0 + img_at(A.img_rows0, 0, sc.off2), *h1 = A.img1 + img_at(A.img_rows1, 0, sc.off2);
-            const int s0 = (int)img_at(A.img_rows0, 0, sc.off), s1 = (int)img_at(A.img_rows1, 0, sc.off);
-            const int t0 = (int)img_at(A.img_rows0, 0, sc.off2), t1 = (int)img_at(A.img_rows1, 0, sc.off2);
-            if (base >= sc.imp_lo && base + SPAN <= sc.imp_hi) {  // wave-uniform: the blocking key implies equality
-                const uint32_t add = (uint32_t)(sc.eq_level + 1) * (uint32_t)sc.stride;
-#pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? add : 0u;
-                continue;
-            }
-#pragma unroll
-            for (int u = 0; u < FP; ++u) {
-                und[u] = false;
-                lev[u] = 0;
-            }
-            switch (sc.cls) {
-                case SC_EQ: {
-                    uint2 va[FP], vb[FP];
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) {
-                        va[u] = BUF ? buf8(r0, ox[u], s0) : *reinterpret_cast<const uint2 *>(b0 + ox[u]);
-                        vb[u] = BUF ? buf8(r1, oy[u], s1) : *reinterpret_cast<const uint2 *>(b1 + oy[u]);
-                    }
-                    img_eq<FP>(sc, va, vb, lev, und);
-                    break;
-                }
-                case SC_JW: {
-                    uint4 va[FP], vb[FP];
-                    uint64_t ha[FP], hb[FP];
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) {
-                        va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
-                        vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
-                        if (BUF) {
-                            const uint2 a2 = buf8(r0, ox[u], t0), b2 = buf8(r1, oy[u], t1);
-                            ha[u] = ((uint64_t)a2.y << 32) | a2.x;
-                            hb[u] = ((uint64_t)b2.y << 32) | b2.x;
-                        } else {
-                            ha[u] = *reinterpret_cast<const uint64_t *>(h0 + ox[u]);
-                            hb[u] = *reinterpret_cast<const uint64_t *>(h1 + oy[u]);
-                        }
-                    }
-                    img_jw<FP>(sc, va, vb, ha, hb, lev, und);
-                    break;
-                }
-                case SC_LEV: {
-                    uint4 va[FP], vb[FP];
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) {
-                        va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
-                        vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
-                    }
-                    img_lev<FP>(sc, va, vb, lev, und, s_thr);
-                    break;
-                }
-                case SC_NUM: {
-                    uint4 va[FP], vb[FP];
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) {
-                        va[u] = BUF ? buf16(r0, ox[u], s0) : *reinterpret_cast<const uint4 *>(b0 + ox[u]);
-                        vb[u] = BUF ? buf16(r1, oy[u], s1) : *reinterpret_cast<const uint4 *>(b1 + oy[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < FP; ++u)
-                        lev[u] = simple_num(sc, va[u].z != 0, bits_to_double(va[u].x, va[u].y), vb[u].z != 0,
-                                            bits_to_double(vb[u].x, vb[u].y));
-                    break;
-                }
-                case SC_NUMRAW: {  // the columns' own records, by table row
-                    const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
-                    for (int u = 0; u < FP; ++u) {
-                        const uint32_t x = ox[u] >> 4, y = oy[u] >> 4;
-                        lev[u] = simple_num(sc, c0.valid[x] != 0, c0.val[x], c1.valid[y] != 0, c1.val[y]);
-                    }
-                    break;
-                }
-                default: {  // SC_GEN: the full row records, one pair at a time (few registers)
-                    const RecMeta *m0 = A.cols0[sc.col].meta, *m1 = A.cols1[sc.col].meta;
-                    for (int u = 0; u < FP; ++u) und[u] = simple_str(sc, m0[ox[u] >> 4], m1[oy[u] >> 4], lev[u]) != ST_DONE;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < FP; ++u) {
-                und[u] = und[u] && act[u];
-                if (!und[u]) acc[u] += (uint32_t)(lev[u] + 1) * (uint32_t)sc.stride;
-            }
-            wave_append_batch(region_list(A, sc.k, R), &s_cnt[j], und, p);
-        }
-#pragma unroll
-        for (int u = 0; u < FP; ++u)
-            if (act[u]) code_set(A, p[u], acc[u]);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
-        A.region_count[(int64_t)simple[i].k * A.n_regions + A.region_base + blockIdx.x] = s_cnt[i];
-}
-
-// Filter pass over rows held in registers: when the image row is at most ROW_MAXQ x 16 bytes,
-// each lane loads its RP pairs' two image rows whole, in one burst (2 x RP x NQ independent 16-byte
-// loads) and evaluates every column from registers -- one gather round trip per iteration
-// instead of one per column -- while the next iteration's pair rows are already in flight.
-// The column's 16-byte chunk is chosen by a wave-uniform index (scalar branches / selects).
-constexpr int ROW_MAXQ = 8;
-constexpr int RP = 2;
-
-// The columns whose fields start at 8-byte slot S of the image row, over the RP pairs' register rows.
-// S is a template parameter and the slots are visited in sequence (slot_cols<0> calls <1> ...), so
-// every row access -- chunk S / 2, half S % 2 -- has a compile-time index and the rows stay in
-// registers (a runtime chunk or half index would send them to scratch).  16-byte fields start at
-// even slots; JW heads sit in the low half of the next chunk (layout_image).
-template <int S, int NQ>
-__device__ __attribute__((always_inline)) inline void slot_cols(const GammaArgs &A, const Region &R,
-                                                                unsigned int *s_cnt, const uint4 (&ra)[RP][NQ],
-                                                                const uint4 (&rb)[RP][NQ], const int64_t (&p)[RP],
-                                                                const bool (&act)[RP], uint32_t (&acc)[RP]) {
-    if constexpr (S < 2 * NQ) {
-        constexpr int CQ = S / 2, HQ = CQ + 1 < NQ ? CQ + 1 : CQ;
-        const int lane = threadIdx.x & 63;
-        for (int j = A.slot_beg[S]; j < A.slot_beg[S + 1]; ++j) {
-            ConstSimpleCol &sc = const_simple(A.simple)[j];
-            bool und[RP];
-            int lev[RP];
-#pragma unroll
-            for (int u = 0; u < RP; ++u) {
-                und[u] = false;
-                lev[u] = 0;
-            }
-            uint4 va[RP], vb[RP];
-#pragma unroll
-            for (int u = 0; u < RP; ++u) {
-                va[u] = ra[u][CQ];
-                vb[u] = rb[u][CQ];
-            }
-            if constexpr (S % 2 == 1) {  // only 8-byte EQ fields start at an odd slot
-                uint2 ea[RP], eb[RP];
-#pragma unroll
-                for (int u = 0; u < RP; ++u) {
-                    ea[u] = make_uint2(va[u].z, va[u].w);
-                    eb[u] = make_uint2(vb[u].z, vb[u].w);
-                }
-                img_eq<RP>(sc, ea, eb, lev, und);
-            } else {
-                switch (sc.cls) {
-                    case SC_EQ: {
-                        uint2 ea[RP], eb[RP];
-#pragma unroll
-                        for (int u = 0; u < RP; ++u) {
-                            ea[u] = make_uint2(va[u].x, va[u].y);
-                            eb[u] = make_uint2(vb[u].x, vb[u].y);
-                        }
-                        img_eq<RP>(sc, ea, eb, lev, und);
-                        break;
-                    }
-                    case SC_JW: {
-                        uint64_t ha[RP], hb[RP];
-#pragma unroll
-                        for (int u = 0; u < RP; ++u) {
-                            ha[u] = ((uint64_t)ra[u][HQ].y << 32) | ra[u][HQ].x;
-                            hb[u] = ((uint64_t)rb[u][HQ].y << 32) | rb[u][HQ].x;
-                        }
-                        img_jw<RP>(sc, va, vb, ha, hb, lev, und);
-                        break;
-                    }
-                    case SC_LEV:
-                        img_lev<RP>(sc, va, vb, lev, und, nullptr);
-                        break;
-                    default:  // SC_NUM
-#pragma unroll
-                        for (int u = 0; u < RP; ++u)
-                            lev[u] = simple_num(sc, ra[u][CQ].z != 0, bits_to_double(ra[u][CQ].x, ra[u][CQ].y),
-                                                rb[u][CQ].z != 0, bits_to_double(rb[u][CQ].x, rb[u][CQ].y));
-                        break;
-                }
-            }
-            unsigned long long m[RP];
-            unsigned int total = 0;
-#pragma unroll
-            for (int u = 0; u < RP; ++u) {
-                und[u] = und[u] && act[u];
-                if (!und[u]) acc[u] += (uint32_t)(lev[u] + 1) * (uint32_t)sc.stride;
-                m[u] = __ballot(und[u]);
-                total += (unsigned int)__popcll(m[u]);
-            }
-            if (total) {
-                int32_t *list = region_list(A, sc.k, R);
-                unsigned int b0 = 0;
-                if (lane == 0) b0 = atomicAdd(&s_cnt[j], total);
-                b0 = __shfl(b0, 0);
-                const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-                for (int u = 0; u < RP; ++u) {
-                    if (und[u]) list[b0 + __popcll(m[u] & below)] = (int32_t)p[u];
-                    b0 += (unsigned int)__popcll(m[u]);
-                }
-            }
-        }
-        slot_cols<S + 1, NQ>(A, R, s_cnt, ra, rb, p, act, acc);
-    }
-}
-
-template <int NQ>
-__global__ __launch_bounds__(F_THREADS) void k_gamma_rows(GammaArgs A) {
-    __shared__ unsigned int s_cnt[MAX_SIMPLE];
-    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS) s_cnt[i] = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const Region R = my_region(A);
-    ConstSimpleCol *simple = const_simple(A.simple);
-    constexpr int64_t SPAN = 64 * RP;
-    constexpr int64_t STEP = (int64_t)(F_THREADS / 64) * SPAN;
-    int64_t base = R.r0 + (int64_t)(threadIdx.x >> 6) * SPAN;
-    int32_t nx[RP], ny[RP];  // pair rows of the next iteration
-#pragma unroll
-    for (int u = 0; u < RP; ++u) {
-        const int64_t q = base + u * 64 + lane;
-        nx[u] = q < R.r1 ? A.pl[q] : 0;
-        ny[u] = q < R.r1 ? A.pr[q] : 0;
-    }
-    for (; base < R.r1; base += STEP) {  // wave-uniform
-        int64_t p[RP];
-        bool act[RP];
-        int32_t x[RP], y[RP];
-        uint32_t acc[RP];
-        uint4 ra[RP][NQ], rb[RP][NQ];
-#pragma unroll
-        for (int u = 0; u < RP; ++u) {
-            p[u] = base + u * 64 + lane;
-            act[u] = p[u] < R.r1;
-            x[u] = nx[u];
-            y[u] = ny[u];
-            acc[u] = 0;
-#pragma unroll
-            for (int k = 0; k < NQ; ++k) {
-                ra[u][k] = *reinterpret_cast<const uint4 *>(A.img0 + img_at(A.img_rows0, x[u], 16 * k));
-                rb[u][k] = *reinterpret_cast<const uint4 *>(A.img1 + img_at(A.img_rows1, y[u], 16 * k));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < RP; ++u) {  // prefetch the next iteration's pair rows
-            const int64_t q = base + STEP + u * 64 + lane;
-            nx[u] = q < R.r1 ? A.pl[q] : 0;
-            ny[u] = q < R.r1 ? A.pr[q] : 0;
-        }
-        slot_cols<0, NQ>(A, R, s_cnt, ra, rb, p, act, acc);
-        // columns outside the image (records read directly), one pair at a time
-        for (int j = A.slot_beg[2 * NQ]; j < A.n_simple; ++j) {
-            ConstSimpleCol &sc = simple[j];
-            bool und[RP];
-            int lev[RP];
-            for (int u = 0; u < RP; ++u) {
-                und[u] = false;
-                lev[u] = 0;
-                if (sc.cls == SC_NUMRAW) {
-                    const ColDesc &c0 = A.cols0[sc.col], &c1 = A.cols1[sc.col];
-                    lev[u] = simple_num(sc, c0.valid[x[u]] != 0, c0.val[x[u]], c1.valid[y[u]] != 0, c1.val[y[u]]);
-                } else {
-                    und[u] = simple_str(sc, A.cols0[sc.col].meta[x[u]], A.cols1[sc.col].meta[y[u]], lev[u]) != ST_DONE;
-                }
-            }
-            bool w[RP];
-            for (int u = 0; u < RP; ++u) {
-                w[u] = und[u] && act[u];
-                if (!w[u]) acc[u] += (uint32_t)(lev[u] + 1) * (uint32_t)sc.stride;
-            }
-            for (int u = 0; u < RP; ++u) wave_append(region_list(A, sc.k, R), &s_cnt[j], w[u], (int32_t)p[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < RP; ++u)
-            if (act[u]) code_set(A, p[u], acc[u]);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < A.n_simple; i += F_THREADS)
-        A.region_count[(int64_t)simple[i].k * A.n_regions + A.region_base + blockIdx.x] = s_cnt[i];
 }
 
 // Filter pass, every other column through the interpreter: adds to code[p].
@@ -1975,7 +1141,7 @@ static void implied_equal(const spk_ctx *ctx, const Table &t0, const Table &t1, 
     sc.eq_level = equal_level(sc);
 }
 
-// Recognise a simple column (see SimpleCol); false leaves it to the interpreter.
+// Filter class of a simple column (see SimpleCol); SC_NONE leaves it to the interpreter.
 static int32_t simple_class(const SimpleCol &s) {
     if (s.kind == SK_NUM) return SC_NUM;
     bool all_eq = true, all_jw = s.n_tests > 0, lev_ok = true;
@@ -1996,22 +1162,25 @@ static int32_t simple_class(const SimpleCol &s) {
     if (all_eq) return SC_EQ;
     if (all_jw) return SC_JW;
     if (lev_ok && n_lev > 0) return SC_LEV;
-    return SC_GEN;
+    return SC_NONE;
 }
 
 // Row-image offsets; returns the row stride (a multiple of 16), 0 when nothing uses the image.
 // JW fields take 24 B at a 16-byte boundary (key, lens, sketch; head units at off + 16, the low half
 // of the next chunk), LEV / NUM 16 B at a boundary, EQ 8 B in the gaps JW leaves, then at the end.
-// Columns that do not fit in IMG_MAX bytes keep reading their own records.
+// Columns that do not fit in IMG_MAX bytes, or past the filter kernel's slots of their class
+// (FJ_MAX ...), go to the interpreter (SC_NONE).
 static int64_t layout_image(std::vector<SimpleCol> &simple) {
     int64_t off = 0;
     std::vector<int64_t> gaps;  // free 8-byte slots
+    int nj = 0, nl = 0, nn = 0, ne = 0;
     for (SimpleCol &s : simple) {
         if (s.cls != SC_JW) continue;
-        if (off + 32 > IMG_MAX) {
-            s.cls = SC_GEN;
+        if (off + 32 > IMG_MAX || nj == FJ_MAX) {
+            s.cls = SC_NONE;
             continue;
         }
+        ++nj;
         s.off = (int32_t)off;
         s.off2 = (int32_t)(off + 16);
         gaps.push_back(off + 24);
@@ -2019,24 +1188,32 @@ static int64_t layout_image(std::vector<SimpleCol> &simple) {
     }
     for (SimpleCol &s : simple) {
         if (s.cls != SC_LEV && s.cls != SC_NUM) continue;
-        if (off + 16 > IMG_MAX) {
-            s.cls = s.cls == SC_NUM ? SC_NUMRAW : SC_GEN;
+        int &n = s.cls == SC_LEV ? nl : nn;
+        if (off + 16 > IMG_MAX || n == (s.cls == SC_LEV ? FL_MAX : FN_MAX)) {
+            s.cls = SC_NONE;
             continue;
         }
+        ++n;
         s.off = (int32_t)off;
         off += 16;
     }
     size_t g = 0;
     for (SimpleCol &s : simple) {
         if (s.cls != SC_EQ) continue;
+        if (ne == FE_MAX) {
+            s.cls = SC_NONE;
+            continue;
+        }
         if (g < gaps.size()) {
             s.off = (int32_t)gaps[g++];
+            ++ne;
             continue;
         }
         if (off + 8 > IMG_MAX) {
-            s.cls = SC_GEN;
+            s.cls = SC_NONE;
             continue;
         }
+        ++ne;
         s.off = (int32_t)off;
         off += 8;
     }
@@ -2065,7 +1242,7 @@ struct ViewLaunch {
 
 static int build_view_images(spk_ctx *ctx, const GammaArgs &A, int64_t stride, ViewLaunch *out, bool *ok) {
     *ok = false;
-    if (stride <= 0 || A.n_simple == 0 || ctx->n_views < 1 || !A.img0 || !A.all_img) return SPK_OK;
+    if (stride <= 0 || A.n_simple == 0 || ctx->n_views < 1 || !A.img0) return SPK_OK;
     const int nq = (int)(stride / 16);
     const int r = 1;
     RuleView &v = ctx->views[r];
@@ -2194,6 +1371,155 @@ static int huge_scratch(int64_t units, int64_t cells, DevBuf<uint8_t> &buf, Scra
     return SPK_OK;
 }
 
+// What the exact / slow / huge passes of the last spk_gammas need, kept so that an overflow of the work
+// lists or cells past SLOW_LIMIT can be settled after the call returned (settle_gammas).
+namespace spk {
+struct GammaPlan {
+    GammaArgs A{};
+    std::vector<SimpleCol> simple;
+    std::vector<int> simple_of;
+    std::vector<char> may_exact, huge_in_slow;
+    int K = 0, n_regions = 0, n_info = 0, n_cnt = 0, n_all = 0;
+    int64_t g_exact = 1, max_units = 1;
+};
+}  // namespace spk
+
+// The exact and slow passes over the lists the filter wrote (list capacity `cap`).  k_prefix sizes the
+// lists on the device; if they exceed `cap` every exact kernel is a no-op and settle_gammas re-runs
+// this phase with the right capacity.
+static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap) {
+    GammaArgs &A = G.A;
+    const int K = G.K;
+    SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));
+    A.slow = ctx->xlist.p + cap;
+    A.slow_off = ctx->xinfo.p;
+    ctx->xcap = cap;
+    if (A.P <= 0) {
+        SPK_HIP(hipMemsetAsync(ctx->xinfo.p, 0, (size_t)G.n_info * 8, ctx->stream));
+        return SPK_OK;
+    }
+    k_prefix<<<(unsigned)K, PFX_THREADS, 0, ctx->stream>>>(
+        ctx->region_count.p, K, G.n_regions, cap, ctx->xpref.p, ctx->xinfo.p,
+        reinterpret_cast<unsigned long long *>(ctx->xinfo.p + G.n_info + G.n_cnt + 1));
+    const std::vector<SimpleCol> &simple = G.simple;
+    // Jaro-Winkler template columns: compact every list, then one exact launch over all of them
+    ExactCols jw{};
+    jw.g = (int)G.g_exact;
+    ColSet jk{};
+    for (int k = 0; k < K; ++k) {
+        if (!G.may_exact[k] || G.simple_of[k] < 0) continue;
+        const SimpleCol &sc = simple[G.simple_of[k]];
+        if (sc.cls == SC_LEV || sc.kind != SK_STR || jw.n == 4) continue;
+        jk.k[jk.n++] = k;
+        jw.si[jw.n++] = G.simple_of[k];
+    }
+    if (jk.n)
+        k_compact<<<dim3((unsigned)G.n_regions, (unsigned)jk.n), 256, 0, ctx->stream>>>(A, jk, ctx->xpref.p,
+                                                                                       ctx->xlist.p, ctx->xinfo.p);
+    // (running this launch on a second stream beside the Levenshtein pass measured no faster:
+    // 1.198-1.205 ms per cfg2 pass either way)
+    if (jw.n) {
+        k_gamma_exact_simple<false><<<(unsigned)(G.g_exact * jw.n), X_THREADS, 0, ctx->stream>>>(A, jw, ctx->xlist.p,
+                                                                                                ctx->xinfo.p);
+        k_gamma_slow<<<dim3((unsigned)(4 * ctx->n_cu), (unsigned)jk.n), 64, 0, ctx->stream>>>(A, jk, ctx->xlist.p,
+                                                                                             ctx->xinfo.p);
+    }
+    for (int k = 0; k < K; ++k) {
+        if (!G.may_exact[k]) continue;
+        const int si = G.simple_of[k];
+        const bool lev = si >= 0 && simple[si].cls == SC_LEV;
+        bool fused = false;
+        for (int c = 0; c < jw.n; ++c) fused = fused || jw.si[c] == si;
+        if (fused) continue;
+        const ColSet one_k{1, {k, 0, 0, 0}};
+        k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
+        if (lev) {
+            ExactCols one{};
+            one.n = 1;
+            one.g = (int)G.g_exact;
+            one.si[0] = si;
+            k_gamma_exact_simple<true><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
+                                                                                          ctx->xinfo.p);
+            k_gamma_slow_lev<<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
+            k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+        } else if (si >= 0 && simple[si].kind == SK_STR) {
+            ExactCols one{};
+            one.n = 1;
+            one.g = (int)G.g_exact;
+            one.si[0] = si;
+            k_gamma_exact_simple<false><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
+                                                                                           ctx->xinfo.p);
+            k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
+        } else {
+            k_gamma_exact<<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+            k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
+        }
+    }
+    SPK_HIP(hipGetLastError());
+    return SPK_OK;
+}
+
+namespace spk {
+// Completes the last spk_gammas once its info block is on the host: a work-list overflow re-runs the
+// exact phase with room for every listed cell, and cells with a string past SLOW_LIMIT units go through
+// the huge pass.  *fixed = true when codes changed after the call returned (a consumer that already
+// read them must read them again).  Called at the consumers' own synchronisation points.
+int settle_gammas(spk_ctx *ctx, bool *fixed) {
+    if (fixed) *fixed = false;
+    if (!ctx->gamma_pending) return SPK_OK;
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->gamma_pending = false;
+    if (!ctx->codes_valid || !ctx->gplan) return SPK_OK;  // the codes were replaced or invalidated since
+    GammaPlan &G = *ctx->gplan;
+    const int K = G.K;
+    if (ctx->h_info[2 * K]) {
+        // the exact lists did not fit: nothing of the phase ran; grow them and run the phase again
+        const int64_t cap = ctx->h_info[2 * K + 1];
+        SPK_HIP(hipMemsetAsync(ctx->xinfo.p + G.n_info, 0, (size_t)(G.n_cnt + 2) * 8, ctx->stream));
+        SPK_TRY(enqueue_phase(ctx, G, cap));
+        SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)G.n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        if (fixed) *fixed = true;
+        if (ctx->h_info[2 * K]) {
+            ctx->codes_valid = false;
+            SPK_REQUIRE(false, SPK_E_STATE, "spk_gammas: exact work list sizing failed");
+        }
+    }
+    const unsigned int *h_slow = reinterpret_cast<const unsigned int *>(ctx->h_info + G.n_info);
+    int err = 0;
+    std::memcpy(&err, ctx->h_info + G.n_info + G.n_cnt, sizeof(err));
+    if (err & 2) {
+        ctx->codes_valid = false;
+        SPK_REQUIRE(false, SPK_E_INVALID, "spk_gammas: unknown instruction");
+    }
+    int64_t n_slow = 0, n_huge = 0, max_huge = 0;
+    ctx->last_exact.assign((size_t)K, 0);
+    for (int k = 0; k < K; ++k) {
+        ctx->last_exact[k] = ctx->h_info[K + k];
+        n_slow += h_slow[k];
+        n_huge += h_slow[2 * K + k];
+        max_huge = std::max<int64_t>(max_huge, h_slow[2 * K + k]);
+    }
+    ctx->last_xbase.assign(ctx->h_info, ctx->h_info + K);
+    ctx->last_deferred = n_slow;
+    if (n_huge) {  // cells with a string longer than SLOW_LIMIT units (none in the benchmark configs)
+        Scratch S;
+        DevBuf<uint8_t> scratch;
+        SPK_TRY(huge_scratch(G.max_units, max_huge, scratch, S));
+        for (int k = 0; k < K; ++k) {
+            const int64_t nk = h_slow[2 * K + k];
+            if (!nk) continue;
+            const int32_t *items = (G.huge_in_slow[k] ? G.A.slow : ctx->xlist.p) + ctx->h_info[k];  // + xinfo[k]
+            k_gamma_huge<<<(unsigned)(S.n_slots / 64), 64, 0, ctx->stream>>>(G.A, k, items, nk, S);
+            SPK_HIP(hipGetLastError());
+        }
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        if (fixed) *fixed = true;
+    }
+    return SPK_OK;
+}
+}  // namespace spk
+
 extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *cols, int n_when,
                           const int32_t *when_first_instr, const int32_t *when_n_instr, const int32_t *when_level,
                           int n_instr, const spk_instr *instr, int n_operands, const spk_operand *operands, int n_lits,
@@ -2202,6 +1528,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_REQUIRE(ctx->pairs_valid, SPK_E_STATE, "spk_gammas: no pairs");
     SPK_REQUIRE(n_operands < 4096 && n_instr >= 0 && n_when >= 0, SPK_E_LIMIT, "spk_gammas: program too large");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));  // the previous call's capacity feedback (its codes are replaced)
     // ---- host-side validation of the program against the loaded tables
     Table &t0 = ctx->table[0];
     Table &t1 = ctx->side_table(1);
@@ -2267,7 +1594,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     std::vector<int32_t> complex_k;
     for (int k = 0; k < K; ++k) {
         SimpleCol sc;
-        if (ctx->simple_columns &&
+        if (ctx->filter_mode != 0 &&
             classify_simple(k, cols[k], when_first_instr, when_n_instr, when_level, instr, operands, t0, t1,
                             ctx->stride, &sc))
             simple.push_back(sc);
@@ -2306,25 +1633,17 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         }
     }
     const int64_t img_stride = layout_image(simple);
-    // image columns first, by field offset (the row filter walks the chunks in order), then the rest
-    std::stable_sort(simple.begin(), simple.end(), [](const SimpleCol &a, const SimpleCol &b) {
-        const bool ia = a.cls != SC_GEN && a.cls != SC_NUMRAW, ib = b.cls != SC_GEN && b.cls != SC_NUMRAW;
-        if (ia != ib) return ia;
-        return ia && a.off < b.off;
-    });
-    int32_t slot_beg[17];
-    {
-        // slot_beg[t] = first image column starting at 8-byte slot >= t; past the row, the end of them
-        int n_img = 0;
-        while (n_img < (int)simple.size() && simple[n_img].cls != SC_GEN && simple[n_img].cls != SC_NUMRAW) ++n_img;
-        int j = 0;
-        for (int t = 0; t <= 16; ++t) {
-            while (j < n_img && (simple[j].off >> 3) < t) ++j;
-            slot_beg[t] = j;
+    // simple columns the filter kernel cannot take (no filter class, no room in the image) join the
+    // interpreter's columns
+    for (size_t i = 0; i < simple.size();) {
+        if (simple[i].cls == SC_NONE) {
+            complex_k.push_back(simple[i].k);
+            simple.erase(simple.begin() + (long)i);
+        } else {
+            ++i;
         }
-        const int ns = (int)(img_stride / 8);
-        for (int t = ns; t <= 16; ++t) slot_beg[t] = n_img;
     }
+    std::sort(complex_k.begin(), complex_k.end());
     // Every program array goes up in one packed copy into a buffer the context keeps.
     std::vector<uint8_t> blob;
     auto put = [&](const auto *src, size_t n) -> size_t {
@@ -2404,308 +1723,90 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.n_regions = n_regions;
     A.slow_count = reinterpret_cast<unsigned int *>(ctx->xinfo.p + n_info);
     A.n_simple = (int)simple.size();
-    A.all_img = 1;
-    for (const SimpleCol &sc : simple) A.all_img &= (sc.cls != SC_GEN && sc.cls != SC_NUMRAW) ? 1 : 0;
     A.n_complex = (int)complex_k.size();
-    for (int t = 0; t <= 16; ++t) A.slot_beg[t] = slot_beg[t];
     ctx->last_simple = (int)simple.size();
 
-    // ---- the plan of the exact and slow passes (host decisions only; sized on the device by k_prefix)
-    std::vector<int> simple_of(K, -1);
-    for (size_t i = 0; i < simple.size(); ++i) simple_of[simple[i].k] = (int)i;
-    std::vector<char> may_exact(K, 1);  // columns whose filter can leave cells undecided
+    // ---- the plan of the exact and slow passes (host decisions only; sized on the device by k_prefix).
+    // It is kept in the context: the lists' overflow and the huge pass are settled at the next sync
+    // (settle_gammas), not by a round trip inside this call.
+    if (!ctx->gplan) {
+        ctx->gplan = new GammaPlan();
+        ctx->gplan_free = [](GammaPlan *g) { delete g; };
+    }
+    GammaPlan &G = *ctx->gplan;
+    G.simple = simple;
+    G.simple_of.assign(K, -1);
+    for (size_t i = 0; i < simple.size(); ++i) G.simple_of[simple[i].k] = (int)i;
+    G.may_exact.assign(K, 1);  // columns whose filter can leave cells undecided
     for (const SimpleCol &sc : simple)
-        if (sc.kind == SK_NUM || sc.cls == SC_NUM || sc.cls == SC_NUMRAW || (sc.cls == SC_EQ && sc.has_ids))
-            may_exact[sc.k] = 0;
+        if (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids)) G.may_exact[sc.k] = 0;
+    G.huge_in_slow.assign(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
+    for (int k = 0; k < K; ++k)
+        G.huge_in_slow[k] = (G.may_exact[k] && G.simple_of[k] >= 0 && simple[G.simple_of[k]].cls == SC_LEV) ? 1 : 0;
+    G.K = K;
+    G.n_regions = n_regions;
+    G.n_info = n_info;
+    G.n_cnt = n_cnt;
+    G.n_all = n_all;
+    G.g_exact = std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ctx->n_cu, (P + X_THREADS - 1) / X_THREADS));
+    // every string a program can meet is a row of a loaded string column (UTF-8 bytes bound its UTF-16
+    // units), a substring of one, or a literal: the huge pass's scratch per lane
+    G.max_units = 1;
+    for (const Table *t : {&t0, &t1})
+        for (const Column *c : t->cols)
+            if (c && c->kind == COL_STR) G.max_units = std::max<int64_t>(G.max_units, c->max_bytes);
+    for (int i = 0; i < n_lits; ++i) G.max_units = std::max<int64_t>(G.max_units, llen[i]);
     SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions + 1)));
-    int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(P, 1 << 16));
-    const int64_t g_exact = std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ctx->n_cu, (P + X_THREADS - 1) / X_THREADS));
-    std::vector<char> huge_in_slow(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
+    const int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(P, 1 << 16));
 
     SPK_TRY(ctx->begin(K_GAMMA));
     // row images and rule-view images: kernels only when a table, the column layout or the pairs changed
-    const int nq = (int)(img_stride / 16);
-    const bool rows_filter = ctx->row_filter && A.n_simple > 0 && nq >= 1 && nq <= ROW_MAXQ;
     ViewLaunch V{};
     int64_t va = n_regions, vb = n_regions;  // regions over rule 1's view-ordered image: [va, vb)
     ctx->last_view_regions = 0;
     if (P > 0) {
         SPK_TRY(build_images(ctx, t0, t1, A, img_stride, simple));
-        if (!rows_filter) {
-            // regions wholly inside rule 1's pairs read its view-ordered image (view launch); the others,
-            // and a region straddling a rule boundary, the table image (table launches)
-            // Only when the image outgrows the caches: at 1M rows (80 MB, held by the 256 MB Infinity
-            // Cache) the second launch's tail cost 4 % (1.41 vs 1.34 ms, cfg2); at 20M rows (1.6 GB) the
-            // view launch takes the pass from 31.1 to 22.8 ms (profiles/r2_ab_views.log).
-            bool have_view = false;
-            const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
-            if ((ctx->use_views == 1 && big) || ctx->use_views == 2)
-                SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
-            if (have_view) {  // regions [i L, min((i + 1) L, P)) inside [V.lo, V.hi)
-                va = std::min<int64_t>(n_regions, (V.lo + region_len - 1) / region_len);
-                vb = V.hi >= P ? n_regions : std::min<int64_t>(n_regions, V.hi / region_len);
-                vb = std::max<int64_t>(va, vb);
-            }
-            ctx->last_view_regions = vb - va;
+        // regions wholly inside rule 1's pairs read its view-ordered image (view launch); the others, and a
+        // region straddling a rule boundary, the table image (table launches).  Only when the image
+        // outgrows the caches: at 1M rows (80 MB, held by the 256 MB Infinity Cache) the second launch's
+        // tail cost 4 % (1.41 vs 1.34 ms, cfg2); at 20M rows (1.6 GB) the view launch took the pass from
+        // 31.1 to 22.8 ms (profiles/archive/r2_ab_views.log).
+        bool have_view = false;
+        const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
+        if ((ctx->use_views == 1 && big) || ctx->use_views == 2) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
+        if (have_view) {  // regions [i L, min((i + 1) L, P)) inside [V.lo, V.hi)
+            va = std::min<int64_t>(n_regions, (V.lo + region_len - 1) / region_len);
+            vb = V.hi >= P ? n_regions : std::min<int64_t>(n_regions, V.hi / region_len);
+            vb = std::max<int64_t>(va, vb);
         }
-    }
-    // the filter pass
-    auto enqueue_filter = [&]() -> int {
-        if (P <= 0) return SPK_OK;
-        if (rows_filter) {
-            switch (nq) {
-                case 1: k_gamma_rows<1><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 2: k_gamma_rows<2><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 3: k_gamma_rows<3><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 4: k_gamma_rows<4><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 5: k_gamma_rows<5><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 6: k_gamma_rows<6><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                case 7: k_gamma_rows<7><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-                default: k_gamma_rows<8><<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A); break;
-            }
-        } else {
-            auto launch = [&](const GammaArgs &LA, int64_t r_lo, int64_t r_hi) {
-                if (r_hi <= r_lo) return;
-                GammaArgs B = LA;
-                B.region_base = (int)r_lo;
-                const unsigned g = (unsigned)(r_hi - r_lo);
-                // buffer-descriptor gathers while every chunk plane fits the 31-bit descriptor range
-                const bool buf = std::max(B.img_rows0, B.img_rows1) * B.img_stride < (int64_t)INT32_MAX;
-                const size_t shm = (size_t)B.n_thr * sizeof(int16_t);
-                switch (buf ? ctx->filter_waves : -1) {  // (waves per SIMD the filter is compiled for, pairs per lane)
-                    case -1: k_gamma_simple<6, 3, false><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    case 1: k_gamma_simple<4, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    case 2: k_gamma_simple<6, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    case 3: k_gamma_simple<5, 4, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    case 4: k_gamma_simple<8, 2, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    case 5: k_gamma_simple<5, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    case 6: k_gamma_simple<6, 3, false><<<g, F_THREADS, shm, ctx->stream>>>(B); break;  // A/B: flat loads
-                    // measured on MI355X (cfg2 pass): <6,3> 1.725 ms, <5,3> 1.725, <6,4> (spills) 1.75,
-                    // <5,4> 1.765, <1,4> (104 VGPRs, 4 waves) 1.87
-                    case 7: k_gamma_simple<6, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    // timing experiment (wrong results): every gather hits the image's first 256 rows
-                    case 9: k_gamma_simple<5, 3, true, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                    // measured on MI355X after the per-test parameter hoist (cfg2 pass, tools/ab_gamma.py):
-                    // <5,3> 1.236 ms, <8,2> 1.260, <6,3> (VGPR spills) 1.306
-                    default: k_gamma_simple<5, 3, true><<<g, F_THREADS, shm, ctx->stream>>>(B); break;
-                }
-            };
-            launch(A, 0, va);
+        ctx->last_view_regions = vb - va;
+        // the filter pass (the interpreter's columns add to the codes the template filter sets)
+        if (simple.empty())
+            SPK_HIP(hipMemsetAsync(ctx->codes.p, 0, (size_t)P * ctx->code_bytes, ctx->stream));
+        if (!simple.empty()) {
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va));
             if (vb > va) {
                 GammaArgs VA = A;
                 VA.pl = ctx->pvl.p - ctx->pv_base;  // pl[p] = view position of pair p (p >= pv_base)
                 VA.pr = ctx->pvr.p - ctx->pv_base;
                 VA.img0 = V.img0;
                 VA.img1 = V.img1;
-                launch(VA, va, vb);
+                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb));
             }
-            launch(A, vb, n_regions);
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions));
         }
-        SPK_HIP(hipGetLastError());
         if (A.n_complex) {
             k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
             SPK_HIP(hipGetLastError());
         }
-        return SPK_OK;
-    };
-    // the exact and slow passes over the lists the filter wrote (list capacity `cap`)
-    auto enqueue_phase = [&]() -> int {
-        SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));
-        A.slow = ctx->xlist.p + cap;
-        A.slow_off = ctx->xinfo.p;
-        ctx->xcap = cap;
-        if (P > 0) {
-        k_prefix<<<(unsigned)K, PFX_THREADS, 0, ctx->stream>>>(
-            ctx->region_count.p, K, n_regions, cap, ctx->xpref.p, ctx->xinfo.p,
-            reinterpret_cast<unsigned long long *>(ctx->xinfo.p + n_info + n_cnt + 1));
-        // Jaro-Winkler template columns: compact every list, then one exact launch over all of them
-        ExactCols jw{};
-        // JW lists are short (cfg2: 0.1-0.3 M cells): fewer blocks give each lane several cells, so
-        // the next cell's loads overlap the current one's work (the pass is load-latency bound)
-        const int64_t g_jw = ctx->jw_grid > 0
-            ? std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->jw_grid * ctx->n_cu, g_exact)) : g_exact;
-        jw.g = (int)g_jw;
-        ColSet jk{};
-        for (int k = 0; k < K; ++k) {
-            if (!may_exact[k] || simple_of[k] < 0) continue;
-            const SimpleCol &sc = simple[simple_of[k]];
-            if (sc.cls == SC_LEV || sc.kind != SK_STR || jw.n == 4) continue;
-            jk.k[jk.n++] = k;
-            jw.si[jw.n++] = simple_of[k];
-        }
-        if (jk.n)
-            k_compact<<<dim3((unsigned)n_regions, (unsigned)jk.n), 256, 0, ctx->stream>>>(A, jk, ctx->xpref.p,
-                                                                                       ctx->xlist.p, ctx->xinfo.p);
-        // (running this launch on a second stream beside the Levenshtein pass measured no faster:
-        // 1.198-1.205 ms per cfg2 pass either way)
-        if (jw.n) {
-            switch (ctx->jw_waves) {  // A/B: waves per SIMD the JW pass is compiled for
-                case 3: k_gamma_exact_simple<false, 3><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
-                            A, jw, ctx->xlist.p, ctx->xinfo.p); break;
-                case 4: k_gamma_exact_simple<false, 4><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
-                            A, jw, ctx->xlist.p, ctx->xinfo.p); break;
-                default: k_gamma_exact_simple<false><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(
-                             A, jw, ctx->xlist.p, ctx->xinfo.p); break;
-            }
-            k_gamma_slow<<<dim3((unsigned)(4 * ctx->n_cu), (unsigned)jk.n), 64, 0, ctx->stream>>>(A, jk, ctx->xlist.p,
-                                                                                                 ctx->xinfo.p);
-        }
-        for (int k = 0; k < K; ++k) {
-            if (!may_exact[k]) continue;
-            const bool simple_str = simple_of[k] >= 0 && simple[simple_of[k]].kind == SK_STR;
-            const bool lev = simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV;
-            bool fused = false;
-            for (int c = 0; c < jw.n; ++c) fused = fused || jw.si[c] == simple_of[k];
-            const ColSet one_k{1, {k, 0, 0, 0}};
-            if (!fused)
-                k_compact<<<(unsigned)n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p,
-                                                                       ctx->xinfo.p);
-            if (lev) {
-                ExactCols one{};
-                one.n = 1;
-                one.g = (int)g_exact;
-                one.si[0] = simple_of[k];
-                switch (ctx->lev_waves) {  // A/B: waves per SIMD the Levenshtein pass is compiled for
-                    case 4: k_gamma_exact_simple<true, 4><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
-                                A, one, ctx->xlist.p, ctx->xinfo.p); break;
-                    case 6: k_gamma_exact_simple<true, 6><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
-                                A, one, ctx->xlist.p, ctx->xinfo.p); break;
-                    default: k_gamma_exact_simple<true><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(
-                                 A, one, ctx->xlist.p, ctx->xinfo.p); break;
-                }
-            } else if (!fused && simple_str) {
-                ExactCols one{};
-                one.n = 1;
-                one.g = (int)g_exact;
-                one.si[0] = simple_of[k];
-                k_gamma_exact_simple<false><<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
-                                                                                             ctx->xinfo.p);
-            } else if (!fused) {
-                k_gamma_exact<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
-            }
-            huge_in_slow[k] = lev ? 1 : 0;
-            if (lev) {
-                k_gamma_slow_lev<<<(unsigned)g_exact, X_THREADS, 0, ctx->stream>>>(A, simple_of[k], ctx->xlist.p,
-                                                                                     ctx->xinfo.p);
-                k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
-            } else if (!fused) {
-                k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
-            }
-        }
-            SPK_HIP(hipGetLastError());
-        } else {
-            SPK_HIP(hipMemsetAsync(ctx->xinfo.p, 0, (size_t)n_info * 8, ctx->stream));
-        }
-        return SPK_OK;
-    };
-    // With ctx->graphs both run as one HIP graph once the same launch sequence (same programs, tables,
-    // pairs, list capacity and variants) has been seen twice -- every call of an EM run -- so the host
-    // issues one launch instead of ~15 (kernel nodes only; the timing events stay outside).  Off by
-    // default: the device already runs the launches back to back, and on MI355X the graph measured
-    // 1.269 / 1.276 ms per bench step against 1.259 / 1.267 without (profiles/r2_ab_graph.log).
-    bool launched = false;
-    if (ctx->graphs && ctx->stream) {
-        SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));  // the pointers the key and the graph hold
-        std::vector<uint8_t> key;
-        auto add = [&](const void *p, size_t n) {
-            const uint8_t *b = static_cast<const uint8_t *>(p);
-            key.insert(key.end(), b, b + n);
-        };
-        GammaArgs AK = A;
-        AK.slow = ctx->xlist.p + cap;
-        AK.slow_off = ctx->xinfo.p;
-        add(&AK, sizeof(AK));
-        add(&V, sizeof(V));
-        const int64_t scal[] = {va, vb, cap, g_exact, n_regions, rows_filter, ctx->filter_waves, ctx->lev_waves,
-                                ctx->jw_waves, ctx->jw_grid, (int64_t)(intptr_t)ctx->xlist.p,
-                                (int64_t)(intptr_t)ctx->xpref.p, (int64_t)(intptr_t)ctx->pvl.p,
-                                (int64_t)(intptr_t)ctx->pvr.p, ctx->pv_base};
-        add(scal, sizeof(scal));
-        add(ctx->last_blob.data(), ctx->last_blob.size());
-        if (ctx->graph_exec && key == ctx->graph_key) {
-            SPK_HIP(hipGraphLaunch(ctx->graph_exec, ctx->stream));
-            launched = true;
-        } else if (key == ctx->graph_seen) {
-            ctx->drop_graph();
-            SPK_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-            const int rf = enqueue_filter();
-            const int rp = rf == SPK_OK ? enqueue_phase() : rf;
-            hipGraph_t g = nullptr;
-            const hipError_t ec = hipStreamEndCapture(ctx->stream, &g);
-            if (rp != SPK_OK) {
-                if (g) (void)hipGraphDestroy(g);
-                return rp;
-            }
-            SPK_HIP(ec);
-            ctx->graph = g;
-            SPK_HIP(hipGraphInstantiate(&ctx->graph_exec, g, nullptr, nullptr, 0));
-            ctx->graph_key = key;
-            SPK_HIP(hipGraphLaunch(ctx->graph_exec, ctx->stream));
-            launched = true;
-        } else {
-            ctx->graph_seen = key;
-        }
     }
-    if (!launched) {
-        SPK_TRY(enqueue_filter());
-        SPK_TRY(enqueue_phase());
-    }
-    for (int k = 0; k < K; ++k) huge_in_slow[k] = (may_exact[k] && simple_of[k] >= 0 && simple[simple_of[k]].cls == SC_LEV) ? 1 : 0;
-    for (int attempt = 0;; ++attempt) {
-        SPK_TRY(ctx->end(K_GAMMA));
-        SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
-        SPK_HIP(hipStreamSynchronize(ctx->stream));
-        if (!ctx->h_info[2 * K]) break;
-        // the exact lists did not fit: nothing of the phase ran; grow them and run the phase again
-        SPK_REQUIRE(attempt == 0, SPK_E_STATE, "spk_gammas: exact work list sizing failed");
-        cap = ctx->h_info[2 * K + 1];
-        ctx->drop_graph();
-        SPK_TRY(enqueue_phase());
-    }
-    std::vector<int64_t> counts((size_t)2 * K, 0);
-    const unsigned int *h_slow = reinterpret_cast<const unsigned int *>(ctx->h_info + n_info);
-    int64_t n_slow = 0;
-    for (int k = 0; k < K; ++k) {
-        counts[k] = ctx->h_info[K + k];
-        counts[K + k] = h_slow[k];
-        n_slow += h_slow[k];
-    }
-    int err = 0;
-    std::memcpy(&err, ctx->h_info + n_info + n_cnt, sizeof(err));
-    SPK_REQUIRE(!(err & 2), SPK_E_INVALID, "spk_gammas: unknown instruction");
-    // ---- huge pass: cells with a string longer than SLOW_LIMIT units (none in the benchmark configs)
-    int64_t n_huge = 0, max_huge = 0;
-    for (int k = 0; k < K; ++k) {
-        n_huge += h_slow[2 * K + k];
-        max_huge = std::max<int64_t>(max_huge, h_slow[2 * K + k]);
-    }
-    if (n_huge) {
-        // every string a program can meet is a row of a loaded string column (UTF-8 bytes bound its
-        // UTF-16 units), a substring of one, or a literal
-        int64_t units = 1;
-        for (const Table *t : {&t0, &t1})
-            for (const Column *c : t->cols)
-                if (c && c->kind == COL_STR) units = std::max<int64_t>(units, c->max_bytes);
-        for (int i = 0; i < n_lits; ++i) units = std::max<int64_t>(units, llen[i]);
-        Scratch S;
-        DevBuf<uint8_t> scratch;
-        SPK_TRY(huge_scratch(units, max_huge, scratch, S));
-        SPK_TRY(ctx->begin(K_GAMMA));
-        for (int k = 0; k < K; ++k) {
-            const int64_t nk = h_slow[2 * K + k];
-            if (!nk) continue;
-            const int32_t *items = (huge_in_slow[k] ? A.slow : ctx->xlist.p) + ctx->h_info[k];  // + xinfo[k]
-            k_gamma_huge<<<(unsigned)(S.n_slots / 64), 64, 0, ctx->stream>>>(A, k, items, nk, S);
-            SPK_HIP(hipGetLastError());
-        }
-        SPK_TRY(ctx->end(K_GAMMA));
-        SPK_HIP(hipStreamSynchronize(ctx->stream));
-    }
+    G.A = A;
+    SPK_TRY(enqueue_phase(ctx, G, cap));
+    SPK_TRY(ctx->end(K_GAMMA));
+    SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->gamma_pending = true;
     ctx->codes_valid = true;
     ctx->mpat_valid = false;
-    ctx->last_deferred = n_slow;
-    ctx->last_exact.assign(counts.begin(), counts.begin() + K);
-    ctx->last_xbase.assign(ctx->h_info, ctx->h_info + K);
     ctx->last_implied.assign((size_t)K, 0);
     for (const SimpleCol &sc : simple) ctx->last_implied[sc.k] = sc.imp_hi - sc.imp_lo;
     return SPK_OK;
@@ -2714,6 +1815,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
 extern "C" int spk_gammas_load(spk_ctx *ctx, int n_cols, const int32_t *n_levels, int64_t n, const int8_t *gammas) {
     SPK_REQUIRE(ctx && n_levels && n >= 0 && (n == 0 || gammas), SPK_E_INVALID, "spk_gammas_load: bad args");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     SPK_TRY(set_pattern_space(ctx, n_cols, n_levels));
     for (int64_t p = 0; p < n; ++p)
         for (int k = 0; k < n_cols; ++k)
@@ -2733,6 +1835,7 @@ extern "C" int spk_gammas_load(spk_ctx *ctx, int n_cols, const int32_t *n_levels
     }
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     ctx->n_pairs = n;
+    ctx->gamma_pending = false;
     ctx->codes_valid = true;
     return SPK_OK;
 }
@@ -2742,6 +1845,7 @@ extern "C" int spk_gammas_copy(spk_ctx *ctx, int64_t start, int64_t count, int8_
     SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_gammas_copy: no gammas");
     SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "range out of bounds");
     SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
     if (!count) return SPK_OK;
     DevBuf<int8_t> d_out;
     DevBuf<int64_t> d_stride;
@@ -2896,12 +2000,15 @@ extern "C" int spk_n_patterns(spk_ctx *ctx, int64_t *out) {
 
 extern "C" int spk_gammas_deferred(spk_ctx *ctx, int64_t *out) {
     SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
+    SPK_TRY(settle_gammas(ctx, nullptr));
     *out = ctx->last_deferred;
     return SPK_OK;
 }
 
 extern "C" int spk_gammas_exact_list(spk_ctx *ctx, int k, int32_t *out, int64_t n) {
-    SPK_REQUIRE(ctx && out && k >= 0 && k < (int)ctx->last_exact.size() && n >= 0, SPK_E_INVALID,
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    SPK_REQUIRE(out && k >= 0 && k < (int)ctx->last_exact.size() && n >= 0, SPK_E_INVALID,
                 "spk_gammas_exact_list: bad args");
     const int64_t m = std::min<int64_t>(n, ctx->last_exact[k]);
     if (m > 0)
@@ -2910,7 +2017,9 @@ extern "C" int spk_gammas_exact_list(spk_ctx *ctx, int k, int32_t *out, int64_t 
 }
 
 extern "C" int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n) {
-    SPK_REQUIRE(ctx && out && n >= (int)ctx->last_exact.size(), SPK_E_INVALID, "spk_gammas_exact_counts: bad args");
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    SPK_REQUIRE(out && n >= (int)ctx->last_exact.size(), SPK_E_INVALID, "spk_gammas_exact_counts: bad args");
     for (size_t k = 0; k < ctx->last_exact.size(); ++k) out[k] = ctx->last_exact[k];
     return SPK_OK;
 }
@@ -2922,21 +2031,9 @@ extern "C" int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n) {
 }
 
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
-    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
-    ctx->graphs = on / 10000000 != 0;  // + 10000000: the pass as a HIP graph (A/B; off by default, see spk_gammas)
-    on %= 10000000;
-    ctx->jw_waves = on / 1000000;  // + W x 1000000: the JW exact pass at W waves per SIMD (A/B)
-    on %= 1000000;
-    ctx->jw_grid = on / 100000;  // + G x 100000: the JW exact launch at G blocks per CU and column (A/B)
-    ctx->lev_waves = (on / 10000) % 10;  // + W x 10000: Levenshtein pass at W waves per SIMD (A/B)
-    on %= 10000;
-    const bool local = on >= 1000;  // + 1000: timing experiment, gathers kept local (wrong results)
-    on %= 1000;
-    ctx->use_views = on >= 20 ? 2 : (on >= 10 ? 0 : 1);  // + 10: never view launches, + 20: always (A/B, tests)
-    on %= 10;
-    ctx->simple_columns = on != 0;
-    ctx->row_filter = on == 2;
-    ctx->filter_waves = local ? 9 : (on >= 3 ? on - 2 : 0);  // A/B variants of the filter (tools/ab_gamma.py)
+    SPK_REQUIRE(ctx && on >= 0 && on % 10 <= 1 && on < 30, SPK_E_INVALID, "spk_gammas_set_simple: mode 0, 1 (+10 / +20)");
+    ctx->use_views = on >= 20 ? 2 : (on >= 10 ? 0 : 1);
+    ctx->filter_mode = on % 10;
     return SPK_OK;
 }
 

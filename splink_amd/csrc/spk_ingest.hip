@@ -174,12 +174,14 @@ __global__ void k_i64_keys(int64_t n, const int64_t *__restrict__ v, const uint8
     nul[i] = ok ? 0 : 1;
 }
 
-__global__ void k_rank(int64_t n, const int64_t *__restrict__ ids, int64_t right_from, int64_t div,
-                       int64_t *__restrict__ rank) {
+// rank of table row i = input row perm[i] (perm null: identity; a table reordered by spk_cluster)
+__global__ void k_rank(int64_t n, const int64_t *__restrict__ ids, const int32_t *__restrict__ perm, int64_t right_from,
+                       int64_t div, int64_t *__restrict__ rank) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int64_t src = i >= right_from ? 1 : 0;
-    rank[i] = src * div + (ids[i] < 0 ? div - 1 : ids[i]);
+    const int64_t r = perm ? perm[i] : i;
+    const int64_t src = r >= right_from ? 1 : 0;
+    rank[i] = src * div + (ids[r] < 0 ? div - 1 : ids[r]);
 }
 
 __global__ void k_cluster_keys(int64_t n, const int64_t *__restrict__ key, const int64_t *__restrict__ rank,
@@ -316,10 +318,18 @@ static int new_raw(spk_ctx *ctx, int raw, RawCol **out) {
     return SPK_OK;
 }
 
+// Keys come in input row order; a table already reordered by spk_cluster takes them through its
+// permutation (table row i = input row perm[i]), so keys always follow the table's rows.
 static int set_key(spk_ctx *ctx, Table &t, int which, int rule, const int64_t *src, int64_t n) {
     while ((int)t.key[which].size() <= rule) t.key[which].push_back(new DevBuf<int64_t>());
     SPK_TRY(t.key[which][rule]->alloc((size_t)n + 1));
-    if (n) SPK_HIP(hipMemcpyAsync(t.key[which][rule]->p, src, (size_t)n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    if (!n) return SPK_OK;
+    if (t.perm.p) {
+        k_gather<int64_t><<<grid(n), 256, 0, ctx->stream>>>(n, src, t.perm.p, t.key[which][rule]->p);
+        SPK_HIP(hipGetLastError());
+    } else {
+        SPK_HIP(hipMemcpyAsync(t.key[which][rule]->p, src, (size_t)n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    }
     return SPK_OK;
 }
 
@@ -386,6 +396,8 @@ int spk_key_build(spk_ctx *ctx, int rule, int n_terms, const spk_key_term *terms
         return false;
     }();
     const int64_t N = n0 + (any_r ? n1 : 0);
+    // k_hash / k_pack_ids / sorted_ids hold the global row (both sides) in an int32
+    SPK_REQUIRE(N < (int64_t)INT32_MAX, SPK_E_LIMIT, "spk_key_build: more than 2^31-1 rows over both tables");
     DevBuf<int64_t> acc, cur;
     int64_t n_ids = 0;
     for (int i = 0; i < n_terms; ++i) {
@@ -451,7 +463,7 @@ int spk_rank_from_raw(spk_ctx *ctx, int raw_uid, int64_t right_from) {
     // a NULL id (possibly sharing the last run's key) never undercounts: div = runs + 1 > any id + 1
     const int64_t div = runs + 1;
     SPK_REQUIRE(2 * div < (int64_t)UINT32_MAX, SPK_E_LIMIT, "rank must be in [0, 2^32)");
-    k_rank<<<grid(n), 256, 0, ctx->stream>>>(n, ids.p, right_from < 0 ? n : right_from, div, t.rank.p);
+    k_rank<<<grid(n), 256, 0, ctx->stream>>>(n, ids.p, t.perm.p, right_from < 0 ? n : right_from, div, t.rank.p);
     SPK_HIP(hipGetLastError());
     // NULL ids present?  (the rank layout then marks them for the link predicate)
     DevBuf<unsigned long long> cnt;
@@ -536,6 +548,8 @@ int spk_table_add_raw_utf8(spk_ctx *ctx, int col, int raw0, int raw1) {
     const bool two = ctx->link_type == SPK_LINK_ONLY;
     SPK_REQUIRE(!two || raw1 >= 0, SPK_E_INVALID, "spk_table_add_raw_utf8: link_only needs the side-1 raw column");
     Table &t0 = ctx->table[0];
+    SPK_REQUIRE(t0.n + (two ? ctx->table[1].n : 0) < (int64_t)INT32_MAX, SPK_E_LIMIT,
+                "spk_table_add_raw_utf8: more than 2^31-1 rows over both tables");
     HashSeg s0{}, s1{};
     SPK_TRY(seg_of(ctx, raw0, t0.n, 0, -1, &s0));
     SPK_REQUIRE(s0.kind == RAW_UTF8, SPK_E_INVALID, "spk_table_add_raw_utf8: not a string raw column");

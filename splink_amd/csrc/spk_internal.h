@@ -208,6 +208,7 @@ struct RuleView {
     int64_t pair_lo = 0, pair_hi = 0;  // this rule's pair ordinals (local shard)
 };
 
+struct GammaPlan;
 enum Kern { K_BLOCK = 0, K_GAMMA = 1, K_EMHIST = 2, K_EMFIN = 3, K_SCORE = 4, K_COUNT = 5 };
 
 }  // namespace spk
@@ -245,14 +246,10 @@ struct spk_ctx {
     std::vector<int64_t> last_exact;  // per column: pairs the last spk_gammas evaluated exactly
     std::vector<int64_t> last_xbase;  // per column: start of its exact list in xlist (diagnostics)
     std::vector<int64_t> last_implied;  // per column: pairs whose level the blocking key implied
-    bool simple_columns = true;       // template-shaped columns take the record-only filter
-    bool row_filter = false;          // short row images: the register-resident filter (k_gamma_rows)
-    int lev_waves = 0;                // Levenshtein exact pass variant (waves per SIMD; 0 = LEV_WAVES), A/B
-    int jw_waves = 0;                 // JW exact pass variant (waves per SIMD; 0 = JW_WAVES), A/B
-    int jw_grid = 0;                  // JW exact launch: blocks per CU and column (0 = the exact passes' 8), A/B
-    int filter_waves = 0;             // k_gamma_simple variant (waves per SIMD, pairs per lane): 0 = <6,3>; 1..5 A/B
+    int filter_mode = 1;              // 1: template-shaped columns through the filter kernel (spk_filter.hip),
+                                      // 0: every column through the interpreter (spk_gammas_set_simple)
     int use_views = 1;                // rule 1's pairs read a view-ordered row image: 0 never, 1 when the
-                                      // image outgrows the caches, 2 always (A/B and tests)
+                                      // image outgrows the caches, 2 always (tests)
     int64_t last_view_regions = 0;    // filter regions the last spk_gammas ran as a view launch
     int last_simple = 0;
 
@@ -284,25 +281,18 @@ struct spk_ctx {
     uint64_t table_epoch = 0;
     spk::DevBuf<uint8_t> prog_blob;   // comparison programs, literals, strides (uploaded when they change)
     std::vector<uint8_t> last_blob;   // host copy of what prog_blob holds
-    // spk_gammas launch sequence as a HIP graph: captured the second time a key (GammaArgs, list
-    // capacity, variants, program blob) repeats, replayed while it does
-    bool graphs = false;
-    std::vector<uint8_t> graph_key, graph_seen;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t graph_exec = nullptr;
-    void drop_graph() {
-        if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
-        if (graph) (void)hipGraphDestroy(graph);
-        graph_exec = nullptr;
-        graph = nullptr;
-        graph_key.clear();
-    }
+    // the last spk_gammas: the plan its exact / huge passes ran with, and whether its info block still
+    // has to be read (settle_gammas, at the next synchronisation of a consumer)
+    spk::GammaPlan *gplan = nullptr;
+    void (*gplan_free)(spk::GammaPlan *) = nullptr;
+    bool gamma_pending = false;
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
     // EM state
     spk::DevBuf<uint64_t> hist;
-    spk::DevBuf<double> mpat, llpat, stats, mu;
-    spk::DevBuf<uint32_t> hist_part;  // per-workgroup pattern counts (k_hist_lanes)
+    spk::DevBuf<double> mpat, llpat, cpat, stats, mu;  // per pattern: mp, ln(...), count; statistics; m / u
+    spk::DevBuf<uint64_t> hist_acc;     // spk_em_iteration's accumulation histogram (kept zero between launches)
+    spk::DevBuf<unsigned int> em_ticket;  // its last-workgroup ticket (kept zero between launches)
     double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;
     int n_cu = 256;                   // compute units of the device (grid sizing)
@@ -324,6 +314,7 @@ struct spk_ctx {
     std::vector<spk::RawCol *> raw;  // device copies of the input columns (spk_raw_*)
     ~spk_ctx() {
         for (spk::RawCol *r : raw) delete r;
+        if (gplan && gplan_free) gplan_free(gplan);
     }
     bool mpat_valid = false;
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
@@ -340,6 +331,9 @@ struct spk_ctx {
 
 namespace spk {
 int ensure_desc(spk_ctx *ctx, Table &t);
+// Finishes the last spk_gammas (work-list overflow, huge pass) once the stream is synchronised;
+// *fixed = true when codes changed after spk_gammas returned.  No-op when nothing is pending.
+int settle_gammas(spk_ctx *ctx, bool *fixed);
 int new_column(spk_ctx *ctx, int side, int col, Column **out);
 int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c);
 int launch_utf8_decode(spk_ctx *ctx, int64_t n, const int64_t *off8, const int64_t *src_off, const int32_t *perm,

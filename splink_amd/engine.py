@@ -399,8 +399,7 @@ class Job:
             D.allreduce_histogram_(hist)
             torch.cuda.synchronize(self.device)
             return self.ctx.em_finalize(hist.data_ptr(), lam_d, one_minus, m, u, n_stats)
-        self.ctx.em_histogram(0)
-        return self.ctx.em_finalize(0, lam_d, one_minus, m, u, n_stats)
+        return self.ctx.em_iteration(lam_d, one_minus, m, u, n_stats)
 
     def log_likelihood(self, lam, level_probs):
         """Σ over pairs of ln(λ·Πm + (1-λ)·Πu) (expectation_step.py:224-272); None if every term is NULL."""

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU round-trip: parity tests, bench, rocprof kernel stats.  Usage: bash scripts_gpu_check.sh TAG
+# One GPU round-trip: parity tests, bench, rocprof kernel stats.  Usage: bash tools/gpu/check.sh TAG
 # Stops at the first step that times out, aborts or faults (only plain test failures continue).
 TAG=${1:-run}
 cd $GRAFT_REPO_ROOT

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Bench line + full-job rows.  Usage: bash scripts_gpu_job.sh TAG RECORDS SHARD
+# Bench line + full-job rows.  Usage: bash tools/gpu/fulljob_cfg4.sh TAG RECORDS SHARD
 TAG=${1:-job}; REC=${2:-1000000}; SHARD=${3:-0/1}
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Perf iteration: quick parity subset, bench line, rocprof kernel stats, one SQ counter pass.
-# Usage: bash scripts_gpu_perf.sh TAG [pytest -k expr]
+# Usage: bash tools/gpu/perf.sh TAG [pytest -k expr]
 TAG=${1:-perf}
 K=${2:-"simple or blocking or cfg5 or levels or case_levels or pipeline or em_at_scale or cfg2_full"}
 cd $GRAFT_REPO_ROOT

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Counter passes of the bench command (round 2) + FETCH_SIZE calibration.  Usage: bash scripts_gpu_pmc2.sh TAG
+# Counter passes of the bench command (end of round 2; the FETCH_SIZE calibration is in profiles/r2_calib_fetch_*).
+# Usage: bash tools/gpu/pmc.sh TAG
 TAG=${1:-pmc}
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/calib_$TAG -o run -- ./tools/calib_fetch > gpurun_out/calib_$TAG.log 2>&1 || exit 1
 B="python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --em-scale 8"
 pass() {
     local n=$1; shift
