@@ -49,7 +49,9 @@ EXPORTS = [
     "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
+    "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum",
 ]
+TF_LIMBS = 14  # SPK_TF_LIMBS
 
 
 class NativeUnavailable(RuntimeError):
@@ -73,6 +75,15 @@ def load_library():
         getattr(lib, name)  # raises AttributeError when a declared symbol is missing
     _lib = lib
     return lib
+
+
+def tf_limbs_to_sum(limbs) -> np.ndarray:
+    """Σmp per value from fixed-point accumulators (host only, no device)."""
+    lib = load_library()
+    limbs = np.ascontiguousarray(limbs, dtype=np.int64).reshape(-1, TF_LIMBS)
+    out = np.zeros(max(len(limbs), 1), dtype=np.float64)
+    check(lib.spk_tf_limbs_to_sum(ctypes.c_int64(len(limbs)), _ptr(limbs), _ptr(out)), "spk_tf_limbs_to_sum")
+    return out[:len(limbs)]
 
 
 def device_count() -> int:
@@ -395,6 +406,24 @@ class Context:
         check(self._lib.spk_tf_accumulate(self._h, ctypes.c_int64(n_values), _ptr(ids0), _ptr(ids1), _ptr(s), _ptr(c)),
               "spk_tf_accumulate")
         return s[:n_values], c[:n_values]
+
+    def tf_accumulate_exact(self, n_values, ids0, ids1):
+        """Fixed-point per-value Σmp accumulators (int64 [n_values, TF_LIMBS]) and counts: exact, so ranks
+        holding shards of the pairs sum them (all-reduce) before tf_limbs_to_sum."""
+        ids0 = np.ascontiguousarray(ids0, dtype=np.int64)
+        ids1 = np.ascontiguousarray(ids1, dtype=np.int64)
+        limbs = np.zeros((max(n_values, 1), TF_LIMBS), dtype=np.int64)
+        c = np.zeros(max(n_values, 1), dtype=np.int64)
+        check(self._lib.spk_tf_accumulate_exact(self._h, ctypes.c_int64(n_values), _ptr(ids0), _ptr(ids1), _ptr(limbs),
+                                                _ptr(c)), "spk_tf_accumulate_exact")
+        return limbs[:n_values], c[:n_values]
+
+    def tf_accumulate_column_exact(self, col: int, n_values: int):
+        limbs = np.zeros((max(n_values, 1), TF_LIMBS), dtype=np.int64)
+        c = np.zeros(max(n_values, 1), dtype=np.int64)
+        check(self._lib.spk_tf_accumulate_column_exact(self._h, ctypes.c_int(col), ctypes.c_int64(n_values), _ptr(limbs),
+                                                       _ptr(c)), "spk_tf_accumulate_column_exact")
+        return limbs[:n_values], c[:n_values]
 
     def tf_column_values(self, col: int) -> int:
         n = ctypes.c_int64(0)

@@ -10,7 +10,7 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = ["spk_ctx.hip", "spk_block.hip", "spk_gamma.hip", "spk_filter.hip", "spk_em.hip", "spk_ingest.hip"]
+SOURCES = ["spk_ctx.hip", "spk_block.hip", "spk_gamma.hip", "spk_filter.hip", "spk_em.hip", "spk_tf.hip", "spk_ingest.hip"]
 HEADERS = ["spk_internal.h", "spk_strsim.h", "spk_gamma.h"]
 OUT = os.path.join(HERE, "libsplink_hip.so")
 OBJ = os.path.join(HERE, "build")

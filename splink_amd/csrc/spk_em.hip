@@ -285,17 +285,16 @@ __global__ __launch_bounds__(EF_THREADS) void k_em_finalize(PatArgs A0, const un
     em_finalize_block(A, [&](int p) { return hist[p]; }, mpat, llpat, cpat, out, s_tab);
 }
 
-// Histogram of the codes with lane-private LDS counters (as k_hist_lanes), each workgroup's counts added
-// to the device accumulator `hist` (integer atomics: exact, order-free; one 128-byte line per bin, so the
-// workgroups' adds to different bins do not serialise on shared lines: 8 bins per line cost 40.6 us per
-// cfg2 iteration against the 20 us of streaming).  The workgroup that finishes last (device-scope
-// ticket) reads the accumulator back -- exchanging every bin with 0, so it is zero again for the next
-// launch -- and either (FIN) runs the E-step and M-step sums, one launch per EM iteration, or writes the
-// plain histogram to out_hist (multi-GPU: the caller all-reduces it).
-constexpr int HIST_PAD = 16;  // u64 per accumulator bin (one 128-byte line)
+// Histogram of the codes with lane-private LDS counters (as k_hist_lanes); each workgroup writes its
+// counts as one row of `part` (plain whole-line stores; device-scope atomics into one histogram cost
+// 15-25 us per cfg2 iteration: every workgroup's adds to a bin serialise at the memory side).  The
+// workgroup that finishes last (device-scope ticket, release / acquire fences) sums the rows in a fixed
+// order -- exact integers -- and either (FIN) runs the E-step and M-step sums, one launch per EM
+// iteration, or writes the plain histogram to out_hist (multi-GPU: the caller all-reduces it).
+__host__ __device__ inline int64_t part_stride(int64_t n_pat) { return (n_pat + 31) / 32 * 32; }  // whole 128-B lines
 template <typename CodeT, int R, bool FIN>
 __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict__ codes, int64_t P, PatArgs A0,
-                                                        unsigned long long *__restrict__ hist,
+                                                        uint32_t *__restrict__ part,
                                                         unsigned int *__restrict__ ticket, double *__restrict__ mpat,
                                                         double *__restrict__ llpat, double *__restrict__ cpat,
                                                         double *__restrict__ out, unsigned long long *__restrict__ out_hist) {
@@ -360,7 +359,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         uint32_t s = 0;
 #pragma unroll
         for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
-        if (s) atomicAdd(&hist[(int64_t)b * HIST_PAD], (unsigned long long)s);
+        part[(int64_t)blockIdx.x * part_stride(n_pat) + b] = s;
     }
     // last-workgroup-done: every wave's atomics complete, then one release + ticket (k_prefix's pattern)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -372,16 +371,29 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     __syncthreads();
     if (!s_last) return;
     __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the rows' sum per bin, in block order (8 independent partial sums keep loads in flight)
+    const int64_t ps = part_stride(n_pat);
+    const int G = (int)gridDim.x;
+    auto total = [&](int p) -> unsigned long long {
+        unsigned long long a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int b = 0;
+        for (; b + 8 <= G; b += 8)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a[q] += part[(int64_t)(b + q) * ps + p];
+        for (; b < G; ++b) a[0] += part[(int64_t)b * ps + p];
+        return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    };
     if (FIN) {
         // the counters are no longer needed: their LDS holds the staged arguments and the pattern table
         PatArgs *sA = reinterpret_cast<PatArgs *>(sh);
         const PatArgs &A = stage_args(A0, sA);
         double *tab = reinterpret_cast<double *>(sh) + (sizeof(PatArgs) + 7) / 8;
         const bool room = ((sizeof(PatArgs) + 7) / 8 + 3 * (size_t)n_pat) * 8 <= (size_t)n_pat * R * 4;
-        em_finalize_block(A, [&](int p) { return atomicExch(&hist[(int64_t)p * HIST_PAD], 0ull); }, mpat, llpat, cpat,
-                          out, room ? tab : nullptr);
+        em_finalize_block(A, total, mpat, llpat, cpat, out, room ? tab : nullptr);
     } else {
-        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) out_hist[p] = atomicExch(&hist[(int64_t)p * HIST_PAD], 0ull);
+        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) out_hist[p] = total(p);
     }
     if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
@@ -436,58 +448,6 @@ __global__ __launch_bounds__(SC_THREADS) void k_score(const CodeT *__restrict__ 
         o.y = T[a.y];
         out[v] = o;
     }
-}
-
-__global__ void k_tf_accumulate(int64_t P, const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
-                                const int64_t *__restrict__ ids0, const int64_t *__restrict__ ids1,
-                                const double *__restrict__ mp, int64_t n_values, double *__restrict__ sum,
-                                unsigned long long *__restrict__ cnt) {
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P) return;
-    int64_t a = ids0[pl[p]], b = ids1[pr[p]];
-    if (a < 0 || a != b || a >= n_values) return;
-    double v = mp[p];
-    if (isnan(v)) return;
-    atomicAdd(&sum[a], v);
-    atomicAdd(&cnt[a], 1ull);
-}
-
-struct TfApply {
-    int n;
-    const int64_t *ids0[8];
-    const int64_t *ids1[8];
-    const double *tab[8];
-    int64_t tab_n[8];
-};
-
-// bayes(mp, adj...) = Πp / (Πp + Π(1-p)) (term_frequencies.py:21-46, :98-117)
-__global__ void k_tf_apply(TfApply T, int64_t start, int64_t n, const int32_t *__restrict__ pl,
-                           const int32_t *__restrict__ pr, const double *__restrict__ mp, double *__restrict__ out,
-                           double *__restrict__ out_adj) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int64_t p = start + i;
-    double m = mp[p];
-    double adj[8];
-    for (int c = 0; c < T.n; ++c) {
-        int64_t a = T.ids0[c][pl[p]], b = T.ids1[c][pr[p]];
-        double v = 0.5;
-        if (a >= 0 && a == b && a < T.tab_n[c]) {
-            double x = T.tab[c][a];
-            if (!isnan(x)) v = x;
-        }
-        adj[c] = v;
-        if (out_adj) out_adj[i * T.n + c] = v;
-    }
-    if (isnan(m)) {
-        out[i] = NAN;
-        return;
-    }
-    double a = m, b = 1.0 - m;
-    for (int c = 0; c < T.n; ++c) a = a * adj[c];
-    for (int c = 0; c < T.n; ++c) b = b * (1.0 - adj[c]);
-    double d = a + b;
-    out[i] = d == 0.0 ? NAN : a / d;
 }
 
 // Pattern arguments for the current pattern space and m / u (one upload only for large tables).
@@ -555,17 +515,14 @@ static int64_t lane_grid(spk_ctx *ctx) {
 
 // The padded accumulation histogram and the ticket of k_em_iter: zero between launches (the last workgroup
 // resets them), zeroed here only when (re)allocated.
-static int em_accumulator(spk_ctx *ctx, unsigned long long **acc, unsigned int **ticket) {
-    const size_t need = (size_t)ctx->n_patterns * HIST_PAD;
-    if (ctx->hist_acc.n < need || !ctx->hist_acc.p) {
-        SPK_TRY(ctx->hist_acc.alloc(need));
-        SPK_HIP(hipMemsetAsync(ctx->hist_acc.p, 0, ctx->hist_acc.n * 8, ctx->stream));
-    }
+static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket) {
+    const size_t need = (size_t)part_stride(ctx->n_patterns) * (size_t)ctx->n_cu;
+    SPK_TRY(ctx->hist_part.alloc(need));
     if (!ctx->em_ticket.p) {
         SPK_TRY(ctx->em_ticket.alloc(1));
         SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, 4, ctx->stream));
     }
-    *acc = reinterpret_cast<unsigned long long *>(ctx->hist_acc.p);
+    *acc = ctx->hist_part.p;
     *ticket = ctx->em_ticket.p;
     return SPK_OK;
 }
@@ -587,7 +544,7 @@ static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
         A.n_pat = (int)n_pat;
         const int64_t g = lane_grid(ctx);
         const size_t sh = (size_t)n_pat * R * 4;
-        unsigned long long *acc = nullptr;
+        uint32_t *acc = nullptr;
         unsigned int *ticket = nullptr;
         SPK_TRY(em_accumulator(ctx, &acc, &ticket));
         double *mpat = nullptr, *llpat = nullptr, *cpat = nullptr, *out = nullptr;
@@ -703,7 +660,8 @@ extern "C" int spk_em_iteration(spk_ctx *ctx, double lambda, double one_minus, c
             SPK_TRY(finalize_from(ctx, reinterpret_cast<const unsigned long long *>(ctx->hist.p), A, out_stats, n_stats));
         } else {
             const int64_t n_pat = ctx->n_patterns;
-            unsigned long long *acc = nullptr, *h = nullptr;
+            uint32_t *acc = nullptr;
+            unsigned long long *h = nullptr;
             unsigned int *ticket = nullptr;
             SPK_TRY(em_accumulator(ctx, &acc, &ticket));
             SPK_TRY(em_buffers(ctx, n_stats));
@@ -774,187 +732,3 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
     return SPK_OK;
 }
 
-extern "C" int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
-                                 double *out_sum, int64_t *out_count) {
-    SPK_REQUIRE(ctx && ids_side0 && ids_side1 && out_sum && out_count && n_values >= 0, SPK_E_INVALID,
-                "spk_tf_accumulate: bad args");
-    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_accumulate: run spk_score over all pairs first");
-    SPK_HIP(hipSetDevice(ctx->device));
-    SPK_TRY(settle_gammas(ctx, nullptr));
-    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
-    DevBuf<int64_t> d0, d1;
-    DevBuf<double> ds;
-    DevBuf<unsigned long long> dc;
-    SPK_TRY(d0.alloc((size_t)t0.n + 1));
-    SPK_TRY(d1.alloc((size_t)t1.n + 1));
-    SPK_TRY(ds.alloc((size_t)n_values + 1));
-    SPK_TRY(dc.alloc((size_t)n_values + 1));
-    SPK_HIP(hipMemcpyAsync(d0.p, ids_side0, (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemcpyAsync(d1.p, ids_side1, (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
-    SPK_HIP(hipMemsetAsync(ds.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
-    SPK_HIP(hipMemsetAsync(dc.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
-    int64_t P = ctx->n_pairs;
-    if (P)
-        k_tf_accumulate<<<(unsigned)((P + 255) / 256), 256, 0, ctx->stream>>>(P, ctx->pl.p, ctx->pr.p, d0.p, d1.p,
-                                                                          ctx->mp.p, n_values, ds.p, dc.p);
-    SPK_HIP(hipGetLastError());
-    if (n_values) {
-        SPK_HIP(hipMemcpyAsync(out_sum, ds.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
-        SPK_HIP(hipMemcpyAsync(out_count, dc.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    return SPK_OK;
-}
-
-// Term-frequency value ids straight from a string column's dictionary ids (spk_table_add_raw_utf8:
-// dense, one id space for both sides, equal iff the strings are): NULL rows get -1.  No host-side
-// factorisation of the column's values.
-__global__ void k_ids_from_meta(int64_t n, const RecMeta *__restrict__ meta, int64_t *__restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = meta[i].len16 < 0 ? -1 : (int64_t)meta[i].key;
-}
-
-static int column_ids(spk_ctx *ctx, Table &t, int col, DevBuf<int64_t> &out, int64_t *n_ids) {
-    SPK_REQUIRE(col >= 0 && col < (int)t.cols.size() && t.cols[col] && t.cols[col]->kind == COL_STR &&
-                    t.cols[col]->n_ids >= 0,
-                SPK_E_STATE, "tf: the column carries no device dictionary ids (spk_table_add_raw_utf8)");
-    *n_ids = t.cols[col]->n_ids;
-    SPK_TRY(out.alloc((size_t)t.n + 1));
-    if (t.n) k_ids_from_meta<<<(unsigned)((t.n + 255) / 256), 256, 0, ctx->stream>>>(t.n, t.cols[col]->meta.p, out.p);
-    SPK_HIP(hipGetLastError());
-    return SPK_OK;
-}
-
-extern "C" int spk_tf_column_values(spk_ctx *ctx, int col, int64_t *out_n_values) {
-    SPK_REQUIRE(ctx && out_n_values, SPK_E_INVALID, "spk_tf_column_values: null arg");
-    Table &t = ctx->table[0];
-    SPK_REQUIRE(col >= 0 && col < (int)t.cols.size() && t.cols[col] && t.cols[col]->kind == COL_STR &&
-                    t.cols[col]->n_ids >= 0,
-                SPK_E_STATE, "spk_tf_column_values: the column carries no device dictionary ids");
-    *out_n_values = t.cols[col]->n_ids;
-    return SPK_OK;
-}
-
-extern "C" int spk_tf_accumulate_column(spk_ctx *ctx, int col, int64_t n_values, double *out_sum, int64_t *out_count) {
-    SPK_REQUIRE(ctx && out_sum && out_count && n_values >= 0, SPK_E_INVALID, "spk_tf_accumulate_column: bad args");
-    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_accumulate_column: run spk_score over all pairs first");
-    SPK_HIP(hipSetDevice(ctx->device));
-    SPK_TRY(settle_gammas(ctx, nullptr));
-    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
-    DevBuf<int64_t> d0, d1;
-    int64_t n0 = 0, n1 = 0;
-    SPK_TRY(column_ids(ctx, t0, col, d0, &n0));
-    if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, col, d1, &n1));
-    SPK_REQUIRE(n_values == n0, SPK_E_INVALID, "spk_tf_accumulate_column: n_values is not the column's value count");
-    DevBuf<double> ds;
-    DevBuf<unsigned long long> dc;
-    SPK_TRY(ds.alloc((size_t)n_values + 1));
-    SPK_TRY(dc.alloc((size_t)n_values + 1));
-    SPK_HIP(hipMemsetAsync(ds.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
-    SPK_HIP(hipMemsetAsync(dc.p, 0, (size_t)(n_values + 1) * 8, ctx->stream));
-    const int64_t P = ctx->n_pairs;
-    if (P)
-        k_tf_accumulate<<<(unsigned)((P + 255) / 256), 256, 0, ctx->stream>>>(
-            P, ctx->pl.p, ctx->pr.p, d0.p, &t1 != &t0 ? d1.p : d0.p, ctx->mp.p, n_values, ds.p, dc.p);
-    SPK_HIP(hipGetLastError());
-    if (n_values) {
-        SPK_HIP(hipMemcpyAsync(out_sum, ds.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
-        SPK_HIP(hipMemcpyAsync(out_count, dc.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    return SPK_OK;
-}
-
-static int tf_apply_dev(spk_ctx *ctx, TfApply &T, const double *const *adj_tables, const int64_t *table_sizes,
-                        int64_t start, int64_t count, double *out_tf_mp, double *out_adj) {
-    DevBuf<double> dt[8], dout, dadj;
-    for (int c = 0; c < T.n; ++c) {
-        SPK_TRY(dt[c].alloc((size_t)table_sizes[c] + 1));
-        if (table_sizes[c])
-            SPK_HIP(hipMemcpyAsync(dt[c].p, adj_tables[c], (size_t)table_sizes[c] * 8, hipMemcpyHostToDevice,
-                                   ctx->stream));
-        T.tab[c] = dt[c].p;
-        T.tab_n[c] = table_sizes[c];
-    }
-    SPK_TRY(dout.alloc((size_t)count + 1));
-    if (out_adj) SPK_TRY(dadj.alloc((size_t)count * T.n + 1));
-    if (count)
-        k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
-                                                                         ctx->mp.p, dout.p,
-                                                                         out_adj ? dadj.p : nullptr);
-    SPK_HIP(hipGetLastError());
-    if (count) {
-        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
-        if (out_adj)
-            SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * T.n * 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    return SPK_OK;
-}
-
-extern "C" int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *cols, const double *const *adj_tables,
-                                    const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
-                                    double *out_adj) {
-    SPK_REQUIRE(ctx && cols && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID,
-                "spk_tf_apply_columns: 1..8 columns");
-    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply_columns: run spk_score first");
-    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply_columns: range");
-    SPK_HIP(hipSetDevice(ctx->device));
-    SPK_TRY(settle_gammas(ctx, nullptr));
-    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
-    DevBuf<int64_t> d0[8], d1[8];
-    TfApply T{};
-    T.n = n_tf_cols;
-    for (int c = 0; c < n_tf_cols; ++c) {
-        int64_t n0 = 0, n1 = 0;
-        SPK_TRY(column_ids(ctx, t0, cols[c], d0[c], &n0));
-        if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, cols[c], d1[c], &n1));
-        T.ids0[c] = d0[c].p;
-        T.ids1[c] = &t1 != &t0 ? d1[c].p : d0[c].p;
-    }
-    return tf_apply_dev(ctx, T, adj_tables, table_sizes, start, count, out_tf_mp, out_adj);
-}
-
-extern "C" int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0,
-                            const int64_t *const *ids_side1, const double *const *adj_tables,
-                            const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
-                            double *out_adj) {
-    SPK_REQUIRE(ctx && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID, "spk_tf_apply: 1..8 columns");
-    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply: run spk_score first");
-    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply: range");
-    SPK_HIP(hipSetDevice(ctx->device));
-    SPK_TRY(settle_gammas(ctx, nullptr));
-    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
-    DevBuf<int64_t> d0[8], d1[8];
-    DevBuf<double> dt[8], dout, dadj;
-    TfApply T{};
-    T.n = n_tf_cols;
-    for (int c = 0; c < n_tf_cols; ++c) {
-        SPK_TRY(d0[c].alloc((size_t)t0.n + 1));
-        SPK_TRY(d1[c].alloc((size_t)t1.n + 1));
-        SPK_TRY(dt[c].alloc((size_t)table_sizes[c] + 1));
-        SPK_HIP(hipMemcpyAsync(d0[c].p, ids_side0[c], (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
-        SPK_HIP(hipMemcpyAsync(d1[c].p, ids_side1[c], (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
-        if (table_sizes[c])
-            SPK_HIP(hipMemcpyAsync(dt[c].p, adj_tables[c], (size_t)table_sizes[c] * 8, hipMemcpyHostToDevice,
-                                   ctx->stream));
-        T.ids0[c] = d0[c].p;
-        T.ids1[c] = d1[c].p;
-        T.tab[c] = dt[c].p;
-        T.tab_n[c] = table_sizes[c];
-    }
-    SPK_TRY(dout.alloc((size_t)count + 1));
-    if (out_adj) SPK_TRY(dadj.alloc((size_t)count * n_tf_cols + 1));
-    if (count)
-        k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
-                                                                         ctx->mp.p, dout.p,
-                                                                         out_adj ? dadj.p : nullptr);
-    SPK_HIP(hipGetLastError());
-    if (count) {
-        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
-        if (out_adj)
-            SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * n_tf_cols * 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    return SPK_OK;
-}

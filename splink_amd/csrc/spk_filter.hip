@@ -146,13 +146,23 @@ __device__ __attribute__((always_inline)) inline bool implied(const FCommon &c, 
 // (m - t)/m <= 1, the head units for the Winkler prefix) is evaluated in fp32 with a 1e-5 margin, far
 // above its rounding; it is computed only when some lane of the wave needs it.
 template <int FP>
-__device__ __attribute__((always_inline)) inline void f_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
-                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
-                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
+struct JwData {
     uint4 a[FP], b[FP];
     uint2 ha[FP], hb[FP];
-    load16<FP>(A, J.c.p0, J.c.p1, ox, oy, a, b);
-    load8<FP>(A, J.h0, J.h1, 0, ox, oy, ha, hb);
+};
+template <int FP>
+__device__ __attribute__((always_inline)) inline void ld_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
+                                                            const uint32_t (&oy)[FP], JwData<FP> &d) {
+    load16<FP>(A, J.c.p0, J.c.p1, ox, oy, d.a, d.b);
+    load8<FP>(A, J.h0, J.h1, 0, ox, oy, d.ha, d.hb);
+}
+template <int FP>
+__device__ __attribute__((always_inline)) inline void ev_jw(const FJw &J, const JwData<FP> &d, const bool (&act)[FP],
+                                                            uint32_t (&acc)[FP], bool (&und)[FP]) {
+    const uint4(&a)[FP] = d.a;
+    const uint4(&b)[FP] = d.b;
+    const uint2(&ha)[FP] = d.ha;
+    const uint2(&hb)[FP] = d.hb;
     bool same[FP], nul[FP], zero[FP];
     int lf[FP], ls[FP];
     bool need = false;
@@ -196,15 +206,25 @@ __device__ __attribute__((always_inline)) inline void f_jw(const FiltArgs &A, co
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * J.c.stride;
     }
 }
+template <int FP>
+__device__ __attribute__((always_inline)) inline void f_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
+                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
+                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
+    JwData<FP> d;
+    ld_jw<FP>(A, J, ox, oy, d);
+    ev_jw<FP>(J, d, act, acc, und);
+}
 
 // ---- Levenshtein template column ---------------------------------------------------------------------
 template <int FP>
-__device__ __attribute__((always_inline)) inline void f_lev(const FiltArgs &A, const FLev &L, const int16_t *s_thr,
-                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
-                                                            const bool (&act)[FP], uint32_t (&acc)[FP],
-                                                            bool (&und)[FP]) {
+struct Data16 {
     uint4 a[FP], b[FP];
-    load16<FP>(A, L.c.p0, L.c.p1, ox, oy, a, b);
+};
+template <int FP>
+__device__ __attribute__((always_inline)) inline void ev_lev(const FLev &L, const int16_t *s_thr, const Data16<FP> &d,
+                                                             const bool (&act)[FP], uint32_t (&acc)[FP], bool (&und)[FP]) {
+    const uint4(&a)[FP] = d.a;
+    const uint4(&b)[FP] = d.b;
     bool same[FP], nul[FP], bmp[FP], u0[FP];
     int lo[FP], hi[FP], S[FP];
     bool need = false;
@@ -278,14 +298,26 @@ __device__ __attribute__((always_inline)) inline void f_lev(const FiltArgs &A, c
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * L.c.stride;
     }
 }
+template <int FP>
+__device__ __attribute__((always_inline)) inline void f_lev(const FiltArgs &A, const FLev &L, const int16_t *s_thr,
+                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
+                                                            const bool (&act)[FP], uint32_t (&acc)[FP],
+                                                            bool (&und)[FP]) {
+    Data16<FP> d;
+    load16<FP>(A, L.c.p0, L.c.p1, ox, oy, d.a, d.b);
+    ev_lev<FP>(L, s_thr, d, act, acc, und);
+}
 
 // ---- strict-equality template column -----------------------------------------------------------------
 template <int FP>
-__device__ __attribute__((always_inline)) inline void f_eq(const FiltArgs &A, const FEq &E, const uint32_t (&ox)[FP],
-                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
-                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
+struct Data8 {
     uint2 a[FP], b[FP];
-    load8<FP>(A, E.c.p0, E.c.p1, E.c.in, ox, oy, a, b);
+};
+template <int FP>
+__device__ __attribute__((always_inline)) inline void ev_eq(const FEq &E, const Data8<FP> &d, const bool (&act)[FP],
+                                                            uint32_t (&acc)[FP], bool (&und)[FP]) {
+    const uint2(&a)[FP] = d.a;
+    const uint2(&b)[FP] = d.b;
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
         const bool same = a[u].x == b[u].x && a[u].y == b[u].y;
@@ -294,6 +326,14 @@ __device__ __attribute__((always_inline)) inline void f_eq(const FiltArgs &A, co
         const int level = nul ? E.c.null_level : (same ? E.lv_same : E.lv_diff);
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * E.c.stride;
     }
+}
+template <int FP>
+__device__ __attribute__((always_inline)) inline void f_eq(const FiltArgs &A, const FEq &E, const uint32_t (&ox)[FP],
+                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
+                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
+    Data8<FP> d;
+    load8<FP>(A, E.c.p0, E.c.p1, E.c.in, ox, oy, d.a, d.b);
+    ev_eq<FP>(E, d, act, acc, und);
 }
 
 // ---- numeric template column --------------------------------------------------------------------------
@@ -403,6 +443,109 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
         A.region_count[(int64_t)A.eq[t - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[t];
     else if (t >= FJ_MAX + FL_MAX + FE_MAX && t < FJ_MAX + FL_MAX + FE_MAX + A.nn)
         A.region_count[(int64_t)A.num[t - FJ_MAX - FL_MAX - FE_MAX].c.k * A.n_regions + slot] = 0;
+}
+
+// The same filter for a fixed column layout (NJ Jaro-Winkler, NL Levenshtein, NE equality columns, no
+// numeric ones): every column's loads for the lane's FP pairs are issued before any column is
+// evaluated, so one iteration pays one memory round trip instead of one per column.
+template <int NJ, int NL, int NE, int FP, int MINW, bool C32>
+__global__ __launch_bounds__(F_THREADS, MINW) void k_filter_sig(const FiltArgs A) {
+    __shared__ unsigned int s_cnt[N_FCOLS];
+    extern __shared__ int16_t s_thr[];
+    if (threadIdx.x < N_FCOLS) s_cnt[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
+    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
+    constexpr int SPAN = 64 * FP;
+    constexpr int STEP = (F_THREADS / 64) * SPAN;
+    const uint32_t end = (uint32_t)r1;
+    uint32_t base = (uint32_t)r0 + (uint32_t)(threadIdx.x >> 6) * SPAN;
+    int32_t nx[FP], ny[FP];
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        const uint32_t q = base + u * 64 + lane;
+        nx[u] = q < end ? A.pl[q] : 0;
+        ny[u] = q < end ? A.pr[q] : 0;
+    }
+    for (; base < end; base += STEP) {  // wave-uniform
+        uint32_t p[FP], ox[FP], oy[FP], acc[FP];
+        bool act[FP], und[FP];
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            p[u] = base + u * 64 + lane;
+            act[u] = p[u] < end;
+            ox[u] = (uint32_t)nx[u] << 4;
+            oy[u] = (uint32_t)ny[u] << 4;
+            acc[u] = 0;
+            const uint32_t q = p[u] + STEP;
+            nx[u] = q < end ? A.pl[q] : 0;
+            ny[u] = q < end ? A.pr[q] : 0;
+        }
+        JwData<FP> dj[NJ > 0 ? NJ : 1];
+        Data16<FP> dl[NL > 0 ? NL : 1];
+        Data8<FP> de[NE > 0 ? NE : 1];
+        bool ij[NJ > 0 ? NJ : 1], il[NL > 0 ? NL : 1], ie[NE > 0 ? NE : 1];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            ij[j] = implied(A.jw[j].c, base, SPAN);
+            if (!ij[j]) ld_jw<FP>(A, A.jw[j], ox, oy, dj[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            il[j] = implied(A.lev[j].c, base, SPAN);
+            if (!il[j]) load16<FP>(A, A.lev[j].c.p0, A.lev[j].c.p1, ox, oy, dl[j].a, dl[j].b);
+        }
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+            ie[j] = implied(A.eq[j].c, base, SPAN);
+            if (!ie[j]) load8<FP>(A, A.eq[j].c.p0, A.eq[j].c.p1, A.eq[j].c.in, ox, oy, de[j].a, de[j].b);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            if (ij[j]) {
+#pragma unroll
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? A.jw[j].c.imp_add : 0u;
+                continue;
+            }
+            ev_jw<FP>(A.jw[j], dj[j], act, acc, und);
+            append<FP>(A, A.jw[j].c, r0, &s_cnt[j], und, p);
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            if (il[j]) {
+#pragma unroll
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? A.lev[j].c.imp_add : 0u;
+                continue;
+            }
+            ev_lev<FP>(A.lev[j], s_thr, dl[j], act, acc, und);
+            append<FP>(A, A.lev[j].c, r0, &s_cnt[FJ_MAX + j], und, p);
+        }
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+            if (ie[j]) {
+#pragma unroll
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? A.eq[j].c.imp_add : 0u;
+                continue;
+            }
+            ev_eq<FP>(A.eq[j], de[j], act, acc, und);
+            if (A.eq[j].c.und_same) append<FP>(A, A.eq[j].c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
+        }
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            if (!act[u]) continue;
+            if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
+            else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
+        }
+    }
+    __syncthreads();
+    const int64_t slot = A.region_base + blockIdx.x;
+    const int t = threadIdx.x;
+    if (t < NJ) A.region_count[(int64_t)A.jw[t].c.k * A.n_regions + slot] = s_cnt[t];
+    else if (t >= FJ_MAX && t < FJ_MAX + NL) A.region_count[(int64_t)A.lev[t - FJ_MAX].c.k * A.n_regions + slot] = s_cnt[t];
+    else if (t >= FJ_MAX + FL_MAX && t < FJ_MAX + FL_MAX + NE)
+        A.region_count[(int64_t)A.eq[t - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[t];
 }
 
 // ---- host: the per-column decision constants --------------------------------------------------------------
@@ -554,6 +697,13 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     }
     const unsigned g = (unsigned)(region_hi - region_lo);
     const size_t shm = (size_t)A.n_thr * sizeof(int16_t);
+#ifdef SPK_FILTER_SIG
+    if (A.code16 && F.nj == 2 && F.nl == 1 && F.ne == 2 && F.nn == 0) {
+        k_filter_sig<2, 1, 2, SPK_FILTER_SIG, SPK_FILTER_SIG_W, false><<<g, F_THREADS, shm, stream>>>(F);
+        SPK_HIP(hipGetLastError());
+        return SPK_OK;
+    }
+#endif
     if (A.code16) k_filter<3, 5, false><<<g, F_THREADS, shm, stream>>>(F);
     else k_filter<3, 5, true><<<g, F_THREADS, shm, stream>>>(F);
     SPK_HIP(hipGetLastError());

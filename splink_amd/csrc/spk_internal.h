@@ -291,7 +291,7 @@ struct spk_ctx {
     // EM state
     spk::DevBuf<uint64_t> hist;
     spk::DevBuf<double> mpat, llpat, cpat, stats, mu;  // per pattern: mp, ln(...), count; statistics; m / u
-    spk::DevBuf<uint64_t> hist_acc;     // spk_em_iteration's accumulation histogram (kept zero between launches)
+    spk::DevBuf<uint32_t> hist_part;    // k_em_iter's per-workgroup pattern counts (rows of part_stride)
     spk::DevBuf<unsigned int> em_ticket;  // its last-workgroup ticket (kept zero between launches)
     double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;

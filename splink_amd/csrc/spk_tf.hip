@@ -1,0 +1,368 @@
+// Term-frequency adjustment (replaces term_frequencies.py:49-117: the per-value GROUP BY of the match
+// probability over pairs with equal values, the broadcast join of the adjustments and the Bayes
+// combination).
+//
+// The per-value sums are exact and order-free, so they are bit-identical for any grid, any run and any
+// number of ranks: mp depends only on the comparison pattern, so Σ_{pairs with value v} mp =
+// Σ_p count(v, p) · mp(p).  The qualifying pairs' keys (v, pattern) are radix-sorted and run-length
+// encoded (integer counts), and each run adds count · mp(p) to value v's accumulator in fixed point:
+// SPK_TF_LIMBS int64 limbs of 20 bits (limb 0 the integer part, limb j the bits 2^-20j .. 2^-20(j-1)+1),
+// mp truncated below 2^-260.  Integer adds are exact, so the device atomics' order, the shard of pairs
+// and the ranks' all-reduce (int64 sum) do not change the result; one conversion to double at the end
+// (spk_tf_limbs_to_sum) gives every caller the same value.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_run_length_encode.hpp>
+
+#include "spk_internal.h"
+
+namespace spk {
+
+constexpr int TF_LIMBS = SPK_TF_LIMBS;
+constexpr int TF_BITS = 20;
+constexpr unsigned long long TF_NONE = ~0ull;  // key of a pair that does not qualify
+
+// key = value << 32 | code for pairs with equal, non-NULL values and a non-NULL mp, else TF_NONE
+template <typename CodeT>
+__global__ void k_tf_keys(int64_t P, const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
+                          const int64_t *__restrict__ ids0, const int64_t *__restrict__ ids1, const CodeT *__restrict__ codes,
+                          const double *__restrict__ mpat, int64_t n_values, unsigned long long *__restrict__ keys) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int64_t a = ids0[pl[p]], b = ids1[pr[p]];
+    const uint32_t c = (uint32_t)codes[p];
+    const bool ok = a >= 0 && a == b && a < n_values && !isnan(mpat[c]);
+    keys[p] = ok ? (((unsigned long long)a << 32) | c) : TF_NONE;
+}
+
+// The fixed-point limbs of x in [0, 1]: x = Σ_j limb_j 2^(-20 j), truncated below 2^-260.
+__device__ inline void tf_limbs(double x, uint32_t (&limb)[TF_LIMBS]) {
+#pragma unroll
+    for (int j = 0; j < TF_LIMBS; ++j) limb[j] = 0;
+    if (!(x > 0.0)) return;
+    if (x >= 1.0) {
+        limb[0] = 1;
+        return;
+    }
+    const uint64_t bits = (uint64_t)__double_as_longlong(x);
+    const int ex = (int)((bits >> 52) & 0x7FF);
+    const uint64_t M = (bits & ((1ull << 52) - 1)) | (ex ? (1ull << 52) : 0ull);
+    // x = M 2^(e - 1075) (subnormals: e = 1); bit b of F = x 2^260 is bit b - s of M
+    const int s = (ex ? ex : 1) - 1075 + TF_BITS * (TF_LIMBS - 1);
+#pragma unroll
+    for (int j = 1; j < TF_LIMBS; ++j) {
+        const int lo = TF_BITS * (TF_LIMBS - 1 - j);  // F's bit of limb j's lowest bit
+        const int sh = lo - s;
+        uint64_t v;
+        if (sh >= 0) v = sh >= 64 ? 0ull : (M >> sh);
+        else v = -sh >= 64 ? 0ull : (M << (-sh));
+        limb[j] = (uint32_t)(v & ((1u << TF_BITS) - 1));
+    }
+}
+
+// One run of equal keys: its count times the pattern's mp, limb by limb, into the value's accumulator.
+__global__ void k_tf_runs(const unsigned long long *__restrict__ keys, const unsigned int *__restrict__ counts,
+                          const unsigned int *__restrict__ n_runs, const double *__restrict__ mpat,
+                          unsigned long long *__restrict__ acc, unsigned long long *__restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)*n_runs) return;
+    const unsigned long long k = keys[i];
+    if (k == TF_NONE) return;
+    const int64_t v = (int64_t)(k >> 32);
+    const uint32_t c = (uint32_t)(k & 0xFFFFFFFFu);
+    const unsigned long long n = counts[i];
+    uint32_t limb[TF_LIMBS];
+    tf_limbs(mpat[c], limb);
+#pragma unroll
+    for (int j = 0; j < TF_LIMBS; ++j)
+        if (limb[j]) atomicAdd(&acc[v * TF_LIMBS + j], n * (unsigned long long)limb[j]);
+    atomicAdd(&cnt[v], n);
+}
+
+// Exact per-value sums over the current pairs, value ids per row on the device (d0 side 0, d1 side 1).
+static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int64_t *out_limbs,
+                    int64_t *out_count) {
+    SPK_REQUIRE(ctx->mpat_valid && ctx->mpat.p, SPK_E_STATE, "tf: run spk_score first (mp per pattern)");
+    SPK_REQUIRE(n_values < ((int64_t)1 << 31), SPK_E_LIMIT, "tf: more than 2^31 distinct values");
+    const int64_t P = ctx->n_pairs;
+    DevBuf<unsigned long long> acc, cnt;
+    SPK_TRY(acc.alloc((size_t)n_values * TF_LIMBS + 1));
+    SPK_TRY(cnt.alloc((size_t)n_values + 1));
+    SPK_HIP(hipMemsetAsync(acc.p, 0, ((size_t)n_values * TF_LIMBS + 1) * 8, ctx->stream));
+    SPK_HIP(hipMemsetAsync(cnt.p, 0, ((size_t)n_values + 1) * 8, ctx->stream));
+    // the sort and the run counts work on uint32 lengths: chunks of at most 2^30 pairs
+    const int64_t CH = (int64_t)1 << 30;
+    DevBuf<unsigned long long> k_in, k_out, uniq;
+    DevBuf<unsigned int> runs, n_runs;
+    DevBuf<uint8_t> tmp;
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(P, 1), CH);
+    SPK_TRY(k_in.alloc((size_t)cap));
+    SPK_TRY(k_out.alloc((size_t)cap));
+    SPK_TRY(uniq.alloc((size_t)cap));
+    SPK_TRY(runs.alloc((size_t)cap));
+    SPK_TRY(n_runs.alloc(1));
+    for (int64_t c0 = 0; c0 < P; c0 += CH) {
+        const int64_t n = std::min<int64_t>(CH, P - c0);
+        const unsigned g = (unsigned)((n + 255) / 256);
+        if (ctx->code_bytes == 2)
+            k_tf_keys<uint16_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
+                                                           reinterpret_cast<const uint16_t *>(ctx->codes.p) + c0,
+                                                           ctx->mpat.p, n_values, k_in.p);
+        else
+            k_tf_keys<uint32_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
+                                                           reinterpret_cast<const uint32_t *>(ctx->codes.p) + c0,
+                                                           ctx->mpat.p, n_values, k_in.p);
+        SPK_HIP(hipGetLastError());
+        size_t bytes = 0, b2 = 0;
+        SPK_HIP(rocprim::radix_sort_keys(nullptr, bytes, k_in.p, k_out.p, (size_t)n, 0, 64, ctx->stream));
+        SPK_HIP(rocprim::run_length_encode(nullptr, b2, k_out.p, (size_t)n, uniq.p, runs.p, n_runs.p, ctx->stream));
+        SPK_TRY(tmp.alloc(std::max(bytes, b2) + 1));
+        SPK_HIP(rocprim::radix_sort_keys(tmp.p, bytes, k_in.p, k_out.p, (size_t)n, 0, 64, ctx->stream));
+        SPK_HIP(rocprim::run_length_encode(tmp.p, b2, k_out.p, (size_t)n, uniq.p, runs.p, n_runs.p, ctx->stream));
+        k_tf_runs<<<g, 256, 0, ctx->stream>>>(uniq.p, runs.p, n_runs.p, ctx->mpat.p, acc.p, cnt.p);
+        SPK_HIP(hipGetLastError());
+    }
+    if (n_values) {
+        SPK_HIP(hipMemcpyAsync(out_limbs, acc.p, (size_t)n_values * TF_LIMBS * 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(out_count, cnt.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+struct TfApply {
+    int n;
+    const int64_t *ids0[8];
+    const int64_t *ids1[8];
+    const double *tab[8];
+    int64_t tab_n[8];
+};
+
+// bayes(mp, adj...) = Πp / (Πp + Π(1-p)) (term_frequencies.py:21-46, :98-117)
+__global__ void k_tf_apply(TfApply T, int64_t start, int64_t n, const int32_t *__restrict__ pl,
+                           const int32_t *__restrict__ pr, const double *__restrict__ mp, double *__restrict__ out,
+                           double *__restrict__ out_adj) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t p = start + i;
+    double m = mp[p];
+    double adj[8];
+    for (int c = 0; c < T.n; ++c) {
+        int64_t a = T.ids0[c][pl[p]], b = T.ids1[c][pr[p]];
+        double v = 0.5;
+        if (a >= 0 && a == b && a < T.tab_n[c]) {
+            double x = T.tab[c][a];
+            if (!isnan(x)) v = x;
+        }
+        adj[c] = v;
+        if (out_adj) out_adj[i * T.n + c] = v;
+    }
+    if (isnan(m)) {
+        out[i] = NAN;
+        return;
+    }
+    double a = m, b = 1.0 - m;
+    for (int c = 0; c < T.n; ++c) a = a * adj[c];
+    for (int c = 0; c < T.n; ++c) b = b * (1.0 - adj[c]);
+    double d = a + b;
+    out[i] = d == 0.0 ? NAN : a / d;
+}
+
+
+__global__ void k_ids_from_meta(int64_t n, const RecMeta *__restrict__ meta, int64_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = meta[i].len16 < 0 ? -1 : (int64_t)meta[i].key;
+}
+
+static int column_ids(spk_ctx *ctx, Table &t, int col, DevBuf<int64_t> &out, int64_t *n_ids) {
+    SPK_REQUIRE(col >= 0 && col < (int)t.cols.size() && t.cols[col] && t.cols[col]->kind == COL_STR &&
+                    t.cols[col]->n_ids >= 0,
+                SPK_E_STATE, "tf: the column carries no device dictionary ids (spk_table_add_raw_utf8)");
+    *n_ids = t.cols[col]->n_ids;
+    SPK_TRY(out.alloc((size_t)t.n + 1));
+    if (t.n) k_ids_from_meta<<<(unsigned)((t.n + 255) / 256), 256, 0, ctx->stream>>>(t.n, t.cols[col]->meta.p, out.p);
+    SPK_HIP(hipGetLastError());
+    return SPK_OK;
+}
+
+
+}  // namespace spk
+
+using namespace spk;
+
+extern "C" int spk_tf_limbs_to_sum(int64_t n_values, const int64_t *limbs, double *out_sum) {
+    SPK_REQUIRE(n_values >= 0 && (n_values == 0 || (limbs && out_sum)), SPK_E_INVALID, "spk_tf_limbs_to_sum: bad args");
+    for (int64_t v = 0; v < n_values; ++v) {
+        int64_t l[TF_LIMBS];
+        for (int j = 0; j < TF_LIMBS; ++j) l[j] = limbs[v * TF_LIMBS + j];
+        for (int j = TF_LIMBS - 1; j > 0; --j) {  // carries: every fraction limb back below 2^20
+            l[j - 1] += l[j] >> TF_BITS;
+            l[j] &= (1 << TF_BITS) - 1;
+        }
+        double acc = 0.0;
+        for (int j = TF_LIMBS - 1; j > 0; --j) acc = (acc + (double)l[j]) * std::ldexp(1.0, -TF_BITS);
+        out_sum[v] = acc + (double)l[0];
+    }
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_accumulate_exact(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
+                                       int64_t *out_limbs, int64_t *out_count) {
+    SPK_REQUIRE(ctx && ids_side0 && ids_side1 && (n_values == 0 || (out_limbs && out_count)) && n_values >= 0,
+                SPK_E_INVALID, "spk_tf_accumulate_exact: bad args");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->codes_valid, SPK_E_STATE, "spk_tf_accumulate_exact: run spk_score first");
+    SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0, d1;
+    SPK_TRY(d0.alloc((size_t)t0.n + 1));
+    SPK_TRY(d1.alloc((size_t)t1.n + 1));
+    if (t0.n) SPK_HIP(hipMemcpyAsync(d0.p, ids_side0, (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (t1.n) SPK_HIP(hipMemcpyAsync(d1.p, ids_side1, (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
+    return tf_exact(ctx, n_values, d0.p, d1.p, out_limbs, out_count);
+}
+
+extern "C" int spk_tf_accumulate_column_exact(spk_ctx *ctx, int col, int64_t n_values, int64_t *out_limbs,
+                                              int64_t *out_count) {
+    SPK_REQUIRE(ctx && n_values >= 0 && (n_values == 0 || (out_limbs && out_count)), SPK_E_INVALID,
+                "spk_tf_accumulate_column_exact: bad args");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->codes_valid, SPK_E_STATE, "spk_tf_accumulate_column_exact: run spk_score first");
+    SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0, d1;
+    int64_t n0 = 0, n1 = 0;
+    SPK_TRY(column_ids(ctx, t0, col, d0, &n0));
+    if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, col, d1, &n1));
+    SPK_REQUIRE(n_values == n0, SPK_E_INVALID, "spk_tf_accumulate_column_exact: n_values is not the column's value count");
+    return tf_exact(ctx, n_values, d0.p, &t1 != &t0 ? d1.p : d0.p, out_limbs, out_count);
+}
+
+// The double forms: the exact sums of this context's pairs, converted (the same values the exact forms
+// give after a one-rank all-reduce).
+static int tf_sums(int64_t n_values, const std::vector<int64_t> &limbs, double *out_sum) {
+    return spk_tf_limbs_to_sum(n_values, limbs.data(), out_sum);
+}
+
+extern "C" int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
+                                 double *out_sum, int64_t *out_count) {
+    SPK_REQUIRE(n_values >= 0 && (n_values == 0 || (out_sum && out_count)), SPK_E_INVALID, "spk_tf_accumulate: bad args");
+    std::vector<int64_t> limbs((size_t)n_values * TF_LIMBS + 1);
+    SPK_TRY(spk_tf_accumulate_exact(ctx, n_values, ids_side0, ids_side1, limbs.data(), out_count));
+    return tf_sums(n_values, limbs, out_sum);
+}
+
+extern "C" int spk_tf_accumulate_column(spk_ctx *ctx, int col, int64_t n_values, double *out_sum, int64_t *out_count) {
+    SPK_REQUIRE(n_values >= 0 && (n_values == 0 || (out_sum && out_count)), SPK_E_INVALID,
+                "spk_tf_accumulate_column: bad args");
+    std::vector<int64_t> limbs((size_t)n_values * TF_LIMBS + 1);
+    SPK_TRY(spk_tf_accumulate_column_exact(ctx, col, n_values, limbs.data(), out_count));
+    return tf_sums(n_values, limbs, out_sum);
+}
+
+extern "C" int spk_tf_column_values(spk_ctx *ctx, int col, int64_t *out_n_values) {
+    SPK_REQUIRE(ctx && out_n_values, SPK_E_INVALID, "spk_tf_column_values: null arg");
+    Table &t = ctx->table[0];
+    SPK_REQUIRE(col >= 0 && col < (int)t.cols.size() && t.cols[col] && t.cols[col]->kind == COL_STR &&
+                    t.cols[col]->n_ids >= 0,
+                SPK_E_STATE, "spk_tf_column_values: the column carries no device dictionary ids");
+    *out_n_values = t.cols[col]->n_ids;
+    return SPK_OK;
+}
+
+static int tf_apply_dev(spk_ctx *ctx, TfApply &T, const double *const *adj_tables, const int64_t *table_sizes,
+                        int64_t start, int64_t count, double *out_tf_mp, double *out_adj) {
+    DevBuf<double> dt[8], dout, dadj;
+    for (int c = 0; c < T.n; ++c) {
+        SPK_TRY(dt[c].alloc((size_t)table_sizes[c] + 1));
+        if (table_sizes[c])
+            SPK_HIP(hipMemcpyAsync(dt[c].p, adj_tables[c], (size_t)table_sizes[c] * 8, hipMemcpyHostToDevice,
+                                   ctx->stream));
+        T.tab[c] = dt[c].p;
+        T.tab_n[c] = table_sizes[c];
+    }
+    SPK_TRY(dout.alloc((size_t)count + 1));
+    if (out_adj) SPK_TRY(dadj.alloc((size_t)count * T.n + 1));
+    if (count)
+        k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
+                                                                         ctx->mp.p, dout.p,
+                                                                         out_adj ? dadj.p : nullptr);
+    SPK_HIP(hipGetLastError());
+    if (count) {
+        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (out_adj)
+            SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * T.n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *cols, const double *const *adj_tables,
+                                    const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
+                                    double *out_adj) {
+    SPK_REQUIRE(ctx && cols && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID,
+                "spk_tf_apply_columns: 1..8 columns");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply_columns: run spk_score first");
+    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply_columns: range");
+    SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0[8], d1[8];
+    TfApply T{};
+    T.n = n_tf_cols;
+    for (int c = 0; c < n_tf_cols; ++c) {
+        int64_t n0 = 0, n1 = 0;
+        SPK_TRY(column_ids(ctx, t0, cols[c], d0[c], &n0));
+        if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, cols[c], d1[c], &n1));
+        T.ids0[c] = d0[c].p;
+        T.ids1[c] = &t1 != &t0 ? d1[c].p : d0[c].p;
+    }
+    return tf_apply_dev(ctx, T, adj_tables, table_sizes, start, count, out_tf_mp, out_adj);
+}
+
+extern "C" int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0,
+                            const int64_t *const *ids_side1, const double *const *adj_tables,
+                            const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
+                            double *out_adj) {
+    SPK_REQUIRE(ctx && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID, "spk_tf_apply: 1..8 columns");
+    SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply: run spk_score first");
+    SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply: range");
+    SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    DevBuf<int64_t> d0[8], d1[8];
+    DevBuf<double> dt[8], dout, dadj;
+    TfApply T{};
+    T.n = n_tf_cols;
+    for (int c = 0; c < n_tf_cols; ++c) {
+        SPK_TRY(d0[c].alloc((size_t)t0.n + 1));
+        SPK_TRY(d1[c].alloc((size_t)t1.n + 1));
+        SPK_TRY(dt[c].alloc((size_t)table_sizes[c] + 1));
+        SPK_HIP(hipMemcpyAsync(d0[c].p, ids_side0[c], (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(d1[c].p, ids_side1[c], (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (table_sizes[c])
+            SPK_HIP(hipMemcpyAsync(dt[c].p, adj_tables[c], (size_t)table_sizes[c] * 8, hipMemcpyHostToDevice,
+                                   ctx->stream));
+        T.ids0[c] = d0[c].p;
+        T.ids1[c] = d1[c].p;
+        T.tab[c] = dt[c].p;
+        T.tab_n[c] = table_sizes[c];
+    }
+    SPK_TRY(dout.alloc((size_t)count + 1));
+    if (out_adj) SPK_TRY(dadj.alloc((size_t)count * n_tf_cols + 1));
+    if (count)
+        k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
+                                                                         ctx->mp.p, dout.p,
+                                                                         out_adj ? dadj.p : nullptr);
+    SPK_HIP(hipGetLastError());
+    if (count) {
+        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (out_adj)
+            SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * n_tf_cols * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}

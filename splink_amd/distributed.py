@@ -27,10 +27,11 @@ def shard() -> tuple:
     return dist.get_rank(), dist.get_world_size()
 
 
-def allreduce_histogram_(hist):
-    """In-place sum of a pattern histogram (int64 tensor, device or host) over all ranks."""
+def allreduce_histogram_(hist, force: bool = False):
+    """In-place sum of a pattern histogram (int64 tensor, device or host) over all ranks.  force: run the
+    collective even with one rank (tests exercise the RCCL path on a one-GPU box)."""
     dist = _dist()
-    if dist is not None and dist.get_world_size() > 1:
+    if dist is not None and (dist.get_world_size() > 1 or force):
         if hist.is_cuda and dist.get_backend() == "gloo":
             # gloo rehearsal of the multi-GPU path (several ranks on one device): host staging
             h = hist.cpu()
@@ -41,7 +42,7 @@ def allreduce_histogram_(hist):
     return hist
 
 
-def allreduce_host_(arr):
+def allreduce_host_(arr, force: bool = False):
     """In-place sum over all ranks of a host numpy array (float64 / int64), e.g. the per-value
     (Σmp, count) tables of the term-frequency adjustment (term_frequencies.py:49-65 groups over all
     pairs, which are sharded here).  RCCL needs device tensors, so under `nccl` the array is staged
@@ -49,7 +50,7 @@ def allreduce_host_(arr):
     import numpy as np
     import torch
     dist = _dist()
-    if dist is None or dist.get_world_size() <= 1 or arr.size == 0:
+    if dist is None or (dist.get_world_size() <= 1 and not force) or arr.size == 0:
         return arr
     t = torch.from_numpy(np.ascontiguousarray(arr))
     if dist.get_backend() != "gloo":

@@ -118,6 +118,7 @@ class Job:
         self.codes_token = None
         self.code_meta = None
         self.timings = {}
+        self.force_reduce = False  # tests: the multi-GPU EM path (histogram -> all-reduce -> finalize) at one rank
         self._set_rank()
 
     @classmethod
@@ -386,7 +387,7 @@ class Job:
         m, u = self.flat_tables(level_probs)
         lam_d, one_minus = float(lam), float(1 - lam)
         n_stats = N_HEAD + 4 * sum(L + 1 for L in n_levels)
-        if self.reduces_across_ranks():
+        if self.reduces_across_ranks() or self.force_reduce:
             import torch
             n_pat = self.ctx.n_patterns()
             hist = getattr(self, "_hist_dev", None)
@@ -396,7 +397,7 @@ class Job:
                 torch.cuda.synchronize(self.device)
                 self._hist_dev = hist
             self.ctx.em_histogram(hist.data_ptr())  # zeroes, fills and synchronises its stream
-            D.allreduce_histogram_(hist)
+            D.allreduce_histogram_(hist, force=self.force_reduce)
             torch.cuda.synchronize(self.device)
             return self.ctx.em_finalize(hist.data_ptr(), lam_d, one_minus, m, u, n_stats)
         return self.ctx.em_iteration(lam_d, one_minus, m, u, n_stats)

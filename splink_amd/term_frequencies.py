@@ -4,8 +4,9 @@ Per tf column c: over pairs whose c_l and c_r are equal and non-NULL, the mean m
 probability per value (adj_lambda, :49-65) is Bayes-combined with 1-λ; pairs without a
 lookup value get 0.5 (:68-95); tf_adjusted_match_prob = bayes(mp, adj_c1, ...) (:98-117).
 The per-value sums and the per-pair Bayes combination run on the GPU
-(spk_tf_accumulate / spk_tf_apply); the per-value lookup arithmetic is a handful of
-operations per distinct value.
+(spk_tf_accumulate_exact / spk_tf_apply): the sums are exact fixed-point accumulators, so ranks
+holding shards of the pairs all-reduce them as integers and every run and rank count gives
+bit-identical adjustments; the per-value lookup arithmetic is a handful of operations per value.
 """
 import warnings
 from collections import OrderedDict
@@ -13,6 +14,7 @@ from collections import OrderedDict
 import numpy as np
 import pandas as pd
 
+from . import _native as N
 from . import distributed as D
 from . import table as T
 from .check_types import check_types
@@ -76,10 +78,11 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
     dev_cols = [job._col_index.get((c, "str")) for c in tf_cols]
     on_device = all(i is not None for i in dev_cols)
     ids0_list, ids1_list, tables = [], [], []
+    shared = job.reduces_across_ranks()  # the reference groups over ALL pairs (:49-65); ranks hold shards
     for c, col in zip(tf_cols, dev_cols):
         if on_device:
             n_values = job.ctx.tf_column_values(col)
-            sums, counts = job.ctx.tf_accumulate_column(col, n_values)
+            limbs, counts = job.ctx.tf_accumulate_column_exact(col, n_values)
         else:
             sides = (0, 1) if job.link_type == "link_only" else (0,)
             vals = [pd.Series([None if T.is_null_scalar(v) else v for v in job.host_values(s, c).tolist()],
@@ -87,13 +90,14 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
             codes, n_values = T.factorize_joint(vals)
             ids0 = codes[0]
             ids1 = codes[1] if len(codes) > 1 else codes[0]
-            sums, counts = job.ctx.tf_accumulate(n_values, ids0, ids1)
+            limbs, counts = job.ctx.tf_accumulate_exact(n_values, ids0, ids1)
             ids0_list.append(ids0)
             ids1_list.append(ids1)
-        if job.reduces_across_ranks():
-            # the reference groups over ALL pairs (:49-65); each rank holds one shard of them
-            D.allreduce_host_(sums)
+        if shared:
+            # exact fixed-point sums and integer counts: the all-reduce gives every rank the one-GPU result
+            D.allreduce_host_(limbs)
             D.allreduce_host_(counts)
+        sums = N.tf_limbs_to_sum(limbs)
         with np.errstate(invalid="ignore", divide="ignore"):
             adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
         tables.append(_bayes_pair(adj_lambda, one_minus))

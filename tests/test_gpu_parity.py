@@ -760,3 +760,27 @@ def test_sharded_link_tf_matches_reference(amd, tmp_path):
         cols = ranks[0][f"{key}_columns"]
         both = pd.concat([pd.DataFrame(rk[key])[cols] for rk in ranks], ignore_index=True)
         compare_frames(both, g[key], g[f"{key}_columns"])
+
+
+def test_tf_bit_identical_across_runs_and_ranks(amd, tmp_path):
+    """term_frequencies.py:49-65 sums mp per value over all pairs.  The device sums are exact fixed-point
+    accumulators (integer adds in any order, all-reduced as integers), so tf_adjusted_match_prob is bit
+    for bit the same in repeated runs and whether the pairs sit on one rank or are sharded over two."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import gpu_dist_worker as W
+    one = W.run_link_tf()
+    again = W.run_link_tf()
+    assert one["df_tf"]["tf_adjusted_match_prob"] == again["df_tf"]["tf_adjusted_match_prob"]
+    ranks = _two_ranks(tmp_path, "link_tf")
+    cols = one["df_tf_columns"]
+    both = pd.concat([pd.DataFrame(rk["df_tf"])[cols] for rk in ranks], ignore_index=True)
+    single = pd.DataFrame(one["df_tf"])[cols]
+    key = ["unique_id_l", "unique_id_r"]
+    both = both.sort_values(key).reset_index(drop=True)
+    single = single.sort_values(key).reset_index(drop=True)
+    assert both[key].equals(single[key])
+    a = both["tf_adjusted_match_prob"].to_numpy(dtype=np.float64)
+    b = single["tf_adjusted_match_prob"].to_numpy(dtype=np.float64)
+    assert np.array_equal(a, b, equal_nan=True)

@@ -108,3 +108,49 @@ def test_cfg2_full_size(amd):
 def test_cfg5_columns_full_size(amd):
     job = run_full(amd, with_address=True, iters=3)
     assert job.n_pairs > 40_000_000
+
+
+def test_cfg4_shard_full_size(amd):
+    """BASELINE configs[3] at one GPU's share: a 20M-record dedupe (blocking surname | dob: 6.2e9 candidate
+    ordinals, past 2^31) whose ordinal space is split over 8 GPUs; this process is rank 0 and generates only
+    its slice (~770M pairs), as each rank of the 8-GPU job does (blocking.py:95-160, int64 ordinals).  A
+    strided sample of 2M comparison vectors is bit-exact against oracle.template_gammas, and 10 EM
+    iterations of λ / m / u plus every pair's match_probability agree with oracle.em_iterate at 1e-9."""
+    from splink_amd.engine import Job, m_step_rows
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    iters = 10
+    df = make_records(20_000_000, surname_vocab=300_000, arrow=True)[["unique_id"] + COLS]
+    params = Params(cfg_settings(4, max_iterations=iters), amd)
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0, shard=(0, 8))
+    job.block(st["blocking_rules"])
+    assert job.n_candidates > 2 ** 31 and job.n_pairs > 500_000_000
+    job.gammas(st)
+    l, r = job.pair_rows()
+    step = max(1, job.n_pairs // 2_000_000)
+    idx = np.arange(0, job.n_pairs, step)
+    sl, sr = l[idx], r[idx]
+    rows, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
+    sub = job.tables[0].take(rows)
+    ocols = [orc.StrCol(sub[c].tolist()) for c in COLS]
+    ref = orc.template_gammas(SPECS[:len(COLS)], ocols, ocols, inv[:len(sl)].astype(np.int32),
+                              inv[len(sl):].astype(np.int32))
+    gam = job.gammas_host()
+    bad = np.nonzero((gam[idx] != ref).any(axis=1))[0]
+    assert len(bad) == 0, (len(bad), idx[bad[:5]])
+    del ref, ocols, sub, l, r
+    names, nlev = job.code_meta
+    lam0, lp0 = params.params["λ"], params._level_probabilities()
+    hist_o, mp_o = orc.em_iterate(gam, nlev, lam0, [m for m, _ in lp0], [u for _, u in lp0], iters, 1e-300)
+    del gam
+    for lam_o, m_o, u_o in hist_o:
+        stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        new_lambda, rows_ = m_step_rows(stats, names, nlev)
+        params._update_params(new_lambda, rows_)
+        assert rel_close(params.params["λ"], lam_o)
+        for k, (m, u) in enumerate(params._level_probabilities()):
+            assert all(rel_close(a, b) for a, b in zip(m, m_o[k])), (k, m, m_o[k])
+            assert all(rel_close(a, b) for a, b in zip(u, u_o[k])), (k, u, u_o[k])
+    mp = job.score(params.params["λ"], params._level_probabilities())
+    assert np.allclose(mp, mp_o, rtol=1e-9, atol=0, equal_nan=True)
