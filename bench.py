@@ -8,8 +8,9 @@ ranks (weak scaling: ~46M pairs per GPU), one RCCL all-reduce of the comparison-
 histogram per EM iteration.
 
 One timed step = the comparison-vector pass over every pair resident in HBM (spk_gammas) +
-one E+M iteration (one GPU: spk_em_iteration, a single launch; N GPUs: spk_em_histogram ->
-RCCL all-reduce -> spk_em_finalize) + the host M-step (Params update).
+one E+M iteration (one GPU: spk_em_iteration_start / _wait, a single launch; N GPUs:
+spk_em_histogram -> RCCL all-reduce -> spk_em_finalize) + the host M-step (Params update).  On one
+GPU the loop is software-pipelined: pass i is queued before the host M-step of iteration i - 1.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--records R] [--no-cpu-baseline]
 """
@@ -104,22 +105,40 @@ def main():
     first_gammas_s = time.time() - t0
     names, nlev = job.code_meta
 
-    host = {"gammas_call": [], "em_call": [], "m_step_host": []}
+    host = {"gammas_call": [], "em_wait": [], "m_step_host": [], "em_start": []}
+    dev = {"gamma": [], "em_hist": [], "em_final": []}
+    pending = [False]
+
+    def finish_m_step():
+        """Statistics of the enqueued E+M iteration, then the host M-step (Params update)."""
+        t0 = time.perf_counter()
+        stats = job.em_wait()
+        t1 = time.perf_counter()
+        lam, rows = m_step_rows(stats, names, nlev)
+        params._update_params(lam, rows)
+        t2 = time.perf_counter()
+        host["em_wait"].append((t1 - t0) * 1e3)
+        host["m_step_host"].append((t2 - t1) * 1e3)
+        pending[0] = False
+        ms = job.ctx.kernel_ms_done()  # the newest completed launches (the next comparison pass may be running)
+        for k in dev:
+            dev[k].append(ms[k])
 
     def step():
+        """Comparison pass i, then E+M iteration i.  Software-pipelined: pass i is queued before the host
+        finishes the M-step of iteration i - 1 (pass i does not depend on it; E+M i does), so the device
+        never waits for the host.  The order of device work and its results are those of the plain loop."""
         t0 = time.perf_counter()
         job.gammas(st)
         t1 = time.perf_counter()
-        stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        if pending[0]:
+            finish_m_step()
         t2 = time.perf_counter()
-        lam, rows = m_step_rows(stats, names, nlev)
-        params._update_params(lam, rows)
+        job.em_start(params.params["λ"], params._level_probabilities())
+        pending[0] = True
         t3 = time.perf_counter()
         host["gammas_call"].append((t1 - t0) * 1e3)
-        host["em_call"].append((t2 - t1) * 1e3)
-        host["m_step_host"].append((t3 - t2) * 1e3)
-        ms = job.ctx.kernel_ms()
-        return ms
+        host["em_start"].append((t3 - t2) * 1e3)
 
     def barrier():
         torch.cuda.synchronize()
@@ -128,18 +147,22 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    for v in host.values():
+    if pending[0]:
+        finish_m_step()
+    for v in list(host.values()) + list(dev.values()):
         v.clear()
-    gamma_ms, hist_ms, fin_ms = [], [], []
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ms = step()
-        gamma_ms.append(ms["gamma"])
-        hist_ms.append(ms["em_hist"])
-        fin_ms.append(max(ms["em_final"], 0.0))  # one GPU: the E-step runs inside the histogram launch
+        step()
+    finish_m_step()  # the last iteration's M-step is part of the timed work
     barrier()
     elapsed = time.perf_counter() - t0
+    # per-launch device times of the timed steps (HIP events on the context stream, read as each
+    # launch completed)
+    gamma_ms = dev["gamma"]
+    hist_ms = dev["em_hist"]
+    fin_ms = [max(x, 0.0) for x in dev["em_final"]]  # one GPU: the E-step runs inside the histogram launch
     local_pairs = job.n_pairs
     elapsed = D.max_over_ranks(elapsed)
     total_pairs = D.sum_over_ranks(local_pairs)

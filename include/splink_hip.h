@@ -55,6 +55,9 @@ int spk_ctx_set_link_type(spk_ctx *ctx, int link_type);
 /* Elapsed milliseconds of the last launch of each kernel family, measured with HIP events
  * on the context stream: [0] block, [1] gamma, [2] em_hist, [3] em_final, [4] score. */
 int spk_ctx_kernel_ms(spk_ctx *ctx, double *out5);
+/* The same without synchronising: per family the newest launch that has completed (-1 = none), so a
+ * caller can read the timings of iteration i while iteration i + 1 is still queued. */
+int spk_ctx_kernel_ms_done(spk_ctx *ctx, double *out5);
 int spk_ctx_enable_timing(spk_ctx *ctx, int on);
 /* LDS bytes one workgroup may allocate on the context's device (sizes the E/M histogram copies). */
 int spk_ctx_lds_per_block(spk_ctx *ctx, int *out);
@@ -245,6 +248,16 @@ int spk_levenshtein(spk_ctx *ctx, int64_t n, const int64_t *l_offsets, const uin
  * sums.  out_stats / m / u / lambda as spk_em_finalize.  For a single GPU (no exchange). */
 int spk_em_iteration(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
                      double *out_stats, int n_stats);
+/* spk_em_iteration in two halves: _start enqueues the launch and the statistics readback (pinned host
+ * memory) and returns; _wait returns the statistics.  In between the caller may enqueue the next
+ * spk_gammas pass and compute the previous M-step on the host, so the device never waits for the host
+ * (the reference's iterate loop, iterate.py:36-56, runs E, M, E, M ...: only the M-step of iteration i
+ * must precede the E-step of i + 1).  If the codes the iteration read are corrected after spk_gammas
+ * returned (work-list overflow, strings past the exact passes), the iteration is repeated before _wait
+ * returns.  One iteration may be pending per context (SPK_E_STATE otherwise). */
+int spk_em_iteration_start(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
+                           int n_stats);
+int spk_em_iteration_wait(spk_ctx *ctx, double *out_stats, int n_stats);
 /* Multi-GPU form of the same iteration: spk_em_histogram streams every pair's code once and writes
  * the pattern histogram (uint64 [n_patterns]) to d_hist, a DEVICE buffer (NULL = context-owned);
  * with a caller buffer it returns once the histogram is final.  Callers sharding pairs over GPUs

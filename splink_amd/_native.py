@@ -50,6 +50,7 @@ EXPORTS = [
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum",
+    "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done",
 ]
 TF_LIMBS = 14  # SPK_TF_LIMBS
 
@@ -146,6 +147,12 @@ class Context:
     def kernel_ms(self):
         out = np.zeros(5, dtype=np.float64)
         check(self._lib.spk_ctx_kernel_ms(self._h, _ptr(out)), "spk_ctx_kernel_ms")
+        return dict(zip(["block", "gamma", "em_hist", "em_final", "score"], out.tolist()))
+
+    def kernel_ms_done(self):
+        """kernel_ms without synchronising: per family the newest launch that has completed (-1 = none)."""
+        out = np.zeros(5, dtype=np.float64)
+        check(self._lib.spk_ctx_kernel_ms_done(self._h, _ptr(out)), "spk_ctx_kernel_ms_done")
         return dict(zip(["block", "gamma", "em_hist", "em_final", "score"], out.tolist()))
 
     def table_create(self, side: int, n_rows: int, n_cols: int):
@@ -367,6 +374,18 @@ class Context:
         out = self._stats_buf(n_stats)
         check(self._lib.spk_em_iteration(self._h, ctypes.c_double(lam), ctypes.c_double(one_minus), _ptr(m), _ptr(u),
                                          _ptr(out), ctypes.c_int(n_stats)), "spk_em_iteration")
+        return out
+
+    def em_iteration_start(self, lam, one_minus, m, u, n_stats):
+        """Enqueue one E+M iteration (spk_em_iteration_start); em_iteration_wait returns its statistics."""
+        m = np.ascontiguousarray(m, dtype=np.float64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        check(self._lib.spk_em_iteration_start(self._h, ctypes.c_double(lam), ctypes.c_double(one_minus), _ptr(m),
+                                               _ptr(u), ctypes.c_int(n_stats)), "spk_em_iteration_start")
+
+    def em_iteration_wait(self, n_stats):
+        out = self._stats_buf(n_stats)
+        check(self._lib.spk_em_iteration_wait(self._h, _ptr(out), ctypes.c_int(n_stats)), "spk_em_iteration_wait")
         return out
 
     def _stats_buf(self, n_stats):

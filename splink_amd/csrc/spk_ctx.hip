@@ -215,13 +215,15 @@ using namespace spk;
 
 int spk_ctx::begin(Kern k) {
     if (!timing) return SPK_OK;
-    SPK_HIP(hipEventRecord(ev0[k], stream));
+    ev_slot[k] ^= 1;
+    ev_used[ev_slot[k]][k] = false;
+    SPK_HIP(hipEventRecord(ev0[ev_slot[k]][k], stream));
     return SPK_OK;
 }
 int spk_ctx::end(Kern k) {
     if (!timing) return SPK_OK;
-    SPK_HIP(hipEventRecord(ev1[k], stream));
-    ev_used[k] = true;
+    SPK_HIP(hipEventRecord(ev1[ev_slot[k]][k], stream));
+    ev_used[ev_slot[k]][k] = true;
     return SPK_OK;
 }
 
@@ -264,10 +266,13 @@ int spk_ctx_create(int device, spk_ctx **out) {
         return SPK_E_HIP;
     }
     c->stream = c->own_stream;
-    for (int k = 0; k < K_COUNT; ++k) {
-        (void)hipEventCreate(&c->ev0[k]);
-        (void)hipEventCreate(&c->ev1[k]);
-    }
+    for (int b = 0; b < 2; ++b)
+        for (int k = 0; k < K_COUNT; ++k) {
+            (void)hipEventCreate(&c->ev0[b][k]);
+            (void)hipEventCreate(&c->ev1[b][k]);
+        }
+    (void)hipEventCreateWithFlags(&c->ev_info, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->ev_stats, hipEventDisableTiming);
     *out = c;
     return SPK_OK;
 }
@@ -276,10 +281,13 @@ void spk_ctx_destroy(spk_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    for (int k = 0; k < K_COUNT; ++k) {
-        (void)hipEventDestroy(ctx->ev0[k]);
-        (void)hipEventDestroy(ctx->ev1[k]);
-    }
+    for (int b = 0; b < 2; ++b)
+        for (int k = 0; k < K_COUNT; ++k) {
+            (void)hipEventDestroy(ctx->ev0[b][k]);
+            (void)hipEventDestroy(ctx->ev1[b][k]);
+        }
+    if (ctx->ev_info) (void)hipEventDestroy(ctx->ev_info);
+    if (ctx->ev_stats) (void)hipEventDestroy(ctx->ev_stats);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);
     if (ctx->h_info) (void)hipHostFree(ctx->h_info);
     hipStream_t own = ctx->own_stream;
@@ -310,9 +318,26 @@ int spk_ctx_kernel_ms(spk_ctx *ctx, double *out5) {
     SPK_REQUIRE(ctx && out5, SPK_E_INVALID, "null arg");
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     for (int k = 0; k < K_COUNT; ++k) {
+        const int b = ctx->ev_slot[k];
         float ms = 0.f;
-        if (ctx->ev_used[k]) SPK_HIP(hipEventElapsedTime(&ms, ctx->ev0[k], ctx->ev1[k]));
-        out5[k] = ctx->ev_used[k] ? (double)ms : -1.0;
+        if (ctx->ev_used[b][k]) SPK_HIP(hipEventElapsedTime(&ms, ctx->ev0[b][k], ctx->ev1[b][k]));
+        out5[k] = ctx->ev_used[b][k] ? (double)ms : -1.0;
+    }
+    return SPK_OK;
+}
+
+int spk_ctx_kernel_ms_done(spk_ctx *ctx, double *out5) {
+    SPK_REQUIRE(ctx && out5, SPK_E_INVALID, "null arg");
+    for (int k = 0; k < K_COUNT; ++k) {
+        out5[k] = -1.0;
+        for (int i = 0; i < 2; ++i) {  // the newest pair whose end event has completed
+            const int b = i == 0 ? ctx->ev_slot[k] : ctx->ev_slot[k] ^ 1;
+            if (!ctx->ev_used[b][k] || hipEventQuery(ctx->ev1[b][k]) != hipSuccess) continue;
+            float ms = 0.f;
+            SPK_HIP(hipEventElapsedTime(&ms, ctx->ev0[b][k], ctx->ev1[b][k]));
+            out5[k] = (double)ms;
+            break;
+        }
     }
     return SPK_OK;
 }

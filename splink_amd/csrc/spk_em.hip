@@ -373,27 +373,52 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     __threadfence();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // the rows' sum per bin, in block order (8 independent partial sums keep loads in flight)
+    // The rows' sum per bin with every thread of the workgroup: work item (quad of 4 bins, row group)
+    // sums the rows b = group, group + Gr, ... with 16-byte loads, 8 in flight; the groups' partials
+    // meet in LDS (the counters are no longer needed).  Counts are exact integers (< 2^32: P < 2^32 is
+    // checked on the host), so the order of the additions does not matter.  One thread per bin summed
+    // all G rows before: G / 8 dependent load rounds from other XCDs' lines, ~90 us per cfg2 iteration.
     const int64_t ps = part_stride(n_pat);
     const int G = (int)gridDim.x;
-    auto total = [&](int p) -> unsigned long long {
-        unsigned long long a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int b = 0;
-        for (; b + 8 <= G; b += 8)
+    const int Q = (n_pat + 3) / 4;
+    int Gr = HL_THREADS / Q;
+    const int fit = (int)(((int64_t)n_pat * R * 4) / ((int64_t)Q * 16));  // partials within the counters' LDS
+    Gr = Gr < fit ? Gr : fit;
+    Gr = Gr < G ? Gr : G;
+    Gr = Gr > 1 ? Gr : 1;
+    u32x4 *sp = reinterpret_cast<u32x4 *>(sh);  // [Gr][Q]
+    for (int it = threadIdx.x; it < Q * Gr; it += HL_THREADS) {
+        const int q = it % Q, gr = it / Q;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(part) + q;
+        const int64_t rs = ps / 4;  // row stride in quads
+        u32x4 a[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] += part[(int64_t)(b + q) * ps + p];
-        for (; b < G; ++b) a[0] += part[(int64_t)b * ps + p];
-        return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-    };
+        for (int j = 0; j < 8; ++j) a[j] = u32x4{0u, 0u, 0u, 0u};
+        int b = gr;
+        for (; b + 7 * Gr < G; b += 8 * Gr)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] += src[(int64_t)(b + j * Gr) * rs];
+        for (; b < G; b += Gr) a[0] += src[(int64_t)b * rs];
+        sp[gr * Q + q] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    }
+    __syncthreads();
+    // thread t owns bins p = t, t + HL_THREADS, ... (the same mapping as em_finalize_block's loop, so
+    // the count it parks in cpat is read back by the thread that wrote it)
+    const uint32_t *sp1 = reinterpret_cast<const uint32_t *>(sh);
+    for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
+        unsigned long long c = 0;
+        for (int gr = 0; gr < Gr; ++gr) c += sp1[gr * 4 * Q + p];
+        if (FIN) cpat[p] = (double)c;
+        else out_hist[p] = c;
+    }
     if (FIN) {
-        // the counters are no longer needed: their LDS holds the staged arguments and the pattern table
+        __syncthreads();  // the partials' LDS is reused for the staged arguments and the pattern table
         PatArgs *sA = reinterpret_cast<PatArgs *>(sh);
         const PatArgs &A = stage_args(A0, sA);
         double *tab = reinterpret_cast<double *>(sh) + (sizeof(PatArgs) + 7) / 8;
         const bool room = ((sizeof(PatArgs) + 7) / 8 + 3 * (size_t)n_pat) * 8 <= (size_t)n_pat * R * 4;
-        em_finalize_block(A, total, mpat, llpat, cpat, out, room ? tab : nullptr);
-    } else {
-        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) out_hist[p] = total(p);
+        em_finalize_block(A, [&](int p) { return (unsigned long long)cpat[p]; }, mpat, llpat, cpat, out,
+                          room ? tab : nullptr);
     }
     if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
@@ -538,6 +563,7 @@ static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     const int64_t P = ctx->n_pairs;
     const int vec = 16 / ctx->code_bytes;
     const int R = lane_copies(ctx);
+    SPK_REQUIRE(P < (int64_t)UINT32_MAX, SPK_E_LIMIT, "EM histogram: 2^32 or more pairs in one context");
     SPK_TRY(ctx->begin(K_EMHIST));
     if (R) {
         PatArgs A{};
@@ -590,6 +616,7 @@ static int em_buffers(spk_ctx *ctx, int n_stats) {
 
 // E-step + M-step sums from the histogram h (one workgroup), statistics copied to out_stats.
 static int finalize_from(spk_ctx *ctx, const unsigned long long *h, const PatArgs &A, double *out_stats, int n_stats) {
+    SPK_REQUIRE(!ctx->em_pending, SPK_E_STATE, "spk_em_finalize: an asynchronous iteration is pending (spk_em_iteration_wait)");
     SPK_TRY(em_buffers(ctx, n_stats));
     SPK_TRY(ctx->begin(K_EMFIN));
     k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, h, ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p);
@@ -645,50 +672,92 @@ extern "C" int spk_em_finalize(spk_ctx *ctx, const uint64_t *d_hist, double lamb
     return SPK_OK;
 }
 
+// Enqueue one E+M iteration on the current codes with the arguments saved in ctx (em_*): the statistics
+// are copied to the pinned h_stats and ev_stats is recorded behind them.  No host synchronisation on the
+// lane-histogram path (one launch); pattern spaces past the lane-private counters take the histogram +
+// finalize launches.
+static int enqueue_em(spk_ctx *ctx) {
+    PatArgs A;
+    SPK_TRY(pat_args(ctx, ctx->em_lambda, ctx->em_one_minus, ctx->em_m.data(), ctx->em_u.data(), A));
+    const int n_stats = ctx->em_n_stats;
+    SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_iteration: n_stats mismatch");
+    SPK_TRY(em_buffers(ctx, n_stats));
+    const int R = lane_copies(ctx);
+    if (!R) {
+        SPK_TRY(enqueue_histogram(ctx, nullptr));
+        SPK_TRY(ctx->begin(K_EMFIN));
+        k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, reinterpret_cast<const unsigned long long *>(ctx->hist.p),
+                                                         ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p);
+        SPK_HIP(hipGetLastError());
+        SPK_TRY(ctx->end(K_EMFIN));
+    } else {
+        const int64_t n_pat = ctx->n_patterns;
+        uint32_t *acc = nullptr;
+        unsigned long long *h = nullptr;
+        unsigned int *ticket = nullptr;
+        SPK_TRY(em_accumulator(ctx, &acc, &ticket));
+        const int64_t P = ctx->n_pairs;
+        SPK_REQUIRE(P < (int64_t)UINT32_MAX, SPK_E_LIMIT, "spk_em_iteration: 2^32 or more pairs in one context");
+        const int64_t g = lane_grid(ctx);
+        const size_t sh = std::max<size_t>((size_t)n_pat * R * 4, sizeof(PatArgs));
+        double *mpat = ctx->mpat.p, *llpat = ctx->llpat.p, *cpat = ctx->cpat.p, *out = ctx->stats.p;
+        SPK_TRY(ctx->begin(K_EMHIST));
+        switch (R) {
+            SPK_EM_ITER(64, true)
+            SPK_EM_ITER(32, true)
+            SPK_EM_ITER(16, true)
+            SPK_EM_ITER(8, true)
+            SPK_EM_ITER(4, true)
+        }
+        SPK_HIP(hipGetLastError());
+        SPK_TRY(ctx->end(K_EMHIST));
+        ctx->ev_used[0][K_EMFIN] = ctx->ev_used[1][K_EMFIN] = false;  // one launch: the E-step is inside it
+    }
+    SPK_HIP(hipMemcpyAsync(ctx->h_stats, ctx->stats.p, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipEventRecord(ctx->ev_stats, ctx->stream));
+    return SPK_OK;
+}
+
+namespace spk {
+int em_requeue(spk_ctx *ctx) { return enqueue_em(ctx); }
+}  // namespace spk
+
+extern "C" int spk_em_iteration_start(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
+                                      int n_stats) {
+    SPK_REQUIRE(ctx && m && u, SPK_E_INVALID, "spk_em_iteration_start: null arg");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_iteration_start: no gammas");
+    SPK_REQUIRE(!ctx->em_pending, SPK_E_STATE, "spk_em_iteration_start: the previous iteration was not waited for");
+    SPK_HIP(hipSetDevice(ctx->device));
+    int tot = 0;
+    for (int k = 0; k < ctx->K; ++k) tot += ctx->n_levels[k];
+    ctx->em_lambda = lambda;
+    ctx->em_one_minus = one_minus;
+    ctx->em_m.assign(m, m + tot);
+    ctx->em_u.assign(u, u + tot);
+    ctx->em_n_stats = n_stats;
+    SPK_TRY(enqueue_em(ctx));
+    ctx->em_pending = true;
+    ctx->em_seq = ctx->gamma_seq;
+    return SPK_OK;
+}
+
+extern "C" int spk_em_iteration_wait(spk_ctx *ctx, double *out_stats, int n_stats) {
+    SPK_REQUIRE(ctx && out_stats, SPK_E_INVALID, "spk_em_iteration_wait: null arg");
+    SPK_REQUIRE(ctx->em_pending, SPK_E_STATE, "spk_em_iteration_wait: no iteration started");
+    SPK_REQUIRE(n_stats == ctx->em_n_stats, SPK_E_INVALID, "spk_em_iteration_wait: n_stats mismatch");
+    SPK_HIP(hipSetDevice(ctx->device));
+    // the codes' info block first: a correction of the codes re-enqueues this iteration (settle_gammas)
+    if (ctx->em_seq == ctx->gamma_seq) SPK_TRY(settle_gammas(ctx, nullptr));
+    SPK_HIP(hipEventSynchronize(ctx->ev_stats));
+    std::memcpy(out_stats, ctx->h_stats, (size_t)n_stats * 8);
+    ctx->em_pending = false;
+    return SPK_OK;
+}
+
 extern "C" int spk_em_iteration(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
                                 double *out_stats, int n_stats) {
-    SPK_REQUIRE(ctx && m && u && out_stats, SPK_E_INVALID, "spk_em_iteration: null arg");
-    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_iteration: no gammas");
-    SPK_HIP(hipSetDevice(ctx->device));
-    PatArgs A;
-    SPK_TRY(pat_args(ctx, lambda, one_minus, m, u, A));
-    SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_iteration: n_stats mismatch");
-    const int R = lane_copies(ctx);
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        if (!R) {  // pattern space past the lane-private counters: histogram, then finalize
-            SPK_TRY(enqueue_histogram(ctx, nullptr));
-            SPK_TRY(finalize_from(ctx, reinterpret_cast<const unsigned long long *>(ctx->hist.p), A, out_stats, n_stats));
-        } else {
-            const int64_t n_pat = ctx->n_patterns;
-            uint32_t *acc = nullptr;
-            unsigned long long *h = nullptr;
-            unsigned int *ticket = nullptr;
-            SPK_TRY(em_accumulator(ctx, &acc, &ticket));
-            SPK_TRY(em_buffers(ctx, n_stats));
-            const int64_t P = ctx->n_pairs;
-            const int64_t g = lane_grid(ctx);
-            const size_t sh = std::max<size_t>((size_t)n_pat * R * 4, sizeof(PatArgs));
-            double *mpat = ctx->mpat.p, *llpat = ctx->llpat.p, *cpat = ctx->cpat.p, *out = ctx->stats.p;
-            SPK_TRY(ctx->begin(K_EMHIST));
-            switch (R) {
-                SPK_EM_ITER(64, true)
-                SPK_EM_ITER(32, true)
-                SPK_EM_ITER(16, true)
-                SPK_EM_ITER(8, true)
-                SPK_EM_ITER(4, true)
-            }
-            SPK_HIP(hipGetLastError());
-            SPK_TRY(ctx->end(K_EMHIST));
-            ctx->ev_used[K_EMFIN] = false;  // one launch: the E-step is inside the histogram kernel
-            SPK_HIP(hipMemcpyAsync(ctx->h_stats, out, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
-            SPK_HIP(hipStreamSynchronize(ctx->stream));
-            std::memcpy(out_stats, ctx->h_stats, (size_t)n_stats * 8);
-        }
-        bool fixed = false;
-        SPK_TRY(settle_gammas(ctx, &fixed));
-        if (!fixed) break;  // else the codes changed after this iteration read them: run it again
-    }
-    return SPK_OK;
+    SPK_TRY(spk_em_iteration_start(ctx, lambda, one_minus, m, u, n_stats));
+    return spk_em_iteration_wait(ctx, out_stats, n_stats);
 }
 
 #undef SPK_EM_ITER

@@ -1464,10 +1464,23 @@ namespace spk {
 // exact phase with room for every listed cell, and cells with a string past SLOW_LIMIT units go through
 // the huge pass.  *fixed = true when codes changed after the call returned (a consumer that already
 // read them must read them again).  Called at the consumers' own synchronisation points.
+static int settle_info(spk_ctx *ctx, bool *fixed);
+
 int settle_gammas(spk_ctx *ctx, bool *fixed) {
+    bool f = false;
+    SPK_TRY(settle_info(ctx, &f));
+    if (fixed) *fixed = f;
+    // an asynchronous EM iteration enqueued on these codes read them before the correction: repeat it
+    if (f && ctx->em_pending && ctx->em_seq == ctx->gamma_seq) SPK_TRY(em_requeue(ctx));
+    return SPK_OK;
+}
+
+static int settle_info(spk_ctx *ctx, bool *fixed) {
     if (fixed) *fixed = false;
     if (!ctx->gamma_pending) return SPK_OK;
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    // the info block is on the host once the readback behind it completed (later work -- an EM
+    // iteration enqueued meanwhile -- keeps running)
+    SPK_HIP(hipEventSynchronize(ctx->ev_info));
     ctx->gamma_pending = false;
     if (!ctx->codes_valid || !ctx->gplan) return SPK_OK;  // the codes were replaced or invalidated since
     GammaPlan &G = *ctx->gplan;
@@ -1804,6 +1817,8 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_TRY(enqueue_phase(ctx, G, cap));
     SPK_TRY(ctx->end(K_GAMMA));
     SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+    ++ctx->gamma_seq;
     ctx->gamma_pending = true;
     ctx->codes_valid = true;
     ctx->mpat_valid = false;
@@ -1836,6 +1851,7 @@ extern "C" int spk_gammas_load(spk_ctx *ctx, int n_cols, const int32_t *n_levels
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     ctx->n_pairs = n;
     ctx->gamma_pending = false;
+    ++ctx->gamma_seq;
     ctx->codes_valid = true;
     return SPK_OK;
 }

@@ -319,10 +319,24 @@ struct spk_ctx {
     bool mpat_valid = false;
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
 
-    // timing
+    // asynchronous EM iteration (spk_em_iteration_start / _wait): the statistics land in h_stats behind
+    // ev_stats; the arguments are kept so that the launch can be repeated when the codes it read are
+    // corrected after spk_gammas returned (settle_gammas -> em_requeue)
+    bool em_pending = false;
+    uint64_t gamma_seq = 0;           // spk_gammas calls so far (the codes' generation)
+    uint64_t em_seq = 0;              // the generation the pending EM iteration read
+    double em_lambda = 0.0, em_one_minus = 0.0;
+    std::vector<double> em_m, em_u;
+    int em_n_stats = 0;
+    hipEvent_t ev_info = nullptr;     // after spk_gammas' info-block readback
+    hipEvent_t ev_stats = nullptr;    // after the EM statistics readback
+
+    // timing: two event pairs per kind, alternating, so the last completed launch of a kind can be read
+    // while a newer one is still in flight (spk_ctx_kernel_ms_done)
     bool timing = false;
-    hipEvent_t ev0[spk::K_COUNT] = {}, ev1[spk::K_COUNT] = {};
-    bool ev_used[spk::K_COUNT] = {};
+    hipEvent_t ev0[2][spk::K_COUNT] = {}, ev1[2][spk::K_COUNT] = {};
+    bool ev_used[2][spk::K_COUNT] = {};
+    int ev_slot[spk::K_COUNT] = {};
 
     int begin(spk::Kern k);
     int end(spk::Kern k);
@@ -334,6 +348,8 @@ int ensure_desc(spk_ctx *ctx, Table &t);
 // Finishes the last spk_gammas (work-list overflow, huge pass) once the stream is synchronised;
 // *fixed = true when codes changed after spk_gammas returned.  No-op when nothing is pending.
 int settle_gammas(spk_ctx *ctx, bool *fixed);
+// Enqueue the pending asynchronous EM iteration again (its codes were corrected after it was enqueued).
+int em_requeue(spk_ctx *ctx);
 int new_column(spk_ctx *ctx, int side, int col, Column **out);
 int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c);
 int launch_utf8_decode(spk_ctx *ctx, int64_t n, const int64_t *off8, const int64_t *src_off, const int32_t *perm,

@@ -402,6 +402,26 @@ class Job:
             return self.ctx.em_finalize(hist.data_ptr(), lam_d, one_minus, m, u, n_stats)
         return self.ctx.em_iteration(lam_d, one_minus, m, u, n_stats)
 
+    def em_start(self, lam, level_probs):
+        """em_stats in two halves: enqueue the iteration now, collect its statistics with em_wait().  On
+        one GPU the launch and the statistics readback are asynchronous (spk_em_iteration_start), so the
+        next comparison pass can be queued and the host M-step computed while the device works; with a
+        cross-rank reduction the iteration runs synchronously here."""
+        if self.reduces_across_ranks() or self.force_reduce:
+            self._em_done = self.em_stats(lam, level_probs)
+            return
+        names, n_levels = self.code_meta
+        m, u = self.flat_tables(level_probs)
+        self._em_n_stats = N_HEAD + 4 * sum(L + 1 for L in n_levels)
+        self._em_done = None
+        self.ctx.em_iteration_start(float(lam), float(1 - lam), m, u, self._em_n_stats)
+
+    def em_wait(self):
+        if self._em_done is not None:
+            out, self._em_done = self._em_done, None
+            return out
+        return self.ctx.em_iteration_wait(self._em_n_stats)
+
     def log_likelihood(self, lam, level_probs):
         """Σ over pairs of ln(λ·Πm + (1-λ)·Πu) (expectation_step.py:224-272); None if every term is NULL."""
         stats = self.em_stats(lam, level_probs)

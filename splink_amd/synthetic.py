@@ -88,11 +88,21 @@ def make_records(n: int, seed: int = SEED, surname_vocab: int = 15000, surname_s
     arrow=True gives Arrow-backed string columns (pd.ArrowDtype(large_string)), the columnar form a
     Spark / Arrow source hands over; the values are identical."""
     rng = np.random.Generator(np.random.PCG64(seed))
+    vocabs = _vocabs(rng, surname_vocab, first_vocab, city_vocab)
+    return _records(rng, n, vocabs, surname_s, with_address, arrow)
+
+
+def _vocabs(rng: np.random.Generator, surname_vocab: int, first_vocab: int, city_vocab: int):
     firsts = _vocab(rng, first_vocab, 3, 12)
     surnames = _vocab(rng, surname_vocab, 3, 14)
     cities = _vocab(rng, city_vocab, 4, 12)
     streets = _vocab(rng, 500, 4, 10)
+    return firsts, surnames, cities, streets
 
+
+def _records(rng: np.random.Generator, n: int, vocabs, surname_s: float, with_address: bool,
+             arrow: bool) -> pd.DataFrame:
+    firsts, surnames, cities, streets = vocabs
     # entities -> cluster sizes
     n_ent = n
     dup = rng.random(n_ent) < 0.2
@@ -177,6 +187,54 @@ def make_records(n: int, seed: int = SEED, surname_vocab: int = 15000, surname_s
         for name in cols:
             df[name] = pd.Series(pa.array(df[name].tolist(), type=pa.large_string()),
                                  dtype=pd.ArrowDtype(pa.large_string()))
+    return df
+
+
+_FORK_VOCABS = None  # the parent's vocabularies, inherited by forked workers
+
+
+def _chunk(args):
+    seed, i, n_i, vocab_args, surname_s, with_address = args
+    vocabs = _FORK_VOCABS if _FORK_VOCABS is not None else \
+        _vocabs(np.random.Generator(np.random.PCG64(seed)), *vocab_args)
+    df = _records(np.random.Generator(np.random.PCG64([seed, i + 1])), n_i, vocabs, surname_s, with_address, True)
+    return {c: (df[c].array._pa_array.combine_chunks() if c not in ("unique_id", "cluster") else df[c].to_numpy())
+            for c in df.columns}
+
+
+def make_records_parallel(n: int, chunks: int, workers: int, seed: int = SEED, surname_vocab: int = 15000,
+                          surname_s: float = 0.3, first_vocab: int = 5000, city_vocab: int = 2000,
+                          with_address: bool = False) -> pd.DataFrame:
+    """`n` records generated as `chunks` independent populations over ONE shared vocabulary (the same
+    name / city / street lists as make_records(seed)), each from its own PCG64 stream [seed, i + 1], in
+    `workers` processes; Arrow-backed string columns.  For the 100M-record rows, where the serial
+    generator would take ~7 minutes.  Deterministic in (n, chunks, seed), but not equal to
+    make_records(n): duplicates stay inside a chunk, unique_id and cluster are offset per chunk."""
+    import multiprocessing as mp
+
+    import pyarrow as pa
+    sizes = [n // chunks + (1 if i < n % chunks else 0) for i in range(chunks)]
+    jobs = [(seed, i, sizes[i], (surname_vocab, first_vocab, city_vocab), surname_s, with_address)
+            for i in range(chunks)]
+    global _FORK_VOCABS
+    _FORK_VOCABS = _vocabs(np.random.Generator(np.random.PCG64(seed)), surname_vocab, first_vocab, city_vocab)
+    try:
+        with mp.get_context("fork").Pool(workers) as pool:
+            parts = pool.map(_chunk, jobs, chunksize=1)
+    finally:
+        _FORK_VOCABS = None
+    df = pd.DataFrame({"unique_id": np.arange(n, dtype=np.int64)})
+    for c in parts[0]:
+        if c == "unique_id":
+            continue
+        if c == "cluster":
+            off = np.cumsum([0] + [int(p["cluster"].max()) + 1 for p in parts[:-1]])
+            df[c] = np.concatenate([p[c] + o for p, o in zip(parts, off)])
+        else:
+            arr = pa.chunked_array([p[c] for p in parts]).combine_chunks()
+            df[c] = pd.Series(arr, dtype=pd.ArrowDtype(pa.large_string()))
+        for p in parts:
+            p[c] = None
     return df
 
 

@@ -11,6 +11,8 @@ import copy
 import json
 import warnings
 
+import numpy as np
+import pandas as pd
 import pytest
 
 from conftest import load_golden
@@ -119,3 +121,58 @@ def test_load_from_json_resumes(amd, tmp_path):
             assert rel_close(linker2.params.params["π"][gname]["prob_dist_match"][f"level_{i}"]["probability"], m)
             assert rel_close(linker2.params.params["π"][gname]["prob_dist_non_match"][f"level_{i}"]["probability"], u)
     compare_frames(df_e.toPandas(), g["df_e"], g["df_e_columns"])
+
+
+def _anagram_job(amd, n=40000):
+    """A comparison table whose undecided cells outgrow the exact-pass lists on the first spk_gammas call
+    (3 Levenshtein columns x 40k anagram pairs), so the codes are corrected after the call returned."""
+    from splink_amd.gammas import _job_from_comparison_table
+    from splink_amd.settings import complete_settings_dict
+    rng = np.random.Generator(np.random.PCG64(33))
+    base = np.array(list("abcdefghij"))
+    data = {}
+    for c in ("x", "y", "z"):
+        data[f"{c}_l"] = ["".join(rng.permutation(base)) for _ in range(n)]
+        data[f"{c}_r"] = ["".join(rng.permutation(base)) for _ in range(n)]
+    expr = ("case when {c}_l is null or {c}_r is null then -1 when levenshtein({c}_l, {c}_r) <= 5 then 2 "
+            "when levenshtein({c}_l, {c}_r) <= 7 then 1 else 0 end")
+    st = complete_settings_dict({"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": c, "custom_columns_used": [c], "num_levels": 3, "case_expression": expr.format(c=c)}
+        for c in ("x", "y", "z")]}, amd)
+    return _job_from_comparison_table(pd.DataFrame(data), amd), st
+
+
+def test_async_em_iteration_matches_sync(amd):
+    """spk_em_iteration_start / _wait (the bench's software-pipelined loop: comparison pass i queued, then
+    the M-step of i - 1, then E+M i) give the statistics of the synchronous spk_em_iteration, including
+    on the first call, whose codes are corrected after spk_gammas returned (the iteration is re-enqueued);
+    a second start without a wait is refused."""
+    from splink_amd.engine import m_step_rows
+    from splink_amd.params import Params
+    job, st = _anagram_job(amd)
+    p_sync, p_async = Params(st, amd), Params(st, amd)
+    job.gammas(st)  # first call: the work lists overflow, the correction happens at the EM's wait
+    job.em_start(p_async.params["λ"], p_async._level_probabilities())
+    with pytest.raises(RuntimeError, match="not waited for"):
+        job.em_start(p_async.params["λ"], p_async._level_probabilities())
+    a = job.em_wait()
+    s = job.em_stats(p_sync.params["λ"], p_sync._level_probabilities())
+    assert np.array_equal(a, s)
+    names, nlev = job.code_meta
+    for p in (p_sync, p_async):
+        p._update_params(*m_step_rows(s, names, nlev))
+    pending = False
+    for _ in range(4):  # pipelined against plain
+        job.gammas(st)
+        if pending:
+            p_async._update_params(*m_step_rows(job.em_wait(), names, nlev))
+        job.em_start(p_async.params["λ"], p_async._level_probabilities())
+        pending = True
+        job.gammas(st)
+        p_sync._update_params(*m_step_rows(job.em_stats(p_sync.params["λ"], p_sync._level_probabilities()),
+                                           names, nlev))
+    p_async._update_params(*m_step_rows(job.em_wait(), names, nlev))
+    assert p_async.params["λ"] == p_sync.params["λ"]
+    assert p_async._level_probabilities() == p_sync._level_probabilities()
+    ms = job.ctx.kernel_ms_done()
+    assert ms["gamma"] > 0 and ms["em_hist"] > 0

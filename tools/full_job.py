@@ -60,6 +60,13 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--out")
     ap.add_argument("--config", type=int, default=4, choices=[3, 4, 5])
+    ap.add_argument("--rules", default=None,
+                    help="blocking rules separated by '|' (default: the config's; e.g. "
+                         "'l.surname = r.surname|l.dob = r.dob and l.city = r.city')")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="generate the records as this many independent chunks over one vocabulary, in parallel "
+                         "(synthetic.make_records_parallel; 0 = the serial make_records)")
+    ap.add_argument("--workers", type=int, default=16)
     a = ap.parse_args()
     global COLS, SPECS
     if a.config == 5:  # + the free-text address column, Levenshtein-4 (cfg5's columns)
@@ -72,12 +79,17 @@ def main():
     from splink_amd.engine import Job, m_step_rows
     from splink_amd.params import Params
     from splink_amd.session import AmdSession
-    from splink_amd.synthetic import cfg_settings, make_records
+    from splink_amd.synthetic import cfg_settings, make_records, make_records_parallel
 
     t0 = time.time()
     link = a.config == 3
-    df = make_records(a.records * (2 if link else 1), surname_vocab=a.surname_vocab, arrow=True,
-                      with_address=a.config == 5)[["unique_id"] + COLS]
+    n_gen = a.records * (2 if link else 1)
+    if a.chunks:
+        df = make_records_parallel(n_gen, a.chunks, a.workers, surname_vocab=a.surname_vocab,
+                                   with_address=a.config == 5)[["unique_id"] + COLS]
+    else:
+        df = make_records(n_gen, surname_vocab=a.surname_vocab, arrow=True,
+                          with_address=a.config == 5)[["unique_id"] + COLS]
     inputs = [df.iloc[:a.records].reset_index(drop=True), df.iloc[a.records:].reset_index(drop=True)] if link else [df]
     del df
     gen_s = time.time() - t0
@@ -89,8 +101,18 @@ def main():
         for c in settings["comparison_columns"]:
             if c["col_name"] == "surname":
                 c["term_frequency_adjustments"] = True
+    if a.rules:
+        settings["blocking_rules"] = [r.strip() for r in a.rules.split("|")]
     params = Params(settings, AmdSession(0))
     st = params.settings
+
+    # device memory in use (hipMemGetInfo: every allocation on the device, the library's included)
+    free0, total_mem = torch.cuda.mem_get_info(0)
+    mem = {"device_total_bytes": int(total_mem), "in_use_before_job_bytes": int(total_mem - free0)}
+
+    def mem_mark(stage):
+        free, _ = torch.cuda.mem_get_info(0)
+        mem[f"after_{stage}_bytes"] = int(total_mem - free)
 
     wall = {}
     t_job = time.perf_counter()
@@ -103,11 +125,13 @@ def main():
     wall["block"] = time.perf_counter() - t
     wall["block_keys_and_cluster"] = job.timings["block_keys_s"]
     block_dev = job.ctx.kernel_ms()["block"]
+    mem_mark("block")
     log(f"shard {shard}/{n_shards}: {job.n_pairs} pairs of {job.n_candidates} candidates, block {wall['block']:.2f}s")
     t = time.perf_counter()
     job.gammas(st)
     wall["gammas_first_call_incl_column_decode"] = time.perf_counter() - t
     gamma_dev = job.ctx.kernel_ms()["gamma"]
+    mem_mark("gammas")
     names, nlev = job.code_meta
     exact_cells = dict(zip(names, job.ctx.gammas_exact_counts(len(names))))
     job.gammas(st)  # a second pass (row images built, lists sized): the per-pass device time
@@ -127,6 +151,7 @@ def main():
     torch.cuda.synchronize()
     wall["score"] = time.perf_counter() - t
     score_dev = job.ctx.kernel_ms()["score"]
+    mem_mark("score")
     tf_mp = None
     if link:  # term-frequency adjustment on surname (term_frequencies.py:122-168), device value ids
         from splink_amd.term_frequencies import _bayes_pair
@@ -155,6 +180,11 @@ def main():
         "pairs_per_s_job": P / total,
         "pairs_per_s_gamma_plus_em_iter": P / ((gamma_warm + float(np.mean(em_dev))) / 1e3),
         "generation_s_excluded": gen_s,
+        "generation": (f"make_records_parallel: {a.chunks} chunks over one vocabulary, {a.workers} processes"
+                       if a.chunks else "make_records (serial)"),
+        "surname_vocab": a.surname_vocab,
+        "blocking_rules": st["blocking_rules"],
+        "device_memory": {**mem, "peak_in_use_bytes": max(v for k, v in mem.items() if k.startswith("after_"))},
         "lambda_final": params.params["λ"],
     }
     if not a.no_parity:

@@ -13,6 +13,8 @@ wave alone every 4 (MI355X_MICROARCH.md, "Wave scheduling" and the issue-cost ro
   wait_frac   = SQ_WAIT_ANY / SQ_WAVE_CYCLES                    share of wave time stalled
   lds_conflict_rate = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS conflict cycles per LDS cycle
   l2_hit      = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
+  ta_busy     = TA_TA_BUSY_sum / (256 CUs x cycles)               texture-address unit busy share
+  issue_stall_frac = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
 """
 import collections
 import csv
@@ -39,6 +41,13 @@ def derive(c):
         c["wait_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
     if c.get("SQ_ACTIVE_INST_LDS"):
         c["lds_conflict_rate"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_ACTIVE_INST_LDS"]
+    if "TA_TA_BUSY_sum" in c:  # summed over the 256 CUs' texture-address units
+        c["ta_busy"] = c["TA_TA_BUSY_sum"] / (256 * cyc)
+        c["ta_stalled_by_tc"] = c.get("TA_ADDR_STALLED_BY_TC_CYCLES_sum", 0.0) / (256 * cyc)
+    if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_INST_ANY" in c:
+        c["issue_stall_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    if c.get("TCP_TCC_READ_REQ_sum"):
+        c["l1_to_l2_read_latency_cycles"] = c.get("TCP_TCC_READ_REQ_LATENCY_sum", 0.0) / c["TCP_TCC_READ_REQ_sum"]
     if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
         c["l2_hit"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
 

@@ -16,7 +16,7 @@ the x 2 stream reading as an upper bound; the E/M kernels stream: x 2.
 Kernel groups, per call of the C-ABI entry point (one "launch" of bench.py's roofline):
   gamma : every kernel spk_gammas launches (k_build_image, k_view_image, k_gamma_*), per call
           (calls = k_prefix dispatches)
-  em    : k_hist_lanes / k_hist + k_hist_reduce, per spk_em_histogram call; the first --head-em calls
+  em    : k_em_iter (histogram + E-step + M-step sums, one launch) per E+M iteration; the first --head-em calls
           (bench.py's warmup + timed steps at the headline size), the rest reported as em_at_scale
 """
 from __future__ import annotations
@@ -30,7 +30,7 @@ import os
 import re
 
 GAMMA = re.compile(r"k_build_image|k_view_image|k_gamma_|k_compact|k_prefix")
-EM = re.compile(r"k_hist")
+EM = re.compile(r"k_hist|k_em_iter|k_em_finalize")
 
 
 def read_counter(d, name):
@@ -48,13 +48,13 @@ def calls_of(rows, pat):
 
 
 def split_em(rows, head):
-    """EM dispatches grouped per spk_em_histogram call (k_hist_lanes/k_hist + k_hist_reduce)."""
+    """EM dispatches grouped per E+M iteration: k_em_iter (one launch), or k_hist + k_em_finalize."""
     calls, cur = [], []
     for d, k, v in rows:
         if not EM.search(k):
             continue
         cur.append(v)
-        if "k_hist_reduce" in k or ("k_hist<" in k):
+        if "k_em_iter" in k or "k_em_finalize" in k:
             calls.append(sum(cur))
             cur = []
     return calls[:head], calls[head:]
