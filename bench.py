@@ -336,30 +336,37 @@ def em_streaming(job, names, nlev, params, reps, iters=10):
 
 
 def string_rates(job, st, pairs, g_ms):
-    """Rates of the string work in one γ pass (Levenshtein GCUPS, JW comparisons/s).
+    """Rates of the string work in the last γ pass (Levenshtein GCUPS, JW comparisons/s).
 
-    `lev_effective_gcups` = Σ over every pair of len_l·len_r (code points) of each Levenshtein column,
-    i.e. the DP cells a full Wagner-Fischer pass would update, ÷ the whole γ-pass time: what the
-    filter bounds plus the bit-parallel exact pass stand in for.  It is an effective rate, not a count
-    of cells computed (most pairs are decided by the filter's bounds, the rest 32-64 cells per
-    word-op)."""
+    Levenshtein GCUPS counts DP cells of the cells the exact pass evaluated, over that launch's own
+    HIP-event time: Σ over the column's exact list of len_l · len_r (code points, before the common
+    prefix / suffix strip and the early exit, so the cells a full DP of those strings would update)
+    ÷ k_gamma_exact_simple<true>'s time.  Pairs the filter settled from bounds are not counted as
+    cells; they appear in `comparisons_per_s` (all pairs x columns over the whole γ pass)."""
     l, r = job.pair_rows()
     t = job.tables[0]
     sec = g_ms / 1e3
-    lev_cells, n_jw, n_lev = 0, 0, 0
-    for c in st["comparison_columns"]:
+    names = [c["col_name"] for c in st["comparison_columns"]]
+    exact = job.ctx.gammas_exact_counts(len(names))
+    xms = job.ctx.gammas_exact_ms(len(names))
+    lev, n_jw, n_lev = {}, 0, 0
+    for k, c in enumerate(st["comparison_columns"]):
         expr = (c.get("case_expression") or "").lower()
         if "levenshtein" in expr:
             n_lev += 1
             ln = t[c["col_name"]].str.len().fillna(0).to_numpy(np.int64)
-            lev_cells += int(np.dot(ln[l], ln[r]))
+            items = job.ctx.gammas_exact_list(k, int(exact[k]))
+            cells = int(np.dot(ln[l[items]], ln[r[items]]))
+            lev[c["col_name"]] = {"exact_cells": int(exact[k]), "dp_cells": cells, "exact_pass_ms": xms[k],
+                                  "gcups": cells / (xms[k] / 1e3) / 1e9 if xms[k] > 0 else None,
+                                  "exact_cells_per_s": exact[k] / (xms[k] / 1e3) if xms[k] > 0 else None}
         elif "jaro_winkler" in expr:
             n_jw += 1
     K = len(st["comparison_columns"])
     return {"comparisons_per_s": pairs * K / sec, "jw_comparisons_per_s": pairs * n_jw / sec,
-            "lev_comparisons_per_s": pairs * n_lev / sec, "lev_dp_cells_per_pass": lev_cells,
-            "lev_effective_gcups": lev_cells / sec / 1e9,
-            "note": "whole γ-pass time; effective GCUPS = Σ len_l·len_r over all pairs' Levenshtein columns ÷ that time"}
+            "lev_comparisons_per_s": pairs * n_lev / sec, "levenshtein_exact_pass": lev,
+            "note": "comparisons/s: all pairs x columns over the whole γ pass; levenshtein_exact_pass.gcups: DP "
+                    "cells (len_l x len_r) of the exactly evaluated cells over that launch's HIP-event time"}
 
 
 def cpu_baseline(job, df, st, seconds, col_names):

@@ -210,6 +210,10 @@ int spk_gammas_deferred(spk_ctx *ctx, int64_t *out);
 /* Per comparison column: pairs the last spk_gammas could not decide from bounds in the filter pass
  * and evaluated with the exact similarity (out[n], n >= number of columns). */
 int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
+/* With timing on (spk_ctx_enable_timing): milliseconds of each column's exact-pass launch in the last
+ * spk_gammas (HIP events; -1 = none; the Jaro-Winkler columns share one launch, reported at the first
+ * of them).  Synchronises. */
+int spk_gammas_exact_ms(spk_ctx *ctx, double *out, int n);
 /* Diagnostics: the first n pair ordinals of column k's exact list of the last spk_gammas (host). */
 int spk_gammas_exact_list(spk_ctx *ctx, int k, int32_t *out, int64_t n);
 /* Per comparison column: pairs of the last spk_gammas whose level the filter took from the blocking
@@ -273,6 +277,14 @@ int spk_em_set_lane_histogram(spk_ctx *ctx, int on);
  * `cast({p:.35f} as double)`; lambda/one_minus are `cast({λ} as double)`/`cast({1-λ} as double)`. */
 int spk_em_finalize(spk_ctx *ctx, const uint64_t *d_hist, double lambda, double one_minus, const double *m,
                     const double *u, double *out_stats, int n_stats);
+/* The multi-GPU iteration without host synchronisation: spk_em_histogram_async settles the last
+ * spk_gammas (so every rank counts final codes and reduces exactly once) and enqueues the histogram into
+ * d_hist; the caller enqueues its all-reduce on the context stream (spk_ctx_set_stream); then
+ * spk_em_finalize_start enqueues the E-step + M-step sums and the statistics readback, and
+ * spk_em_iteration_wait returns them. */
+int spk_em_histogram_async(spk_ctx *ctx, uint64_t *d_hist);
+int spk_em_finalize_start(spk_ctx *ctx, const uint64_t *d_hist, double lambda, double one_minus, const double *m,
+                          const double *u, int n_stats);
 /* Final E-step: match_probability per pair (NaN = NULL).  out_mp = host buffer for
  * [start, start+count), or NULL to keep the result on the device only. */
 int spk_score(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u, int64_t start,

@@ -50,7 +50,8 @@ EXPORTS = [
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum",
-    "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done",
+    "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
+    "spk_em_finalize_start", "spk_gammas_exact_ms",
 ]
 TF_LIMBS = 14  # SPK_TF_LIMBS
 
@@ -347,6 +348,11 @@ class Context:
         check(self._lib.spk_gammas_view_regions(self._h, ctypes.byref(n)), "spk_gammas_view_regions")
         return n.value
 
+    def gammas_exact_ms(self, n: int):
+        out = np.zeros(max(n, 1), dtype=np.float64)
+        check(self._lib.spk_gammas_exact_ms(self._h, _ptr(out), ctypes.c_int(n)), "spk_gammas_exact_ms")
+        return out[:n].tolist()
+
     def gammas_simple_count(self) -> int:
         n = ctypes.c_int(0)
         check(self._lib.spk_gammas_simple_count(self._h, ctypes.byref(n)), "spk_gammas_simple_count")
@@ -357,6 +363,16 @@ class Context:
 
     def em_histogram(self, d_hist_ptr: int = 0):
         check(self._lib.spk_em_histogram(self._h, ctypes.c_void_p(d_hist_ptr)), "spk_em_histogram")
+
+    def em_histogram_async(self, d_hist_ptr: int):
+        check(self._lib.spk_em_histogram_async(self._h, ctypes.c_void_p(d_hist_ptr)), "spk_em_histogram_async")
+
+    def em_finalize_start(self, d_hist_ptr, lam, one_minus, m, u, n_stats):
+        m = np.ascontiguousarray(m, dtype=np.float64)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        check(self._lib.spk_em_finalize_start(self._h, ctypes.c_void_p(d_hist_ptr), ctypes.c_double(lam),
+                                              ctypes.c_double(one_minus), _ptr(m), _ptr(u), ctypes.c_int(n_stats)),
+              "spk_em_finalize_start")
 
     def em_finalize(self, d_hist_ptr, lam, one_minus, m, u, n_stats):
         m = np.ascontiguousarray(m, dtype=np.float64)

@@ -227,6 +227,27 @@ int spk_ctx::end(Kern k) {
     return SPK_OK;
 }
 
+int spk_ctx::xbegin(int k) {
+    if (!timing) return SPK_OK;
+    while ((int)xev0.size() <= k) {
+        hipEvent_t a = nullptr, b = nullptr;
+        SPK_HIP(hipEventCreate(&a));
+        SPK_HIP(hipEventCreate(&b));
+        xev0.push_back(a);
+        xev1.push_back(b);
+        xev_used.push_back(0);
+    }
+    xev_used[k] = 0;
+    SPK_HIP(hipEventRecord(xev0[k], stream));
+    return SPK_OK;
+}
+int spk_ctx::xend(int k) {
+    if (!timing) return SPK_OK;
+    SPK_HIP(hipEventRecord(xev1[k], stream));
+    xev_used[k] = 1;
+    return SPK_OK;
+}
+
 extern "C" {
 
 const char *spk_last_error(void) { return g_last_error.c_str(); }
@@ -286,6 +307,10 @@ void spk_ctx_destroy(spk_ctx *ctx) {
             (void)hipEventDestroy(ctx->ev0[b][k]);
             (void)hipEventDestroy(ctx->ev1[b][k]);
         }
+    for (size_t k = 0; k < ctx->xev0.size(); ++k) {
+        (void)hipEventDestroy(ctx->xev0[k]);
+        (void)hipEventDestroy(ctx->xev1[k]);
+    }
     if (ctx->ev_info) (void)hipEventDestroy(ctx->ev_info);
     if (ctx->ev_stats) (void)hipEventDestroy(ctx->ev_stats);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);

@@ -428,8 +428,17 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
 // output is the dominant stream); the per-pattern table sits in LDS when it fits.  Plain stores:
 // 0.704 ms against 0.757 with nontemporal ones over 368M pairs (65 % of HBM peak).  The odd pair at
 // either end (when start or start + n is odd) is written by lane 0 of block 0.
-constexpr int SC_THREADS = 256;
-constexpr int SC_UNROLL = 4;
+#ifndef SPK_SC_THREADS
+#define SPK_SC_THREADS 256
+#endif
+#ifndef SPK_SC_UNROLL
+#define SPK_SC_UNROLL 4
+#endif
+#ifndef SPK_SC_WG_PER_CU
+#define SPK_SC_WG_PER_CU 8
+#endif
+constexpr int SC_THREADS = SPK_SC_THREADS;
+constexpr int SC_UNROLL = SPK_SC_UNROLL;
 constexpr int SC_LDS_PAT = 4096;
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
@@ -437,7 +446,7 @@ template <typename CodeT, bool LDS>
 __global__ __launch_bounds__(SC_THREADS) void k_score(const CodeT *__restrict__ codes, int64_t start, int64_t n,
                                                       const double *__restrict__ mpat, int n_pat,
                                                       double *__restrict__ mp) {
-    __shared__ double tab[LDS ? SC_LDS_PAT : 1];
+    extern __shared__ double tab[];  // n_pat doubles (dynamic: a 576-pattern table leaves room for 8 workgroups per CU)
     if (LDS) {
         for (int b = threadIdx.x; b < n_pat; b += SC_THREADS) tab[b] = mpat[b];
         __syncthreads();
@@ -735,7 +744,42 @@ extern "C" int spk_em_iteration_start(spk_ctx *ctx, double lambda, double one_mi
     ctx->em_m.assign(m, m + tot);
     ctx->em_u.assign(u, u + tot);
     ctx->em_n_stats = n_stats;
+    ctx->em_kind = 0;
     SPK_TRY(enqueue_em(ctx));
+    ctx->em_pending = true;
+    ctx->em_seq = ctx->gamma_seq;
+    return SPK_OK;
+}
+
+extern "C" int spk_em_histogram_async(spk_ctx *ctx, uint64_t *d_hist) {
+    SPK_REQUIRE(ctx && d_hist, SPK_E_INVALID, "spk_em_histogram_async: null arg");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_histogram_async: no gammas");
+    SPK_HIP(hipSetDevice(ctx->device));
+    // the codes must be final before they are counted: every rank then reduces exactly one histogram
+    // per iteration (a correction after the collective could not be repeated on one rank alone)
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    return enqueue_histogram(ctx, d_hist);
+}
+
+extern "C" int spk_em_finalize_start(spk_ctx *ctx, const uint64_t *d_hist, double lambda, double one_minus,
+                                     const double *m, const double *u, int n_stats) {
+    SPK_REQUIRE(ctx && d_hist && m && u, SPK_E_INVALID, "spk_em_finalize_start: null arg");
+    SPK_REQUIRE(ctx->codes_valid, SPK_E_STATE, "spk_em_finalize_start: no gammas");
+    SPK_REQUIRE(!ctx->em_pending, SPK_E_STATE, "spk_em_finalize_start: the previous iteration was not waited for");
+    SPK_HIP(hipSetDevice(ctx->device));
+    PatArgs A;
+    SPK_TRY(pat_args(ctx, lambda, one_minus, m, u, A));
+    SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_finalize_start: n_stats mismatch");
+    SPK_TRY(em_buffers(ctx, n_stats));
+    SPK_TRY(ctx->begin(K_EMFIN));
+    k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, reinterpret_cast<const unsigned long long *>(d_hist),
+                                                     ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p);
+    SPK_HIP(hipGetLastError());
+    SPK_TRY(ctx->end(K_EMFIN));
+    SPK_HIP(hipMemcpyAsync(ctx->h_stats, ctx->stats.p, (size_t)n_stats * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipEventRecord(ctx->ev_stats, ctx->stream));
+    ctx->em_n_stats = n_stats;
+    ctx->em_kind = 1;
     ctx->em_pending = true;
     ctx->em_seq = ctx->gamma_seq;
     return SPK_OK;
@@ -778,18 +822,19 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
     ctx->mpat_valid = true;
     if (count) {
         int64_t g = (count / 2 + SC_THREADS - 1) / SC_THREADS;
-        if (g > 8 * (int64_t)ctx->n_cu) g = 8 * (int64_t)ctx->n_cu;  // grid-stride: 8 workgroups per CU
+        if (g > SPK_SC_WG_PER_CU * (int64_t)ctx->n_cu) g = SPK_SC_WG_PER_CU * (int64_t)ctx->n_cu;  // grid-stride
         if (g < 1) g = 1;
         const int np = (int)ctx->n_patterns;
         const bool lds = ctx->n_patterns <= SC_LDS_PAT;  // LDS table: 0.795 ms vs 0.828 from L1 (368M pairs)
         const auto *c16 = reinterpret_cast<const uint16_t *>(ctx->codes.p);
         const auto *c32 = reinterpret_cast<const uint32_t *>(ctx->codes.p);
         double *o = ctx->mp.p + start;
+        const size_t shm = lds ? (size_t)np * 8 : 0;
         if (ctx->code_bytes == 2) {
-            if (lds) k_score<uint16_t, true><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c16, start, count, ctx->mpat.p, np, o);
+            if (lds) k_score<uint16_t, true><<<(unsigned)g, SC_THREADS, shm, ctx->stream>>>(c16, start, count, ctx->mpat.p, np, o);
             else k_score<uint16_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c16, start, count, ctx->mpat.p, np, o);
         } else {
-            if (lds) k_score<uint32_t, true><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c32, start, count, ctx->mpat.p, np, o);
+            if (lds) k_score<uint32_t, true><<<(unsigned)g, SC_THREADS, shm, ctx->stream>>>(c32, start, count, ctx->mpat.p, np, o);
             else k_score<uint32_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c32, start, count, ctx->mpat.p, np, o);
         }
         SPK_HIP(hipGetLastError());

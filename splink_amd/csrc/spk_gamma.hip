@@ -1418,9 +1418,13 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap) {
                                                                                        ctx->xlist.p, ctx->xinfo.p);
     // (running this launch on a second stream beside the Levenshtein pass measured no faster:
     // 1.198-1.205 ms per cfg2 pass either way)
+    for (int c = 0; c < K; ++c)
+        if (c < (int)ctx->xev_used.size()) ctx->xev_used[c] = 0;
     if (jw.n) {
+        SPK_TRY(ctx->xbegin(jk.k[0]));
         k_gamma_exact_simple<false><<<(unsigned)(G.g_exact * jw.n), X_THREADS, 0, ctx->stream>>>(A, jw, ctx->xlist.p,
                                                                                                 ctx->xinfo.p);
+        SPK_TRY(ctx->xend(jk.k[0]));
         k_gamma_slow<<<dim3((unsigned)(4 * ctx->n_cu), (unsigned)jk.n), 64, 0, ctx->stream>>>(A, jk, ctx->xlist.p,
                                                                                              ctx->xinfo.p);
     }
@@ -1438,8 +1442,10 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap) {
             one.n = 1;
             one.g = (int)G.g_exact;
             one.si[0] = si;
+            SPK_TRY(ctx->xbegin(k));
             k_gamma_exact_simple<true><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
                                                                                           ctx->xinfo.p);
+            SPK_TRY(ctx->xend(k));
             k_gamma_slow_lev<<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
             k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
         } else if (si >= 0 && simple[si].kind == SK_STR) {
@@ -1471,7 +1477,10 @@ int settle_gammas(spk_ctx *ctx, bool *fixed) {
     SPK_TRY(settle_info(ctx, &f));
     if (fixed) *fixed = f;
     // an asynchronous EM iteration enqueued on these codes read them before the correction: repeat it
-    if (f && ctx->em_pending && ctx->em_seq == ctx->gamma_seq) SPK_TRY(em_requeue(ctx));
+    if (f && ctx->em_pending && ctx->em_seq == ctx->gamma_seq) {
+        SPK_REQUIRE(ctx->em_kind == 0, SPK_E_STATE, "codes corrected under a pending finalize (settle before the histogram)");
+        SPK_TRY(em_requeue(ctx));
+    }
     return SPK_OK;
 }
 
@@ -2011,6 +2020,22 @@ extern "C" int spk_levenshtein(spk_ctx *ctx, int64_t n, const int64_t *l_off, co
 extern "C" int spk_n_patterns(spk_ctx *ctx, int64_t *out) {
     SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
     *out = ctx->n_patterns;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_exact_ms(spk_ctx *ctx, double *out, int n) {
+    SPK_REQUIRE(ctx && out && n >= 0, SPK_E_INVALID, "spk_gammas_exact_ms: bad args");
+    SPK_HIP(hipSetDevice(ctx->device));
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    for (int k = 0; k < n; ++k) {
+        out[k] = -1.0;
+        if (k < (int)ctx->xev_used.size() && ctx->xev_used[k]) {
+            float ms = 0.f;
+            SPK_HIP(hipEventElapsedTime(&ms, ctx->xev0[k], ctx->xev1[k]));
+            out[k] = (double)ms;
+        }
+    }
     return SPK_OK;
 }
 

@@ -328,6 +328,8 @@ struct spk_ctx {
     double em_lambda = 0.0, em_one_minus = 0.0;
     std::vector<double> em_m, em_u;
     int em_n_stats = 0;
+    int em_kind = 0;                  // 0: one-launch iteration (re-enqueued on a code fix), 1: finalize of a
+                                      // caller's (all-reduced) histogram, whose codes were settled before
     hipEvent_t ev_info = nullptr;     // after spk_gammas' info-block readback
     hipEvent_t ev_stats = nullptr;    // after the EM statistics readback
 
@@ -337,6 +339,13 @@ struct spk_ctx {
     hipEvent_t ev0[2][spk::K_COUNT] = {}, ev1[2][spk::K_COUNT] = {};
     bool ev_used[2][spk::K_COUNT] = {};
     int ev_slot[spk::K_COUNT] = {};
+
+    // per comparison column: HIP events around its exact-pass launch in the last spk_gammas (timing on;
+    // the fused Jaro-Winkler launch is shared by its columns)
+    std::vector<hipEvent_t> xev0, xev1;
+    std::vector<char> xev_used;
+    int xbegin(int k);
+    int xend(int k);
 
     int begin(spk::Kern k);
     int end(spk::Kern k);

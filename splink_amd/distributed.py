@@ -42,6 +42,13 @@ def allreduce_histogram_(hist, force: bool = False):
     return hist
 
 
+def stream_ordered_reduce(device: int) -> bool:
+    """True when the histogram all-reduce can be queued on a device stream (backend nccl = RCCL), so the
+    EM exchange needs no host synchronisation; False under gloo (host-staged rehearsal)."""
+    dist = _dist()
+    return dist is not None and dist.get_backend() != "gloo"
+
+
 def allreduce_host_(arr, force: bool = False):
     """In-place sum over all ranks of a host numpy array (float64 / int64), e.g. the per-value
     (Σmp, count) tables of the term-frequency adjustment (term_frequencies.py:49-65 groups over all

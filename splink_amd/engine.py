@@ -389,31 +389,61 @@ class Job:
         n_stats = N_HEAD + 4 * sum(L + 1 for L in n_levels)
         if self.reduces_across_ranks() or self.force_reduce:
             import torch
-            n_pat = self.ctx.n_patterns()
-            hist = getattr(self, "_hist_dev", None)
-            if hist is None or hist.numel() != n_pat:
-                hist = torch.empty(n_pat, dtype=torch.int64, device=f"cuda:{self.device}")
-                # the buffer is written on the context's stream: torch's allocation work must be done
-                torch.cuda.synchronize(self.device)
-                self._hist_dev = hist
+            hist = self._device_hist()
             self.ctx.em_histogram(hist.data_ptr())  # zeroes, fills and synchronises its stream
             D.allreduce_histogram_(hist, force=self.force_reduce)
             torch.cuda.synchronize(self.device)
             return self.ctx.em_finalize(hist.data_ptr(), lam_d, one_minus, m, u, n_stats)
         return self.ctx.em_iteration(lam_d, one_minus, m, u, n_stats)
 
+    def _device_hist(self):
+        import torch
+        n_pat = self.ctx.n_patterns()
+        hist = getattr(self, "_hist_dev", None)
+        if hist is None or hist.numel() != n_pat:
+            hist = torch.empty(n_pat, dtype=torch.int64, device=f"cuda:{self.device}")
+            # the buffer is written on the context's stream: torch's allocation work must be done
+            torch.cuda.synchronize(self.device)
+            self._hist_dev = hist
+        return hist
+
+    def _collective_stream(self):
+        """The torch stream this job's context runs on once its EM exchange is stream-ordered (RCCL):
+        histogram -> all-reduce -> finalize are then queued back to back with no host synchronisation."""
+        import torch
+        s = getattr(self, "_dist_stream", None)
+        if s is None:
+            s = torch.cuda.Stream(device=self.device)
+            torch.cuda.synchronize(self.device)
+            self.ctx.sync()
+            self.ctx.set_stream(s.cuda_stream)
+            self._dist_stream = s
+        return s
+
     def em_start(self, lam, level_probs):
         """em_stats in two halves: enqueue the iteration now, collect its statistics with em_wait().  On
         one GPU the launch and the statistics readback are asynchronous (spk_em_iteration_start), so the
-        next comparison pass can be queued and the host M-step computed while the device works; with a
-        cross-rank reduction the iteration runs synchronously here."""
-        if self.reduces_across_ranks() or self.force_reduce:
-            self._em_done = self.em_stats(lam, level_probs)
-            return
+        next comparison pass can be queued and the host M-step computed while the device works.  With a
+        cross-rank reduction over RCCL the histogram, the all-reduce and the finalize are queued on one
+        stream (spk_em_histogram_async, dist.all_reduce, spk_em_finalize_start); under gloo (host staging)
+        the iteration runs synchronously here."""
         names, n_levels = self.code_meta
-        m, u = self.flat_tables(level_probs)
         self._em_n_stats = N_HEAD + 4 * sum(L + 1 for L in n_levels)
         self._em_done = None
+        if self.reduces_across_ranks() or self.force_reduce:
+            if not D.stream_ordered_reduce(self.device):
+                self._em_done = self.em_stats(lam, level_probs)
+                return
+            import torch
+            m, u = self.flat_tables(level_probs)
+            s = self._collective_stream()
+            hist = self._device_hist()
+            self.ctx.em_histogram_async(hist.data_ptr())
+            with torch.cuda.stream(s):
+                D.allreduce_histogram_(hist, force=self.force_reduce)
+            self.ctx.em_finalize_start(hist.data_ptr(), float(lam), float(1 - lam), m, u, self._em_n_stats)
+            return
+        m, u = self.flat_tables(level_probs)
         self.ctx.em_iteration_start(float(lam), float(1 - lam), m, u, self._em_n_stats)
 
     def em_wait(self):

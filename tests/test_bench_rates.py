@@ -1,5 +1,5 @@
-"""bench.string_rates on a stub job (host logic only, no GPU): Σ len_l·len_r over the pairs of each
-Levenshtein column, comparisons per second over the γ-pass time."""
+"""bench.string_rates on a stub job (host logic only, no GPU): DP cells (len_l·len_r) of the cells in each
+Levenshtein column's exact list over that launch's time, comparisons per second over the γ-pass time."""
 import os
 import sys
 
@@ -10,10 +10,23 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 
+class _StubCtx:
+    def gammas_exact_counts(self, n):
+        return [0, 2][:n]
+
+    def gammas_exact_ms(self, n):
+        return [-1.0, 0.5][:n]
+
+    def gammas_exact_list(self, k, n):
+        assert k == 1 and n == 2
+        return np.array([1, 3], dtype=np.int32)  # pair ordinals the Levenshtein exact pass evaluated
+
+
 class _StubJob:
     def __init__(self, table, l, r):
         self.tables = [table]
         self._lr = (np.asarray(l, dtype=np.int32), np.asarray(r, dtype=np.int32))
+        self.ctx = _StubCtx()
 
     def pair_rows(self):
         return self._lr
@@ -27,9 +40,11 @@ def test_string_rates_counts_dp_cells_and_rates():
     ]}
     l, r = [0, 0, 1, 2], [1, 3, 3, 3]
     out = bench.string_rates(_StubJob(t, l, r), st, len(l), g_ms=2.0)
-    # email code points: 3, null (0), 4, 3 -> 3*0 + 3*3 + 0*3 + 4*3
-    assert out["lev_dp_cells_per_pass"] == 21
-    assert np.isclose(out["lev_effective_gcups"], 21 / 2e-3 / 1e9)
+    lev = out["levenshtein_exact_pass"]["email"]
+    # listed pairs 1 (rows 0, 3: 3 x 3 code points) and 3 (rows 2, 3: 4 x 3)
+    assert lev["dp_cells"] == 21 and lev["exact_cells"] == 2
+    assert np.isclose(lev["gcups"], 21 / 0.5e-3 / 1e9)
+    assert np.isclose(lev["exact_cells_per_s"], 2 / 0.5e-3)
     assert np.isclose(out["comparisons_per_s"], 4 * 2 / 2e-3)
     assert np.isclose(out["jw_comparisons_per_s"], 4 / 2e-3)
     assert np.isclose(out["lev_comparisons_per_s"], 4 / 2e-3)

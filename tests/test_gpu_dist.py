@@ -70,3 +70,45 @@ def test_nccl_histogram_allreduce_matches_single_gpu(nccl_group):
     D.allreduce_histogram_(hist, force=True)
     torch.cuda.synchronize()
     assert int(hist.sum().item()) == job.n_pairs and int(hist.min().item()) >= 0
+
+
+def test_nccl_stream_ordered_em_matches_single_gpu(nccl_group):
+    """The N-GPU iteration with no host synchronisation (bench.py's pipelined multi-GPU step): the context
+    moves onto a torch stream, spk_em_histogram_async -> dist.all_reduce on that stream (RCCL) ->
+    spk_em_finalize_start, collected by em_wait while the next comparison pass is already queued.  The
+    statistics equal the one-launch single-GPU iteration every iteration."""
+    import copy
+
+    from splink_amd.engine import Job, m_step_rows
+    from splink_amd.params import Params
+    from splink_amd.session import AmdSession
+    from splink_amd.synthetic import cfg_settings, make_records
+    df = make_records(30000, seed=32, surname_vocab=600, first_vocab=400, city_vocab=100)[["unique_id"] + COLS]
+    st = cfg_settings(2, max_iterations=4)
+    pa, pb = Params(copy.deepcopy(st), AmdSession(0)), Params(copy.deepcopy(st), AmdSession(0))
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(pa.settings["blocking_rules"])
+    job.gammas(pa.settings)
+    names, nlev = job.code_meta
+    hist_a = []
+    job.force_reduce = True
+    pending = False
+    for _ in range(4):  # pipelined, stream-ordered RCCL exchange
+        job.gammas(pa.settings)
+        if pending:
+            s = job.em_wait()
+            hist_a.append(s)
+            pa._update_params(*m_step_rows(s, names, nlev))
+        job.em_start(pa.params["λ"], pa._level_probabilities())
+        pending = True
+    s = job.em_wait()
+    hist_a.append(s)
+    pa._update_params(*m_step_rows(s, names, nlev))
+    assert getattr(job, "_dist_stream", None) is not None
+    job.force_reduce = False
+    for i in range(4):  # one-launch iteration on the same context (now on the torch stream)
+        job.gammas(pb.settings)
+        s = job.em_stats(pb.params["λ"], pb._level_probabilities())
+        assert np.array_equal(s, hist_a[i], equal_nan=True), i
+        pb._update_params(*m_step_rows(s, names, nlev))
+    assert pa.params["λ"] == pb.params["λ"]
