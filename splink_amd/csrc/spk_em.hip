@@ -89,6 +89,8 @@ __global__ __launch_bounds__(H_THREADS) void k_hist(const CodeT *__restrict__ co
 constexpr int HL_THREADS = 1024;
 constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS (gfx950), capped by the device attribute
 constexpr int HL_UNROLL = 4;
+constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups per group
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Comparison-pattern arithmetic.  The pattern space description (mixed-radix strides, levels,
@@ -355,59 +357,86 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     if (blockIdx.x == 0)  // tail (P not a multiple of VEC)
         for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
     __syncthreads();
-    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
-        uint32_t s = 0;
-#pragma unroll
-        for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
-        part[(int64_t)blockIdx.x * part_stride(n_pat) + b] = s;
-    }
-    // last-workgroup-done: every wave's atomics complete, then one release + ticket (k_prefix's pattern)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // The rows' sum per bin with every thread of the workgroup: work item (quad of 4 bins, row group)
-    // sums the rows b = group, group + Gr, ... with 16-byte loads, 8 in flight; the groups' partials
-    // meet in LDS (the counters are no longer needed).  Counts are exact integers (< 2^32: P < 2^32 is
-    // checked on the host), so the order of the additions does not matter.  One thread per bin summed
-    // all G rows before: G / 8 dependent load rounds from other XCDs' lines, ~90 us per cfg2 iteration.
+    // Two-level last-arriver reduction of the workgroups' count rows (exact integers, so the order of
+    // the additions does not matter).  Each row is stored write-through (sc1, 16 B per lane) and drained
+    // by every storing wave, then one lane's ticket atomic: no release fence (its L2 write-back costs
+    // 1.7 us or more per workgroup; MI355X_MICROARCH.md visibility table, cdna_hip_programming.md G16 R1).
+    // The last of each group of EM_GROUP workgroups sums the group's rows into a group row; the last
+    // group sums those.  One workgroup summing all G rows was bound by one CU's load bandwidth (590 KB
+    // for cfg2's 576 patterns, ~15 us of a 60 us iteration).
     const int64_t ps = part_stride(n_pat);
+    const int Q = (int)(ps / 4);  // quads of 4 bins per row (the row's padding bins are zero)
     const int G = (int)gridDim.x;
-    const int Q = (n_pat + 3) / 4;
-    int Gr = HL_THREADS / Q;
-    const int fit = (int)(((int64_t)n_pat * R * 4) / ((int64_t)Q * 16));  // partials within the counters' LDS
-    Gr = Gr < fit ? Gr : fit;
-    Gr = Gr < G ? Gr : G;
-    Gr = Gr > 1 ? Gr : 1;
-    u32x4 *sp = reinterpret_cast<u32x4 *>(sh);  // [Gr][Q]
-    for (int it = threadIdx.x; it < Q * Gr; it += HL_THREADS) {
-        const int q = it % Q, gr = it / Q;
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(part) + q;
-        const int64_t rs = ps / 4;  // row stride in quads
-        u32x4 a[8];
+    const int NG = (G + EM_GROUP - 1) / EM_GROUP;
+    const int grp = (int)blockIdx.x / EM_GROUP;
+    const int gsz = G - grp * EM_GROUP < EM_GROUP ? G - grp * EM_GROUP : EM_GROUP;
+    uint32_t *part2 = part + (int64_t)G * ps;  // group rows follow the workgroup rows
+    auto publish = [&](uint32_t *row, const u32x4 *vals_lds) {
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void *)row, (short)0, (int)(ps * 4), 0x00020000);
+        for (int q = threadIdx.x; q < Q; q += HL_THREADS) __builtin_amdgcn_raw_buffer_store_b128(vals_lds[q], prs, q * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+        __syncthreads();
+    };
+    auto arrive = [&](unsigned int *t, unsigned int last) {  // true in the last arriver (whole workgroup)
+        if (threadIdx.x == 0) s_last = atomicAdd(t, 1u) == last;
+        __syncthreads();
+        if (!s_last) return false;
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        return true;
+    };
+    // rows [r0, r0 + n) summed per quad into LDS (up to 16 loads in flight per thread)
+    u32x4 *sq = reinterpret_cast<u32x4 *>(sh);
+    auto sum_rows = [&](const uint32_t *rows, int n) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(rows);
+        for (int q = threadIdx.x; q < Q; q += HL_THREADS) {
+            u32x4 a[16];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = u32x4{0u, 0u, 0u, 0u};
-        int b = gr;
-        for (; b + 7 * Gr < G; b += 8 * Gr)
+            for (int j = 0; j < 16; ++j) a[j] = u32x4{0u, 0u, 0u, 0u};
+            for (int b = 0; b < n; b += 16)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) a[j] += src[(int64_t)(b + j * Gr) * rs];
-        for (; b < G; b += Gr) a[0] += src[(int64_t)b * rs];
-        sp[gr * Q + q] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+                for (int j = 0; j < 16; ++j)
+                    if (b + j < n) a[j] += src[(int64_t)(b + j) * (ps / 4) + q];
+#pragma unroll
+            for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+                for (int j = 0; j < w; ++j) a[j] += a[j + w];
+            sq[q] = a[0];
+        }
+        __syncthreads();
+    };
+    // this workgroup's row straight from its counters (a quad of bins per lane, 16-byte sc1 stores)
+    {
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(part + (int64_t)blockIdx.x * ps), (short)0, (int)(ps * 4), 0x00020000);
+        for (int q = threadIdx.x; q < Q; q += HL_THREADS) {
+            u32x4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int b = 4 * q + j;
+                uint32_t s = 0;
+                if (b < n_pat)
+#pragma unroll
+                    for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
+                v[j] = s;
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, prs, q * 16, 0, 16);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+        __syncthreads();
     }
-    __syncthreads();
+    if (!arrive(ticket + 1 + grp, (unsigned int)(gsz - 1))) return;
+    if (threadIdx.x == 0) atomicExch(ticket + 1 + grp, 0u);  // ready for the next launch
+    sum_rows(part + (int64_t)grp * EM_GROUP * ps, gsz);
+    publish(part2 + (int64_t)grp * ps, sq);
+    if (!arrive(ticket, (unsigned int)(NG - 1))) return;
+    sum_rows(part2, NG);
     // thread t owns bins p = t, t + HL_THREADS, ... (the same mapping as em_finalize_block's loop, so
     // the count it parks in cpat is read back by the thread that wrote it)
     const uint32_t *sp1 = reinterpret_cast<const uint32_t *>(sh);
     for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
-        unsigned long long c = 0;
-        for (int gr = 0; gr < Gr; ++gr) c += sp1[gr * 4 * Q + p];
+        const unsigned long long c = sp1[p];
         if (FIN) cpat[p] = (double)c;
         else out_hist[p] = c;
     }
@@ -550,11 +579,14 @@ static int64_t lane_grid(spk_ctx *ctx) {
 // The padded accumulation histogram and the ticket of k_em_iter: zero between launches (the last workgroup
 // resets them), zeroed here only when (re)allocated.
 static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket) {
-    const size_t need = (size_t)part_stride(ctx->n_patterns) * (size_t)ctx->n_cu;
+    // k_em_iter: one count row per workgroup (<= n_cu), then one per group of EM_GROUP workgroups;
+    // tickets [final | per group]
+    const int64_t n_groups = ((int64_t)ctx->n_cu + EM_GROUP - 1) / EM_GROUP;
+    const size_t need = (size_t)part_stride(ctx->n_patterns) * (size_t)(ctx->n_cu + n_groups);
     SPK_TRY(ctx->hist_part.alloc(need));
-    if (!ctx->em_ticket.p) {
-        SPK_TRY(ctx->em_ticket.alloc(1));
-        SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, 4, ctx->stream));
+    if (!ctx->em_ticket.p || ctx->em_ticket.n < (size_t)(1 + n_groups)) {
+        SPK_TRY(ctx->em_ticket.alloc((size_t)(1 + n_groups)));
+        SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, (size_t)(1 + n_groups) * 4, ctx->stream));
     }
     *acc = ctx->hist_part.p;
     *ticket = ctx->em_ticket.p;

@@ -36,11 +36,20 @@ struct FCommon {
     int32_t und_same;        // equal keys without dictionary ids: the exact pass compares the units
 };
 
+struct FEq {
+    FCommon c;
+    int32_t lv_same, lv_diff;
+};
+
 struct FJw {
     FCommon c;
     int64_t h0, h1;  // planes of the four head units (low 8 bytes of the next chunk)
     int32_t lv_one, lv_zero, lv_bound;
     float cf;        // undecided iff the fp32 upper bound >= cf (+inf: never)
+    // An equality column whose 8-byte field fills the high half of the head chunk (layout_image puts
+    // EQ fields in those gaps): one 16-byte load per side serves both, instead of two 8-byte loads.
+    int32_t geq;
+    FEq ge;
 };
 
 struct FLev {
@@ -49,11 +58,6 @@ struct FLev {
     int32_t n;  // the chain of tests that can hold for unequal strings
     int32_t kind[MAX_TESTS], a[MAX_TESTS], cmp[MAX_TESTS], level[MAX_TESTS];
     double t[MAX_TESTS];
-};
-
-struct FEq {
-    FCommon c;
-    int32_t lv_same, lv_diff;
 };
 
 struct FNum {
@@ -148,21 +152,35 @@ __device__ __attribute__((always_inline)) inline bool implied(const FCommon &c, 
 template <int FP>
 struct JwData {
     uint4 a[FP], b[FP];
-    uint2 ha[FP], hb[FP];
+    uint4 qa[FP], qb[FP];  // head chunk: head units in .x / .y, the gap EQ field (if any) in .z / .w
 };
 template <int FP>
 __device__ __attribute__((always_inline)) inline void ld_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
                                                             const uint32_t (&oy)[FP], JwData<FP> &d) {
     load16<FP>(A, J.c.p0, J.c.p1, ox, oy, d.a, d.b);
-    load8<FP>(A, J.h0, J.h1, 0, ox, oy, d.ha, d.hb);
+    if (J.geq) {  // kernel-argument (wave-uniform) branch
+        load16<FP>(A, J.h0, J.h1, ox, oy, d.qa, d.qb);
+    } else {
+        uint2 ha[FP], hb[FP];
+        load8<FP>(A, J.h0, J.h1, 0, ox, oy, ha, hb);
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            d.qa[u] = make_uint4(ha[u].x, ha[u].y, 0u, 0u);
+            d.qb[u] = make_uint4(hb[u].x, hb[u].y, 0u, 0u);
+        }
+    }
 }
 template <int FP>
 __device__ __attribute__((always_inline)) inline void ev_jw(const FJw &J, const JwData<FP> &d, const bool (&act)[FP],
                                                             uint32_t (&acc)[FP], bool (&und)[FP]) {
     const uint4(&a)[FP] = d.a;
     const uint4(&b)[FP] = d.b;
-    const uint2(&ha)[FP] = d.ha;
-    const uint2(&hb)[FP] = d.hb;
+    uint2 ha[FP], hb[FP];
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        ha[u] = make_uint2(d.qa[u].x, d.qa[u].y);
+        hb[u] = make_uint2(d.qb[u].x, d.qb[u].y);
+    }
     bool same[FP], nul[FP], zero[FP];
     int lf[FP], ls[FP];
     bool need = false;
@@ -357,9 +375,9 @@ constexpr int N_FCOLS = FJ_MAX + FL_MAX + FE_MAX + FN_MAX;
 // their evaluation, then one wave-aggregated append of the undecided cells.
 template <int FP, int MINW, bool C32>
 __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
-    __shared__ unsigned int s_cnt[N_FCOLS];
+    __shared__ unsigned int s_cnt[N_FCOLS + FJ_MAX];  // work-list lengths: per column slot, then JW gap EQs
     extern __shared__ int16_t s_thr[];  // A.thr (dynamic LDS: n_thr entries)
-    if (threadIdx.x < N_FCOLS) s_cnt[threadIdx.x] = 0;
+    if (threadIdx.x < N_FCOLS + FJ_MAX) s_cnt[threadIdx.x] = 0;
     for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -393,13 +411,37 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
 #pragma unroll 1
         for (int j = 0; j < A.nj; ++j) {
             const FJw &J = A.jw[j];
-            if (implied(J.c, base, SPAN)) {
+            const bool ji = implied(J.c, base, SPAN);
+            const bool gi = J.geq && implied(J.ge.c, base, SPAN);
+            if (ji) {
 #pragma unroll
                 for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
+            }
+            if (gi) {
+#pragma unroll
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
+            }
+            if (ji) {
+                if (J.geq && !gi) {  // only the gap EQ field is needed
+                    f_eq<FP>(A, J.ge, ox, oy, act, acc, und);
+                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+                }
                 continue;
             }
-            f_jw<FP>(A, J, ox, oy, act, acc, und);
+            JwData<FP> d;
+            ld_jw<FP>(A, J, ox, oy, d);
+            ev_jw<FP>(J, d, act, acc, und);
             append<FP>(A, J.c, r0, &s_cnt[j], und, p);
+            if (J.geq && !gi) {
+                Data8<FP> e;
+#pragma unroll
+                for (int u = 0; u < FP; ++u) {
+                    e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
+                    e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
+                }
+                ev_eq<FP>(J.ge, e, act, acc, und);
+                if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+            }
         }
 #pragma unroll 1
         for (int j = 0; j < A.nl; ++j) {
@@ -443,109 +485,8 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
         A.region_count[(int64_t)A.eq[t - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[t];
     else if (t >= FJ_MAX + FL_MAX + FE_MAX && t < FJ_MAX + FL_MAX + FE_MAX + A.nn)
         A.region_count[(int64_t)A.num[t - FJ_MAX - FL_MAX - FE_MAX].c.k * A.n_regions + slot] = 0;
-}
-
-// The same filter for a fixed column layout (NJ Jaro-Winkler, NL Levenshtein, NE equality columns, no
-// numeric ones): every column's loads for the lane's FP pairs are issued before any column is
-// evaluated, so one iteration pays one memory round trip instead of one per column.
-template <int NJ, int NL, int NE, int FP, int MINW, bool C32>
-__global__ __launch_bounds__(F_THREADS, MINW) void k_filter_sig(const FiltArgs A) {
-    __shared__ unsigned int s_cnt[N_FCOLS];
-    extern __shared__ int16_t s_thr[];
-    if (threadIdx.x < N_FCOLS) s_cnt[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
-    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
-    constexpr int SPAN = 64 * FP;
-    constexpr int STEP = (F_THREADS / 64) * SPAN;
-    const uint32_t end = (uint32_t)r1;
-    uint32_t base = (uint32_t)r0 + (uint32_t)(threadIdx.x >> 6) * SPAN;
-    int32_t nx[FP], ny[FP];
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        const uint32_t q = base + u * 64 + lane;
-        nx[u] = q < end ? A.pl[q] : 0;
-        ny[u] = q < end ? A.pr[q] : 0;
-    }
-    for (; base < end; base += STEP) {  // wave-uniform
-        uint32_t p[FP], ox[FP], oy[FP], acc[FP];
-        bool act[FP], und[FP];
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            p[u] = base + u * 64 + lane;
-            act[u] = p[u] < end;
-            ox[u] = (uint32_t)nx[u] << 4;
-            oy[u] = (uint32_t)ny[u] << 4;
-            acc[u] = 0;
-            const uint32_t q = p[u] + STEP;
-            nx[u] = q < end ? A.pl[q] : 0;
-            ny[u] = q < end ? A.pr[q] : 0;
-        }
-        JwData<FP> dj[NJ > 0 ? NJ : 1];
-        Data16<FP> dl[NL > 0 ? NL : 1];
-        Data8<FP> de[NE > 0 ? NE : 1];
-        bool ij[NJ > 0 ? NJ : 1], il[NL > 0 ? NL : 1], ie[NE > 0 ? NE : 1];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            ij[j] = implied(A.jw[j].c, base, SPAN);
-            if (!ij[j]) ld_jw<FP>(A, A.jw[j], ox, oy, dj[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            il[j] = implied(A.lev[j].c, base, SPAN);
-            if (!il[j]) load16<FP>(A, A.lev[j].c.p0, A.lev[j].c.p1, ox, oy, dl[j].a, dl[j].b);
-        }
-#pragma unroll
-        for (int j = 0; j < NE; ++j) {
-            ie[j] = implied(A.eq[j].c, base, SPAN);
-            if (!ie[j]) load8<FP>(A, A.eq[j].c.p0, A.eq[j].c.p1, A.eq[j].c.in, ox, oy, de[j].a, de[j].b);
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            if (ij[j]) {
-#pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? A.jw[j].c.imp_add : 0u;
-                continue;
-            }
-            ev_jw<FP>(A.jw[j], dj[j], act, acc, und);
-            append<FP>(A, A.jw[j].c, r0, &s_cnt[j], und, p);
-        }
-#pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            if (il[j]) {
-#pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? A.lev[j].c.imp_add : 0u;
-                continue;
-            }
-            ev_lev<FP>(A.lev[j], s_thr, dl[j], act, acc, und);
-            append<FP>(A, A.lev[j].c, r0, &s_cnt[FJ_MAX + j], und, p);
-        }
-#pragma unroll
-        for (int j = 0; j < NE; ++j) {
-            if (ie[j]) {
-#pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? A.eq[j].c.imp_add : 0u;
-                continue;
-            }
-            ev_eq<FP>(A.eq[j], de[j], act, acc, und);
-            if (A.eq[j].c.und_same) append<FP>(A, A.eq[j].c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
-        }
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            if (!act[u]) continue;
-            if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
-            else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
-        }
-    }
-    __syncthreads();
-    const int64_t slot = A.region_base + blockIdx.x;
-    const int t = threadIdx.x;
-    if (t < NJ) A.region_count[(int64_t)A.jw[t].c.k * A.n_regions + slot] = s_cnt[t];
-    else if (t >= FJ_MAX && t < FJ_MAX + NL) A.region_count[(int64_t)A.lev[t - FJ_MAX].c.k * A.n_regions + slot] = s_cnt[t];
-    else if (t >= FJ_MAX + FL_MAX && t < FJ_MAX + FL_MAX + NE)
-        A.region_count[(int64_t)A.eq[t - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[t];
+    else if (t >= N_FCOLS && t < N_FCOLS + A.nj && A.jw[t - N_FCOLS].geq)
+        A.region_count[(int64_t)A.jw[t - N_FCOLS].ge.c.k * A.n_regions + slot] = s_cnt[t];
 }
 
 // ---- host: the per-column decision constants --------------------------------------------------------------
@@ -686,24 +627,35 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     F.region_base = (int)region_lo;
     F.thr = A.thr;
     F.n_thr = A.n_thr;
+    std::vector<int> jw_off2;  // head-chunk offset of each JW slot
     for (const SimpleCol &s : simple) {
         switch (s.cls) {
-            case SC_JW: SPK_REQUIRE(F.nj < FJ_MAX, SPK_E_INVALID, "filter: JW slots"); make_jw(s, A, F.jw[F.nj++]); break;
+            case SC_JW:
+                SPK_REQUIRE(F.nj < FJ_MAX, SPK_E_INVALID, "filter: JW slots");
+                jw_off2.push_back(s.off2);
+                make_jw(s, A, F.jw[F.nj++]);
+                break;
             case SC_LEV: SPK_REQUIRE(F.nl < FL_MAX, SPK_E_INVALID, "filter: LEV slots"); make_lev(s, A, F.lev[F.nl++]); break;
-            case SC_EQ: SPK_REQUIRE(F.ne < FE_MAX, SPK_E_INVALID, "filter: EQ slots"); make_eq(s, A, F.eq[F.ne++]); break;
+            case SC_EQ: break;  // below
             case SC_NUM: SPK_REQUIRE(F.nn < FN_MAX, SPK_E_INVALID, "filter: NUM slots"); make_num(s, A, F.num[F.nn++]); break;
             default: SPK_REQUIRE(false, SPK_E_INVALID, "filter: column without a filter class");
         }
     }
+    for (const SimpleCol &s : simple) {
+        if (s.cls != SC_EQ) continue;
+        int host = -1;  // a JW slot whose head chunk's high half is this column's field
+        for (int j = 0; j < F.nj && host < 0; ++j)
+            if (!F.jw[j].geq && (jw_off2[j] & 15) == 0 && s.off == jw_off2[j] + 8) host = j;
+        if (host >= 0) {
+            F.jw[host].geq = 1;
+            make_eq(s, A, F.jw[host].ge);
+            continue;
+        }
+        SPK_REQUIRE(F.ne < FE_MAX, SPK_E_INVALID, "filter: EQ slots");
+        make_eq(s, A, F.eq[F.ne++]);
+    }
     const unsigned g = (unsigned)(region_hi - region_lo);
     const size_t shm = (size_t)A.n_thr * sizeof(int16_t);
-#ifdef SPK_FILTER_SIG
-    if (A.code16 && F.nj == 2 && F.nl == 1 && F.ne == 2 && F.nn == 0) {
-        k_filter_sig<2, 1, 2, SPK_FILTER_SIG, SPK_FILTER_SIG_W, false><<<g, F_THREADS, shm, stream>>>(F);
-        SPK_HIP(hipGetLastError());
-        return SPK_OK;
-    }
-#endif
     if (A.code16) k_filter<3, 5, false><<<g, F_THREADS, shm, stream>>>(F);
     else k_filter<3, 5, true><<<g, F_THREADS, shm, stream>>>(F);
     SPK_HIP(hipGetLastError());
