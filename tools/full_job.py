@@ -142,7 +142,7 @@ def main():
     for _ in range(a.iters):
         stats = job.em_stats(params.params["λ"], params._level_probabilities())
         ms = job.ctx.kernel_ms()
-        em_dev.append(ms["em_hist"] + ms["em_final"])
+        em_dev.append(ms["em_hist"] + max(ms["em_final"], 0.0))  # em_final = -1: one launch
         lam, rows = m_step_rows(stats, names, nlev)
         params._update_params(lam, rows)
     wall["em_iterations"] = time.perf_counter() - t
