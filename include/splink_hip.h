@@ -227,7 +227,9 @@ int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n);
  * (spk_filter.hip); every other column by the general interpreter.  on = 1 (default): template
  * columns through the filter kernel; on = 0: every column through the interpreter; + 10: the second
  * blocking rule's pairs always read the table-ordered row image, + 20: always their rule's
- * view-ordered copy (default: the copy once the image outgrows the caches).  All modes give
+ * view-ordered copy (default: the copy once the image outgrows the caches); + 100: leave every slow-list
+ * launch to the settlement at the next synchronising call (by default only those of columns whose slow
+ * lists were empty in the last call with the same pairs, tables and program).  All modes give
  * identical results (for testing).  spk_gammas_simple_count: how many columns the last spk_gammas
  * took as template columns. */
 int spk_gammas_set_simple(spk_ctx *ctx, int on);

@@ -159,6 +159,20 @@ __global__ void k_pattern_mp(PatArgs A0, double *__restrict__ mpat, double *__re
 
 constexpr int N_HEAD = 5;  // [Σmp, rows, non-null rows, Σ ln(...), non-null ln rows]
 
+// Diagnostic build only (-DSPK_EM_STAMPS): wall-clock stamps (100 MHz) of k_em_iter's stages in the
+// workgroup that finishes the reduction, read with spk_debug_em_stamps (tools/ab_em_stamps.py).
+#ifdef SPK_EM_STAMPS
+__device__ unsigned long long g_em_stamps[16];
+#define EM_STAMP(i) \
+    do {            \
+        if (threadIdx.x == 0) g_em_stamps[i] = wall_clock64(); \
+    } while (0)
+#else
+#define EM_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
 // ---- one EM iteration in one launch (single GPU) ----------------------------------------------------------
 // The E-step per pattern and the M-step sums of the whole pattern space, by ONE workgroup of
 // EF_THREADS: each thread evaluates its strided patterns (mp, ln, count) into LDS (global arrays past
@@ -223,6 +237,7 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
     }
     __threadfence_block();
     __syncthreads();
+    EM_STAMP(8);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n_waves = blockDim.x >> 6;
     for (int slot = wave; slot <= A.n_slots; slot += n_waves) {  // wave-uniform
         int kk = -1, vv = 0;
@@ -303,6 +318,10 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     extern __shared__ uint32_t sh[];
     __shared__ bool s_last;
     const int n_pat = A0.n_pat;
+#ifdef SPK_EM_STAMPS
+    const unsigned long long t_start = wall_clock64();
+    if (blockIdx.x == 0) EM_STAMP(0);
+#endif
     for (int b = threadIdx.x; b < n_pat * R; b += HL_THREADS) sh[b] = 0;
     __syncthreads();
     constexpr int VEC = 16 / sizeof(CodeT);
@@ -426,12 +445,31 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
         __syncthreads();
     }
+#ifdef SPK_EM_STAMPS
+    const unsigned long long t_pub = wall_clock64();
+#endif
     if (!arrive(ticket + 1 + grp, (unsigned int)(gsz - 1))) return;
     if (threadIdx.x == 0) atomicExch(ticket + 1 + grp, 0u);  // ready for the next launch
+#ifdef SPK_EM_STAMPS
+    const unsigned long long t_g0 = wall_clock64();
+#endif
     sum_rows(part + (int64_t)grp * EM_GROUP * ps, gsz);
     publish(part2 + (int64_t)grp * ps, sq);
+#ifdef SPK_EM_STAMPS
+    const unsigned long long t_g1 = wall_clock64();
+#endif
     if (!arrive(ticket, (unsigned int)(NG - 1))) return;
+#ifdef SPK_EM_STAMPS
+    if (threadIdx.x == 0) {
+        g_em_stamps[1] = t_start;
+        g_em_stamps[2] = t_pub;
+        g_em_stamps[3] = t_g0;
+        g_em_stamps[4] = t_g1;
+    }
+    EM_STAMP(5);
+#endif
     sum_rows(part2, NG);
+    EM_STAMP(6);
     // thread t owns bins p = t, t + HL_THREADS, ... (the same mapping as em_finalize_block's loop, so
     // the count it parks in cpat is read back by the thread that wrote it)
     const uint32_t *sp1 = reinterpret_cast<const uint32_t *>(sh);
@@ -446,9 +484,11 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         const PatArgs &A = stage_args(A0, sA);
         double *tab = reinterpret_cast<double *>(sh) + (sizeof(PatArgs) + 7) / 8;
         const bool room = ((sizeof(PatArgs) + 7) / 8 + 3 * (size_t)n_pat) * 8 <= (size_t)n_pat * R * 4;
+        EM_STAMP(7);
         em_finalize_block(A, [&](int p) { return (unsigned long long)cpat[p]; }, mpat, llpat, cpat, out,
                           room ? tab : nullptr);
     }
+    EM_STAMP(9);
     if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
@@ -762,6 +802,14 @@ static int enqueue_em(spk_ctx *ctx) {
 namespace spk {
 int em_requeue(spk_ctx *ctx) { return enqueue_em(ctx); }
 }  // namespace spk
+
+#ifdef SPK_EM_STAMPS
+extern "C" int spk_debug_em_stamps(uint64_t *out) {
+    SPK_HIP(hipDeviceSynchronize());
+    SPK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_em_stamps), sizeof(uint64_t) * 16));
+    return SPK_OK;
+}
+#endif
 
 extern "C" int spk_em_iteration_start(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
                                       int n_stats) {

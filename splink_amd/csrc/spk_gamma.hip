@@ -1379,6 +1379,7 @@ struct GammaPlan {
     std::vector<SimpleCol> simple;
     std::vector<int> simple_of;
     std::vector<char> may_exact, huge_in_slow;
+    std::vector<char> slow_skipped;  // columns whose slow-list kernels this call did not launch
     int K = 0, n_regions = 0, n_info = 0, n_cnt = 0, n_all = 0;
     int64_t g_exact = 1, max_units = 1;
 };
@@ -1387,9 +1388,36 @@ struct GammaPlan {
 // The exact and slow passes over the lists the filter wrote (list capacity `cap`).  k_prefix sizes the
 // lists on the device; if they exceed `cap` every exact kernel is a no-op and settle_gammas re-runs
 // this phase with the right capacity.
-static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap) {
+// The slow-list kernels of column k (or of the fused JW columns jk): the cells the exact pass left.
+static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
+    GammaArgs &A = G.A;
+    if (jk) {
+        k_gamma_slow<<<dim3((unsigned)(4 * ctx->n_cu), (unsigned)jk->n), 64, 0, ctx->stream>>>(A, *jk, ctx->xlist.p,
+                                                                                              ctx->xinfo.p);
+    } else {
+        const int si = G.simple_of[k];
+        const bool lev = si >= 0 && G.simple[si].cls == SC_LEV;
+        const ColSet one_k{1, {k, 0, 0, 0}};
+        if (lev) {
+            k_gamma_slow_lev<<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
+            k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+        } else {
+            k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
+        }
+    }
+    SPK_HIP(hipGetLastError());
+    return SPK_OK;
+}
+
+// skip: leave out the slow-list kernels of columns whose slow lists were empty in the last settled call
+static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = false) {
     GammaArgs &A = G.A;
     const int K = G.K;
+    G.slow_skipped.assign((size_t)K, 0);
+    auto quiet = [&](int k) {
+        return skip && (ctx->slow_force_skip ||
+                        (ctx->slow_seen_valid && k < (int)ctx->slow_seen.size() && !ctx->slow_seen[k]));
+    };
     SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));
     A.slow = ctx->xlist.p + cap;
     A.slow_off = ctx->xinfo.p;
@@ -1425,8 +1453,13 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap) {
         k_gamma_exact_simple<false><<<(unsigned)(G.g_exact * jw.n), X_THREADS, 0, ctx->stream>>>(A, jw, ctx->xlist.p,
                                                                                                 ctx->xinfo.p);
         SPK_TRY(ctx->xend(jk.k[0]));
-        k_gamma_slow<<<dim3((unsigned)(4 * ctx->n_cu), (unsigned)jk.n), 64, 0, ctx->stream>>>(A, jk, ctx->xlist.p,
-                                                                                             ctx->xinfo.p);
+        bool all_quiet = true;
+        for (int c = 0; c < jk.n; ++c) all_quiet = all_quiet && quiet(jk.k[c]);
+        if (all_quiet) {
+            for (int c = 0; c < jk.n; ++c) G.slow_skipped[jk.k[c]] = 1;
+        } else {
+            SPK_TRY(enqueue_slow(ctx, G, -1, &jk));
+        }
     }
     for (int k = 0; k < K; ++k) {
         if (!G.may_exact[k]) continue;
@@ -1446,8 +1479,8 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap) {
             k_gamma_exact_simple<true><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
                                                                                           ctx->xinfo.p);
             SPK_TRY(ctx->xend(k));
-            k_gamma_slow_lev<<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
-            k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+            if (quiet(k)) G.slow_skipped[k] = 1;
+            else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
         } else if (si >= 0 && simple[si].kind == SK_STR) {
             ExactCols one{};
             one.n = 1;
@@ -1455,7 +1488,8 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap) {
             one.si[0] = si;
             k_gamma_exact_simple<false><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
                                                                                            ctx->xinfo.p);
-            k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
+            if (quiet(k)) G.slow_skipped[k] = 1;
+            else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
         } else {
             k_gamma_exact<<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
             k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
@@ -1508,6 +1542,28 @@ static int settle_info(spk_ctx *ctx, bool *fixed) {
         }
     }
     const unsigned int *h_slow = reinterpret_cast<const unsigned int *>(ctx->h_info + G.n_info);
+    {  // slow-list kernels this call left out although the exact pass did list cells: run them now
+        bool ran = false;
+        ColSet jk{};
+        for (int k = 0; k < K; ++k) {
+            if (k >= (int)G.slow_skipped.size() || !G.slow_skipped[k] || !h_slow[k]) continue;
+            const int si = G.simple_of[k];
+            const bool lev = si >= 0 && G.simple[si].cls == SC_LEV;
+            if (!lev && jk.n < 4) jk.k[jk.n++] = k;
+            else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
+            ran = true;
+        }
+        if (jk.n) SPK_TRY(enqueue_slow(ctx, G, -1, &jk));
+        if (ran) {
+            SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)G.n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+            SPK_HIP(hipStreamSynchronize(ctx->stream));
+            if (fixed) *fixed = true;
+        }
+        G.slow_skipped.assign((size_t)K, 0);
+    }
+    ctx->slow_seen.assign((size_t)K, 0);
+    for (int k = 0; k < K; ++k) ctx->slow_seen[k] = h_slow[k] ? 1 : 0;
+    ctx->slow_seen_valid = true;
     int err = 0;
     std::memcpy(&err, ctx->h_info + G.n_info + G.n_cnt, sizeof(err));
     if (err & 2) {
@@ -1683,6 +1739,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                  o_complex = put(complex_k.data(), complex_k.size()), o_thr = put(thr_tab.data(), thr_tab.size());
     // the device keeps the last blob: an unchanged program (every call of an EM run) is not re-sent
     const bool fresh_blob = ctx->prog_blob.p && ctx->prog_blob.n >= blob.size() && ctx->last_blob == blob;
+    if (!fresh_blob || ctx->slow_key_pairs != ctx->pairs_epoch || ctx->slow_key_tables != ctx->table_epoch)
+        ctx->slow_seen_valid = false;
+    ctx->slow_key_pairs = ctx->pairs_epoch;
+    ctx->slow_key_tables = ctx->table_epoch;
     if (!fresh_blob) {
         SPK_TRY(ctx->prog_blob.alloc(blob.size()));
         SPK_HIP(hipMemcpyAsync(ctx->prog_blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, ctx->stream));
@@ -1823,7 +1883,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         }
     }
     G.A = A;
-    SPK_TRY(enqueue_phase(ctx, G, cap));
+    SPK_TRY(enqueue_phase(ctx, G, cap, /*skip=*/true));
     SPK_TRY(ctx->end(K_GAMMA));
     SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
@@ -2072,9 +2132,11 @@ extern "C" int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n) {
 }
 
 extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
-    SPK_REQUIRE(ctx && on >= 0 && on % 10 <= 1 && on < 30, SPK_E_INVALID, "spk_gammas_set_simple: mode 0, 1 (+10 / +20)");
-    ctx->use_views = on >= 20 ? 2 : (on >= 10 ? 0 : 1);
+    SPK_REQUIRE(ctx && on >= 0 && on % 10 <= 1 && on % 100 < 30 && on < 200, SPK_E_INVALID,
+                "spk_gammas_set_simple: mode 0, 1 (+10 / +20) (+100)");
+    ctx->use_views = on % 100 >= 20 ? 2 : (on % 100 >= 10 ? 0 : 1);
     ctx->filter_mode = on % 10;
+    ctx->slow_force_skip = on >= 100;
     return SPK_OK;
 }
 

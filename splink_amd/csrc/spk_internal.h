@@ -286,6 +286,13 @@ struct spk_ctx {
     spk::GammaPlan *gplan = nullptr;
     void (*gplan_free)(spk::GammaPlan *) = nullptr;
     bool gamma_pending = false;
+    // per column: whether the last settled spk_gammas found cells on its slow list; with the same pairs,
+    // tables and program the next call does not launch the slow-list kernels of columns that had none
+    // (settle_gammas runs them if the list is not empty after all)
+    std::vector<uint8_t> slow_seen;
+    bool slow_seen_valid = false;
+    bool slow_force_skip = false;  // tests: leave every slow-list launch to settle_gammas
+    uint64_t slow_key_pairs = 0, slow_key_tables = 0;
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
     // EM state
