@@ -203,6 +203,9 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
                                   double *__restrict__ cpat, double *__restrict__ out, double *s_tab) {
     const bool lds = s_tab != nullptr && A.n_pat <= EF_LDS_PAT;  // block-uniform
     double *tc = lds ? s_tab : cpat, *tm = lds ? s_tab + A.n_pat : mpat, *tl = lds ? s_tab + 2 * A.n_pat : llpat;
+    __shared__ double s_rr[PA_MAXK];  // 1 / (L_k + 1): the digits' reciprocals, once per launch
+    if (threadIdx.x < A.K) s_rr[threadIdx.x] = 1.0 / (double)(A.nlev[threadIdx.x] + 1);
+    __syncthreads();
     for (int p = threadIdx.x; p < A.n_pat; p += blockDim.x) {
         const unsigned long long c = count(p);
         // mixed-radix digits, then the reference's left-associative products (pattern_mp)
@@ -211,7 +214,7 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
         for (int k = 0; k < A.K; ++k) {
             const int radix = A.nlev[k] + 1;
             int g;
-            q = udiv_uniform(q, radix, 1.0 / (double)radix, g);
+            q = udiv_uniform(q, radix, s_rr[k], g);
             --g;
             num = num * (g < 0 ? 1.0 : pa_m(A, A.moff[k] + g));
         }
@@ -219,7 +222,7 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
         for (int k = 0; k < A.K; ++k) {
             const int radix = A.nlev[k] + 1;
             int g;
-            q = udiv_uniform(q, radix, 1.0 / (double)radix, g);
+            q = udiv_uniform(q, radix, s_rr[k], g);
             --g;
             den = den * (g < 0 ? 1.0 : pa_u(A, A.moff[k] + g));
         }
@@ -246,19 +249,17 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
             for (kk = 0; kk < A.K && r > A.nlev[kk]; ++kk) r -= A.nlev[kk] + 1;
             vv = r - 1;
         }
+        // the slot's patterns directly: digit vv + 1 of column kk, p = a·(st·radix) + (vv + 1)·st + b
         const int st = kk >= 0 ? A.stride[kk] : 1, radix = kk >= 0 ? A.nlev[kk] + 1 : 1;
-        const double rst = 1.0 / (double)st, rrad = 1.0 / (double)radix;
+        const int n_sel = A.n_pat / radix, base = kk >= 0 ? (vv + 1) * st : 0;
+        const double rst = 1.0 / (double)st;
         double v[6] = {0, 0, 0, 0, 0, 0};  // rows, non-null rows, Σmp, Σ(1-mp), Σ ln, non-null ln rows
-        for (int p = lane; p < A.n_pat; p += 64) {
+        for (int t = lane; t < n_sel; t += 64) {
+            int b;
+            const int a = kk >= 0 ? udiv_uniform(t, st, rst, b) : 0;
+            const int p = kk >= 0 ? a * (st * radix) + base + b : t;
             const double c = tc[p], mp = tm[p], ll = tl[p];
-            bool in = c != 0.0;
-            if (kk >= 0) {
-                int rem, g;
-                const int hi = udiv_uniform(p, st, rst, rem);
-                udiv_uniform(hi, radix, rrad, g);
-                in = in && g - 1 == vv;
-            }
-            if (!in) continue;
+            if (c == 0.0) continue;
             v[0] += c;
             if (!isnan(mp)) {
                 v[1] += c;

@@ -94,8 +94,15 @@ __device__ __attribute__((always_inline)) inline void load16(const FiltArgs &A, 
     const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
+#ifdef SPK_DIAG_NO_LEFT  // timing diagnostic only (wrong results): no left-row loads (the right row, id flipped)
+        const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(r1, oy[u], 0, 0);
+        u32x4_t x = y;
+        x.x ^= 1u;
+        (void)r0;
+#else
         const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r0, ox[u], 0, 0);
         const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(r1, oy[u], 0, 0);
+#endif
         a[u] = make_uint4(x.x, x.y, x.z, x.w);
         b[u] = make_uint4(y.x, y.y, y.z, y.w);
     }
@@ -108,8 +115,15 @@ __device__ __attribute__((always_inline)) inline void load8(const FiltArgs &A, i
     const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
+#ifdef SPK_DIAG_NO_LEFT
+        const u32x2_t y = __builtin_amdgcn_raw_buffer_load_b64(r1, oy[u] + in, 0, 0);
+        u32x2_t x = y;
+        x.x ^= 1u;
+        (void)r0;
+#else
         const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(r0, ox[u] + in, 0, 0);
         const u32x2_t y = __builtin_amdgcn_raw_buffer_load_b64(r1, oy[u] + in, 0, 0);
+#endif
         a[u] = make_uint2(x.x, x.y);
         b[u] = make_uint2(y.x, y.y);
     }
@@ -401,7 +415,11 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
         for (int u = 0; u < FP; ++u) {
             p[u] = base + u * 64 + lane;
             act[u] = p[u] < end;
+#ifdef SPK_DIAG_LEFT_UNIFORM  // timing diagnostic only (wrong results): every lane reads lane 0's left row
+            ox[u] = (uint32_t)__builtin_amdgcn_readfirstlane(nx[u]) << 4;
+#else
             ox[u] = (uint32_t)nx[u] << 4;
+#endif
             oy[u] = (uint32_t)ny[u] << 4;
             acc[u] = 0;
             const uint32_t q = p[u] + STEP;
