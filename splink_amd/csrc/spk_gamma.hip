@@ -1399,7 +1399,11 @@ static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
         const bool lev = si >= 0 && G.simple[si].cls == SC_LEV;
         const ColSet one_k{1, {k, 0, 0, 0}};
         if (lev) {
-            k_gamma_slow_lev<<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
+#ifndef SPK_SLOWLEV_WG_PER_CU
+#define SPK_SLOWLEV_WG_PER_CU 8  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU fit at once
+#endif
+            const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SPK_SLOWLEV_WG_PER_CU * ctx->n_cu));
+            k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
             k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
         } else {
             k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
@@ -1431,8 +1435,15 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         reinterpret_cast<unsigned long long *>(ctx->xinfo.p + G.n_info + G.n_cnt + 1));
     const std::vector<SimpleCol> &simple = G.simple;
     // Jaro-Winkler template columns: compact every list, then one exact launch over all of them
+    // JW exact launches: a JW cell is one short latency-bound evaluation, and the kernel holds 3 waves per
+    // SIMD, so a grid of 8 workgroups per CU ran in rounds of dispatch latency; SPK_JW_WG_PER_CU per
+    // column keeps it near one resident round with the grid-stride loop's prefetch
+#ifndef SPK_JW_WG_PER_CU
+#define SPK_JW_WG_PER_CU 8
+#endif
+    const int64_t g_jw = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SPK_JW_WG_PER_CU * ctx->n_cu));
     ExactCols jw{};
-    jw.g = (int)G.g_exact;
+    jw.g = (int)g_jw;
     ColSet jk{};
     for (int k = 0; k < K; ++k) {
         if (!G.may_exact[k] || G.simple_of[k] < 0) continue;
@@ -1450,7 +1461,7 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         if (c < (int)ctx->xev_used.size()) ctx->xev_used[c] = 0;
     if (jw.n) {
         SPK_TRY(ctx->xbegin(jk.k[0]));
-        k_gamma_exact_simple<false><<<(unsigned)(G.g_exact * jw.n), X_THREADS, 0, ctx->stream>>>(A, jw, ctx->xlist.p,
+        k_gamma_exact_simple<false><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(A, jw, ctx->xlist.p,
                                                                                                 ctx->xinfo.p);
         SPK_TRY(ctx->xend(jk.k[0]));
         bool all_quiet = true;
@@ -1473,11 +1484,17 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         if (lev) {
             ExactCols one{};
             one.n = 1;
-            one.g = (int)G.g_exact;
+            // one resident round: the grid-stride loop gives every block a fixed share of the list, so a
+            // grid larger than what fits at once (LEV_WAVES per SIMD) runs a second, partly empty round
+#ifndef SPK_LEV_WG_PER_CU
+#define SPK_LEV_WG_PER_CU 8
+#endif
+            const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SPK_LEV_WG_PER_CU * ctx->n_cu));
+            one.g = (int)g_lev;
             one.si[0] = si;
             SPK_TRY(ctx->xbegin(k));
-            k_gamma_exact_simple<true><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
-                                                                                          ctx->xinfo.p);
+            k_gamma_exact_simple<true><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
+                                                                                      ctx->xinfo.p);
             SPK_TRY(ctx->xend(k));
             if (quiet(k)) G.slow_skipped[k] = 1;
             else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
