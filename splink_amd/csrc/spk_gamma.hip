@@ -721,17 +721,20 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
 // any lane needs.  So each workgroup's 256 cells are regrouped by (longer > 32 units, shorter length)
 // before they are evaluated: lanes of a wave then get similar trip counts and most waves stay at
 // 32-bit words.  Only the assignment of cells to lanes changes; every cell is evaluated once, as
-// before.  Bin LEV_BINS - 1 also holds the empty slots past the end of the list.
-constexpr int LEV_BINS = 128;
+// before.  Cells with a row past 64 units (no 64-bit planes: the 128-bit slow pass takes them) get bins
+// of their own, 128 + shorter length, so their waves hold no cell the exact pass evaluates and they
+// reach the slow list sorted by that pass's trip count.  Bin LEV_BINS - 1 also holds the empty slots
+// past the end of the list.
+constexpr int LEV_BINS = 192;
 __device__ inline int lev_work_bin(int la, int lb) {
     la = la < 0 ? 0 : la;
     lb = lb < 0 ? 0 : lb;
     const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
-    return (mx > 32 ? 64 : 0) + (mn < 63 ? mn : 63);
+    return (mx > 64 ? 128 : (mx > 32 ? 64 : 0)) + (mn < 63 ? mn : 63);
 }
 
 // Counting sort of the workgroup's (key, item) by key through LDS: one LDS atomic per lane, a
-// 128-bin exclusive scan in wave 0, one scatter and one gather.  Three barriers.
+// LEV_BINS exclusive scan in wave 0 (three bins per lane), one scatter and one gather.  Three barriers.
 __device__ inline void lev_sort_items(int key, bool &have, int32_t &p, int32_t &x, int32_t &y) {
     __shared__ unsigned int s_bin[LEV_BINS];
     __shared__ int32_t s_p[X_THREADS], s_x[X_THREADS], s_y[X_THREADS];
@@ -741,17 +744,19 @@ __device__ inline void lev_sort_items(int key, bool &have, int32_t &p, int32_t &
     __syncthreads();
     const unsigned int r = atomicAdd(&s_bin[key], 1u);
     __syncthreads();
-    if (t < 64) {  // wave 0: two bins per lane
-        const unsigned int a = s_bin[2 * t], b = s_bin[2 * t + 1];
-        unsigned int v = a + b;
+    static_assert(LEV_BINS == 3 * 64, "lev_sort_items scans three bins per lane");
+    if (t < 64) {  // wave 0: three bins per lane
+        const unsigned int a = s_bin[3 * t], b = s_bin[3 * t + 1], c = s_bin[3 * t + 2];
+        unsigned int v = a + b + c;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const unsigned int u = __shfl_up(v, off, 64);
             if (t >= off) v += u;
         }
-        const unsigned int ex = v - a - b;
-        s_bin[2 * t] = ex;
-        s_bin[2 * t + 1] = ex + a;
+        const unsigned int ex = v - a - b - c;
+        s_bin[3 * t] = ex;
+        s_bin[3 * t + 1] = ex + a;
+        s_bin[3 * t + 2] = ex + a + b;
     }
     __syncthreads();
     const unsigned int pos = s_bin[key] + r;

@@ -179,3 +179,6 @@ def test_async_em_iteration_matches_sync(amd):
     assert p_async._level_probabilities() == p_sync._level_probabilities()
     ms = job.ctx.kernel_ms_done()
     assert ms["gamma"] > 0 and ms["em_hist"] > 0
+    # each Levenshtein column's exact-pass launch was timed (spk_gammas_exact_ms, bench.py string_rates)
+    xms = job.ctx.gammas_exact_ms(3)
+    assert all(x > 0 for x in xms), xms

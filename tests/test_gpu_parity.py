@@ -245,6 +245,48 @@ def test_strings_past_slow_limit(amd):
     assert list(got[-1]) == [-1, -1, -1]
 
 
+def test_jw_filter_field_edges(amd):
+    """The filter bounds a Jaro-Winkler column from the row image's fields: the sketch (matches) and the
+    four head units (the Winkler prefix, which this jar does not cap at four).  Pairs at those edges --
+    shared prefixes of 0-5 units, units equal in their low byte ('a' U+0061 / 'Š' U+0160, 'b' / 'ţ'
+    U+0163), lengths 1-20 and 250-300 -- must give the reference's levels at thresholds on either side
+    of their similarities."""
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(11))
+    alpha = list("abcdefghij")
+    left, right = [], []
+    for n in (1, 2, 3, 4, 5, 6, 8, 11, 12, 20):
+        for pre in range(0, 6):
+            for _ in range(6):
+                a = "".join(rng.choice(alpha, size=n))
+                tail = "".join(rng.choice(alpha, size=max(0, n + int(rng.integers(-2, 3)) - min(pre, n))))
+                left.append(a)
+                right.append(a[:pre] + tail)
+    for a, b in (("abcd", "Šbcd"), ("abcdx", "Šbcdy"), ("abba", "aţba"), ("abcdefghijk", "abcŠefghijk"),
+                 ("Šţa", "abŠ"), ("ab", "Šţ"), ("aaaa", "aaaŠ")):
+        left.append(a)
+        right.append(b)
+    for n in (250, 252, 253, 254, 255, 256, 258, 300):
+        for r in range(4):
+            a = "".join(rng.choice(alpha, size=n))
+            b = _mutate(rng, a, int(rng.integers(1, 6)), alpha) if r % 2 == 0 else a[:n - 1] + "z"
+            left.append(a)
+            right.append(b)
+    ref = [orc.jaro_winkler(a, b) for a, b in zip(left, right)]
+    ts = (0.98, 0.94, 0.9, 0.85, 0.8, 0.7)
+    jw_lv = ("case when a_l is null or a_r is null then -1 "
+             + " ".join(f"when jaro_winkler_sim(a_l, a_r) >= {t} then {len(ts) - k}" for k, t in enumerate(ts))
+             + " else 0 end")
+    df = pd.DataFrame({"a_l": left, "a_r": right})
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "jw", "custom_columns_used": ["a"], "num_levels": len(ts) + 1, "case_expression": jw_lv,
+         "m_probabilities": [0.05, 0.05, 0.1, 0.1, 0.1, 0.2, 0.4], "u_probabilities": [0.4, 0.2, 0.1, 0.1, 0.1, 0.05, 0.05]}]}
+    got = add_gammas(df, st, amd).gamma_matrix()[:, 0]
+    for i, j in enumerate(ref):
+        want = next((len(ts) - k for k, t in enumerate(ts) if j >= t), 0)
+        assert got[i] == want, (left[i], right[i], j, got[i])
+
+
 def _synthetic(n, seed, **kw):
     from splink_amd.synthetic import make_records
     return make_records(n, seed=seed, **kw)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
