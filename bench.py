@@ -51,8 +51,8 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--records", type=int, default=1_000_000, help="records at N=1 (scaled by sqrt(N))")
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
                     help="2: the headline workload; 5: + free-text address Levenshtein-4 (cfg5's columns at cfg2's size)")

@@ -198,6 +198,27 @@ __device__ __forceinline__ int udiv_uniform(int p, int d, double rd, int &rem) {
     return q;
 }
 
+// Wave-level helpers for doubles: a DPP move within rows of 16 lanes and a lane read (both halves).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false));
+}
+// Sum over each row of 16 lanes, left in every lane of the row: quad_perm xor 1 (0xB1), xor 2 (0x4E),
+// row_half_mirror (0x141), row_mirror (0x140).  Each step adds a lane's value and its partner's, and
+// a + b == b + a exactly, so every lane of a row ends with the same bits.
+__device__ __forceinline__ double row_sum16(double x) {
+    x += dpp_d<0xB1>(x);
+    x += dpp_d<0x4E>(x);
+    x += dpp_d<0x141>(x);
+    x += dpp_d<0x140>(x);
+    return x;
+}
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l), __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+
 template <class Count>
 __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restrict__ mpat, double *__restrict__ llpat,
                                   double *__restrict__ cpat, double *__restrict__ out, double *s_tab) {
@@ -229,53 +250,63 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
         const double d = num + den;
         const double ll = d > 0.0 ? log(d) : NAN;
         const double mp = d == 0.0 ? NAN : num / d;
-        mpat[p] = mp;
-        llpat[p] = ll;
-        cpat[p] = (double)c;
-        if (lds) {
+        if (lds) {  // the global copies are written after the M-step sums, off the critical path
             tc[p] = (double)c;
             tm[p] = mp;
             tl[p] = ll;
+        } else {
+            mpat[p] = mp;
+            llpat[p] = ll;
+            cpat[p] = (double)c;
         }
     }
-    __threadfence_block();
+    if (!lds) __threadfence_block();
     __syncthreads();
     EM_STAMP(8);
+    // Two slots per wave, one per half-wave (32 lanes): cfg2's 19 slots fit 16 waves in one round.  Each
+    // half sums its strided patterns, then a fixed DPP tree within rows of 16 lanes and two readlanes per
+    // half -- VALU latency, where a 64-lane shuffle butterfly of six doubles cost ~72 LDS-crossbar
+    // round trips.  Deterministic: the same tree whatever the counts.
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n_waves = blockDim.x >> 6;
-    for (int slot = wave; slot <= A.n_slots; slot += n_waves) {  // wave-uniform
-        int kk = -1, vv = 0;
-        if (slot > 0) {
-            int r = slot - 1;
-            for (kk = 0; kk < A.K && r > A.nlev[kk]; ++kk) r -= A.nlev[kk] + 1;
-            vv = r - 1;
-        }
-        // the slot's patterns directly: digit vv + 1 of column kk, p = a·(st·radix) + (vv + 1)·st + b
-        const int st = kk >= 0 ? A.stride[kk] : 1, radix = kk >= 0 ? A.nlev[kk] + 1 : 1;
-        const int n_sel = A.n_pat / radix, base = kk >= 0 ? (vv + 1) * st : 0;
-        const double rst = 1.0 / (double)st;
+    const int half = lane >> 5, l32 = lane & 31;
+    for (int s0 = 2 * wave; s0 <= A.n_slots; s0 += 2 * n_waves) {  // wave-uniform
+        const int slot = s0 + half;
         double v[6] = {0, 0, 0, 0, 0, 0};  // rows, non-null rows, Σmp, Σ(1-mp), Σ ln, non-null ln rows
-        for (int t = lane; t < n_sel; t += 64) {
-            int b;
-            const int a = kk >= 0 ? udiv_uniform(t, st, rst, b) : 0;
-            const int p = kk >= 0 ? a * (st * radix) + base + b : t;
-            const double c = tc[p], mp = tm[p], ll = tl[p];
-            if (c == 0.0) continue;
-            v[0] += c;
-            if (!isnan(mp)) {
-                v[1] += c;
-                v[2] += c * mp;
-                v[3] += c * (1.0 - mp);
+        if (slot <= A.n_slots) {
+            int kk = -1, vv = 0;
+            if (slot > 0) {
+                int r = slot - 1;
+                for (kk = 0; kk < A.K && r > A.nlev[kk]; ++kk) r -= A.nlev[kk] + 1;
+                vv = r - 1;
             }
-            if (!isnan(ll)) {
-                v[5] += c;
-                v[4] += c * ll;
+            // the slot's patterns directly: digit vv + 1 of column kk, p = a·(st·radix) + (vv + 1)·st + b
+            const int st = kk >= 0 ? A.stride[kk] : 1, radix = kk >= 0 ? A.nlev[kk] + 1 : 1;
+            const int n_sel = A.n_pat / radix, base = kk >= 0 ? (vv + 1) * st : 0;
+            const double rst = 1.0 / (double)st;
+            for (int t = l32; t < n_sel; t += 32) {
+                int b;
+                const int a = kk >= 0 ? udiv_uniform(t, st, rst, b) : 0;
+                const int p = kk >= 0 ? a * (st * radix) + base + b : t;
+                const double c = tc[p], mp = tm[p], ll = tl[p];
+                if (c == 0.0) continue;
+                v[0] += c;
+                if (!isnan(mp)) {
+                    v[1] += c;
+                    v[2] += c * mp;
+                    v[3] += c * (1.0 - mp);
+                }
+                if (!isnan(ll)) {
+                    v[5] += c;
+                    v[4] += c * ll;
+                }
             }
         }
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-            for (int q = 0; q < 6; ++q) v[q] += __shfl_xor(v[q], off);
-        if (lane == 0) {
+        for (int q = 0; q < 6; ++q) {
+            const double r = row_sum16(v[q]);
+            v[q] = half ? readlane_d(r, 32) + readlane_d(r, 48) : readlane_d(r, 0) + readlane_d(r, 16);
+        }
+        if (l32 == 0 && slot <= A.n_slots) {
             if (slot == 0) {
                 out[0] = v[2];
                 out[1] = v[0];
@@ -289,6 +320,13 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
                 o[2] = v[2];
                 o[3] = v[3];
             }
+        }
+    }
+    if (lds) {
+        for (int p = threadIdx.x; p < A.n_pat; p += blockDim.x) {
+            mpat[p] = tm[p];
+            llpat[p] = tl[p];
+            cpat[p] = tc[p];
         }
     }
 }
