@@ -477,6 +477,19 @@ __device__ inline W low_mask(int m) {  // bits [0, m), 1 <= m <= bits of W
     return m >= (int)(8 * sizeof(W)) ? ~(W)0 : (((W)1 << m) - 1);
 }
 
+// Early-exit score of the scans (pattern m >= text n): after text unit j, the cell of the end cell's
+// diagonal, D[i*][j + 1] with i* = j + 1 + (m - n) = (j + 1) + popc(VP & low i* rows) - popc(VN & ...).
+// Values never decrease along a diagonal (Ukkonen), and this one ends at D[m][n], so D[i*][j + 1] > cut
+// proves the distance > cut.  It dominates the score-minus-units-left test (D[m][j + 1] <= D[i*][j + 1]
+// + (n - j - 1)) and cuts the scan ~18 % earlier on cfg5's dissimilar addresses (host simulation over
+// 600 cells).  In the lazy scans the rows that entered late hold upper bounds that differ from the true
+// values only where both are > cut, so the test reads the same there.
+template <typename W>
+__device__ inline int diag_score(W vp, W vn, int j, int m, int n) {
+    const W M = low_mask<W>(j + 1 + (m - n));
+    return j + 1 + popc_w(vp & M) - popc_w(vn & M);
+}
+
 // NP: the scans read planes 0..NP-1 only.  A caller passes NP < 8 when every unit of the column
 // (both sides) has the same bits NP..7 (e.g. 7 for ASCII text): those planes' terms then only touch
 // mask bits above the pattern, which never reach the rows below (carries and shifts move upward).
@@ -504,13 +517,12 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
             const W hn = (d0 & vp) << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
-            // The bound dist - (units left) never decreases and ends at dist, so testing it every
-            // fourth unit plus clamping at the end returns cut + 1 for exactly the cells a per-unit
-            // test cuts.
+            // Early exit on the end cell's diagonal (diag_bound): it never decreases and ends at the
+            // distance, so testing it every fourth unit plus clamping at the end returns cut + 1 for
+            // exactly the cells a per-unit test cuts.
             if ((jj & 3) == 3) {
                 const int j = 32 * h + jj;
-                const int dist = j + 1 + popc_w(vp & M) - popc_w(vn & M);
-                if (dist - (n - 1 - j) > cut) return cut + 1;
+                if (diag_score<W>(vp, vn, j, m, n) > cut) return cut + 1;
             }
         }
     }
@@ -558,10 +570,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
         const uint32_t hn = (d0 & vp) << 1;
         vp = hn | ~(d0 | hp);
         vn = hp & d0;
-        if (!wide && (j & 3) == 3) {
-            const int dist = j + 1 + popc_w(vp & M1) - popc_w(vn & M1);
-            if (dist - (n - 1 - j) > cut) return cut + 1;
-        }
+        if (!wide && (j & 3) == 3 && diag_score<uint32_t>(vp, vn, j, m, n) > cut) return cut + 1;
     }
     if (n <= J0) {
         const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 32 : 0);
@@ -586,11 +595,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
             const uint64_t hn = (d0 & VP) << 1;
             VP = hn | ~(d0 | hp);
             VN = hp & d0;
-            if ((jj & 3) == 3) {
-                const int j = 32 * h + jj;
-                const int dist = j + 1 + popc_w(VP & M2) - popc_w(VN & M2);
-                if (dist - (n - 1 - j) > cut) return cut + 1;
-            }
+            if ((jj & 3) == 3 && diag_score<uint64_t>(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
     const int dist = n + popc_w(VP & M2) - popc_w(VN & M2);
@@ -665,6 +670,12 @@ __device__ inline int popc128(u128 x) {
     return __builtin_popcountll((unsigned long long)x) + __builtin_popcountll((unsigned long long)(x >> 64));
 }
 
+__device__ inline int diag_score128(u128 vp, u128 vn, int j, int m, int n) {  // diag_score over 128-bit words
+    const int i = j + 1 + (m - n);
+    const u128 M = i >= 128 ? ~(u128)0 : (((u128)1 << i) - 1);
+    return j + 1 + popc128(vp & M) - popc128(vn & M);
+}
+
 template <int NP = N_PLANES>
 __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
                                           int cut) {
@@ -689,11 +700,7 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
             const u128 hn = (d0 & vp) << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
-            if ((jj & 3) == 3) {  // as in myers_plane_text
-                const int j = 32 * h + jj;
-                const int dist = j + 1 + popc128(vp & M) - popc128(vn & M);
-                if (dist - (n - 1 - j) > cut) return cut + 1;
-            }
+            if ((jj & 3) == 3 && diag_score128(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;  // as in myers_plane_text
         }
     }
     const int dist = n + popc128(vp & M) - popc128(vn & M);
@@ -739,11 +746,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
             const uint64_t hn = (d0 & vp) << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
-            if (!wide && (jj & 3) == 3) {
-                const int j = 32 * h + jj;
-                const int dist = j + 1 + popc_w(vp & M1) - popc_w(vn & M1);
-                if (dist - (n - 1 - j) > cut) return cut + 1;
-            }
+            if (!wide && (jj & 3) == 3 && diag_score<uint64_t>(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
     if (n <= J0) {
@@ -773,11 +776,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
             const u128 hn = (d0 & VP) << 1;
             VP = hn | ~(d0 | hp);
             VN = hp & d0;
-            if ((jj & 3) == 3) {
-                const int j = 32 * h + jj;
-                const int dist = j + 1 + popc128(VP & M2) - popc128(VN & M2);
-                if (dist - (n - 1 - j) > cut) return cut + 1;
-            }
+            if ((jj & 3) == 3 && diag_score128(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
     const int dist = n + popc128(VP & M2) - popc128(VN & M2);

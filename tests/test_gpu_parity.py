@@ -245,6 +245,52 @@ def test_strings_past_slow_limit(amd):
     assert list(got[-1]) == [-1, -1, -1]
 
 
+def test_levenshtein_cut_around_thresholds(amd):
+    """The exact passes stop a scan once the end cell's diagonal exceeds the largest distance any test can
+    still pass (the cut).  Pairs whose distance straddles that cut -- 0 to 0.7 x length edits, insertion-
+    and deletion-heavy so the lengths differ, rows of 20-128 units through every word width, free text
+    and a four-letter alphabet -- must give the reference's levels for ratio tests at 0.2 / 0.3 / 0.4 and
+    absolute tests at 3 / 9 / 20."""
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(77))
+    alphas = [list("abcd"), list("abcdefghijklmnopqrstuvwxyz0123456789 ,.")]
+    left, right = [], []
+    for n in (20, 31, 33, 45, 63, 64, 66, 90, 127, 128):
+        for alpha in alphas:
+            for frac in (0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.7):
+                for _ in range(3):
+                    a = "".join(rng.choice(alpha, size=n))
+                    b = list(a)
+                    for _e in range(int(round(frac * n))):
+                        op = int(rng.integers(4))
+                        i = int(rng.integers(len(b) + 1))
+                        if op <= 1 and len(b) < 128:
+                            b.insert(i, alpha[int(rng.integers(len(alpha)))])
+                        elif op == 2 and b:
+                            del b[min(i, len(b) - 1)]
+                        elif b:
+                            b[min(i, len(b) - 1)] = alpha[int(rng.integers(len(alpha)))]
+                    left.append(a)
+                    right.append("".join(b))
+    ratio = "levenshtein(a_l, a_r)/((length(a_l) + length(a_r))/2)"
+    lr = ("case when a_l is null or a_r is null then -1 when a_l = a_r then 3 "
+          f"when {ratio} <= 0.2 then 2 when {ratio} <= 0.3 then 1 when {ratio} <= 0.4 then 0 else 0 end")
+    la = ("case when a_l is null or a_r is null then -1 when levenshtein(a_l, a_r) <= 3 then 3 "
+          "when levenshtein(a_l, a_r) <= 9 then 2 when levenshtein(a_l, a_r) <= 20 then 1 else 0 end")
+    df = pd.DataFrame({"a_l": left, "a_r": right})
+    mu = {"m_probabilities": [0.1, 0.2, 0.3, 0.4], "u_probabilities": [0.4, 0.3, 0.2, 0.1]}
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "lr", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": lr, **mu},
+        {"custom_name": "la", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": la, **mu}]}
+    got = add_gammas(df, st, amd).gamma_matrix()
+    for i, (a, b) in enumerate(zip(left, right)):
+        d = orc.levenshtein(a, b)
+        r = d / ((len(a) + len(b)) / 2)
+        want_r = 3 if a == b else 2 if r <= 0.2 else 1 if r <= 0.3 else 0
+        want_a = 3 if d <= 3 else 2 if d <= 9 else 1 if d <= 20 else 0
+        assert list(got[i]) == [want_r, want_a], (len(a), len(b), d, r, list(got[i]))
+
+
 def test_jw_filter_field_edges(amd):
     """The filter bounds a Jaro-Winkler column from the row image's fields: the sketch (matches) and the
     four head units (the Winkler prefix, which this jar does not cap at four).  Pairs at those edges --
