@@ -500,7 +500,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
     W vp = ~(W)0, vn = 0;
-    const W M = low_mask<W>(m);
+    // (the final score is diag_score at the last unit: i* = m)
     for (int h = 0; h < 2 && 32 * h < n; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -526,7 +526,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
             }
         }
     }
-    const int dist = n + popc_w(vp & M) - popc_w(vn & M);
+    const int dist = diag_score<W>(vp, vn, n - 1, m, n);
     return dist > cut ? cut + 1 : dist;
 }
 
@@ -578,7 +578,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
     }
     // rows 33..m enter with vertical deltas +1 (D[32][J0] + (i - 32))
     uint64_t VP = (uint64_t)vp | 0xFFFFFFFF00000000ull, VN = vn;
-    const uint64_t M2 = low_mask<uint64_t>(m);
+
     for (int h = J0 >> 5; h < 2 && 32 * h < n; ++h) {
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
@@ -598,7 +598,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
             if ((jj & 3) == 3 && diag_score<uint64_t>(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
-    const int dist = n + popc_w(VP & M2) - popc_w(VN & M2);
+    const int dist = diag_score<uint64_t>(VP, VN, n - 1, m, n);
     return dist > cut ? cut + 1 : dist;
 }
 
@@ -680,7 +680,7 @@ template <int NP = N_PLANES>
 __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
                                           int cut) {
     u128 vp = ~(u128)0, vn = 0;
-    const u128 M = m >= 128 ? ~(u128)0 : (((u128)1 << m) - 1);  // score from the deltas, as in myers_plane_text
+
     for (int h = 0; h < 4 && 32 * h < n; ++h) {  // text units [32h, 32h + 32)
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -703,7 +703,7 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
             if ((jj & 3) == 3 && diag_score128(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;  // as in myers_plane_text
         }
     }
-    const int dist = n + popc128(vp & M) - popc128(vn & M);
+    const int dist = diag_score128(vp, vn, n - 1, m, n);
     return dist > cut ? cut + 1 : dist;
 }
 
@@ -755,7 +755,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
     }
     // rows 65..m enter with vertical deltas +1 (D[64][J0] + (i - 64))
     u128 VP = (u128)vp | ((u128)~0ull << 64), VN = vn;
-    const u128 M2 = m >= 128 ? ~(u128)0 : (((u128)1 << m) - 1);
+
     for (int h = J0 >> 5; h < 4 && 32 * h < n; ++h) {
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -779,7 +779,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
             if ((jj & 3) == 3 && diag_score128(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
-    const int dist = n + popc128(VP & M2) - popc128(VN & M2);
+    const int dist = diag_score128(VP, VN, n - 1, m, n);
     return dist > cut ? cut + 1 : dist;
 }
 
