@@ -483,7 +483,10 @@ __device__ inline W low_mask(int m) {  // bits [0, m), 1 <= m <= bits of W
 // proves the distance > cut.  It dominates the score-minus-units-left test (D[m][j + 1] <= D[i*][j + 1]
 // + (n - j - 1)) and cuts the scan ~18 % earlier on cfg5's dissimilar addresses (host simulation over
 // 600 cells).  In the lazy scans the rows that entered late hold upper bounds that differ from the true
-// values only where both are > cut, so the test reads the same there.
+// values only where both are > cut, so the test reads the same there.  Used by the 128-bit scans (the
+// slow pass, 141 VGPRs); in the 32 / 64-bit scans of the exact pass it pushed that kernel 4 VGPRs past
+// its 96-VGPR cap (scratch spills: 67 -> 176 MB of writes per cfg2 call at the same time), so those keep
+// the score-minus-units-left test.
 template <typename W>
 __device__ inline int diag_score(W vp, W vn, int j, int m, int n) {
     const W M = low_mask<W>(j + 1 + (m - n));
@@ -500,7 +503,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
     W vp = ~(W)0, vn = 0;
-    // (the final score is diag_score at the last unit: i* = m)
+    const W M = low_mask<W>(m);
     for (int h = 0; h < 2 && 32 * h < n; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -517,16 +520,17 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
             const W hn = (d0 & vp) << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
-            // Early exit on the end cell's diagonal (diag_bound): it never decreases and ends at the
-            // distance, so testing it every fourth unit plus clamping at the end returns cut + 1 for
-            // exactly the cells a per-unit test cuts.
+            // The bound dist - (units left) never decreases and ends at dist, so testing it every
+            // fourth unit plus clamping at the end returns cut + 1 for exactly the cells a per-unit
+            // test cuts.
             if ((jj & 3) == 3) {
                 const int j = 32 * h + jj;
-                if (diag_score<W>(vp, vn, j, m, n) > cut) return cut + 1;
+                const int dist = j + 1 + popc_w(vp & M) - popc_w(vn & M);
+                if (dist - (n - 1 - j) > cut) return cut + 1;
             }
         }
     }
-    const int dist = diag_score<W>(vp, vn, n - 1, m, n);
+    const int dist = n + popc_w(vp & M) - popc_w(vn & M);
     return dist > cut ? cut + 1 : dist;
 }
 
@@ -570,7 +574,10 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
         const uint32_t hn = (d0 & vp) << 1;
         vp = hn | ~(d0 | hp);
         vn = hp & d0;
-        if (!wide && (j & 3) == 3 && diag_score<uint32_t>(vp, vn, j, m, n) > cut) return cut + 1;
+        if (!wide && (j & 3) == 3) {
+            const int dist = j + 1 + popc_w(vp & M1) - popc_w(vn & M1);
+            if (dist - (n - 1 - j) > cut) return cut + 1;
+        }
     }
     if (n <= J0) {
         const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 32 : 0);
@@ -578,7 +585,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
     }
     // rows 33..m enter with vertical deltas +1 (D[32][J0] + (i - 32))
     uint64_t VP = (uint64_t)vp | 0xFFFFFFFF00000000ull, VN = vn;
-
+    const uint64_t M2 = low_mask<uint64_t>(m);
     for (int h = J0 >> 5; h < 2 && 32 * h < n; ++h) {
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
@@ -595,10 +602,14 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
             const uint64_t hn = (d0 & VP) << 1;
             VP = hn | ~(d0 | hp);
             VN = hp & d0;
-            if ((jj & 3) == 3 && diag_score<uint64_t>(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
+            if ((jj & 3) == 3) {
+                const int j = 32 * h + jj;
+                const int dist = j + 1 + popc_w(VP & M2) - popc_w(VN & M2);
+                if (dist - (n - 1 - j) > cut) return cut + 1;
+            }
         }
     }
-    const int dist = diag_score<uint64_t>(VP, VN, n - 1, m, n);
+    const int dist = n + popc_w(VP & M2) - popc_w(VN & M2);
     return dist > cut ? cut + 1 : dist;
 }
 
