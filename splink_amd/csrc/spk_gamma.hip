@@ -658,6 +658,31 @@ __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDe
     return ST_DONE;
 }
 
+// Exact pass cell of a Jaro-Winkler template column (every test `jaro_winkler_sim > / >= t`): the JW
+// code alone, so its kernel keeps a small register budget (X_JW).
+__device__ int jw_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level) {
+    const RecMeta ma = c0.meta[x], mb = c1.meta[y];
+    if (ma.len16 < 0 || mb.len16 < 0) {
+        level = sc.null_level;
+        return ST_DONE;
+    }
+    const StrView a = row_view(c0, ma, x, sc.col), b = row_view(c1, mb, y, sc.col);
+    int eq = meta_equal(ma, mb);
+    if (eq < 0) eq = units_equal(a, b) ? 1 : 0;
+    double jw;
+    if (eq == 1) jw = a.n > 0 ? 1.0 : 0.0;
+    else if (a.n > 64 || b.n > 64) return ST_NEEDS_SLOW;
+    else jw = jw_exact(a, b);
+    for (int i = 0; i < sc.n_tests; ++i) {
+        if (cmpd(jw, sc.t[i], sc.cmp[i]) == KT) {
+            level = sc.level[i];
+            return ST_DONE;
+        }
+    }
+    level = sc.else_level;
+    return ST_DONE;
+}
+
 // Exact pass cell of a Levenshtein-class template column (tests: `=` / `<>`, levenshtein [ratio]):
 // both rows' bit-planes are loaded in the same round trip as the records and the distance comes
 // from them alone (lev_rows_planes).  Rows without planes (> 64 units or a unit >= 256) go to the
@@ -775,50 +800,77 @@ constexpr int LEV_WAVES = 5;
 // The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD): capped at
 // 4 waves (128 VGPRs, 40 B of spills) it measured the same on MI355X (52.1 vs 52.3 us per call).
 constexpr int JW_WAVES = 1;
+// The JW-only cells (jw_cell) take 120 VGPRs: 4 waves per SIMD, twice the workgroups the generic kernel keeps resident.
+constexpr int JWC_WAVES = 4;
 // Columns of one exact launch: blocks [c g, (c + 1) g) work through column si[c]'s list, so the
 // short Jaro-Winkler lists of several columns share one launch (and its tail).
 struct ExactCols {
     int n;
     int g;  // blocks per column
     int si[4];
+    int k[4], col[4];  // the columns' code positions and table columns (= simple[si].k / .col): the
+                       // list bounds and the column descriptors load in one round, not after simple[si]
 };
 
-template <bool LEV, int XW = (LEV ? LEV_WAVES : JW_WAVES)>
+// Diagnostic build only (-DSPK_X_STAMPS): per-workgroup start / end wall-clock stamps (100 MHz) of the JW
+// exact launch and the number of cells each workgroup evaluated, read with spk_debug_x_stamps
+// (tools/ab_x_stamps.py).
+#ifdef SPK_X_STAMPS
+constexpr int X_STAMP_BLOCKS = 16384;
+__device__ unsigned long long g_x_stamps[5 * X_STAMP_BLOCKS];
+#endif
+// MODE: X_GENERIC (simple_exact: any simple string column), X_LEV (lev_cell), X_JW (jw_cell).  Each mode
+// is its own kernel so its register budget is that of its own cell code: simple_exact carries the
+// Levenshtein scans too, and at its 190 VGPRs the JW cells ran 2 waves per SIMD.
+enum XMode : int { X_GENERIC = 0, X_LEV = 1, X_JW = 2 };
+template <int MODE, int XW = (MODE == X_LEV ? LEV_WAVES : (MODE == X_JW ? JWC_WAVES : JW_WAVES))>
 __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs A, ExactCols C,
                                                                    const int32_t *xlist, const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
+#ifdef SPK_X_STAMPS
+    unsigned long long x_t0 = wall_clock64(), x_cells = 0, x_t1 = 0, x_t2 = 0;
+#endif
     const int col_slot = (int)(blockIdx.x / (unsigned)C.g);  // block-uniform
     const int64_t bid = (int64_t)blockIdx.x - (int64_t)col_slot * C.g;
-    if (threadIdx.x == 0) {
-        int si = C.si[0];
+    int si = C.si[0], k = C.k[0], colx = C.col[0];
 #pragma unroll
-        for (int c = 1; c < 4; ++c)
-            if (c == col_slot) si = C.si[c];
+    for (int c = 1; c < 4; ++c)
+        if (c == col_slot) {
+            si = C.si[c];
+            k = C.k[c];
+            colx = C.col[c];
+        }
+    // one round of independent loads: the column's descriptors (thread 0), the list bounds and every
+    // thread's first item and pair rows
+    if (threadIdx.x == 0) {
         s_sc = A.simple[si];
-        s_c0 = A.cols0[s_sc.col];
-        s_c1 = A.cols1[s_sc.col];
+        s_c0 = A.cols0[colx];
+        s_c1 = A.cols1[colx];
     }
-    __syncthreads();
-    const SimpleCol &sc = s_sc;
-    const int k = sc.k;
     const int64_t n = exact_count(A, xinfo, k);
     const int32_t *items = xlist + xinfo[k];
     const int64_t stride = (int64_t)C.g * X_THREADS;
     // software pipeline: the next item's pair rows (and, for Levenshtein, the rows' lengths) are in
     // flight while this one is evaluated
     int64_t i = bid * X_THREADS + threadIdx.x;
-    // Regroup by work bin only in free-text columns (rows past 64 units, so planes_hi exists): there the
-    // trip counts spread widely (cfg5 addresses: 2.98 -> 2.67 ms per call).  In short-string columns
-    // the sort's barriers cost more than it saves (cfg2 email: 475 -> 505 us), so they keep the old order.
-    const bool regroup = LEV && s_c0.planes_hi != nullptr && s_c1.planes_hi != nullptr;  // block-uniform
     int32_t p = 0, x = 0, y = 0, key = LEV_BINS - 1;
     if (i < n) {
         p = items[i];
         x = A.pl[p];
         y = A.pr[p];
-        if (regroup) key = lev_work_bin(s_c0.meta[x].len16, s_c1.meta[y].len16);
     }
+    __syncthreads();
+#ifdef SPK_X_STAMPS
+    x_t1 = wall_clock64();
+#endif
+    const SimpleCol &sc = s_sc;
+    // Regroup by work bin only in free-text columns (rows past 64 units, so planes_hi exists): there the
+    // trip counts spread widely (cfg5 addresses: 2.98 -> 2.67 ms per call).  In short-string columns
+    // the sort's barriers cost more than it saves (cfg2 email: 475 -> 505 us), so they keep the old order.
+    constexpr bool LEV = MODE == X_LEV;
+    const bool regroup = LEV && s_c0.planes_hi != nullptr && s_c1.planes_hi != nullptr;  // block-uniform
+    if (regroup && i < n) key = lev_work_bin(s_c0.meta[x].len16, s_c1.meta[y].len16);
     for (int64_t base = bid * X_THREADS; base < n; base += stride) {  // block-uniform
         bool have = i < n;
         const int64_t i2 = i + stride;
@@ -833,19 +885,44 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         bool to_slow = false;
         if (have) {
             int level = 0;
-            const int st = LEV ? lev_cell(sc, s_c0, s_c1, x, y, level) : simple_exact(A, sc, s_c0, s_c1, x, y, level);
+            int st;
+            if constexpr (MODE == X_LEV) st = lev_cell(sc, s_c0, s_c1, x, y, level);
+            else if constexpr (MODE == X_JW) st = jw_cell(sc, s_c0, s_c1, x, y, level);
+            else st = simple_exact(A, sc, s_c0, s_c1, x, y, level);
+#ifdef SPK_X_STAMPS
+            if (x_t2 == 0) x_t2 = wall_clock64() + (unsigned long long)(level & 0);
+#endif
             if (st != ST_DONE) to_slow = true;
             else if (C.n > 1) code_add_atomic(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
             else code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
         }
         wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
+#ifdef SPK_X_STAMPS
+        x_cells += have ? 1 : 0;
+#endif
         i = i2;
         p = p2;
         x = x2;
         y = y2;
         key = key2;
     }
+#ifdef SPK_X_STAMPS
+    if (MODE == X_JW && threadIdx.x == 0 && blockIdx.x < X_STAMP_BLOCKS) {
+        g_x_stamps[5 * blockIdx.x] = x_t0;
+        g_x_stamps[5 * blockIdx.x + 1] = wall_clock64();
+        g_x_stamps[5 * blockIdx.x + 2] = x_cells;
+        g_x_stamps[5 * blockIdx.x + 3] = x_t1;
+        g_x_stamps[5 * blockIdx.x + 4] = x_t2;
+    }
+#endif
 }
+#ifdef SPK_X_STAMPS
+extern "C" int spk_debug_x_stamps(uint64_t *out, int n) {
+    SPK_HIP(hipDeviceSynchronize());
+    SPK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x_stamps), sizeof(uint64_t) * (size_t)std::min(n, 5 * X_STAMP_BLOCKS)));
+    return SPK_OK;
+}
+#endif
 
 // Global-memory pass over column k's slow list (length on the device; usually empty).  Cells with a
 // string past SLOW_LIMIT units go on to the huge pass: their list (counter slow_count[2K + k]) takes
@@ -1453,8 +1530,10 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
     for (int k = 0; k < K; ++k) {
         if (!G.may_exact[k] || G.simple_of[k] < 0) continue;
         const SimpleCol &sc = simple[G.simple_of[k]];
-        if (sc.cls == SC_LEV || sc.kind != SK_STR || jw.n == 4) continue;
+        if (sc.cls != SC_JW || sc.kind != SK_STR || jw.n == 4) continue;
         jk.k[jk.n++] = k;
+        jw.k[jw.n] = sc.k;
+        jw.col[jw.n] = sc.col;
         jw.si[jw.n++] = G.simple_of[k];
     }
     if (jk.n)
@@ -1466,7 +1545,7 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         if (c < (int)ctx->xev_used.size()) ctx->xev_used[c] = 0;
     if (jw.n) {
         SPK_TRY(ctx->xbegin(jk.k[0]));
-        k_gamma_exact_simple<false><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(A, jw, ctx->xlist.p,
+        k_gamma_exact_simple<X_JW><<<(unsigned)(g_jw * jw.n), X_THREADS, 0, ctx->stream>>>(A, jw, ctx->xlist.p,
                                                                                                 ctx->xinfo.p);
         SPK_TRY(ctx->xend(jk.k[0]));
         bool all_quiet = true;
@@ -1497,8 +1576,10 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
             const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SPK_LEV_WG_PER_CU * ctx->n_cu));
             one.g = (int)g_lev;
             one.si[0] = si;
+            one.k[0] = simple[si].k;
+            one.col[0] = simple[si].col;
             SPK_TRY(ctx->xbegin(k));
-            k_gamma_exact_simple<true><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
+            k_gamma_exact_simple<X_LEV><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
                                                                                       ctx->xinfo.p);
             SPK_TRY(ctx->xend(k));
             if (quiet(k)) G.slow_skipped[k] = 1;
@@ -1508,7 +1589,9 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
             one.n = 1;
             one.g = (int)G.g_exact;
             one.si[0] = si;
-            k_gamma_exact_simple<false><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
+            one.k[0] = simple[si].k;
+            one.col[0] = simple[si].col;
+            k_gamma_exact_simple<X_GENERIC><<<(unsigned)G.g_exact, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
                                                                                            ctx->xinfo.p);
             if (quiet(k)) G.slow_skipped[k] = 1;
             else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
