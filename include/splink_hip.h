@@ -270,7 +270,9 @@ int spk_em_iteration_wait(spk_ctx *ctx, double *out_stats, int n_stats);
  * all-reduce it (exact integer sum), then spk_em_finalize. */
 int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist);
 /* Histogram kernel choice (same result): 1 = lane-private LDS counters when the pattern space fits
- * (default), 0 = wave-ballot aggregation into one LDS histogram.  For testing and measurement. */
+ * (default), 0 = wave-ballot aggregation into one LDS histogram, 2 = as 1 with an agent-scope release
+ * fence before each last-arriver ticket (the memory model's own ordering; 1 relies on gfx950's
+ * write-through stores).  For testing and measurement. */
 int spk_em_set_lane_histogram(spk_ctx *ctx, int on);
 /* E-step per pattern with the reference's literal arithmetic, then the M-step sums:
  * out_stats (host) = [Σmp, rows, non-null rows, Σ ln(λΠm + (1-λ)Πu), non-null ln rows] + per column k,

@@ -373,3 +373,34 @@ def tf_adjust(cols_l, cols_r, mp, lam):
     out = np.array([float("nan") if np.isnan(p) else _bayes([p] + [c[i] for c in adjs])
                     for i, p in enumerate(mp)], dtype=np.float64)
     return out, adjs
+
+
+def tf_adjust_codes(codes_l, codes_r, mp, lam):
+    """tf_adjust for ONE tf column over integer value codes (-1 = NULL), vectorised for pair counts the
+    scalar loop cannot take (term_frequencies.py:49-117, the same steps as tf_adjust): per value v,
+    adj_lambda = mean mp over pairs with code_l = code_r = v (NULL mp out of sum and count), adj =
+    bayes(adj_lambda, 1 - λ), 0.5 where the pair has no lookup (or a NULL one), then
+    bayes(mp, adj).  Σmp per value is np.bincount's running sum in pair order, as the scalar loop."""
+    codes_l = np.asarray(codes_l, dtype=np.int64)
+    codes_r = np.asarray(codes_r, dtype=np.int64)
+    mp = np.asarray(mp, dtype=np.float64)
+    one_minus = float(repr(1 - lam))
+    ok = (codes_l >= 0) & (codes_l == codes_r)
+    good = ok & ~np.isnan(mp)
+    n_v = int(max(codes_l.max(initial=-1), codes_r.max(initial=-1))) + 1
+    s = np.bincount(codes_l[good], weights=mp[good], minlength=n_v)
+    c = np.bincount(codes_l[good], minlength=n_v)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        adj_lambda = np.where(c > 0, s / np.maximum(c, 1), np.nan)
+        tnum = adj_lambda * one_minus
+        tden = tnum + (1.0 - adj_lambda) * (1.0 - one_minus)
+        tab = np.where(tden == 0, np.nan, tnum / tden)
+        adj = np.full(len(mp), 0.5)
+        look = tab[np.where(ok, codes_l, 0)] if n_v else np.full(len(mp), np.nan)
+        sel = ok & ~np.isnan(look)
+        adj[sel] = look[sel]
+        num = mp * adj
+        den = num + (1.0 - mp) * (1.0 - adj)
+        out = np.where(den == 0, np.nan, num / den)
+    out[np.isnan(mp)] = np.nan
+    return out, adj

@@ -358,8 +358,10 @@ class Context:
         check(self._lib.spk_gammas_simple_count(self._h, ctypes.byref(n)), "spk_gammas_simple_count")
         return n.value
 
-    def em_set_lane_histogram(self, on: bool):
-        check(self._lib.spk_em_set_lane_histogram(self._h, ctypes.c_int(1 if on else 0)), "spk_em_set_lane_histogram")
+    def em_set_lane_histogram(self, on):
+        """True / 1: lane-private counters (default); False / 0: wave-ballot histogram; 2: lane counters with a
+        release fence before each last-arriver ticket."""
+        check(self._lib.spk_em_set_lane_histogram(self._h, ctypes.c_int(int(on))), "spk_em_set_lane_histogram")
 
     def em_histogram(self, d_hist_ptr: int = 0):
         check(self._lib.spk_em_histogram(self._h, ctypes.c_void_p(d_hist_ptr)), "spk_em_histogram")

@@ -13,6 +13,12 @@
 
 #include "spk_internal.h"
 
+// The count rows' publication below relies on gfx950's cache behaviour (sc1 write-through stores drained
+// before the ticket atomic, no release fence); build for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "spk_em.hip targets gfx950 (MI355X) only"
+#endif
+
 namespace spk {
 
 constexpr int H_THREADS = 512;
@@ -353,7 +359,8 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
                                                         uint32_t *__restrict__ part,
                                                         unsigned int *__restrict__ ticket, double *__restrict__ mpat,
                                                         double *__restrict__ llpat, double *__restrict__ cpat,
-                                                        double *__restrict__ out, unsigned long long *__restrict__ out_hist) {
+                                                        double *__restrict__ out, unsigned long long *__restrict__ out_hist,
+                                                        int fence) {
     extern __shared__ uint32_t sh[];
     __shared__ bool s_last;
     const int n_pat = A0.n_pat;
@@ -435,8 +442,14 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
         __syncthreads();
     };
+    // fence != 0 (spk_em_set_lane_histogram mode 2): an agent-scope release fence before each ticket, the
+    // ordering the HSA memory model itself guarantees (after the barrier it is cumulative over the
+    // workgroup's stores); the A/B test checks both forms give the same statistics
     auto arrive = [&](unsigned int *t, unsigned int last) {  // true in the last arriver (whole workgroup)
-        if (threadIdx.x == 0) s_last = atomicAdd(t, 1u) == last;
+        if (threadIdx.x == 0) {
+            if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            s_last = atomicAdd(t, 1u) == last;
+        }
         __syncthreads();
         if (!s_last) return false;
         if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -631,12 +644,13 @@ static int pat_args(spk_ctx *ctx, double lambda, double one_minus, const double 
 using namespace spk;
 
 
-// Lane-private copies of the counters that fit the LDS budget (R = 64 .. 4), 0 when none fits.
+// Lane-private copies of the counters that fit the LDS budget (R = 64 .. 4), 0 when none fits.  k_em_iter
+// sums its count rows in uint32: 2^32 or more pairs in one context take the k_hist path (uint64 counters).
 static int lane_copies(spk_ctx *ctx) {
     int R = 64;
     const int64_t lds_budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block);
     while (R >= 4 && ctx->n_patterns * R * 4 > lds_budget) R >>= 1;
-    return (R >= 4 && ctx->hist_lanes) ? R : 0;
+    return (R >= 4 && ctx->hist_lanes && ctx->n_pairs < (int64_t)UINT32_MAX) ? R : 0;
 }
 
 // Grid of the lane-histogram launches: one 1024-thread workgroup per CU.
@@ -649,10 +663,12 @@ static int64_t lane_grid(spk_ctx *ctx) {
     case RR:                                                                                                     \
         if (ctx->code_bytes == 2)                                                                                \
             k_em_iter<uint16_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
-                reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h); \
+                reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
+                ctx->em_fence ? 1 : 0);                                                                          \
         else                                                                                                     \
             k_em_iter<uint32_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
-                reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h); \
+                reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
+                ctx->em_fence ? 1 : 0);                                                                          \
         break;
 
 // The padded accumulation histogram and the ticket of k_em_iter: zero between launches (the last workgroup
@@ -683,7 +699,6 @@ static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     const int64_t P = ctx->n_pairs;
     const int vec = 16 / ctx->code_bytes;
     const int R = lane_copies(ctx);
-    SPK_REQUIRE(P < (int64_t)UINT32_MAX, SPK_E_LIMIT, "EM histogram: 2^32 or more pairs in one context");
     SPK_TRY(ctx->begin(K_EMHIST));
     if (R) {
         PatArgs A{};
@@ -749,8 +764,9 @@ static int finalize_from(spk_ctx *ctx, const unsigned long long *h, const PatArg
 }
 
 extern "C" int spk_em_set_lane_histogram(spk_ctx *ctx, int on) {
-    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    SPK_REQUIRE(ctx && on >= 0 && on <= 2, SPK_E_INVALID, "spk_em_set_lane_histogram: mode 0, 1 or 2");
     ctx->hist_lanes = on != 0;
+    ctx->em_fence = on == 2;
     return SPK_OK;
 }
 
@@ -817,7 +833,6 @@ static int enqueue_em(spk_ctx *ctx) {
         unsigned int *ticket = nullptr;
         SPK_TRY(em_accumulator(ctx, &acc, &ticket));
         const int64_t P = ctx->n_pairs;
-        SPK_REQUIRE(P < (int64_t)UINT32_MAX, SPK_E_LIMIT, "spk_em_iteration: 2^32 or more pairs in one context");
         const int64_t g = lane_grid(ctx);
         const size_t sh = std::max<size_t>((size_t)n_pat * R * 4, sizeof(PatArgs));
         double *mpat = ctx->mpat.p, *llpat = ctx->llpat.p, *cpat = ctx->cpat.p, *out = ctx->stats.p;
@@ -933,10 +948,10 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
     SPK_TRY(settle_gammas(ctx, nullptr));
     PatArgs A;
     SPK_TRY(pat_args(ctx, lambda, one_minus, m, u, A));
-    SPK_TRY(ctx->mpat.alloc((size_t)ctx->n_patterns));
+    SPK_TRY(ctx->mpat_score.alloc((size_t)ctx->n_patterns));
     SPK_TRY(ctx->mp.alloc((size_t)ctx->n_pairs + 1));
     SPK_TRY(ctx->begin(K_SCORE));
-    k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat.p, nullptr);
+    k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat_score.p, nullptr);
     SPK_HIP(hipGetLastError());
     ctx->mpat_valid = true;
     if (count) {
@@ -950,11 +965,11 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
         double *o = ctx->mp.p + start;
         const size_t shm = lds ? (size_t)np * 8 : 0;
         if (ctx->code_bytes == 2) {
-            if (lds) k_score<uint16_t, true><<<(unsigned)g, SC_THREADS, shm, ctx->stream>>>(c16, start, count, ctx->mpat.p, np, o);
-            else k_score<uint16_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c16, start, count, ctx->mpat.p, np, o);
+            if (lds) k_score<uint16_t, true><<<(unsigned)g, SC_THREADS, shm, ctx->stream>>>(c16, start, count, ctx->mpat_score.p, np, o);
+            else k_score<uint16_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c16, start, count, ctx->mpat_score.p, np, o);
         } else {
-            if (lds) k_score<uint32_t, true><<<(unsigned)g, SC_THREADS, shm, ctx->stream>>>(c32, start, count, ctx->mpat.p, np, o);
-            else k_score<uint32_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c32, start, count, ctx->mpat.p, np, o);
+            if (lds) k_score<uint32_t, true><<<(unsigned)g, SC_THREADS, shm, ctx->stream>>>(c32, start, count, ctx->mpat_score.p, np, o);
+            else k_score<uint32_t, false><<<(unsigned)g, SC_THREADS, 0, ctx->stream>>>(c32, start, count, ctx->mpat_score.p, np, o);
         }
         SPK_HIP(hipGetLastError());
     }

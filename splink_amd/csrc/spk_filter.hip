@@ -28,6 +28,7 @@ enum LevKind : int32_t { LK_GE = 0, LK_LE = 1, LK_EXACT = 2, LK_RATIO = 3 };
 struct FCommon {
     int64_t p0, p1;        // byte offset of the chunk plane holding the column's field, side 0 / side 1
     uint32_t in;           // byte offset of the field inside its 16-byte chunk (0 or 8)
+    int32_t ci;            // index of that chunk in a row (its plane in a staged tile)
     uint32_t stride;       // code stride of the column
     int32_t k;             // comparison column (work list)
     int32_t null_level;
@@ -44,6 +45,7 @@ struct FEq {
 struct FJw {
     FCommon c;
     int64_t h0, h1;  // planes of the four head units (low 8 bytes of the next chunk)
+    int32_t hci;     // the head chunk's index in a row
     int32_t lv_one, lv_zero, lv_bound;
     float cf;        // undecided iff the fp32 upper bound >= cf (+inf: never)
     // An equality column whose 8-byte field fills the high half of the head chunk (layout_image puts
@@ -79,6 +81,14 @@ struct FiltArgs {
     const int16_t *thr;
     int n_thr;
     int nj, nl, ne, nn;
+    // LDS staging (k_filter): a chunk's rows are copied into a tile of `cap` rows x `nck` 16-byte chunks
+    // (chunk-major, like the image), then its pairs read their fields from the tile.
+    int nck, cap;
+    // Pairs [vlo, vhi) of rule 1 also carry view positions (vpl / vpr, indexed by pair ordinal): a block
+    // of rule 1 is contiguous in view order, so a chunk of them stages its rows by view position
+    // through vrows0 / vrows1 (view position -> table row) instead of by their scattered table rows.
+    const int32_t *vpl, *vpr, *vrows0, *vrows1;
+    int64_t vlo, vhi;
     FJw jw[FJ_MAX];
     FLev lev[FL_MAX];
     FEq eq[FE_MAX];
@@ -86,46 +96,57 @@ struct FiltArgs {
 };
 static_assert(sizeof(FiltArgs) <= 4096, "kernel argument size");
 
-// Loads of one field of FP pairs' rows (ox / oy = row x 16) from the planes of a column.
-template <int FP>
-__device__ __attribute__((always_inline)) inline void load16(const FiltArgs &A, int64_t p0, int64_t p1,
-                                                             const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
-                                                             uint4 (&a)[FP], uint4 (&b)[FP]) {
-    const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
+// Where a lane's FP pairs read their fields: from the global row image by 32-bit byte offsets (ox / oy =
+// row x 16) through one buffer descriptor per side (ST = false), or from the LDS tile a chunk staged
+// (ST = true: ox / oy = the rows' indices in the tile, field plane ci at ci x cap).
+struct Tile {
+    const uint4 *t;
+    int cap;
+};
+
+template <int FP, bool ST>
+__device__ __attribute__((always_inline)) inline void load16(const FiltArgs &A, const Tile &T, int ci, int64_t p0,
+                                                             int64_t p1, const uint32_t (&ox)[FP],
+                                                             const uint32_t (&oy)[FP], uint4 (&a)[FP], uint4 (&b)[FP]) {
+    if constexpr (ST) {
+        const uint4 *t = T.t + ci * T.cap;
 #pragma unroll
-    for (int u = 0; u < FP; ++u) {
-#ifdef SPK_DIAG_NO_LEFT  // timing diagnostic only (wrong results): no left-row loads (the right row, id flipped)
-        const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(r1, oy[u], 0, 0);
-        u32x4_t x = y;
-        x.x ^= 1u;
-        (void)r0;
-#else
-        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r0, ox[u], 0, 0);
-        const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(r1, oy[u], 0, 0);
-#endif
-        a[u] = make_uint4(x.x, x.y, x.z, x.w);
-        b[u] = make_uint4(y.x, y.y, y.z, y.w);
+        for (int u = 0; u < FP; ++u) {
+            a[u] = t[ox[u]];
+            b[u] = t[oy[u]];
+        }
+    } else {
+        const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r0, ox[u], 0, 0);
+            const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(r1, oy[u], 0, 0);
+            a[u] = make_uint4(x.x, x.y, x.z, x.w);
+            b[u] = make_uint4(y.x, y.y, y.z, y.w);
+        }
     }
 }
 
-template <int FP>
-__device__ __attribute__((always_inline)) inline void load8(const FiltArgs &A, int64_t p0, int64_t p1, uint32_t in,
-                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
-                                                            uint2 (&a)[FP], uint2 (&b)[FP]) {
-    const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
+template <int FP, bool ST>
+__device__ __attribute__((always_inline)) inline void load8(const FiltArgs &A, const Tile &T, int ci, int64_t p0,
+                                                            int64_t p1, uint32_t in, const uint32_t (&ox)[FP],
+                                                            const uint32_t (&oy)[FP], uint2 (&a)[FP], uint2 (&b)[FP]) {
+    if constexpr (ST) {
+        const uint2 *t = reinterpret_cast<const uint2 *>(T.t + ci * T.cap) + (in >> 3);
 #pragma unroll
-    for (int u = 0; u < FP; ++u) {
-#ifdef SPK_DIAG_NO_LEFT
-        const u32x2_t y = __builtin_amdgcn_raw_buffer_load_b64(r1, oy[u] + in, 0, 0);
-        u32x2_t x = y;
-        x.x ^= 1u;
-        (void)r0;
-#else
-        const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(r0, ox[u] + in, 0, 0);
-        const u32x2_t y = __builtin_amdgcn_raw_buffer_load_b64(r1, oy[u] + in, 0, 0);
-#endif
-        a[u] = make_uint2(x.x, x.y);
-        b[u] = make_uint2(y.x, y.y);
+        for (int u = 0; u < FP; ++u) {
+            a[u] = t[2 * ox[u]];
+            b[u] = t[2 * oy[u]];
+        }
+    } else {
+        const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(r0, ox[u] + in, 0, 0);
+            const u32x2_t y = __builtin_amdgcn_raw_buffer_load_b64(r1, oy[u] + in, 0, 0);
+            a[u] = make_uint2(x.x, x.y);
+            b[u] = make_uint2(y.x, y.y);
+        }
     }
 }
 
@@ -168,15 +189,16 @@ struct JwData {
     uint4 a[FP], b[FP];
     uint4 qa[FP], qb[FP];  // head chunk: head units in .x / .y, the gap EQ field (if any) in .z / .w
 };
-template <int FP>
-__device__ __attribute__((always_inline)) inline void ld_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
-                                                            const uint32_t (&oy)[FP], JwData<FP> &d) {
-    load16<FP>(A, J.c.p0, J.c.p1, ox, oy, d.a, d.b);
+template <int FP, bool ST>
+__device__ __attribute__((always_inline)) inline void ld_jw(const FiltArgs &A, const Tile &T, const FJw &J,
+                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
+                                                            JwData<FP> &d) {
+    load16<FP, ST>(A, T, J.c.ci, J.c.p0, J.c.p1, ox, oy, d.a, d.b);
     if (J.geq) {  // kernel-argument (wave-uniform) branch
-        load16<FP>(A, J.h0, J.h1, ox, oy, d.qa, d.qb);
+        load16<FP, ST>(A, T, J.hci, J.h0, J.h1, ox, oy, d.qa, d.qb);
     } else {
         uint2 ha[FP], hb[FP];
-        load8<FP>(A, J.h0, J.h1, 0, ox, oy, ha, hb);
+        load8<FP, ST>(A, T, J.hci, J.h0, J.h1, 0, ox, oy, ha, hb);
 #pragma unroll
         for (int u = 0; u < FP; ++u) {
             d.qa[u] = make_uint4(ha[u].x, ha[u].y, 0u, 0u);
@@ -237,14 +259,6 @@ __device__ __attribute__((always_inline)) inline void ev_jw(const FJw &J, const 
         const int level = nul[u] ? J.c.null_level : lv;
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * J.c.stride;
     }
-}
-template <int FP>
-__device__ __attribute__((always_inline)) inline void f_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
-                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
-                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
-    JwData<FP> d;
-    ld_jw<FP>(A, J, ox, oy, d);
-    ev_jw<FP>(J, d, act, acc, und);
 }
 
 // ---- Levenshtein template column ---------------------------------------------------------------------
@@ -330,15 +344,6 @@ __device__ __attribute__((always_inline)) inline void ev_lev(const FLev &L, cons
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * L.c.stride;
     }
 }
-template <int FP>
-__device__ __attribute__((always_inline)) inline void f_lev(const FiltArgs &A, const FLev &L, const int16_t *s_thr,
-                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
-                                                            const bool (&act)[FP], uint32_t (&acc)[FP],
-                                                            bool (&und)[FP]) {
-    Data16<FP> d;
-    load16<FP>(A, L.c.p0, L.c.p1, ox, oy, d.a, d.b);
-    ev_lev<FP>(L, s_thr, d, act, acc, und);
-}
 
 // ---- strict-equality template column -----------------------------------------------------------------
 template <int FP>
@@ -359,21 +364,14 @@ __device__ __attribute__((always_inline)) inline void ev_eq(const FEq &E, const 
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * E.c.stride;
     }
 }
-template <int FP>
-__device__ __attribute__((always_inline)) inline void f_eq(const FiltArgs &A, const FEq &E, const uint32_t (&ox)[FP],
-                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
-                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
-    Data8<FP> d;
-    load8<FP>(A, E.c.p0, E.c.p1, E.c.in, ox, oy, d.a, d.b);
-    ev_eq<FP>(E, d, act, acc, und);
-}
 
 // ---- numeric template column --------------------------------------------------------------------------
-template <int FP>
-__device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, const FNum &N, const uint32_t (&ox)[FP],
-                                                            const uint32_t (&oy)[FP], uint32_t (&acc)[FP]) {
+template <int FP, bool ST>
+__device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, const Tile &T, const FNum &N,
+                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
+                                                            uint32_t (&acc)[FP]) {
     uint4 a[FP], b[FP];
-    load16<FP>(A, N.c.p0, N.c.p1, ox, oy, a, b);
+    load16<FP, ST>(A, T, N.c.ci, N.c.p0, N.c.p1, ox, oy, a, b);
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
         const int level = simple_num(N, a[u].z != 0, bits_to_double(a[u].x, a[u].y), b[u].z != 0,
@@ -384,114 +382,241 @@ __device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, c
 
 constexpr int N_FCOLS = FJ_MAX + FL_MAX + FE_MAX + FN_MAX;
 
-// One workgroup per region of consecutive pair ordinals; each lane takes FP pairs per iteration (the
-// next iteration's pair rows are in flight meanwhile).  Per column: the FP pairs' field loads, then
-// their evaluation, then one wave-aggregated append of the undecided cells.
-template <int FP, int MINW, bool C32>
-__global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
-    __shared__ unsigned int s_cnt[N_FCOLS + FJ_MAX];  // work-list lengths: per column slot, then JW gap EQs
-    extern __shared__ int16_t s_thr[];  // A.thr (dynamic LDS: n_thr entries)
-    if (threadIdx.x < N_FCOLS + FJ_MAX) s_cnt[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
-    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
+// The columns of FP pairs per lane (pairs base + u * 64 + lane, u < FP, those below `end`): per column
+// the FP pairs' field loads (tile or global image), their evaluation, one wave-aggregated append of the
+// undecided cells; then the codes.
+template <int FP, bool ST, bool C32>
+__device__ __attribute__((always_inline)) inline void eval_pairs(const FiltArgs &A, const Tile &T,
+                                                                 const int16_t *s_thr, unsigned int *s_cnt,
+                                                                 int64_t r0, uint32_t base, uint32_t end,
+                                                                 const uint32_t (&ox)[FP], const uint32_t (&oy)[FP]) {
     constexpr int SPAN = 64 * FP;
-    constexpr int STEP = (F_THREADS / 64) * SPAN;
-    const uint32_t end = (uint32_t)r1;
-    uint32_t base = (uint32_t)r0 + (uint32_t)(threadIdx.x >> 6) * SPAN;
-    int32_t nx[FP], ny[FP];
+    const int lane = threadIdx.x & 63;
+    uint32_t p[FP], acc[FP];
+    bool act[FP], und[FP];
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
-        const uint32_t q = base + u * 64 + lane;
-        nx[u] = q < end ? A.pl[q] : 0;  // inactive lanes read row 0 harmlessly
-        ny[u] = q < end ? A.pr[q] : 0;
+        p[u] = base + u * 64 + lane;
+        act[u] = p[u] < end;
+        acc[u] = 0;
     }
-    for (; base < end; base += STEP) {  // wave-uniform
-        uint32_t p[FP], ox[FP], oy[FP], acc[FP];
-        bool act[FP], und[FP];
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            p[u] = base + u * 64 + lane;
-            act[u] = p[u] < end;
-#ifdef SPK_DIAG_LEFT_UNIFORM  // timing diagnostic only (wrong results): every lane reads lane 0's left row
-            ox[u] = (uint32_t)__builtin_amdgcn_readfirstlane(nx[u]) << 4;
-#else
-            ox[u] = (uint32_t)nx[u] << 4;
-#endif
-            oy[u] = (uint32_t)ny[u] << 4;
-            acc[u] = 0;
-            const uint32_t q = p[u] + STEP;
-            nx[u] = q < end ? A.pl[q] : 0;
-            ny[u] = q < end ? A.pr[q] : 0;
-        }
 #pragma unroll 1
-        for (int j = 0; j < A.nj; ++j) {
-            const FJw &J = A.jw[j];
-            const bool ji = implied(J.c, base, SPAN);
-            const bool gi = J.geq && implied(J.ge.c, base, SPAN);
-            if (ji) {
+    for (int j = 0; j < A.nj; ++j) {
+        const FJw &J = A.jw[j];
+        const bool ji = implied(J.c, base, SPAN);
+        const bool gi = J.geq && implied(J.ge.c, base, SPAN);
+        if (ji) {
 #pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
-            }
-            if (gi) {
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
+        }
+        if (gi) {
 #pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
-            }
-            if (ji) {
-                if (J.geq && !gi) {  // only the gap EQ field is needed
-                    f_eq<FP>(A, J.ge, ox, oy, act, acc, und);
-                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
-                }
-                continue;
-            }
-            JwData<FP> d;
-            ld_jw<FP>(A, J, ox, oy, d);
-            ev_jw<FP>(J, d, act, acc, und);
-            append<FP>(A, J.c, r0, &s_cnt[j], und, p);
-            if (J.geq && !gi) {
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
+        }
+        if (ji) {
+            if (J.geq && !gi) {  // only the gap EQ field is needed
                 Data8<FP> e;
-#pragma unroll
-                for (int u = 0; u < FP; ++u) {
-                    e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
-                    e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
-                }
+                load8<FP, ST>(A, T, J.ge.c.ci, J.ge.c.p0, J.ge.c.p1, J.ge.c.in, ox, oy, e.a, e.b);
                 ev_eq<FP>(J.ge, e, act, acc, und);
                 if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
             }
+            continue;
         }
-#pragma unroll 1
-        for (int j = 0; j < A.nl; ++j) {
-            const FLev &L = A.lev[j];
-            if (implied(L.c, base, SPAN)) {
+        JwData<FP> d;
+        ld_jw<FP, ST>(A, T, J, ox, oy, d);
+        ev_jw<FP>(J, d, act, acc, und);
+        append<FP>(A, J.c, r0, &s_cnt[j], und, p);
+        if (J.geq && !gi) {
+            Data8<FP> e;
 #pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? L.c.imp_add : 0u;
-                continue;
+            for (int u = 0; u < FP; ++u) {
+                e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
+                e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
             }
-            f_lev<FP>(A, L, s_thr, ox, oy, act, acc, und);
-            append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
+            ev_eq<FP>(J.ge, e, act, acc, und);
+            if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
         }
+    }
 #pragma unroll 1
-        for (int j = 0; j < A.ne; ++j) {
-            const FEq &E = A.eq[j];
-            if (implied(E.c, base, SPAN)) {
+    for (int j = 0; j < A.nl; ++j) {
+        const FLev &L = A.lev[j];
+        if (implied(L.c, base, SPAN)) {
 #pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? E.c.imp_add : 0u;
-                continue;
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? L.c.imp_add : 0u;
+            continue;
+        }
+        Data16<FP> d;
+        load16<FP, ST>(A, T, L.c.ci, L.c.p0, L.c.p1, ox, oy, d.a, d.b);
+        ev_lev<FP>(L, s_thr, d, act, acc, und);
+        append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
+    }
+#pragma unroll 1
+    for (int j = 0; j < A.ne; ++j) {
+        const FEq &E = A.eq[j];
+        if (implied(E.c, base, SPAN)) {
+#pragma unroll
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? E.c.imp_add : 0u;
+            continue;
+        }
+        Data8<FP> d;
+        load8<FP, ST>(A, T, E.c.ci, E.c.p0, E.c.p1, E.c.in, ox, oy, d.a, d.b);
+        ev_eq<FP>(E, d, act, acc, und);
+        if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
+    }
+#pragma unroll 1
+    for (int j = 0; j < A.nn; ++j) f_num<FP, ST>(A, T, A.num[j], ox, oy, acc);
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        if (!act[u]) continue;
+        if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
+        else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
+    }
+}
+
+// Copy rows [lo, lo + span) of one side (table rows, or view positions mapped through `rows`) into tile
+// rows [dst, dst + span), every 16-byte chunk of the row (chunk-major, chunk c at c x cap).
+__device__ __attribute__((always_inline)) inline void stage_rows(const FiltArgs &A, uint4 *tile, const uint8_t *img,
+                                                                 uint32_t plane, const int32_t *rows, int32_t lo,
+                                                                 int span, int dst) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(img);
+    const int64_t prow = plane >> 4;
+    for (int r = threadIdx.x; r < span; r += F_THREADS) {
+        const int64_t row = rows ? (int64_t)rows[lo + r] : (int64_t)(lo + r);
+        for (int c = 0; c < A.nck; ++c) tile[c * A.cap + dst + r] = src[c * prow + row];
+    }
+}
+
+__device__ __attribute__((always_inline)) inline int32_t wave_min(int32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int32_t w = __shfl_xor(v, o);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+__device__ __attribute__((always_inline)) inline int32_t wave_max(int32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int32_t w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+// One workgroup per region of consecutive pair ordinals, walked in chunks of F_THREADS x NPL pairs (wave
+// w takes the chunk's w-th quarter, NPL pairs per lane).  Candidate pairs are within-block cross
+// products (blocking.py:145-158), so a chunk's pairs touch few rows, each of them many times: the
+// workgroup copies those rows' image rows into an LDS tile once (coalesced: consecutive rows are
+// consecutive in a chunk plane) and every pair then reads its two rows' fields from the tile instead of
+// gathering them from the image, one texture-addressed load per pair, field and side.  A chunk whose
+// rows do not fit the tile (a block of more rows than `cap`) gathers from the image as before.
+template <int NPL, int FP, int MINW, bool C32>
+__global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
+    static_assert(NPL % FP == 0, "pairs per lane");
+    __shared__ unsigned int s_cnt[N_FCOLS + FJ_MAX];  // work-list lengths: per column slot, then JW gap EQs
+    __shared__ int32_t s_red[F_THREADS / 64][4];      // per wave: lo / hi of the chunk's l- and r-side rows
+    extern __shared__ uint4 s_dyn[];                  // the tile (cap x nck), then A.thr (n_thr entries)
+    uint4 *tile = s_dyn;
+    int16_t *s_thr = reinterpret_cast<int16_t *>(s_dyn + (int64_t)A.cap * A.nck);
+    if (threadIdx.x < N_FCOLS + FJ_MAX) s_cnt[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
+    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
+    constexpr int WCH = 64 * NPL, CH = (F_THREADS / 64) * WCH;
+    const Tile T{tile, A.cap};
+    for (int64_t c0 = r0; c0 < r1; c0 += CH) {  // workgroup-uniform
+        const int64_t c1 = c0 + CH < r1 ? c0 + CH : r1;
+        const bool vg = A.vpl && c0 >= A.vlo && c1 <= A.vhi;  // rule-1 chunk: stage by view position
+        const int32_t *SL = vg ? A.vpl : A.pl, *SR = vg ? A.vpr : A.pr;
+        const uint32_t wb = (uint32_t)c0 + (uint32_t)(wv * WCH);
+        const uint32_t we = (int64_t)wb + WCH < c1 ? wb + WCH : (uint32_t)(c1 > (int64_t)wb ? c1 : wb);
+        int32_t x[NPL], y[NPL];
+        int32_t loL = INT32_MAX, hiL = -1, loR = INT32_MAX, hiR = -1;
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) {
+            const uint32_t q = wb + u * 64 + lane;
+            const bool on = q < we;
+            x[u] = on ? SL[q] : 0;
+            y[u] = on ? SR[q] : 0;
+            if (on) {
+                loL = x[u] < loL ? x[u] : loL;
+                hiL = x[u] > hiL ? x[u] : hiL;
+                loR = y[u] < loR ? y[u] : loR;
+                hiR = y[u] > hiR ? y[u] : hiR;
             }
-            f_eq<FP>(A, E, ox, oy, act, acc, und);
-            if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
         }
-#pragma unroll 1
-        for (int j = 0; j < A.nn; ++j) {
-            f_num<FP>(A, A.num[j], ox, oy, acc);
+        loL = wave_min(loL);
+        hiL = wave_max(hiL);
+        loR = wave_min(loR);
+        hiR = wave_max(hiR);
+        __syncthreads();  // the previous chunk's tile reads and s_red reads are done
+        if (lane == 0) {
+            s_red[wv][0] = loL;
+            s_red[wv][1] = hiL;
+            s_red[wv][2] = loR;
+            s_red[wv][3] = hiR;
         }
+        __syncthreads();
 #pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            if (!act[u]) continue;
-            if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
-            else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
+        for (int w = 0; w < F_THREADS / 64; ++w) {
+            loL = s_red[w][0] < loL ? s_red[w][0] : loL;
+            hiL = s_red[w][1] > hiL ? s_red[w][1] : hiL;
+            loR = s_red[w][2] < loR ? s_red[w][2] : loR;
+            hiR = s_red[w][3] > hiR ? s_red[w][3] : hiR;
+        }
+        // the tile holds one range when the two sides' ranges overlap or touch (a symmetric self-join:
+        // both sides are rows of the same blocks), else the l range then the r range
+        const int32_t *rowsL = vg ? A.vrows0 : nullptr, *rowsR = vg ? A.vrows1 : nullptr;
+        const bool one_img = A.img0 == A.img1 && rowsL == rowsR;
+        const bool merged = one_img && loR <= hiL + 1 && loL <= hiR + 1;
+        const int64_t spanL = (int64_t)hiL - loL + 1, spanR = (int64_t)hiR - loR + 1;
+        const int32_t lo = loL < loR ? loL : loR;
+        const int64_t span = merged ? (int64_t)(hiL > hiR ? hiL : hiR) - lo + 1 : spanL + spanR;
+        const bool staged = hiL >= 0 && span <= A.cap;
+        if (staged) {
+            if (merged) {
+                stage_rows(A, tile, A.img0, A.plane0, rowsL, lo, (int)span, 0);
+            } else {
+                stage_rows(A, tile, A.img0, A.plane0, rowsL, loL, (int)spanL, 0);
+                stage_rows(A, tile, A.img1, A.plane1, rowsR, loR, (int)spanR, (int)spanL);
+            }
+            __syncthreads();
+            const int32_t bx = merged ? lo : loL, by = merged ? lo : loR - (int32_t)spanL;
+#pragma unroll
+            for (int it = 0; it < NPL; it += FP) {
+                const uint32_t base = wb + it * 64;
+                if (base >= we) break;  // wave-uniform
+                uint32_t ox[FP], oy[FP];
+#pragma unroll
+                for (int u = 0; u < FP; ++u) {
+                    const bool on = base + u * 64 + lane < we;
+                    ox[u] = on ? (uint32_t)(x[it + u] - bx) : 0u;
+                    oy[u] = on ? (uint32_t)(y[it + u] - by) : 0u;
+                }
+                eval_pairs<FP, true, C32>(A, T, s_thr, s_cnt, r0, base, we, ox, oy);
+            }
+        } else {
+            if (vg) {  // the fallback gathers by table row
+#pragma unroll
+                for (int u = 0; u < NPL; ++u) {
+                    const uint32_t q = wb + u * 64 + lane;
+                    x[u] = q < we ? A.pl[q] : 0;
+                    y[u] = q < we ? A.pr[q] : 0;
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < NPL; it += FP) {
+                const uint32_t base = wb + it * 64;
+                if (base >= we) break;
+                uint32_t ox[FP], oy[FP];
+#pragma unroll
+                for (int u = 0; u < FP; ++u) {
+                    ox[u] = (uint32_t)x[it + u] << 4;
+                    oy[u] = (uint32_t)y[it + u] << 4;
+                }
+                eval_pairs<FP, false, C32>(A, T, s_thr, s_cnt, r0, base, we, ox, oy);
+            }
         }
     }
     __syncthreads();
@@ -523,6 +648,7 @@ static void common(const SimpleCol &s, const GammaArgs &A, int off, FCommon &c) 
     c.p0 = (int64_t)(off >> 4) * A.img_rows0 * 16;
     c.p1 = (int64_t)(off >> 4) * A.img_rows1 * 16;
     c.in = (uint32_t)(off & 15);
+    c.ci = off >> 4;
     c.stride = (uint32_t)s.stride;
     c.k = s.k;
     c.null_level = s.null_level;
@@ -543,6 +669,7 @@ static void make_jw(const SimpleCol &s, const GammaArgs &A, FJw &J) {
     common(s, A, s.off, J.c);
     J.h0 = (int64_t)(s.off2 >> 4) * A.img_rows0 * 16;
     J.h1 = (int64_t)(s.off2 >> 4) * A.img_rows1 * 16;
+    J.hci = s.off2 >> 4;
     auto first_pass = [&](double v) {
         for (int i = 0; i < s.n_tests; ++i)
             if (hcmp(v, s.t[i], s.cmp[i])) return s.level[i];
@@ -624,7 +751,7 @@ static void make_num(const SimpleCol &s, const GammaArgs &A, FNum &N) {
 }
 
 int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::vector<SimpleCol> &simple,
-                           int64_t region_lo, int64_t region_hi) {
+                           int64_t region_lo, int64_t region_hi, const FilterView *fv) {
     if (region_hi <= region_lo || simple.empty()) return SPK_OK;
     SPK_REQUIRE(A.img_rows0 <= IMG_MAX_ROWS && A.img_rows1 <= IMG_MAX_ROWS, SPK_E_LIMIT,
                 "spk_gammas: more than 2^27 rows in one table (row-image planes are limited to 2^31 bytes)");
@@ -672,10 +799,23 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
         SPK_REQUIRE(F.ne < FE_MAX, SPK_E_INVALID, "filter: EQ slots");
         make_eq(s, A, F.eq[F.ne++]);
     }
+    if (fv) {
+        F.vpl = fv->vpl;
+        F.vpr = fv->vpr;
+        F.vrows0 = fv->rows0;
+        F.vrows1 = fv->rows1;
+        F.vlo = fv->lo;
+        F.vhi = fv->hi;
+    }
+    // the staging tile: SPK_F_TILE_KB KiB of rows (at cfg2's 80-byte rows: 460 rows), so that
+    // SPK_F_MINW workgroups fit a CU's 160 KiB of LDS
+    F.nck = (int)(A.img_stride / 16);
+    SPK_REQUIRE(F.nck >= 1 && F.nck * 16 <= IMG_MAX, SPK_E_INVALID, "filter: image stride");
+    F.cap = (int)((int64_t)SPK_F_TILE_KB * 1024 / (F.nck * 16));
     const unsigned g = (unsigned)(region_hi - region_lo);
-    const size_t shm = (size_t)A.n_thr * sizeof(int16_t);
-    if (A.code16) k_filter<3, 5, false><<<g, F_THREADS, shm, stream>>>(F);
-    else k_filter<3, 5, true><<<g, F_THREADS, shm, stream>>>(F);
+    const size_t shm = (size_t)F.cap * F.nck * 16 + (size_t)A.n_thr * sizeof(int16_t);
+    if (A.code16) k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, false><<<g, F_THREADS, shm, stream>>>(F);
+    else k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, true><<<g, F_THREADS, shm, stream>>>(F);
     SPK_HIP(hipGetLastError());
     return SPK_OK;
 }

@@ -320,8 +320,29 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
 // Filter regions [region_lo, region_hi) of A's pair range over the simple columns (every one of class
 // SC_EQ / SC_JW / SC_LEV / SC_NUM, laid out in A's row image), `shm` bytes of LDS for the threshold
 // tables.  Writes each pair's code over those columns, their work lists and region counts.
+// fv: rule 1's view positions (pairs [lo, hi)), through which the filter stages that rule's rows
+// (null: every chunk stages by the rows in A.pl / A.pr).
+struct FilterView {
+    const int32_t *vpl, *vpr;      // view position of each pair, indexed by pair ordinal
+    const int32_t *rows0, *rows1;  // view position -> table row, l / r side
+    int64_t lo, hi;
+};
 int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::vector<SimpleCol> &simple,
-                           int64_t region_lo, int64_t region_hi);
+                           int64_t region_lo, int64_t region_hi, const FilterView *fv);
+// Filter kernel shape (build options for A/B runs): pairs per lane per chunk, pairs per lane evaluated at
+// once, waves per SIMD, LDS tile KiB per workgroup.
+#ifndef SPK_F_NPL
+#define SPK_F_NPL 4
+#endif
+#ifndef SPK_F_FP
+#define SPK_F_FP 2
+#endif
+#ifndef SPK_F_MINW
+#define SPK_F_MINW 4
+#endif
+#ifndef SPK_F_TILE_KB
+#define SPK_F_TILE_KB 36
+#endif
 // Columns of each class the filter kernel handles (more go to the interpreter).
 constexpr int FJ_MAX = 4, FL_MAX = 3, FE_MAX = 6, FN_MAX = 4;
 

@@ -1970,17 +1970,31 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         // the filter pass (the interpreter's columns add to the codes the template filter sets)
         if (simple.empty())
             SPK_HIP(hipMemsetAsync(ctx->codes.p, 0, (size_t)P * ctx->code_bytes, ctx->stream));
+        // rule 1's pairs stage their rows by view position (table launches; a view launch reads a
+        // view-ordered image directly)
+        FilterView fv{};
+        const FilterView *pfv = nullptr;
+        if (ctx->n_views >= 1 && ctx->pvl.p && ctx->views[1].pair_hi > ctx->views[1].pair_lo) {
+            const RuleView &rv = ctx->views[1];
+            fv.vpl = ctx->pvl.p - ctx->pv_base;
+            fv.vpr = ctx->pvr.p - ctx->pv_base;
+            fv.rows0 = rv.rowsL.p;
+            fv.rows1 = rv.tri ? rv.rowsL.p : rv.rowsR.p;
+            fv.lo = rv.pair_lo;
+            fv.hi = rv.pair_hi;
+            pfv = &fv;
+        }
         if (!simple.empty()) {
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va));
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va, pfv));
             if (vb > va) {
                 GammaArgs VA = A;
                 VA.pl = ctx->pvl.p - ctx->pv_base;  // pl[p] = view position of pair p (p >= pv_base)
                 VA.pr = ctx->pvr.p - ctx->pv_base;
                 VA.img0 = V.img0;
                 VA.img1 = V.img1;
-                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb));
+                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb, nullptr));
             }
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions));
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions, pfv));
         }
         if (A.n_complex) {
             k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);

@@ -318,13 +318,17 @@ struct spk_ctx {
         return SPK_OK;
     }
     spk::DevBuf<double> mp;  // per-pair scores (final E-step)
+    // mp per pattern of the last spk_score (the tf sums read it): a table of its own, since every EM
+    // launch rewrites mpat with its iteration's parameters
+    spk::DevBuf<double> mpat_score;
     std::vector<spk::RawCol *> raw;  // device copies of the input columns (spk_raw_*)
     ~spk_ctx() {
         for (spk::RawCol *r : raw) delete r;
         if (gplan && gplan_free) gplan_free(gplan);
     }
-    bool mpat_valid = false;
+    bool mpat_valid = false;  // mpat_score holds the mp per pattern of the current codes' last spk_score
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
+    bool em_fence = false;   // k_em_iter: release fence before each ticket (spk_em_set_lane_histogram mode 2)
 
     // asynchronous EM iteration (spk_em_iteration_start / _wait): the statistics land in h_stats behind
     // ev_stats; the arguments are kept so that the launch can be repeated when the codes it read are

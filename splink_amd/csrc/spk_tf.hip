@@ -85,7 +85,7 @@ __global__ void k_tf_runs(const unsigned long long *__restrict__ keys, const uns
 // Exact per-value sums over the current pairs, value ids per row on the device (d0 side 0, d1 side 1).
 static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int64_t *out_limbs,
                     int64_t *out_count) {
-    SPK_REQUIRE(ctx->mpat_valid && ctx->mpat.p, SPK_E_STATE, "tf: run spk_score first (mp per pattern)");
+    SPK_REQUIRE(ctx->mpat_valid && ctx->mpat_score.p, SPK_E_STATE, "tf: run spk_score first (mp per pattern)");
     SPK_REQUIRE(n_values < ((int64_t)1 << 31), SPK_E_LIMIT, "tf: more than 2^31 distinct values");
     const int64_t P = ctx->n_pairs;
     DevBuf<unsigned long long> acc, cnt;
@@ -110,11 +110,11 @@ static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int
         if (ctx->code_bytes == 2)
             k_tf_keys<uint16_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
                                                            reinterpret_cast<const uint16_t *>(ctx->codes.p) + c0,
-                                                           ctx->mpat.p, n_values, k_in.p);
+                                                           ctx->mpat_score.p, n_values, k_in.p);
         else
             k_tf_keys<uint32_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
                                                            reinterpret_cast<const uint32_t *>(ctx->codes.p) + c0,
-                                                           ctx->mpat.p, n_values, k_in.p);
+                                                           ctx->mpat_score.p, n_values, k_in.p);
         SPK_HIP(hipGetLastError());
         size_t bytes = 0, b2 = 0;
         SPK_HIP(rocprim::radix_sort_keys(nullptr, bytes, k_in.p, k_out.p, (size_t)n, 0, 64, ctx->stream));
@@ -122,7 +122,7 @@ static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int
         SPK_TRY(tmp.alloc(std::max(bytes, b2) + 1));
         SPK_HIP(rocprim::radix_sort_keys(tmp.p, bytes, k_in.p, k_out.p, (size_t)n, 0, 64, ctx->stream));
         SPK_HIP(rocprim::run_length_encode(tmp.p, b2, k_out.p, (size_t)n, uniq.p, runs.p, n_runs.p, ctx->stream));
-        k_tf_runs<<<g, 256, 0, ctx->stream>>>(uniq.p, runs.p, n_runs.p, ctx->mpat.p, acc.p, cnt.p);
+        k_tf_runs<<<g, 256, 0, ctx->stream>>>(uniq.p, runs.p, n_runs.p, ctx->mpat_score.p, acc.p, cnt.p);
         SPK_HIP(hipGetLastError());
     }
     if (n_values) {

@@ -23,3 +23,29 @@ def load_golden(name):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+@pytest.fixture
+def heartbeat(request):
+    """For tests that run for minutes in one call (the per-GPU-share scale tests): a progress line on the
+    process's real stderr every 30 s (pytest captures the test's own output until it ends), so a
+    watchdog that takes a silent command for a hung one sees it working."""
+    import threading
+    import time
+    stop = threading.Event()
+    t0 = time.time()
+    name = request.node.name
+
+    def beat():
+        while not stop.wait(30.0):
+            try:
+                sys.__stderr__.write(f"[heartbeat] {name}: {time.time() - t0:.0f}s\n")
+                sys.__stderr__.flush()
+            except Exception:
+                pass
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
+    th.join(timeout=5)

@@ -182,3 +182,26 @@ def test_async_em_iteration_matches_sync(amd):
     # each Levenshtein column's exact-pass launch was timed (spk_gammas_exact_ms, bench.py string_rates)
     xms = job.ctx.gammas_exact_ms(3)
     assert all(x > 0 for x in xms), xms
+
+
+def test_tf_sums_use_the_scores_not_a_later_em_iteration(amd):
+    """tf's per-value Σmp come from the last spk_score's parameters (term_frequencies.py:49-65 averages
+    the scored df_e's match_probability), even when an E+M iteration with other parameters ran after the
+    score (it rewrites the EM's own per-pattern table)."""
+    from splink_amd import _native as N
+    rng = np.random.Generator(np.random.PCG64(5))
+    n_levels = [3, 3, 2]
+    P = 200_000
+    g = np.stack([rng.integers(-1, L, P) for L in n_levels], axis=1).astype(np.int8)
+    ctx = N.Context(0)
+    ctx.gammas_load(n_levels, g)
+    m = [0.1, 0.2, 0.7, 0.2, 0.3, 0.5, 0.4, 0.6]
+    u = [0.7, 0.2, 0.1, 0.6, 0.3, 0.1, 0.9, 0.1]
+    mp = ctx.score(0.2, 0.8, m, u, 0, P)
+    n_stats = 5 + 4 * sum(L + 1 for L in n_levels)
+    ctx.em_iteration(0.6, 0.4, u, m, n_stats)  # other parameters: a different mp per pattern
+    ids = rng.integers(0, 50, P).astype(np.int64)
+    s, c = ctx.tf_accumulate(50, ids, ids)
+    want = np.bincount(ids, weights=mp, minlength=50)
+    assert np.array_equal(c, np.bincount(ids, minlength=50))
+    assert np.allclose(s, want, rtol=1e-12, atol=0.0)

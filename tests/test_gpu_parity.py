@@ -587,7 +587,7 @@ def test_em_histogram_kernels_agree(amd, n_levels):
     codes = ((g.astype(np.int64) + 1) * stride).sum(axis=1)
     want = np.bincount(codes, minlength=n_pat)
     got = []
-    for lanes in (True, False):
+    for lanes in (1, 0, 2):  # 2: lane counters with a release fence before each last-arriver ticket
         ctx.em_set_lane_histogram(lanes)
         hist = np.zeros(n_pat, dtype=np.uint64)
         import torch
@@ -596,7 +596,20 @@ def test_em_histogram_kernels_agree(amd, n_levels):
         ctx.em_histogram(d.data_ptr())  # zeroes the buffer itself
         hist[:] = d.cpu().numpy().astype(np.uint64)
         got.append(hist)
-    assert (got[0] == want).all() and (got[1] == want).all()
+    assert (got[0] == want).all() and (got[1] == want).all() and (got[2] == want).all()
+    # the one-launch E+M iteration (finalize in the last workgroup) with and without the fence: the same
+    # statistics bit for bit
+    lam, m, u = 0.3, [], []
+    for L in n_levels:
+        pm = np.linspace(1.0, 2.0, L)
+        m += list(pm / pm.sum())
+        u += list(pm[::-1] / pm.sum())
+    n_stats = 5 + 4 * sum(L + 1 for L in n_levels)
+    stats = []
+    for mode in (1, 2):
+        ctx.em_set_lane_histogram(mode)
+        stats.append(ctx.em_iteration(lam, 1.0 - lam, m, u, n_stats))
+    assert np.array_equal(stats[0], stats[1])
 
 
 def _mutate(rng, s, k, alpha):

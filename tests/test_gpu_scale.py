@@ -110,40 +110,51 @@ def test_cfg5_columns_full_size(amd):
     assert job.n_pairs > 40_000_000
 
 
-def test_cfg4_shard_full_size(amd):
-    """BASELINE configs[3] at one GPU's share: a 20M-record dedupe (blocking surname | dob: 6.2e9 candidate
-    ordinals, past 2^31) whose ordinal space is split over 8 GPUs; this process is rank 0 and generates only
-    its slice (~770M pairs), as each rank of the 8-GPU job does (blocking.py:95-160, int64 ordinals).  A
-    strided sample of 2M comparison vectors is bit-exact against oracle.template_gammas, and 10 EM
-    iterations of λ / m / u plus every pair's match_probability agree with oracle.em_iterate at 1e-9."""
-    from splink_amd.engine import Job, m_step_rows
-    from splink_amd.params import Params
-    from splink_amd.synthetic import cfg_settings, make_records
-    iters = 10
-    df = make_records(20_000_000, surname_vocab=300_000, arrow=True)[["unique_id"] + COLS]
-    params = Params(cfg_settings(4, max_iterations=iters), amd)
-    st = params.settings
-    job = Job("dedupe_only", [df], "unique_id", 0, shard=(0, 8))
-    job.block(st["blocking_rules"])
-    assert job.n_candidates > 2 ** 31 and job.n_pairs > 500_000_000
-    job.gammas(st)
+def rows_of(job, side, rows):
+    """Table rows (device row order) of one side as a frame, without materialising the permuted table."""
+    perm = job.perm[side]
+    return job.inputs[side].take(rows if perm is None else np.asarray(perm)[rows]).reset_index(drop=True)
+
+
+def column_in_row_order(job, side, col):
+    perm = job.perm[side]
+    v = job.inputs[side][col]
+    return v if perm is None else v.take(np.asarray(perm)).reset_index(drop=True)
+
+
+def check_shard(job, params, cols, iters, sample=2_000_000):
+    """Parity of one GPU's share of a big job: every comparison vector of a strided sample of `sample`
+    pairs bit-exact against oracle.template_gammas, `iters` EM iterations of λ / m / u and every pair's
+    match_probability at 1e-9 against oracle.em_iterate.  Returns (match probabilities, pair rows)."""
+    from splink_amd.engine import m_step_rows
+    specs = SPECS[:len(cols)]
     l, r = job.pair_rows()
-    step = max(1, job.n_pairs // 2_000_000)
+    step = max(1, job.n_pairs // sample)
     idx = np.arange(0, job.n_pairs, step)
     sl, sr = l[idx], r[idx]
-    rows, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
-    sub = job.tables[0].take(rows)
-    ocols = [orc.StrCol(sub[c].tolist()) for c in COLS]
-    ref = orc.template_gammas(SPECS[:len(COLS)], ocols, ocols, inv[:len(sl)].astype(np.int32),
-                              inv[len(sl):].astype(np.int32))
+    if job.link_type == "link_only":  # rows index the two tables
+        ul, il = np.unique(sl, return_inverse=True)
+        ur, ir = np.unique(sr, return_inverse=True)
+        tl, tr = rows_of(job, 0, ul), rows_of(job, job.r_side(), ur)
+        ocl = [orc.StrCol(tl[c].tolist()) for c in cols]
+        ocr = [orc.StrCol(tr[c].tolist()) for c in cols]
+        ref = orc.template_gammas(specs, ocl, ocr, il.astype(np.int32), ir.astype(np.int32))
+        del ocl, ocr, tl, tr
+    else:
+        rows, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
+        sub = rows_of(job, 0, rows)
+        ocols = [orc.StrCol(sub[c].tolist()) for c in cols]
+        ref = orc.template_gammas(specs, ocols, ocols, inv[:len(sl)].astype(np.int32), inv[len(sl):].astype(np.int32))
+        del ocols, sub
     gam = job.gammas_host()
     bad = np.nonzero((gam[idx] != ref).any(axis=1))[0]
     assert len(bad) == 0, (len(bad), idx[bad[:5]])
-    del ref, ocols, sub, l, r
+    del ref
     names, nlev = job.code_meta
     lam0, lp0 = params.params["λ"], params._level_probabilities()
     hist_o, mp_o = orc.em_iterate(gam, nlev, lam0, [m for m, _ in lp0], [u for _, u in lp0], iters, 1e-300)
     del gam
+    assert len(hist_o) == iters
     for lam_o, m_o, u_o in hist_o:
         stats = job.em_stats(params.params["λ"], params._level_probabilities())
         new_lambda, rows_ = m_step_rows(stats, names, nlev)
@@ -154,3 +165,93 @@ def test_cfg4_shard_full_size(amd):
             assert all(rel_close(a, b) for a, b in zip(u, u_o[k])), (k, u, u_o[k])
     mp = job.score(params.params["λ"], params._level_probabilities())
     assert np.allclose(mp, mp_o, rtol=1e-9, atol=0, equal_nan=True)
+    return mp, l, r
+
+
+def test_cfg4_shard_full_size(amd, heartbeat):
+    """BASELINE configs[3] at one GPU's share: a 20M-record dedupe (blocking surname | dob: 6.2e9 candidate
+    ordinals, past 2^31) whose ordinal space is split over 8 GPUs; this process is rank 0 and generates only
+    its slice (~770M pairs), as each rank of the 8-GPU job does (blocking.py:95-160, int64 ordinals).  A
+    strided sample of 2M comparison vectors is bit-exact against oracle.template_gammas, and 10 EM
+    iterations of λ / m / u plus every pair's match_probability agree with oracle.em_iterate at 1e-9."""
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    df = make_records(20_000_000, surname_vocab=300_000, arrow=True)[["unique_id"] + COLS]
+    params = Params(cfg_settings(4, max_iterations=10), amd)
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0, shard=(0, 8))
+    del df
+    job.block(st["blocking_rules"])
+    assert job.n_candidates > 2 ** 31 and job.n_pairs > 500_000_000
+    job.gammas(st)
+    check_shard(job, params, COLS, 10)
+
+
+CFG5_RULES = ["l.surname = r.surname", "l.dob = r.dob and l.city = r.city"]
+
+
+def test_cfg5_shard_full_size(amd, heartbeat):
+    """BASELINE configs[4] at one GPU's share: 100M records with the free-text address column (6 columns,
+    address Levenshtein-4), pair-ordinal shard 0 of 8 (~1.21B of ~9.7e9 candidate pairs).  Blocking is
+    surname | (dob AND city): surname | dob gives ~1.6e11 pairs at 100M records (29k dates put ~3,400
+    records in each dob block), so the dob rule is narrowed by city to reach cfg5's ~1e10.
+    Records: synthetic.make_records_parallel (64 chunks over one vocabulary).  A 2M-pair strided sample of
+    comparison vectors bit-exact, 10 EM iterations and every match_probability at 1e-9 (README.md:14,
+    case_statements.py:117-141)."""
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records_parallel
+    cols = COLS + ["address"]
+    df = make_records_parallel(100_000_000, 64, 16, surname_vocab=1_000_000, with_address=True)[["unique_id"] + cols]
+    settings = cfg_settings(5, max_iterations=10)
+    settings["blocking_rules"] = list(CFG5_RULES)
+    params = Params(settings, amd)
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0, shard=(0, 8))
+    del df
+    job.block(st["blocking_rules"])
+    assert job.n_candidates > 9_000_000_000 and job.n_pairs > 1_100_000_000
+    job.gammas(st)
+    check_shard(job, params, cols, 10)
+
+
+def test_cfg3_shard_full_size(amd, heartbeat):
+    """BASELINE configs[2] at one GPU's share: link_only between two 10M-record tables (halves of one 20M
+    population, so duplicates straddle them), rules surname | dob | email (~3.1e9 candidates, past 2^31),
+    shard 0 of 8 (~386M pairs), tf on surname.  Comparison-vector sample, EM and match_probability as
+    check_shard; then every pair's tf_adjusted_match_prob against oracle.tf_adjust_codes over
+    host-factorised surnames at 1e-9 (blocking.py:95-160, term_frequencies.py:49-168)."""
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records_parallel
+    from splink_amd.term_frequencies import _bayes_pair
+    df = make_records_parallel(20_000_000, 16, 16, surname_vocab=300_000)[["unique_id"] + COLS]
+    inputs = [df.iloc[:10_000_000].reset_index(drop=True), df.iloc[10_000_000:].reset_index(drop=True)]
+    del df
+    settings = cfg_settings(4, max_iterations=10)
+    settings["link_type"] = "link_only"
+    settings["blocking_rules"] = ["l.surname = r.surname", "l.dob = r.dob", "l.email = r.email"]
+    for c in settings["comparison_columns"]:
+        if c["col_name"] == "surname":
+            c["term_frequency_adjustments"] = True
+    params = Params(settings, amd)
+    st = params.settings
+    job = Job("link_only", inputs, "unique_id", 0, shard=(0, 8))
+    del inputs
+    job.block(st["blocking_rules"])
+    assert job.n_candidates > 2 ** 31 and job.n_pairs > 300_000_000
+    job.gammas(st)
+    mp, l, r = check_shard(job, params, COLS, 10)
+    # tf on surname with the device dictionary ids (the product path: term_frequencies.py's GPU stage)
+    col = job._col_index[("surname", "str")]
+    n_values = job.ctx.tf_column_values(col)
+    sums, counts = job.ctx.tf_accumulate_column(col, n_values)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
+    table = _bayes_pair(adj_lambda, float(1 - params.params["λ"]))
+    tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
+    vl, vr = column_in_row_order(job, 0, "surname"), column_in_row_order(job, job.r_side(), "surname")
+    codes, _ = pd.factorize(pd.concat([vl, vr], ignore_index=True), use_na_sentinel=True)
+    want, _ = orc.tf_adjust_codes(codes[:len(vl)][l], codes[len(vl):][r], mp, params.params["λ"])
+    assert np.allclose(tf_mp, want, rtol=1e-9, atol=0, equal_nan=True)

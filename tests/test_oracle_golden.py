@@ -155,6 +155,13 @@ def test_tf_adjust():
     exp = tf["tf_adjusted_match_prob"].astype(float).to_numpy()
     assert np.allclose(out, exp, rtol=1e-9, atol=0)
     assert np.allclose(adjs[0], tf["surname_adj"].astype(float).to_numpy(), rtol=1e-9, atol=0)
+    # the vectorised restatement (the scale tests' checker) over integer value codes
+    import pandas as pd
+    codes, _ = pd.factorize(pd.concat([df_e["surname_l"], df_e["surname_r"]], ignore_index=True))
+    n = len(df_e)
+    out2, adj2 = orc.tf_adjust_codes(codes[:n], codes[n:], mp, lam)
+    assert np.array_equal(out2, out, equal_nan=True)
+    assert np.array_equal(adj2, adjs[0], equal_nan=True)
 
 
 EDGE = ["first_estep_test1", "first_estep_nulls", "tiny_numbers_estep", "tiny_numbers_em", "ll_test1", "ll_nulls",
