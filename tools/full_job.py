@@ -170,7 +170,8 @@ def main():
         "row": "full job, one GPU (separately labelled; never the headline)",
         "workload": (f"cfg3 per-GPU share: link_only {a.records} x {a.records} records, blocking surname|dob|email, "
                      f"5 columns, tf on surname, pair-ordinal shard {shard}/{n_shards}") if link else
-                    (f"cfg{a.config} columns at {a.records} records: blocking surname|dob, {len(COLS)} columns, "
+                    (f"cfg{a.config} columns at {a.records} records: blocking "
+                     f"{' | '.join('(' + r + ')' for r in st['blocking_rules'])}, {len(COLS)} columns, "
                      f"pair-ordinal shard {shard}/{n_shards}"),
         "records": a.records, "candidates_total": int(job.n_candidates), "pairs_this_gpu": int(P),
         "iterations": a.iters, "wall_s": wall, "job_wall_s": total,
