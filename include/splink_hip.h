@@ -297,24 +297,30 @@ int spk_score(spk_ctx *ctx, double lambda, double one_minus, const double *m, co
 /* ---- term-frequency adjustment (term_frequencies.py:122-168) ------------------- */
 /* For value ids of one column (per row, -1 NULL; both sides in one id space) accumulate, over
  * pairs with equal non-null values, Σ mp and count(mp) per value id (n_values slots), after spk_score.
- * The sums are exact and order-free (fixed point, mp truncated below 2^-260), so they are identical
- * for any run, grid and sharding.  The _exact forms return the fixed-point accumulators
- * (int64 [n_values x SPK_TF_LIMBS]) that ranks holding shards of the pairs all-reduce (int64 sum)
- * before spk_tf_limbs_to_sum; the double forms are that conversion of one context's accumulators. */
+ * The sums are exact and order-free, so they are identical for any run, grid and sharding.  Each value
+ * has a scale E_v (spk_tf_scales: ilogb of its largest term + 1, INT32_MIN for none) and is summed in
+ * fixed point relative to 2^E_v (20-bit limbs down to 2^(E_v - 260)), so tiny match probabilities keep
+ * their relative precision.  Ranks holding shards of the pairs all-reduce the scales with MAX, pass
+ * them to the _exact forms, all-reduce the returned accumulators (int64 [n_values x SPK_TF_LIMBS],
+ * sum) and convert them with spk_tf_limbs_to_sum; the double forms do all of that for one context. */
 #define SPK_TF_LIMBS 14
 int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
                       double *out_sum, int64_t *out_count);
+int spk_tf_scales(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
+                  int32_t *out_scale);
 int spk_tf_accumulate_exact(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
-                            int64_t *out_limbs, int64_t *out_count);
-/* Host only (no device): Σ mp per value from (all-reduced) accumulators. */
-int spk_tf_limbs_to_sum(int64_t n_values, const int64_t *limbs, double *out_sum);
+                            const int32_t *scale, int64_t *out_limbs, int64_t *out_count);
+/* Host only (no device): Σ mp per value from (all-reduced) accumulators and their scales. */
+int spk_tf_limbs_to_sum(int64_t n_values, const int64_t *limbs, const int32_t *scale, double *out_sum);
 /* The same with the value ids taken on the device from a string column's dictionary ids (columns
  * added with spk_table_add_raw_utf8: dense in [0, n_values), one id space for both sides, NULL
  * rows excluded), so no host-side factorisation of the tf column is needed.  spk_tf_column_values
  * gives n_values (SPK_E_STATE for a column without device ids). */
 int spk_tf_column_values(spk_ctx *ctx, int col, int64_t *out_n_values);
 int spk_tf_accumulate_column(spk_ctx *ctx, int col, int64_t n_values, double *out_sum, int64_t *out_count);
-int spk_tf_accumulate_column_exact(spk_ctx *ctx, int col, int64_t n_values, int64_t *out_limbs, int64_t *out_count);
+int spk_tf_scales_column(spk_ctx *ctx, int col, int64_t n_values, int32_t *out_scale);
+int spk_tf_accumulate_column_exact(spk_ctx *ctx, int col, int64_t n_values, const int32_t *scale,
+                                   int64_t *out_limbs, int64_t *out_count);
 int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *cols, const double *const *adj_tables,
                          const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
                          double *out_adj /* [count x n_tf_cols] or NULL */);

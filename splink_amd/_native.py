@@ -49,7 +49,8 @@ EXPORTS = [
     "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
-    "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum",
+    "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
+    "spk_tf_scales_column",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
     "spk_em_finalize_start", "spk_gammas_exact_ms",
 ]
@@ -79,13 +80,19 @@ def load_library():
     return lib
 
 
-def tf_limbs_to_sum(limbs) -> np.ndarray:
-    """Σmp per value from fixed-point accumulators (host only, no device)."""
+def tf_limbs_to_sum(limbs, scale) -> np.ndarray:
+    """Σmp per value from fixed-point accumulators and the values' scales (host only, no device)."""
     lib = load_library()
     limbs = np.ascontiguousarray(limbs, dtype=np.int64).reshape(-1, TF_LIMBS)
+    scale = np.ascontiguousarray(scale, dtype=np.int32)
+    assert len(scale) == len(limbs)
     out = np.zeros(max(len(limbs), 1), dtype=np.float64)
-    check(lib.spk_tf_limbs_to_sum(ctypes.c_int64(len(limbs)), _ptr(limbs), _ptr(out)), "spk_tf_limbs_to_sum")
+    check(lib.spk_tf_limbs_to_sum(ctypes.c_int64(len(limbs)), _ptr(limbs), _ptr(scale), _ptr(out)),
+          "spk_tf_limbs_to_sum")
     return out[:len(limbs)]
+
+
+TF_NO_SCALE = np.iinfo(np.int32).min  # a value without a positive term
 
 
 def device_count() -> int:
@@ -444,22 +451,40 @@ class Context:
               "spk_tf_accumulate")
         return s[:n_values], c[:n_values]
 
-    def tf_accumulate_exact(self, n_values, ids0, ids1):
-        """Fixed-point per-value Σmp accumulators (int64 [n_values, TF_LIMBS]) and counts: exact, so ranks
-        holding shards of the pairs sum them (all-reduce) before tf_limbs_to_sum."""
+    def tf_scales(self, n_values, ids0, ids1):
+        """Per-value scales (int32: ilogb of the value's largest mp + 1) of this context's pairs; ranks
+        holding shards of the pairs all-reduce them with MAX before tf_accumulate_exact."""
         ids0 = np.ascontiguousarray(ids0, dtype=np.int64)
         ids1 = np.ascontiguousarray(ids1, dtype=np.int64)
+        sc = np.zeros(max(n_values, 1), dtype=np.int32)
+        check(self._lib.spk_tf_scales(self._h, ctypes.c_int64(n_values), _ptr(ids0), _ptr(ids1), _ptr(sc)),
+              "spk_tf_scales")
+        return sc[:n_values]
+
+    def tf_scales_column(self, col: int, n_values: int):
+        sc = np.zeros(max(n_values, 1), dtype=np.int32)
+        check(self._lib.spk_tf_scales_column(self._h, ctypes.c_int(col), ctypes.c_int64(n_values), _ptr(sc)),
+              "spk_tf_scales_column")
+        return sc[:n_values]
+
+    def tf_accumulate_exact(self, n_values, ids0, ids1, scale):
+        """Fixed-point per-value Σmp accumulators (int64 [n_values, TF_LIMBS]) relative to 2^scale, and counts:
+        exact, so ranks holding shards of the pairs sum them (all-reduce) before tf_limbs_to_sum."""
+        ids0 = np.ascontiguousarray(ids0, dtype=np.int64)
+        ids1 = np.ascontiguousarray(ids1, dtype=np.int64)
+        scale = np.ascontiguousarray(scale, dtype=np.int32)
         limbs = np.zeros((max(n_values, 1), TF_LIMBS), dtype=np.int64)
         c = np.zeros(max(n_values, 1), dtype=np.int64)
-        check(self._lib.spk_tf_accumulate_exact(self._h, ctypes.c_int64(n_values), _ptr(ids0), _ptr(ids1), _ptr(limbs),
-                                                _ptr(c)), "spk_tf_accumulate_exact")
+        check(self._lib.spk_tf_accumulate_exact(self._h, ctypes.c_int64(n_values), _ptr(ids0), _ptr(ids1), _ptr(scale),
+                                                _ptr(limbs), _ptr(c)), "spk_tf_accumulate_exact")
         return limbs[:n_values], c[:n_values]
 
-    def tf_accumulate_column_exact(self, col: int, n_values: int):
+    def tf_accumulate_column_exact(self, col: int, n_values: int, scale):
+        scale = np.ascontiguousarray(scale, dtype=np.int32)
         limbs = np.zeros((max(n_values, 1), TF_LIMBS), dtype=np.int64)
         c = np.zeros(max(n_values, 1), dtype=np.int64)
-        check(self._lib.spk_tf_accumulate_column_exact(self._h, ctypes.c_int(col), ctypes.c_int64(n_values), _ptr(limbs),
-                                                       _ptr(c)), "spk_tf_accumulate_column_exact")
+        check(self._lib.spk_tf_accumulate_column_exact(self._h, ctypes.c_int(col), ctypes.c_int64(n_values), _ptr(scale),
+                                                       _ptr(limbs), _ptr(c)), "spk_tf_accumulate_column_exact")
         return limbs[:n_values], c[:n_values]
 
     def tf_column_values(self, col: int) -> int:

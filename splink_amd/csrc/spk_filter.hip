@@ -81,14 +81,13 @@ struct FiltArgs {
     const int16_t *thr;
     int n_thr;
     int nj, nl, ne, nn;
-    // LDS staging (k_filter): a chunk's rows are copied into a tile of `cap` rows x `nck` 16-byte chunks
-    // (chunk-major, like the image), then its pairs read their fields from the tile.
+    // LDS staging (k_filter): a chunk's rows are copied into one of two tiles of `cap` rows x `nck`
+    // 16-byte chunks (chunk-major, like the image), then its pairs read their fields from the tile.
+    // plan[region][k] = {lo, hi} of the l-side and r-side rows of chunk k of the region (k_chunk_plan).
     int nck, cap;
-    // Pairs [vlo, vhi) of rule 1 also carry view positions (vpl / vpr, indexed by pair ordinal): a block
-    // of rule 1 is contiguous in view order, so a chunk of them stages its rows by view position
-    // through vrows0 / vrows1 (view position -> table row) instead of by their scattered table rows.
-    const int32_t *vpl, *vpr, *vrows0, *vrows1;
-    int64_t vlo, vhi;
+    const int4 *plan;
+    int cpr;  // chunks per region
+    int64_t rows0, rows1;  // image rows (staging clamps the last 64-row block to them)
     FJw jw[FJ_MAX];
     FLev lev[FL_MAX];
     FEq eq[FE_MAX];
@@ -155,6 +154,9 @@ template <int FP>
 __device__ __attribute__((always_inline)) inline void append(const FiltArgs &A, const FCommon &c, int64_t r0,
                                                              unsigned int *cnt, const bool (&und)[FP],
                                                              const uint32_t (&p)[FP]) {
+#ifdef SPK_DIAG_NO_APPEND  // timing diagnostic only (wrong results): no work-list appends
+    return;
+#endif
     unsigned long long m[FP];
     unsigned int total = 0;
 #pragma unroll
@@ -382,254 +384,347 @@ __device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, c
 
 constexpr int N_FCOLS = FJ_MAX + FL_MAX + FE_MAX + FN_MAX;
 
-// The columns of FP pairs per lane (pairs base + u * 64 + lane, u < FP, those below `end`): per column
-// the FP pairs' field loads (tile or global image), their evaluation, one wave-aggregated append of the
-// undecided cells; then the codes.
-template <int FP, bool ST, bool C32>
-__device__ __attribute__((always_inline)) inline void eval_pairs(const FiltArgs &A, const Tile &T,
+// The columns of a wave's NPL pairs per lane (pairs wb + i * 64 + lane, i < NPL, those below `we`),
+// column by column: each column's parameters are read once per chunk, then its fields are loaded (tile or
+// global image), evaluated and appended FP pairs per lane at a time; acc keeps every pair's code.
+template <int NPL, int FP, bool ST, bool C32>
+__device__ __attribute__((always_inline)) inline void eval_chunk(const FiltArgs &A, const Tile &T,
                                                                  const int16_t *s_thr, unsigned int *s_cnt,
-                                                                 int64_t r0, uint32_t base, uint32_t end,
-                                                                 const uint32_t (&ox)[FP], const uint32_t (&oy)[FP]) {
+                                                                 int64_t r0, uint32_t wb, uint32_t we,
+                                                                 const uint32_t (&ox)[NPL], const uint32_t (&oy)[NPL]) {
     constexpr int SPAN = 64 * FP;
     const int lane = threadIdx.x & 63;
-    uint32_t p[FP], acc[FP];
-    bool act[FP], und[FP];
+    uint32_t acc[NPL];
 #pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        p[u] = base + u * 64 + lane;
-        act[u] = p[u] < end;
-        acc[u] = 0;
+    for (int i = 0; i < NPL; ++i) acc[i] = 0;
+    // the FP-pair group starting at pair i0: its pair ordinals, active flags and tile / image offsets
+#define SPK_GROUP(i0)                                                  \
+    const uint32_t base = wb + (i0) * 64;                              \
+    uint32_t p[FP], gx[FP], gy[FP];                                    \
+    bool act[FP], und[FP];                                             \
+    _Pragma("unroll") for (int u = 0; u < FP; ++u) {                   \
+        p[u] = base + u * 64 + lane;                                   \
+        act[u] = p[u] < we;                                            \
+        gx[u] = ox[(i0) + u];                                          \
+        gy[u] = oy[(i0) + u];                                          \
     }
 #pragma unroll 1
     for (int j = 0; j < A.nj; ++j) {
         const FJw &J = A.jw[j];
-        const bool ji = implied(J.c, base, SPAN);
-        const bool gi = J.geq && implied(J.ge.c, base, SPAN);
-        if (ji) {
+#ifdef SPK_DIAG_SKIP_JW  // timing diagnostic only (wrong results)
+        break;
+#endif
 #pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
-        }
-        if (gi) {
+        for (int i0 = 0; i0 < NPL; i0 += FP) {
+            if (wb + i0 * 64 >= we) break;  // wave-uniform
+            SPK_GROUP(i0)
+            uint32_t a2[FP];
 #pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
-        }
-        if (ji) {
-            if (J.geq && !gi) {  // only the gap EQ field is needed
-                Data8<FP> e;
-                load8<FP, ST>(A, T, J.ge.c.ci, J.ge.c.p0, J.ge.c.p1, J.ge.c.in, ox, oy, e.a, e.b);
-                ev_eq<FP>(J.ge, e, act, acc, und);
-                if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+            for (int u = 0; u < FP; ++u) a2[u] = 0;
+            const bool ji = implied(J.c, base, SPAN);
+            const bool gi = J.geq && implied(J.ge.c, base, SPAN);
+            if (ji) {
+#pragma unroll
+                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? J.c.imp_add : 0u;
             }
-            continue;
-        }
-        JwData<FP> d;
-        ld_jw<FP, ST>(A, T, J, ox, oy, d);
-        ev_jw<FP>(J, d, act, acc, und);
-        append<FP>(A, J.c, r0, &s_cnt[j], und, p);
-        if (J.geq && !gi) {
-            Data8<FP> e;
+            if (gi) {
 #pragma unroll
-            for (int u = 0; u < FP; ++u) {
-                e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
-                e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
+                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? J.ge.c.imp_add : 0u;
             }
-            ev_eq<FP>(J.ge, e, act, acc, und);
-            if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+            if (ji) {
+                if (J.geq && !gi) {  // only the gap EQ field is needed
+                    Data8<FP> e;
+                    load8<FP, ST>(A, T, J.ge.c.ci, J.ge.c.p0, J.ge.c.p1, J.ge.c.in, gx, gy, e.a, e.b);
+                    ev_eq<FP>(J.ge, e, act, a2, und);
+                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+                }
+            } else {
+                JwData<FP> d;
+                ld_jw<FP, ST>(A, T, J, gx, gy, d);
+                ev_jw<FP>(J, d, act, a2, und);
+                append<FP>(A, J.c, r0, &s_cnt[j], und, p);
+                if (J.geq && !gi) {
+                    Data8<FP> e;
+#pragma unroll
+                    for (int u = 0; u < FP; ++u) {
+                        e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
+                        e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
+                    }
+                    ev_eq<FP>(J.ge, e, act, a2, und);
+                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
         }
     }
 #pragma unroll 1
     for (int j = 0; j < A.nl; ++j) {
         const FLev &L = A.lev[j];
-        if (implied(L.c, base, SPAN)) {
+#ifdef SPK_DIAG_SKIP_LEV  // timing diagnostic only (wrong results)
+        break;
+#endif
 #pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? L.c.imp_add : 0u;
-            continue;
+        for (int i0 = 0; i0 < NPL; i0 += FP) {
+            if (wb + i0 * 64 >= we) break;
+            SPK_GROUP(i0)
+            uint32_t a2[FP];
+#pragma unroll
+            for (int u = 0; u < FP; ++u) a2[u] = 0;
+            if (implied(L.c, base, SPAN)) {
+#pragma unroll
+                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? L.c.imp_add : 0u;
+            } else {
+                Data16<FP> d;
+                load16<FP, ST>(A, T, L.c.ci, L.c.p0, L.c.p1, gx, gy, d.a, d.b);
+                ev_lev<FP>(L, s_thr, d, act, a2, und);
+                append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
+            }
+#pragma unroll
+            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
         }
-        Data16<FP> d;
-        load16<FP, ST>(A, T, L.c.ci, L.c.p0, L.c.p1, ox, oy, d.a, d.b);
-        ev_lev<FP>(L, s_thr, d, act, acc, und);
-        append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
     }
 #pragma unroll 1
     for (int j = 0; j < A.ne; ++j) {
         const FEq &E = A.eq[j];
-        if (implied(E.c, base, SPAN)) {
 #pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? E.c.imp_add : 0u;
-            continue;
+        for (int i0 = 0; i0 < NPL; i0 += FP) {
+            if (wb + i0 * 64 >= we) break;
+            SPK_GROUP(i0)
+            uint32_t a2[FP];
+#pragma unroll
+            for (int u = 0; u < FP; ++u) a2[u] = 0;
+            if (implied(E.c, base, SPAN)) {
+#pragma unroll
+                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? E.c.imp_add : 0u;
+            } else {
+                Data8<FP> d;
+                load8<FP, ST>(A, T, E.c.ci, E.c.p0, E.c.p1, E.c.in, gx, gy, d.a, d.b);
+                ev_eq<FP>(E, d, act, a2, und);
+                if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
+            }
+#pragma unroll
+            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
         }
-        Data8<FP> d;
-        load8<FP, ST>(A, T, E.c.ci, E.c.p0, E.c.p1, E.c.in, ox, oy, d.a, d.b);
-        ev_eq<FP>(E, d, act, acc, und);
-        if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
     }
 #pragma unroll 1
-    for (int j = 0; j < A.nn; ++j) f_num<FP, ST>(A, T, A.num[j], ox, oy, acc);
+    for (int j = 0; j < A.nn; ++j) {
 #pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        if (!act[u]) continue;
-        if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
-        else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
+        for (int i0 = 0; i0 < NPL; i0 += FP) {
+            if (wb + i0 * 64 >= we) break;
+            SPK_GROUP(i0)
+            (void)act;
+            (void)und;
+            (void)p;
+            uint32_t a2[FP];
+#pragma unroll
+            for (int u = 0; u < FP; ++u) a2[u] = 0;
+            f_num<FP, ST>(A, T, A.num[j], gx, gy, a2);
+#pragma unroll
+            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
+        }
+    }
+#undef SPK_GROUP
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const uint32_t q = wb + i * 64 + lane;
+        if (q >= we) continue;
+        if (C32) static_cast<uint32_t *>(A.codes)[q] = acc[i];
+        else static_cast<uint16_t *>(A.codes)[q] = (uint16_t)acc[i];
     }
 }
 
-// Copy rows [lo, lo + span) of one side (table rows, or view positions mapped through `rows`) into tile
-// rows [dst, dst + span), every 16-byte chunk of the row (chunk-major, chunk c at c x cap).
-__device__ __attribute__((always_inline)) inline void stage_rows(const FiltArgs &A, uint4 *tile, const uint8_t *img,
-                                                                 uint32_t plane, const int32_t *rows, int32_t lo,
-                                                                 int span, int dst) {
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// LDS-DMA of rows [lo, lo + span) of one side's image into tile rows [dst, dst + span) (every 16-byte
+// chunk of the row, chunk-major): one global_load_lds_dwordx4 moves 64 consecutive rows of one chunk
+// plane (the destination is the wave's base + lane x 16).  Waves take the (plane, 64-row block) pieces
+// in turn.  Source rows past the image are clamped (their tile slots are never read).
+__device__ __attribute__((always_inline)) inline void stage_dma(const FiltArgs &A, uint4 *tile, const uint8_t *img,
+                                                                int64_t rows, int32_t lo, int span, int dst) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int nb = (span + 63) >> 6;
     const uint4 *src = reinterpret_cast<const uint4 *>(img);
-    const int64_t prow = plane >> 4;
-    for (int r = threadIdx.x; r < span; r += F_THREADS) {
-        const int64_t row = rows ? (int64_t)rows[lo + r] : (int64_t)(lo + r);
-        for (int c = 0; c < A.nck; ++c) tile[c * A.cap + dst + r] = src[c * prow + row];
+    for (int piece = wv; piece < nb * A.nck; piece += F_THREADS / 64) {  // wave-uniform
+        const int c = piece / nb, b = piece - c * nb;
+        int64_t row = (int64_t)lo + b * 64 + lane;
+        row = row < rows ? row : rows - 1;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + (int64_t)c * rows + row),
+                                         (lds_void_t *)(tile + c * A.cap + dst + b * 64), 16, 0, 0);
     }
 }
 
-__device__ __attribute__((always_inline)) inline int32_t wave_min(int32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const int32_t w = __shfl_xor(v, o);
-        v = w < v ? w : v;
-    }
-    return v;
+// What a chunk's plan entry says: stage (the rows fit the tile) and where its rows sit in the tile.
+struct ChunkTile {
+    bool staged, merged;
+    int32_t lo, loL, loR;
+    int span, spanL, spanR;
+};
+__device__ __attribute__((always_inline)) inline ChunkTile chunk_tile(const FiltArgs &A, int4 m) {
+    ChunkTile t;
+    const int32_t loL = m.x, hiL = m.y, loR = m.z, hiR = m.w;
+    t.loL = loL;
+    t.loR = loR;
+    t.merged = A.img0 == A.img1 && loR <= hiL + 1 && loL <= hiR + 1;
+    t.spanL = hiL - loL + 1;
+    t.spanR = hiR - loR + 1;
+    t.lo = loL < loR ? loL : loR;
+    const int64_t span = t.merged ? (int64_t)(hiL > hiR ? hiL : hiR) - t.lo + 1 : (int64_t)t.spanL + t.spanR;
+    // the r range starts on a 64-row boundary of the tile (whole DMA pieces)
+    const int64_t need = t.merged ? span : (((int64_t)t.spanL + 63) & ~63) + t.spanR;
+    t.staged = hiL >= 0 && need <= A.cap;
+    t.span = (int)span;
+    return t;
 }
-__device__ __attribute__((always_inline)) inline int32_t wave_max(int32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const int32_t w = __shfl_xor(v, o);
-        v = w > v ? w : v;
+__device__ __attribute__((always_inline)) inline void stage_chunk(const FiltArgs &A, uint4 *tile, const ChunkTile &t) {
+    if (t.merged) {
+        stage_dma(A, tile, A.img0, A.rows0, t.lo, t.span, 0);
+    } else {
+        stage_dma(A, tile, A.img0, A.rows0, t.loL, t.spanL, 0);
+        stage_dma(A, tile, A.img1, A.rows1, t.loR, t.spanR, (t.spanL + 63) & ~63);
     }
-    return v;
 }
 
 // One workgroup per region of consecutive pair ordinals, walked in chunks of F_THREADS x NPL pairs (wave
 // w takes the chunk's w-th quarter, NPL pairs per lane).  Candidate pairs are within-block cross
 // products (blocking.py:145-158), so a chunk's pairs touch few rows, each of them many times: the
-// workgroup copies those rows' image rows into an LDS tile once (coalesced: consecutive rows are
+// workgroup copies those rows' image rows into an LDS tile once (LDS-DMA: consecutive rows are
 // consecutive in a chunk plane) and every pair then reads its two rows' fields from the tile instead of
-// gathering them from the image, one texture-addressed load per pair, field and side.  A chunk whose
-// rows do not fit the tile (a block of more rows than `cap`) gathers from the image as before.
+// gathering them from the image with one texture-addressed load per pair, field and side.  Software
+// pipeline, one barrier per chunk: chunk k+1's tile (the other buffer) and pair rows are in flight while
+// chunk k is evaluated.  A chunk whose rows do not fit the tile gathers from the image.
 template <int NPL, int FP, int MINW, bool C32>
 __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
-    static_assert(NPL % FP == 0, "pairs per lane");
     __shared__ unsigned int s_cnt[N_FCOLS + FJ_MAX];  // work-list lengths: per column slot, then JW gap EQs
-    __shared__ int32_t s_red[F_THREADS / 64][4];      // per wave: lo / hi of the chunk's l- and r-side rows
-    extern __shared__ uint4 s_dyn[];                  // the tile (cap x nck), then A.thr (n_thr entries)
-    uint4 *tile = s_dyn;
-    int16_t *s_thr = reinterpret_cast<int16_t *>(s_dyn + (int64_t)A.cap * A.nck);
+    extern __shared__ uint4 s_dyn[];                  // tiles 0 and 1 (cap x nck each), then A.thr
+    const int64_t tile_n = (int64_t)A.cap * A.nck;
+    int16_t *s_thr = reinterpret_cast<int16_t *>(s_dyn + 2 * tile_n);
     if (threadIdx.x < N_FCOLS + FJ_MAX) s_cnt[threadIdx.x] = 0;
     for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
+    const int64_t region = (int64_t)A.region_base + blockIdx.x;
+    const int64_t r0 = region * A.region_len;
     const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
     constexpr int WCH = 64 * NPL, CH = (F_THREADS / 64) * WCH;
-    const Tile T{tile, A.cap};
-    for (int64_t c0 = r0; c0 < r1; c0 += CH) {  // workgroup-uniform
-        const int64_t c1 = c0 + CH < r1 ? c0 + CH : r1;
-        const bool vg = A.vpl && c0 >= A.vlo && c1 <= A.vhi;  // rule-1 chunk: stage by view position
-        const int32_t *SL = vg ? A.vpl : A.pl, *SR = vg ? A.vpr : A.pr;
-        const uint32_t wb = (uint32_t)c0 + (uint32_t)(wv * WCH);
-        const uint32_t we = (int64_t)wb + WCH < c1 ? wb + WCH : (uint32_t)(c1 > (int64_t)wb ? c1 : wb);
-        int32_t x[NPL], y[NPL];
-        int32_t loL = INT32_MAX, hiL = -1, loR = INT32_MAX, hiR = -1;
+    const int nch = r1 > r0 ? (int)((r1 - r0 + CH - 1) / CH) : 0;
+    const int4 *plan = A.plan + region * A.cpr;
+    auto wave_range = [&](int k, uint32_t &wb, uint32_t &we) {
+        const int64_t c0 = r0 + (int64_t)k * CH, c1 = c0 + CH < r1 ? c0 + CH : r1;
+        wb = (uint32_t)c0 + (uint32_t)(wv * WCH);
+        we = (int64_t)wb + WCH < c1 ? wb + WCH : (uint32_t)(c1 > (int64_t)wb ? c1 : wb);
+    };
+    auto load_pairs = [&](uint32_t wb, uint32_t we, int32_t (&x)[NPL], int32_t (&y)[NPL]) {
 #pragma unroll
         for (int u = 0; u < NPL; ++u) {
             const uint32_t q = wb + u * 64 + lane;
-            const bool on = q < we;
-            x[u] = on ? SL[q] : 0;
-            y[u] = on ? SR[q] : 0;
-            if (on) {
-                loL = x[u] < loL ? x[u] : loL;
-                hiL = x[u] > hiL ? x[u] : hiL;
-                loR = y[u] < loR ? y[u] : loR;
-                hiR = y[u] > hiR ? y[u] : hiR;
-            }
+            x[u] = q < we ? A.pl[q] : 0;
+            y[u] = q < we ? A.pr[q] : 0;
         }
-        loL = wave_min(loL);
-        hiL = wave_max(hiL);
-        loR = wave_min(loR);
-        hiR = wave_max(hiR);
-        __syncthreads();  // the previous chunk's tile reads and s_red reads are done
-        if (lane == 0) {
-            s_red[wv][0] = loL;
-            s_red[wv][1] = hiL;
-            s_red[wv][2] = loR;
-            s_red[wv][3] = hiR;
-        }
+    };
+    int32_t x[NPL], y[NPL];
+    uint32_t wb = 0, we = 0;
+    ChunkTile t{};
+    if (nch > 0) {
+        wave_range(0, wb, we);
+        load_pairs(wb, we, x, y);
+        t = chunk_tile(A, plan[0]);
+        if (t.staged) stage_chunk(A, s_dyn, t);
+    }
+    for (int k = 0; k < nch; ++k) {  // workgroup-uniform
+        // chunk k's tile and pair rows have landed; every wave is done with chunk k - 1 (the other tile)
         __syncthreads();
-#pragma unroll
-        for (int w = 0; w < F_THREADS / 64; ++w) {
-            loL = s_red[w][0] < loL ? s_red[w][0] : loL;
-            hiL = s_red[w][1] > hiL ? s_red[w][1] : hiL;
-            loR = s_red[w][2] < loR ? s_red[w][2] : loR;
-            hiR = s_red[w][3] > hiR ? s_red[w][3] : hiR;
+        int32_t nx[NPL], ny[NPL];
+        uint32_t nwb = 0, nwe = 0;
+        ChunkTile nt{};
+        if (k + 1 < nch) {
+            wave_range(k + 1, nwb, nwe);
+            nt = chunk_tile(A, plan[k + 1]);
+            if (nt.staged) stage_chunk(A, s_dyn + ((k + 1) & 1) * tile_n, nt);
+            load_pairs(nwb, nwe, nx, ny);
         }
-        // the tile holds one range when the two sides' ranges overlap or touch (a symmetric self-join:
-        // both sides are rows of the same blocks), else the l range then the r range
-        const int32_t *rowsL = vg ? A.vrows0 : nullptr, *rowsR = vg ? A.vrows1 : nullptr;
-        const bool one_img = A.img0 == A.img1 && rowsL == rowsR;
-        const bool merged = one_img && loR <= hiL + 1 && loL <= hiR + 1;
-        const int64_t spanL = (int64_t)hiL - loL + 1, spanR = (int64_t)hiR - loR + 1;
-        const int32_t lo = loL < loR ? loL : loR;
-        const int64_t span = merged ? (int64_t)(hiL > hiR ? hiL : hiR) - lo + 1 : spanL + spanR;
-        const bool staged = hiL >= 0 && span <= A.cap;
-        if (staged) {
-            if (merged) {
-                stage_rows(A, tile, A.img0, A.plane0, rowsL, lo, (int)span, 0);
-            } else {
-                stage_rows(A, tile, A.img0, A.plane0, rowsL, loL, (int)spanL, 0);
-                stage_rows(A, tile, A.img1, A.plane1, rowsR, loR, (int)spanR, (int)spanL);
-            }
-            __syncthreads();
-            const int32_t bx = merged ? lo : loL, by = merged ? lo : loR - (int32_t)spanL;
+        if (t.staged) {
+            const Tile T{s_dyn + (k & 1) * tile_n, A.cap};
+            const int32_t bx = t.merged ? t.lo : t.loL;
+            const int32_t by = t.merged ? t.lo : t.loR - ((t.spanL + 63) & ~63);
+            uint32_t ox[NPL], oy[NPL];
 #pragma unroll
-            for (int it = 0; it < NPL; it += FP) {
-                const uint32_t base = wb + it * 64;
-                if (base >= we) break;  // wave-uniform
-                uint32_t ox[FP], oy[FP];
-#pragma unroll
-                for (int u = 0; u < FP; ++u) {
-                    const bool on = base + u * 64 + lane < we;
-                    ox[u] = on ? (uint32_t)(x[it + u] - bx) : 0u;
-                    oy[u] = on ? (uint32_t)(y[it + u] - by) : 0u;
-                }
-                eval_pairs<FP, true, C32>(A, T, s_thr, s_cnt, r0, base, we, ox, oy);
+            for (int u = 0; u < NPL; ++u) {
+                const bool on = wb + u * 64 + lane < we;
+                ox[u] = on ? (uint32_t)(x[u] - bx) : 0u;
+                oy[u] = on ? (uint32_t)(y[u] - by) : 0u;
             }
+            eval_chunk<NPL, FP, true, C32>(A, T, s_thr, s_cnt, r0, wb, we, ox, oy);
         } else {
-            if (vg) {  // the fallback gathers by table row
+            const Tile T{s_dyn, A.cap};
+            uint32_t ox[NPL], oy[NPL];
 #pragma unroll
-                for (int u = 0; u < NPL; ++u) {
-                    const uint32_t q = wb + u * 64 + lane;
-                    x[u] = q < we ? A.pl[q] : 0;
-                    y[u] = q < we ? A.pr[q] : 0;
-                }
+            for (int u = 0; u < NPL; ++u) {
+                ox[u] = (uint32_t)x[u] << 4;
+                oy[u] = (uint32_t)y[u] << 4;
             }
-#pragma unroll
-            for (int it = 0; it < NPL; it += FP) {
-                const uint32_t base = wb + it * 64;
-                if (base >= we) break;
-                uint32_t ox[FP], oy[FP];
-#pragma unroll
-                for (int u = 0; u < FP; ++u) {
-                    ox[u] = (uint32_t)x[it + u] << 4;
-                    oy[u] = (uint32_t)y[it + u] << 4;
-                }
-                eval_pairs<FP, false, C32>(A, T, s_thr, s_cnt, r0, base, we, ox, oy);
-            }
+            eval_chunk<NPL, FP, false, C32>(A, T, s_thr, s_cnt, r0, wb, we, ox, oy);
         }
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) {
+            x[u] = nx[u];
+            y[u] = ny[u];
+        }
+        wb = nwb;
+        we = nwe;
+        t = nt;
     }
     __syncthreads();
     const int64_t slot = A.region_base + blockIdx.x;
-    const int t = threadIdx.x;
-    if (t < A.nj) A.region_count[(int64_t)A.jw[t].c.k * A.n_regions + slot] = s_cnt[t];
-    else if (t >= FJ_MAX && t < FJ_MAX + A.nl) A.region_count[(int64_t)A.lev[t - FJ_MAX].c.k * A.n_regions + slot] = s_cnt[t];
-    else if (t >= FJ_MAX + FL_MAX && t < FJ_MAX + FL_MAX + A.ne)
-        A.region_count[(int64_t)A.eq[t - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[t];
-    else if (t >= FJ_MAX + FL_MAX + FE_MAX && t < FJ_MAX + FL_MAX + FE_MAX + A.nn)
-        A.region_count[(int64_t)A.num[t - FJ_MAX - FL_MAX - FE_MAX].c.k * A.n_regions + slot] = 0;
-    else if (t >= N_FCOLS && t < N_FCOLS + A.nj && A.jw[t - N_FCOLS].geq)
-        A.region_count[(int64_t)A.jw[t - N_FCOLS].ge.c.k * A.n_regions + slot] = s_cnt[t];
+    const int tt = threadIdx.x;
+    if (tt < A.nj) A.region_count[(int64_t)A.jw[tt].c.k * A.n_regions + slot] = s_cnt[tt];
+    else if (tt >= FJ_MAX && tt < FJ_MAX + A.nl) A.region_count[(int64_t)A.lev[tt - FJ_MAX].c.k * A.n_regions + slot] = s_cnt[tt];
+    else if (tt >= FJ_MAX + FL_MAX && tt < FJ_MAX + FL_MAX + A.ne)
+        A.region_count[(int64_t)A.eq[tt - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[tt];
+    else if (tt >= FJ_MAX + FL_MAX + FE_MAX && tt < FJ_MAX + FL_MAX + FE_MAX + A.nn)
+        A.region_count[(int64_t)A.num[tt - FJ_MAX - FL_MAX - FE_MAX].c.k * A.n_regions + slot] = 0;
+    else if (tt >= N_FCOLS && tt < N_FCOLS + A.nj && A.jw[tt - N_FCOLS].geq)
+        A.region_count[(int64_t)A.jw[tt - N_FCOLS].ge.c.k * A.n_regions + slot] = s_cnt[tt];
+}
+
+// The filter's chunk plan: for chunk k of region g (pairs [g L + k CH, ...) of the region's L), the lo / hi
+// row of each side ({INT32_MAX, -1} for an empty side).  Rows are A.pl / A.pr, or the view positions for
+// regions [va, vb) (vpl / vpr, rule 1's view launch).  Once per pair set.
+__global__ __launch_bounds__(256) void k_chunk_plan(const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
+                                                    const int32_t *__restrict__ vpl, const int32_t *__restrict__ vpr,
+                                                    int64_t va, int64_t vb, int64_t P, int64_t region_len, int cpr,
+                                                    int ch, int4 *__restrict__ plan) {
+    const int64_t g = blockIdx.x;
+    const int64_t region = g / cpr, k = g - region * cpr;
+    const bool view = region >= va && region < vb;
+    const int32_t *L = view ? vpl : pl, *R = view ? vpr : pr;
+    const int64_t r0 = region * region_len, r1 = r0 + region_len < P ? r0 + region_len : P;
+    const int64_t c0 = r0 + k * ch, c1 = c0 + ch < r1 ? c0 + ch : r1;
+    int32_t loL = INT32_MAX, hiL = -1, loR = INT32_MAX, hiR = -1;
+    for (int64_t q = c0 + threadIdx.x; q < c1; q += 256) {
+        const int32_t a = L[q], b = R[q];
+        loL = a < loL ? a : loL;
+        hiL = a > hiL ? a : hiL;
+        loR = b < loR ? b : loR;
+        hiR = b > hiR ? b : hiR;
+    }
+    __shared__ int32_t s[4][256];
+    s[0][threadIdx.x] = loL;
+    s[1][threadIdx.x] = hiL;
+    s[2][threadIdx.x] = loR;
+    s[3][threadIdx.x] = hiR;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            const int i = threadIdx.x, j = threadIdx.x + o;
+            s[0][i] = s[0][j] < s[0][i] ? s[0][j] : s[0][i];
+            s[1][i] = s[1][j] > s[1][i] ? s[1][j] : s[1][i];
+            s[2][i] = s[2][j] < s[2][i] ? s[2][j] : s[2][i];
+            s[3][i] = s[3][j] > s[3][i] ? s[3][j] : s[3][i];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) plan[g] = make_int4(s[0][0], s[1][0], s[2][0], s[3][0]);
 }
 
 // ---- host: the per-column decision constants --------------------------------------------------------------
@@ -751,7 +846,7 @@ static void make_num(const SimpleCol &s, const GammaArgs &A, FNum &N) {
 }
 
 int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::vector<SimpleCol> &simple,
-                           int64_t region_lo, int64_t region_hi, const FilterView *fv) {
+                           int64_t region_lo, int64_t region_hi, const int4 *plan, int cpr) {
     if (region_hi <= region_lo || simple.empty()) return SPK_OK;
     SPK_REQUIRE(A.img_rows0 <= IMG_MAX_ROWS && A.img_rows1 <= IMG_MAX_ROWS, SPK_E_LIMIT,
                 "spk_gammas: more than 2^27 rows in one table (row-image planes are limited to 2^31 bytes)");
@@ -799,23 +894,28 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
         SPK_REQUIRE(F.ne < FE_MAX, SPK_E_INVALID, "filter: EQ slots");
         make_eq(s, A, F.eq[F.ne++]);
     }
-    if (fv) {
-        F.vpl = fv->vpl;
-        F.vpr = fv->vpr;
-        F.vrows0 = fv->rows0;
-        F.vrows1 = fv->rows1;
-        F.vlo = fv->lo;
-        F.vhi = fv->hi;
-    }
-    // the staging tile: SPK_F_TILE_KB KiB of rows (at cfg2's 80-byte rows: 460 rows), so that
+    // the staging tiles: two of SPK_F_TILE_KB KiB of rows each (cfg2's 80-byte rows: 192 rows), so that
     // SPK_F_MINW workgroups fit a CU's 160 KiB of LDS
     F.nck = (int)(A.img_stride / 16);
     SPK_REQUIRE(F.nck >= 1 && F.nck * 16 <= IMG_MAX, SPK_E_INVALID, "filter: image stride");
-    F.cap = (int)((int64_t)SPK_F_TILE_KB * 1024 / (F.nck * 16));
+    F.cap = (int)((int64_t)SPK_F_TILE_KB * 1024 / (F.nck * 16)) / 64 * 64;
+    F.plan = plan;
+    F.cpr = cpr;
+    F.rows0 = A.img_rows0;
+    F.rows1 = A.img_rows1;
     const unsigned g = (unsigned)(region_hi - region_lo);
-    const size_t shm = (size_t)F.cap * F.nck * 16 + (size_t)A.n_thr * sizeof(int16_t);
+    const size_t shm = (size_t)2 * F.cap * F.nck * 16 + (size_t)A.n_thr * sizeof(int16_t);
     if (A.code16) k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, false><<<g, F_THREADS, shm, stream>>>(F);
     else k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, true><<<g, F_THREADS, shm, stream>>>(F);
+    SPK_HIP(hipGetLastError());
+    return SPK_OK;
+}
+
+int launch_chunk_plan(hipStream_t stream, const GammaArgs &A, const int32_t *vpl, const int32_t *vpr, int64_t va,
+                      int64_t vb, int4 *plan, int cpr) {
+    if (A.n_regions <= 0 || A.P <= 0) return SPK_OK;
+    k_chunk_plan<<<(unsigned)((int64_t)A.n_regions * cpr), 256, 0, stream>>>(A.pl, A.pr, vpl, vpr, va, vb, A.P, A.region_len,
+                                                                           cpr, filter_chunk_pairs(), plan);
     SPK_HIP(hipGetLastError());
     return SPK_OK;
 }

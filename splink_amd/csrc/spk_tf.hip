@@ -5,11 +5,14 @@
 // The per-value sums are exact and order-free, so they are bit-identical for any grid, any run and any
 // number of ranks: mp depends only on the comparison pattern, so Σ_{pairs with value v} mp =
 // Σ_p count(v, p) · mp(p).  The qualifying pairs' keys (v, pattern) are radix-sorted and run-length
-// encoded (integer counts), and each run adds count · mp(p) to value v's accumulator in fixed point:
-// SPK_TF_LIMBS int64 limbs of 20 bits (limb 0 the integer part, limb j the bits 2^-20j .. 2^-20(j-1)+1),
-// mp truncated below 2^-260.  Integer adds are exact, so the device atomics' order, the shard of pairs
-// and the ranks' all-reduce (int64 sum) do not change the result; one conversion to double at the end
-// (spk_tf_limbs_to_sum) gives every caller the same value.
+// encoded (integer counts).  Each value v has a scale E_v = max over its terms of ilogb(mp) + 1 (a first
+// pass, spk_tf_scales: ranks holding shards of the pairs all-reduce it with MAX), and each run adds
+// count · mp(p) · 2^-E_v to v's accumulator in fixed point: SPK_TF_LIMBS int64 limbs of 20 bits (limb 0
+// the integer part, limb j the bits 2^-20j .. 2^-20(j-1)+1), truncated below 2^-260.  The window follows
+// the value's largest term, so a value whose pairs all score tiny (mp ~ 1e-300, subnormals included)
+// keeps its relative precision (2^-200 or better); integer adds are exact, so the device atomics' order,
+// the shard of pairs and the ranks' all-reduce (int64 sum) do not change the result, and one conversion
+// to double at the end (spk_tf_limbs_to_sum, scaled back by 2^E_v) gives every caller the same value.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -38,22 +41,19 @@ __global__ void k_tf_keys(int64_t P, const int32_t *__restrict__ pl, const int32
     keys[p] = ok ? (((unsigned long long)a << 32) | c) : TF_NONE;
 }
 
-// The fixed-point limbs of x in [0, 1]: x = Σ_j limb_j 2^(-20 j), truncated below 2^-260.
-__device__ inline void tf_limbs(double x, uint32_t (&limb)[TF_LIMBS]) {
+// The fixed-point limbs of y = x 2^-E (x > 0, y < 1 for E >= ilogb(x) + 1): y = Σ_j limb_j 2^(-20 j),
+// truncated below 2^-260.
+__device__ inline void tf_limbs(double x, int E, uint32_t (&limb)[TF_LIMBS]) {
 #pragma unroll
     for (int j = 0; j < TF_LIMBS; ++j) limb[j] = 0;
     if (!(x > 0.0)) return;
-    if (x >= 1.0) {
-        limb[0] = 1;
-        return;
-    }
     const uint64_t bits = (uint64_t)__double_as_longlong(x);
     const int ex = (int)((bits >> 52) & 0x7FF);
     const uint64_t M = (bits & ((1ull << 52) - 1)) | (ex ? (1ull << 52) : 0ull);
-    // x = M 2^(e - 1075) (subnormals: e = 1); bit b of F = x 2^260 is bit b - s of M
-    const int s = (ex ? ex : 1) - 1075 + TF_BITS * (TF_LIMBS - 1);
+    // x = M 2^(e - 1075) (subnormals: e = 1); bit b of F = y 2^260 is bit b - s of M
+    const int s = (ex ? ex : 1) - 1075 - E + TF_BITS * (TF_LIMBS - 1);
 #pragma unroll
-    for (int j = 1; j < TF_LIMBS; ++j) {
+    for (int j = 0; j < TF_LIMBS; ++j) {
         const int lo = TF_BITS * (TF_LIMBS - 1 - j);  // F's bit of limb j's lowest bit
         const int sh = lo - s;
         uint64_t v;
@@ -63,10 +63,34 @@ __device__ inline void tf_limbs(double x, uint32_t (&limb)[TF_LIMBS]) {
     }
 }
 
-// One run of equal keys: its count times the pattern's mp, limb by limb, into the value's accumulator.
+// ilogb(x) + 1 for x > 0 (subnormals included): the smallest E with x < 2^E
+__device__ inline int tf_exponent(double x) {
+    const uint64_t bits = (uint64_t)__double_as_longlong(x);
+    const int ex = (int)((bits >> 52) & 0x7FF);
+    if (ex) return ex - 1022;
+    const uint64_t M = bits & ((1ull << 52) - 1);
+    return (63 - __clzll((long long)M)) - 1073;  // x = M 2^-1074
+}
+
+constexpr int TF_NO_SCALE = INT32_MIN;  // a value with no (positive) term
+
+// One run of equal keys: the value's scale (max of its terms' exponents).
+__global__ void k_tf_scale(const unsigned long long *__restrict__ keys, const unsigned int *__restrict__ n_runs,
+                           const double *__restrict__ mpat, int *__restrict__ scale) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)*n_runs) return;
+    const unsigned long long k = keys[i];
+    if (k == TF_NONE) return;
+    const double x = mpat[(uint32_t)(k & 0xFFFFFFFFu)];
+    if (x > 0.0) atomicMax(&scale[(int64_t)(k >> 32)], tf_exponent(x));
+}
+
+// One run of equal keys: its count times the pattern's mp, scaled by the value's 2^-E, limb by limb, into
+// the value's accumulator.
 __global__ void k_tf_runs(const unsigned long long *__restrict__ keys, const unsigned int *__restrict__ counts,
                           const unsigned int *__restrict__ n_runs, const double *__restrict__ mpat,
-                          unsigned long long *__restrict__ acc, unsigned long long *__restrict__ cnt) {
+                          const int *__restrict__ scale, unsigned long long *__restrict__ acc,
+                          unsigned long long *__restrict__ cnt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)*n_runs) return;
     const unsigned long long k = keys[i];
@@ -74,25 +98,25 @@ __global__ void k_tf_runs(const unsigned long long *__restrict__ keys, const uns
     const int64_t v = (int64_t)(k >> 32);
     const uint32_t c = (uint32_t)(k & 0xFFFFFFFFu);
     const unsigned long long n = counts[i];
+    atomicAdd(&cnt[v], n);
+    const double x = mpat[c];
+    const int E = scale[v];
+    if (!(x > 0.0) || E == TF_NO_SCALE) return;
     uint32_t limb[TF_LIMBS];
-    tf_limbs(mpat[c], limb);
+    tf_limbs(x, E, limb);
 #pragma unroll
     for (int j = 0; j < TF_LIMBS; ++j)
         if (limb[j]) atomicAdd(&acc[v * TF_LIMBS + j], n * (unsigned long long)limb[j]);
-    atomicAdd(&cnt[v], n);
 }
 
-// Exact per-value sums over the current pairs, value ids per row on the device (d0 side 0, d1 side 1).
-static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int64_t *out_limbs,
-                    int64_t *out_count) {
+// The runs of (value, pattern) keys of the current pairs, value ids per row on the device (d0 side 0, d1
+// side 1), chunk by chunk: scale pass (acc null: each value's scale into d_scale) or sum pass (the counts
+// and the scaled fixed-point sums at the given d_scale).
+static int tf_pass(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int *d_scale,
+                   unsigned long long *acc, unsigned long long *cnt) {
     SPK_REQUIRE(ctx->mpat_valid && ctx->mpat_score.p, SPK_E_STATE, "tf: run spk_score first (mp per pattern)");
     SPK_REQUIRE(n_values < ((int64_t)1 << 31), SPK_E_LIMIT, "tf: more than 2^31 distinct values");
     const int64_t P = ctx->n_pairs;
-    DevBuf<unsigned long long> acc, cnt;
-    SPK_TRY(acc.alloc((size_t)n_values * TF_LIMBS + 1));
-    SPK_TRY(cnt.alloc((size_t)n_values + 1));
-    SPK_HIP(hipMemsetAsync(acc.p, 0, ((size_t)n_values * TF_LIMBS + 1) * 8, ctx->stream));
-    SPK_HIP(hipMemsetAsync(cnt.p, 0, ((size_t)n_values + 1) * 8, ctx->stream));
     // the sort and the run counts work on uint32 lengths: chunks of at most 2^30 pairs
     const int64_t CH = (int64_t)1 << 30;
     DevBuf<unsigned long long> k_in, k_out, uniq;
@@ -122,9 +146,41 @@ static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int
         SPK_TRY(tmp.alloc(std::max(bytes, b2) + 1));
         SPK_HIP(rocprim::radix_sort_keys(tmp.p, bytes, k_in.p, k_out.p, (size_t)n, 0, 64, ctx->stream));
         SPK_HIP(rocprim::run_length_encode(tmp.p, b2, k_out.p, (size_t)n, uniq.p, runs.p, n_runs.p, ctx->stream));
-        k_tf_runs<<<g, 256, 0, ctx->stream>>>(uniq.p, runs.p, n_runs.p, ctx->mpat_score.p, acc.p, cnt.p);
+        if (acc) k_tf_runs<<<g, 256, 0, ctx->stream>>>(uniq.p, runs.p, n_runs.p, ctx->mpat_score.p, d_scale, acc, cnt);
+        else k_tf_scale<<<g, 256, 0, ctx->stream>>>(uniq.p, n_runs.p, ctx->mpat_score.p, d_scale);
         SPK_HIP(hipGetLastError());
     }
+    return SPK_OK;
+}
+
+__global__ void k_fill_i32(int64_t n, int v, int *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = v;
+}
+
+// Per-value scales of this context's pairs (TF_NO_SCALE: no positive term).
+static int tf_scales(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int32_t *out_scale) {
+    DevBuf<int> sc;
+    SPK_TRY(sc.alloc((size_t)n_values + 1));
+    k_fill_i32<<<(unsigned)((n_values + 256) / 256), 256, 0, ctx->stream>>>(n_values + 1, TF_NO_SCALE, sc.p);
+    SPK_TRY(tf_pass(ctx, n_values, d0, d1, sc.p, nullptr, nullptr));
+    if (n_values) SPK_HIP(hipMemcpyAsync(out_scale, sc.p, (size_t)n_values * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+// Exact per-value sums at the given scales (every rank's scales all-reduced with MAX).
+static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, const int32_t *scale,
+                    int64_t *out_limbs, int64_t *out_count) {
+    DevBuf<unsigned long long> acc, cnt;
+    DevBuf<int> sc;
+    SPK_TRY(acc.alloc((size_t)n_values * TF_LIMBS + 1));
+    SPK_TRY(cnt.alloc((size_t)n_values + 1));
+    SPK_TRY(sc.alloc((size_t)n_values + 1));
+    SPK_HIP(hipMemsetAsync(acc.p, 0, ((size_t)n_values * TF_LIMBS + 1) * 8, ctx->stream));
+    SPK_HIP(hipMemsetAsync(cnt.p, 0, ((size_t)n_values + 1) * 8, ctx->stream));
+    if (n_values) SPK_HIP(hipMemcpyAsync(sc.p, scale, (size_t)n_values * 4, hipMemcpyHostToDevice, ctx->stream));
+    SPK_TRY(tf_pass(ctx, n_values, d0, d1, sc.p, acc.p, cnt.p));
     if (n_values) {
         SPK_HIP(hipMemcpyAsync(out_limbs, acc.p, (size_t)n_values * TF_LIMBS * 8, hipMemcpyDeviceToHost, ctx->stream));
         SPK_HIP(hipMemcpyAsync(out_count, cnt.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -193,8 +249,9 @@ static int column_ids(spk_ctx *ctx, Table &t, int col, DevBuf<int64_t> &out, int
 
 using namespace spk;
 
-extern "C" int spk_tf_limbs_to_sum(int64_t n_values, const int64_t *limbs, double *out_sum) {
-    SPK_REQUIRE(n_values >= 0 && (n_values == 0 || (limbs && out_sum)), SPK_E_INVALID, "spk_tf_limbs_to_sum: bad args");
+extern "C" int spk_tf_limbs_to_sum(int64_t n_values, const int64_t *limbs, const int32_t *scale, double *out_sum) {
+    SPK_REQUIRE(n_values >= 0 && (n_values == 0 || (limbs && scale && out_sum)), SPK_E_INVALID,
+                "spk_tf_limbs_to_sum: bad args");
     for (int64_t v = 0; v < n_values; ++v) {
         int64_t l[TF_LIMBS];
         for (int j = 0; j < TF_LIMBS; ++j) l[j] = limbs[v * TF_LIMBS + j];
@@ -204,63 +261,101 @@ extern "C" int spk_tf_limbs_to_sum(int64_t n_values, const int64_t *limbs, doubl
         }
         double acc = 0.0;
         for (int j = TF_LIMBS - 1; j > 0; --j) acc = (acc + (double)l[j]) * std::ldexp(1.0, -TF_BITS);
-        out_sum[v] = acc + (double)l[0];
+        acc += (double)l[0];
+        out_sum[v] = scale[v] == TF_NO_SCALE ? 0.0 : std::ldexp(acc, scale[v]);
     }
     return SPK_OK;
 }
 
-extern "C" int spk_tf_accumulate_exact(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
-                                       int64_t *out_limbs, int64_t *out_count) {
-    SPK_REQUIRE(ctx && ids_side0 && ids_side1 && (n_values == 0 || (out_limbs && out_count)) && n_values >= 0,
-                SPK_E_INVALID, "spk_tf_accumulate_exact: bad args");
-    SPK_REQUIRE(ctx->pairs_valid && ctx->codes_valid, SPK_E_STATE, "spk_tf_accumulate_exact: run spk_score first");
-    SPK_HIP(hipSetDevice(ctx->device));
-    SPK_TRY(settle_gammas(ctx, nullptr));
-    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+// Value ids per row of both sides on the device: host arrays (ids_side0 / 1) or the column's dictionary ids.
+struct TfIds {
     DevBuf<int64_t> d0, d1;
-    SPK_TRY(d0.alloc((size_t)t0.n + 1));
-    SPK_TRY(d1.alloc((size_t)t1.n + 1));
-    if (t0.n) SPK_HIP(hipMemcpyAsync(d0.p, ids_side0, (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
-    if (t1.n) SPK_HIP(hipMemcpyAsync(d1.p, ids_side1, (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
-    return tf_exact(ctx, n_values, d0.p, d1.p, out_limbs, out_count);
+    const int64_t *p0 = nullptr, *p1 = nullptr;
+};
+static int tf_host_ids(spk_ctx *ctx, const int64_t *ids_side0, const int64_t *ids_side1, TfIds &I) {
+    Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
+    SPK_TRY(I.d0.alloc((size_t)t0.n + 1));
+    SPK_TRY(I.d1.alloc((size_t)t1.n + 1));
+    if (t0.n) SPK_HIP(hipMemcpyAsync(I.d0.p, ids_side0, (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (t1.n) SPK_HIP(hipMemcpyAsync(I.d1.p, ids_side1, (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
+    I.p0 = I.d0.p;
+    I.p1 = I.d1.p;
+    return SPK_OK;
 }
-
-extern "C" int spk_tf_accumulate_column_exact(spk_ctx *ctx, int col, int64_t n_values, int64_t *out_limbs,
-                                              int64_t *out_count) {
-    SPK_REQUIRE(ctx && n_values >= 0 && (n_values == 0 || (out_limbs && out_count)), SPK_E_INVALID,
-                "spk_tf_accumulate_column_exact: bad args");
-    SPK_REQUIRE(ctx->pairs_valid && ctx->codes_valid, SPK_E_STATE, "spk_tf_accumulate_column_exact: run spk_score first");
-    SPK_HIP(hipSetDevice(ctx->device));
-    SPK_TRY(settle_gammas(ctx, nullptr));
+static int tf_column_ids(spk_ctx *ctx, int col, int64_t n_values, TfIds &I) {
     Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
-    DevBuf<int64_t> d0, d1;
     int64_t n0 = 0, n1 = 0;
-    SPK_TRY(column_ids(ctx, t0, col, d0, &n0));
-    if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, col, d1, &n1));
-    SPK_REQUIRE(n_values == n0, SPK_E_INVALID, "spk_tf_accumulate_column_exact: n_values is not the column's value count");
-    return tf_exact(ctx, n_values, d0.p, &t1 != &t0 ? d1.p : d0.p, out_limbs, out_count);
+    SPK_TRY(column_ids(ctx, t0, col, I.d0, &n0));
+    if (&t1 != &t0) SPK_TRY(column_ids(ctx, t1, col, I.d1, &n1));
+    SPK_REQUIRE(n_values == n0, SPK_E_INVALID, "tf: n_values is not the column's value count");
+    I.p0 = I.d0.p;
+    I.p1 = &t1 != &t0 ? I.d1.p : I.d0.p;
+    return SPK_OK;
+}
+static int tf_ready(spk_ctx *ctx, const char *what) {
+    SPK_REQUIRE(ctx->pairs_valid && ctx->codes_valid, SPK_E_STATE, std::string(what) + ": run spk_score first");
+    SPK_HIP(hipSetDevice(ctx->device));
+    return settle_gammas(ctx, nullptr);
 }
 
-// The double forms: the exact sums of this context's pairs, converted (the same values the exact forms
-// give after a one-rank all-reduce).
-static int tf_sums(int64_t n_values, const std::vector<int64_t> &limbs, double *out_sum) {
-    return spk_tf_limbs_to_sum(n_values, limbs.data(), out_sum);
+extern "C" int spk_tf_scales(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
+                             int32_t *out_scale) {
+    SPK_REQUIRE(ctx && ids_side0 && ids_side1 && n_values >= 0 && (n_values == 0 || out_scale), SPK_E_INVALID,
+                "spk_tf_scales: bad args");
+    SPK_TRY(tf_ready(ctx, "spk_tf_scales"));
+    TfIds I;
+    SPK_TRY(tf_host_ids(ctx, ids_side0, ids_side1, I));
+    return tf_scales(ctx, n_values, I.p0, I.p1, out_scale);
 }
 
+extern "C" int spk_tf_scales_column(spk_ctx *ctx, int col, int64_t n_values, int32_t *out_scale) {
+    SPK_REQUIRE(ctx && n_values >= 0 && (n_values == 0 || out_scale), SPK_E_INVALID, "spk_tf_scales_column: bad args");
+    SPK_TRY(tf_ready(ctx, "spk_tf_scales_column"));
+    TfIds I;
+    SPK_TRY(tf_column_ids(ctx, col, n_values, I));
+    return tf_scales(ctx, n_values, I.p0, I.p1, out_scale);
+}
+
+extern "C" int spk_tf_accumulate_exact(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
+                                       const int32_t *scale, int64_t *out_limbs, int64_t *out_count) {
+    SPK_REQUIRE(ctx && ids_side0 && ids_side1 && (n_values == 0 || (scale && out_limbs && out_count)) && n_values >= 0,
+                SPK_E_INVALID, "spk_tf_accumulate_exact: bad args");
+    SPK_TRY(tf_ready(ctx, "spk_tf_accumulate_exact"));
+    TfIds I;
+    SPK_TRY(tf_host_ids(ctx, ids_side0, ids_side1, I));
+    return tf_exact(ctx, n_values, I.p0, I.p1, scale, out_limbs, out_count);
+}
+
+extern "C" int spk_tf_accumulate_column_exact(spk_ctx *ctx, int col, int64_t n_values, const int32_t *scale,
+                                              int64_t *out_limbs, int64_t *out_count) {
+    SPK_REQUIRE(ctx && n_values >= 0 && (n_values == 0 || (scale && out_limbs && out_count)), SPK_E_INVALID,
+                "spk_tf_accumulate_column_exact: bad args");
+    SPK_TRY(tf_ready(ctx, "spk_tf_accumulate_column_exact"));
+    TfIds I;
+    SPK_TRY(tf_column_ids(ctx, col, n_values, I));
+    return tf_exact(ctx, n_values, I.p0, I.p1, scale, out_limbs, out_count);
+}
+
+// The double forms: the exact sums of this context's pairs at its own scales, converted (the values the
+// exact forms give after a one-rank all-reduce).
 extern "C" int spk_tf_accumulate(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
                                  double *out_sum, int64_t *out_count) {
     SPK_REQUIRE(n_values >= 0 && (n_values == 0 || (out_sum && out_count)), SPK_E_INVALID, "spk_tf_accumulate: bad args");
+    std::vector<int32_t> scale((size_t)n_values + 1);
     std::vector<int64_t> limbs((size_t)n_values * TF_LIMBS + 1);
-    SPK_TRY(spk_tf_accumulate_exact(ctx, n_values, ids_side0, ids_side1, limbs.data(), out_count));
-    return tf_sums(n_values, limbs, out_sum);
+    SPK_TRY(spk_tf_scales(ctx, n_values, ids_side0, ids_side1, scale.data()));
+    SPK_TRY(spk_tf_accumulate_exact(ctx, n_values, ids_side0, ids_side1, scale.data(), limbs.data(), out_count));
+    return spk_tf_limbs_to_sum(n_values, limbs.data(), scale.data(), out_sum);
 }
 
 extern "C" int spk_tf_accumulate_column(spk_ctx *ctx, int col, int64_t n_values, double *out_sum, int64_t *out_count) {
     SPK_REQUIRE(n_values >= 0 && (n_values == 0 || (out_sum && out_count)), SPK_E_INVALID,
                 "spk_tf_accumulate_column: bad args");
+    std::vector<int32_t> scale((size_t)n_values + 1);
     std::vector<int64_t> limbs((size_t)n_values * TF_LIMBS + 1);
-    SPK_TRY(spk_tf_accumulate_column_exact(ctx, col, n_values, limbs.data(), out_count));
-    return tf_sums(n_values, limbs, out_sum);
+    SPK_TRY(spk_tf_scales_column(ctx, col, n_values, scale.data()));
+    SPK_TRY(spk_tf_accumulate_column_exact(ctx, col, n_values, scale.data(), limbs.data(), out_count));
+    return spk_tf_limbs_to_sum(n_values, limbs.data(), scale.data(), out_sum);
 }
 
 extern "C" int spk_tf_column_values(spk_ctx *ctx, int col, int64_t *out_n_values) {

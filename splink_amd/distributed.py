@@ -49,11 +49,12 @@ def stream_ordered_reduce(device: int) -> bool:
     return dist is not None and dist.get_backend() != "gloo"
 
 
-def allreduce_host_(arr, force: bool = False):
-    """In-place sum over all ranks of a host numpy array (float64 / int64), e.g. the per-value
-    (Σmp, count) tables of the term-frequency adjustment (term_frequencies.py:49-65 groups over all
-    pairs, which are sharded here).  RCCL needs device tensors, so under `nccl` the array is staged
-    through the rank's GPU; under `gloo` it is reduced on the host."""
+def allreduce_host_(arr, force: bool = False, op: str = "sum"):
+    """In-place sum (op "sum") or maximum (op "max") over all ranks of a host numpy array (float64 / int64 /
+    int32), e.g. the per-value fixed-point sums, counts and scales of the term-frequency adjustment
+    (term_frequencies.py:49-65 groups over all pairs, which are sharded here).  RCCL needs device
+    tensors, so under `nccl` the array is staged through the rank's GPU; under `gloo` it is reduced on
+    the host."""
     import numpy as np
     import torch
     dist = _dist()
@@ -62,7 +63,7 @@ def allreduce_host_(arr, force: bool = False):
     t = torch.from_numpy(np.ascontiguousarray(arr))
     if dist.get_backend() != "gloo":
         t = t.to(f"cuda:{torch.cuda.current_device()}")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     arr[...] = t.cpu().numpy()
     return arr
 

@@ -4,7 +4,8 @@ Per tf column c: over pairs whose c_l and c_r are equal and non-NULL, the mean m
 probability per value (adj_lambda, :49-65) is Bayes-combined with 1-λ; pairs without a
 lookup value get 0.5 (:68-95); tf_adjusted_match_prob = bayes(mp, adj_c1, ...) (:98-117).
 The per-value sums and the per-pair Bayes combination run on the GPU
-(spk_tf_accumulate_exact / spk_tf_apply): the sums are exact fixed-point accumulators, so ranks
+(spk_tf_scales, spk_tf_accumulate_exact / spk_tf_apply): the sums are exact fixed-point accumulators
+relative to each value's largest term, so ranks
 holding shards of the pairs all-reduce them as integers and every run and rank count gives
 bit-identical adjustments; the per-value lookup arithmetic is a handful of operations per value.
 """
@@ -80,9 +81,12 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
     ids0_list, ids1_list, tables = [], [], []
     shared = job.reduces_across_ranks()  # the reference groups over ALL pairs (:49-65); ranks hold shards
     for c, col in zip(tf_cols, dev_cols):
+        # two passes over the pairs: each value's scale (the exponent of its largest mp; MAX over ranks),
+        # then the fixed-point sums relative to it (integer SUM over ranks): every rank ends with the
+        # one-GPU result, and tiny match probabilities keep their relative precision
         if on_device:
             n_values = job.ctx.tf_column_values(col)
-            limbs, counts = job.ctx.tf_accumulate_column_exact(col, n_values)
+            scale = job.ctx.tf_scales_column(col, n_values)
         else:
             sides = (0, 1) if job.link_type == "link_only" else (0,)
             vals = [pd.Series([None if T.is_null_scalar(v) else v for v in job.host_values(s, c).tolist()],
@@ -90,14 +94,20 @@ def make_adjustment_for_term_frequencies(df_e: object, params: Params, settings:
             codes, n_values = T.factorize_joint(vals)
             ids0 = codes[0]
             ids1 = codes[1] if len(codes) > 1 else codes[0]
-            limbs, counts = job.ctx.tf_accumulate_exact(n_values, ids0, ids1)
+            scale = job.ctx.tf_scales(n_values, ids0, ids1)
             ids0_list.append(ids0)
             ids1_list.append(ids1)
+        if shared:
+            D.allreduce_host_(scale, op="max")
+        if on_device:
+            limbs, counts = job.ctx.tf_accumulate_column_exact(col, n_values, scale)
+        else:
+            limbs, counts = job.ctx.tf_accumulate_exact(n_values, ids0, ids1, scale)
         if shared:
             # exact fixed-point sums and integer counts: the all-reduce gives every rank the one-GPU result
             D.allreduce_host_(limbs)
             D.allreduce_host_(counts)
-        sums = N.tf_limbs_to_sum(limbs)
+        sums = N.tf_limbs_to_sum(limbs, scale)
         with np.errstate(invalid="ignore", divide="ignore"):
             adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
         tables.append(_bayes_pair(adj_lambda, one_minus))

@@ -129,9 +129,13 @@ def _tf_rank_main(rank, world, port, out_dir):
     lo, hi = 4000 * rank // world, 4000 * (rank + 1) // world
     sums = np.bincount(ids[lo:hi], weights=mp[lo:hi], minlength=50).astype(np.float64)
     counts = np.bincount(ids[lo:hi], minlength=50).astype(np.int64)
+    # per-value scales (the exponent of each value's largest term) combine with MAX
+    scale = np.full(50, np.iinfo(np.int32).min, dtype=np.int32)
+    np.maximum.at(scale, ids[lo:hi], np.frexp(mp[lo:hi])[1].astype(np.int32))
+    D.allreduce_host_(scale, op="max")
     D.allreduce_host_(sums)
     D.allreduce_host_(counts)
-    np.savez(os.path.join(out_dir, f"tf{rank}.npz"), sums=sums, counts=counts)
+    np.savez(os.path.join(out_dir, f"tf{rank}.npz"), sums=sums, counts=counts, scale=scale)
     dist.destroy_process_group()
 
 
@@ -146,3 +150,6 @@ def test_two_rank_gloo_tf_tables(tmp_path):
         x = np.load(tmp_path / f"tf{k}.npz")
         assert (x["counts"] == np.bincount(ids, minlength=50)).all()
         assert np.allclose(x["sums"], np.bincount(ids, weights=mpv, minlength=50), rtol=1e-12, atol=0)
+        want = np.full(50, np.iinfo(np.int32).min, dtype=np.int32)
+        np.maximum.at(want, ids, np.frexp(mpv)[1].astype(np.int32))
+        assert np.array_equal(x["scale"], want)

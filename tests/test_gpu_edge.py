@@ -188,20 +188,61 @@ def test_tf_sums_use_the_scores_not_a_later_em_iteration(amd):
     """tf's per-value Σmp come from the last spk_score's parameters (term_frequencies.py:49-65 averages
     the scored df_e's match_probability), even when an E+M iteration with other parameters ran after the
     score (it rewrites the EM's own per-pattern table)."""
-    from splink_amd import _native as N
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    df = make_records(20_000, surname_vocab=400)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
+    params = Params(cfg_settings(2), amd)
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    P = job.n_pairs
+    assert P > 100_000
+    lp = params._level_probabilities()
+    mp = job.score(0.2, lp)
+    swapped = [(u, m) for m, u in lp]
+    job.em_stats(0.6, swapped)  # other parameters: a different mp per pattern
     rng = np.random.Generator(np.random.PCG64(5))
-    n_levels = [3, 3, 2]
-    P = 200_000
-    g = np.stack([rng.integers(-1, L, P) for L in n_levels], axis=1).astype(np.int8)
-    ctx = N.Context(0)
-    ctx.gammas_load(n_levels, g)
-    m = [0.1, 0.2, 0.7, 0.2, 0.3, 0.5, 0.4, 0.6]
-    u = [0.7, 0.2, 0.1, 0.6, 0.3, 0.1, 0.9, 0.1]
-    mp = ctx.score(0.2, 0.8, m, u, 0, P)
-    n_stats = 5 + 4 * sum(L + 1 for L in n_levels)
-    ctx.em_iteration(0.6, 0.4, u, m, n_stats)  # other parameters: a different mp per pattern
-    ids = rng.integers(0, 50, P).astype(np.int64)
-    s, c = ctx.tf_accumulate(50, ids, ids)
-    want = np.bincount(ids, weights=mp, minlength=50)
-    assert np.array_equal(c, np.bincount(ids, minlength=50))
+    ids = rng.integers(0, 50, len(df)).astype(np.int64)  # a value id per table row
+    s, c = job.ctx.tf_accumulate(50, ids, ids)
+    l, r = job.pair_rows()
+    ok = (ids[l] == ids[r]) & ~np.isnan(mp)
+    assert ok.sum() > 1000
+    want = np.bincount(ids[l][ok], weights=mp[ok], minlength=50)
+    assert np.array_equal(c, np.bincount(ids[l][ok], minlength=50))
     assert np.allclose(s, want, rtol=1e-12, atol=0.0)
+
+
+def test_tf_sums_keep_tiny_match_probabilities(amd):
+    """Per-value Σmp (term_frequencies.py:49-65) when every pair scores far below 2^-260 (mp ~ 1e-290 and
+    subnormal): the sums keep their relative precision (1e-12 against a host sum), so adj_lambda stays
+    the small positive mean the reference computes instead of 0 (parameters as tests/test_spark.py:130-160's
+    tiny m, pushed further)."""
+    import pandas as pd
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    df = make_records(20_000, surname_vocab=400)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
+    params = Params(cfg_settings(2), amd)
+    st = params.settings
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    tiny = []
+    for k, (m, u) in enumerate(params._level_probabilities()):
+        tiny.append(([1e-60 * (j + 1) * (k + 1) for j in range(len(m))], list(u)))
+    codes, _ = pd.factorize(job.tables[0]["surname"], use_na_sentinel=True)
+    codes = codes.astype(np.int64)
+    n = int(codes.max()) + 1
+    l, r = job.pair_rows()
+    for lam in (1e-3, 0.2):
+        mp = job.score(lam, tiny)
+        assert np.nanmax(mp) < 1e-250 and np.nanmin(mp) > 0.0
+        s, c = job.ctx.tf_accumulate(n, codes, codes)  # host value ids: the same scale and sum kernels
+        ok = (codes[l] >= 0) & (codes[l] == codes[r]) & ~np.isnan(mp)
+        want = np.bincount(codes[l][ok], weights=mp[ok], minlength=n)
+        assert np.array_equal(c, np.bincount(codes[l][ok], minlength=n))
+        has = c > 0
+        assert has.sum() > 50 and (s[has] > 0.0).all()
+        assert np.allclose(s, want, rtol=1e-12, atol=0.0)
