@@ -93,6 +93,18 @@ int spk_table_set_key(spk_ctx *ctx, int side, int rule, int which, const int64_t
  * Input columns are handed over once as Arrow buffers ("raw" columns, input row order, indexed by
  * `raw`, borrowed for the call).  Everything derived from them is computed on the device. */
 int spk_raw_utf8(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const uint8_t *data, const uint8_t *valid);
+/* The same from Arrow buffers as they are (zero-copy on the host side): `offsets` (n + 1, any base: a
+ * sliced array's first offset may be past 0), `data` the value buffer those offsets index, `validity`
+ * the Arrow validity bitmap (LSB first, from bit validity_bit_offset; NULL = no NULLs; offset -1: one byte
+ * per row instead, 0 = NULL).  on_device = 1:
+ * all three are device pointers (e.g. rows all-gathered from the ranks that uploaded them) and are
+ * copied device to device.  Rebasing, validity expansion and the length scan run on the device. */
+int spk_raw_utf8_arrow(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const uint8_t *data,
+                       const uint8_t *validity, int64_t validity_bit_offset, int on_device);
+/* 64-bit digest of a table's encoded device form (row permutation, ranks, every comparison column's
+ * metadata / bit-planes / values, blocking keys): two contexts that ingested the same rows by
+ * different routes (local upload, or rows gathered from other ranks) give the same digest. */
+int spk_table_digest(spk_ctx *ctx, int side, uint64_t *out);
 /* 8-byte values compared as bit patterns (int64 ids, canonical float64 bits, host-computed key ids). */
 int spk_raw_i64(spk_ctx *ctx, int raw, int64_t n, const int64_t *values, const uint8_t *valid);
 /* One equality term of a blocking rule: l-side column `raw_l` (table 0) = r-side column `raw_r` (the

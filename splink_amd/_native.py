@@ -50,7 +50,7 @@ EXPORTS = [
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
-    "spk_tf_scales_column",
+    "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_table_digest",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
     "spk_em_finalize_start", "spk_gammas_exact_ms",
 ]
@@ -200,6 +200,24 @@ class Context:
         valid = np.ascontiguousarray(valid, dtype=np.uint8)
         check(self._lib.spk_raw_utf8(self._h, ctypes.c_int(raw), ctypes.c_int64(len(offsets) - 1), _ptr(offsets),
                                      _ptr(data), _ptr(valid)), "spk_raw_utf8")
+
+    def raw_utf8_arrow(self, raw, n, offsets, data, bitmap=None, bit_offset=0):
+        """Arrow buffers as numpy views (no copies): offsets int64[n+1] (any base), data uint8, validity bitmap
+        (None = no NULLs; bit_offset -1 = one byte per row)."""
+        check(self._lib.spk_raw_utf8_arrow(self._h, ctypes.c_int(raw), ctypes.c_int64(n), _ptr(offsets), _ptr(data),
+                                           _ptr(bitmap), ctypes.c_int64(bit_offset), ctypes.c_int(0)),
+              "spk_raw_utf8_arrow")
+
+    def raw_utf8_device(self, raw, n, d_offsets, d_data, d_valid_bytes):
+        """The same from device buffers (int pointers: offsets int64[n+1], data, one validity byte per row)."""
+        check(self._lib.spk_raw_utf8_arrow(self._h, ctypes.c_int(raw), ctypes.c_int64(n), ctypes.c_void_p(d_offsets),
+                                           ctypes.c_void_p(d_data), ctypes.c_void_p(d_valid_bytes),
+                                           ctypes.c_int64(-1), ctypes.c_int(1)), "spk_raw_utf8_arrow")
+
+    def table_digest(self, side: int) -> int:
+        out = ctypes.c_uint64(0)
+        check(self._lib.spk_table_digest(self._h, ctypes.c_int(side), ctypes.byref(out)), "spk_table_digest")
+        return out.value
 
     def raw_i64(self, raw, values, valid):
         values = np.ascontiguousarray(values, dtype=np.int64)

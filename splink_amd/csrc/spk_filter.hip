@@ -384,29 +384,23 @@ __device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, c
 
 constexpr int N_FCOLS = FJ_MAX + FL_MAX + FE_MAX + FN_MAX;
 
-// The columns of a wave's NPL pairs per lane (pairs wb + i * 64 + lane, i < NPL, those below `we`),
-// column by column: each column's parameters are read once per chunk, then its fields are loaded (tile or
-// global image), evaluated and appended FP pairs per lane at a time; acc keeps every pair's code.
-template <int NPL, int FP, bool ST, bool C32>
-__device__ __attribute__((always_inline)) inline void eval_chunk(const FiltArgs &A, const Tile &T,
+// The columns of FP pairs per lane (pairs base + u * 64 + lane, u < FP, those below `end`): per column
+// the FP pairs' field loads (tile or global image), their evaluation, one wave-aggregated append of the
+// undecided cells; then the codes.
+template <int FP, bool ST, bool C32>
+__device__ __attribute__((always_inline)) inline void eval_pairs(const FiltArgs &A, const Tile &T,
                                                                  const int16_t *s_thr, unsigned int *s_cnt,
-                                                                 int64_t r0, uint32_t wb, uint32_t we,
-                                                                 const uint32_t (&ox)[NPL], const uint32_t (&oy)[NPL]) {
+                                                                 int64_t r0, uint32_t base, uint32_t end,
+                                                                 const uint32_t (&ox)[FP], const uint32_t (&oy)[FP]) {
     constexpr int SPAN = 64 * FP;
     const int lane = threadIdx.x & 63;
-    uint32_t acc[NPL];
+    uint32_t p[FP], acc[FP];
+    bool act[FP], und[FP];
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) acc[i] = 0;
-    // the FP-pair group starting at pair i0: its pair ordinals, active flags and tile / image offsets
-#define SPK_GROUP(i0)                                                  \
-    const uint32_t base = wb + (i0) * 64;                              \
-    uint32_t p[FP], gx[FP], gy[FP];                                    \
-    bool act[FP], und[FP];                                             \
-    _Pragma("unroll") for (int u = 0; u < FP; ++u) {                   \
-        p[u] = base + u * 64 + lane;                                   \
-        act[u] = p[u] < we;                                            \
-        gx[u] = ox[(i0) + u];                                          \
-        gy[u] = oy[(i0) + u];                                          \
+    for (int u = 0; u < FP; ++u) {
+        p[u] = base + u * 64 + lane;
+        act[u] = p[u] < end;
+        acc[u] = 0;
     }
 #pragma unroll 1
     for (int j = 0; j < A.nj; ++j) {
@@ -414,48 +408,38 @@ __device__ __attribute__((always_inline)) inline void eval_chunk(const FiltArgs 
 #ifdef SPK_DIAG_SKIP_JW  // timing diagnostic only (wrong results)
         break;
 #endif
+        const bool ji = implied(J.c, base, SPAN);
+        const bool gi = J.geq && implied(J.ge.c, base, SPAN);
+        if (ji) {
 #pragma unroll
-        for (int i0 = 0; i0 < NPL; i0 += FP) {
-            if (wb + i0 * 64 >= we) break;  // wave-uniform
-            SPK_GROUP(i0)
-            uint32_t a2[FP];
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
+        }
+        if (gi) {
 #pragma unroll
-            for (int u = 0; u < FP; ++u) a2[u] = 0;
-            const bool ji = implied(J.c, base, SPAN);
-            const bool gi = J.geq && implied(J.ge.c, base, SPAN);
-            if (ji) {
-#pragma unroll
-                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? J.c.imp_add : 0u;
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
+        }
+        if (ji) {
+            if (J.geq && !gi) {  // only the gap EQ field is needed
+                Data8<FP> e;
+                load8<FP, ST>(A, T, J.ge.c.ci, J.ge.c.p0, J.ge.c.p1, J.ge.c.in, ox, oy, e.a, e.b);
+                ev_eq<FP>(J.ge, e, act, acc, und);
+                if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
             }
-            if (gi) {
+            continue;
+        }
+        JwData<FP> d;
+        ld_jw<FP, ST>(A, T, J, ox, oy, d);
+        ev_jw<FP>(J, d, act, acc, und);
+        append<FP>(A, J.c, r0, &s_cnt[j], und, p);
+        if (J.geq && !gi) {
+            Data8<FP> e;
 #pragma unroll
-                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? J.ge.c.imp_add : 0u;
+            for (int u = 0; u < FP; ++u) {
+                e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
+                e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
             }
-            if (ji) {
-                if (J.geq && !gi) {  // only the gap EQ field is needed
-                    Data8<FP> e;
-                    load8<FP, ST>(A, T, J.ge.c.ci, J.ge.c.p0, J.ge.c.p1, J.ge.c.in, gx, gy, e.a, e.b);
-                    ev_eq<FP>(J.ge, e, act, a2, und);
-                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
-                }
-            } else {
-                JwData<FP> d;
-                ld_jw<FP, ST>(A, T, J, gx, gy, d);
-                ev_jw<FP>(J, d, act, a2, und);
-                append<FP>(A, J.c, r0, &s_cnt[j], und, p);
-                if (J.geq && !gi) {
-                    Data8<FP> e;
-#pragma unroll
-                    for (int u = 0; u < FP; ++u) {
-                        e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
-                        e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
-                    }
-                    ev_eq<FP>(J.ge, e, act, a2, und);
-                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
+            ev_eq<FP>(J.ge, e, act, acc, und);
+            if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
         }
     }
 #pragma unroll 1
@@ -464,73 +448,57 @@ __device__ __attribute__((always_inline)) inline void eval_chunk(const FiltArgs 
 #ifdef SPK_DIAG_SKIP_LEV  // timing diagnostic only (wrong results)
         break;
 #endif
+        if (implied(L.c, base, SPAN)) {
 #pragma unroll
-        for (int i0 = 0; i0 < NPL; i0 += FP) {
-            if (wb + i0 * 64 >= we) break;
-            SPK_GROUP(i0)
-            uint32_t a2[FP];
-#pragma unroll
-            for (int u = 0; u < FP; ++u) a2[u] = 0;
-            if (implied(L.c, base, SPAN)) {
-#pragma unroll
-                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? L.c.imp_add : 0u;
-            } else {
-                Data16<FP> d;
-                load16<FP, ST>(A, T, L.c.ci, L.c.p0, L.c.p1, gx, gy, d.a, d.b);
-                ev_lev<FP>(L, s_thr, d, act, a2, und);
-                append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
-            }
-#pragma unroll
-            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? L.c.imp_add : 0u;
+            continue;
         }
+        Data16<FP> d;
+        load16<FP, ST>(A, T, L.c.ci, L.c.p0, L.c.p1, ox, oy, d.a, d.b);
+        ev_lev<FP>(L, s_thr, d, act, acc, und);
+        append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
     }
 #pragma unroll 1
     for (int j = 0; j < A.ne; ++j) {
         const FEq &E = A.eq[j];
+        if (implied(E.c, base, SPAN)) {
 #pragma unroll
-        for (int i0 = 0; i0 < NPL; i0 += FP) {
-            if (wb + i0 * 64 >= we) break;
-            SPK_GROUP(i0)
-            uint32_t a2[FP];
-#pragma unroll
-            for (int u = 0; u < FP; ++u) a2[u] = 0;
-            if (implied(E.c, base, SPAN)) {
-#pragma unroll
-                for (int u = 0; u < FP; ++u) a2[u] += act[u] ? E.c.imp_add : 0u;
-            } else {
-                Data8<FP> d;
-                load8<FP, ST>(A, T, E.c.ci, E.c.p0, E.c.p1, E.c.in, gx, gy, d.a, d.b);
-                ev_eq<FP>(E, d, act, a2, und);
-                if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
-            }
-#pragma unroll
-            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
+            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? E.c.imp_add : 0u;
+            continue;
         }
+        Data8<FP> d;
+        load8<FP, ST>(A, T, E.c.ci, E.c.p0, E.c.p1, E.c.in, ox, oy, d.a, d.b);
+        ev_eq<FP>(E, d, act, acc, und);
+        if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
     }
 #pragma unroll 1
-    for (int j = 0; j < A.nn; ++j) {
+    for (int j = 0; j < A.nn; ++j) f_num<FP, ST>(A, T, A.num[j], ox, oy, acc);
 #pragma unroll
-        for (int i0 = 0; i0 < NPL; i0 += FP) {
-            if (wb + i0 * 64 >= we) break;
-            SPK_GROUP(i0)
-            (void)act;
-            (void)und;
-            (void)p;
-            uint32_t a2[FP];
-#pragma unroll
-            for (int u = 0; u < FP; ++u) a2[u] = 0;
-            f_num<FP, ST>(A, T, A.num[j], gx, gy, a2);
-#pragma unroll
-            for (int u = 0; u < FP; ++u) acc[i0 + u] += a2[u];
-        }
+    for (int u = 0; u < FP; ++u) {
+        if (!act[u]) continue;
+        if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
+        else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
     }
-#undef SPK_GROUP
+}
+
+// A wave's NPL pairs per lane of a chunk, FP at a time.
+template <int NPL, int FP, bool ST, bool C32>
+__device__ __attribute__((always_inline)) inline void eval_chunk(const FiltArgs &A, const Tile &T,
+                                                                 const int16_t *s_thr, unsigned int *s_cnt,
+                                                                 int64_t r0, uint32_t wb, uint32_t we,
+                                                                 const uint32_t (&ox)[NPL], const uint32_t (&oy)[NPL]) {
+    static_assert(NPL % FP == 0, "pairs per lane");
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-        const uint32_t q = wb + i * 64 + lane;
-        if (q >= we) continue;
-        if (C32) static_cast<uint32_t *>(A.codes)[q] = acc[i];
-        else static_cast<uint16_t *>(A.codes)[q] = (uint16_t)acc[i];
+    for (int i0 = 0; i0 < NPL; i0 += FP) {
+        const uint32_t base = wb + i0 * 64;
+        if (base >= we) break;  // wave-uniform
+        uint32_t gx[FP], gy[FP];
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            gx[u] = ox[i0 + u];
+            gy[u] = oy[i0 + u];
+        }
+        eval_pairs<FP, ST, C32>(A, T, s_thr, s_cnt, r0, base, we, gx, gy);
     }
 }
 

@@ -337,6 +337,69 @@ static int set_key(spk_ctx *ctx, Table &t, int which, int rule, const int64_t *s
 
 using namespace spk;
 
+// Arrow buffers as handed over: offsets rebased to 0 (sliced arrays start past 0), the validity bitmap
+// (LSB first, from bit `bit0`) expanded to bytes, and the longest row / empty-string flag reduced, all on
+// the device (no per-row host pass).
+__global__ void k_arrow_rebase(int64_t n, int64_t *__restrict__ off, int64_t base, const uint8_t *__restrict__ bitmap,
+                               int64_t bit0, uint8_t *__restrict__ valid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) off[i] -= base;
+    if (i < n) {
+        const int64_t b = bit0 + i;
+        valid[i] = !bitmap ? (uint8_t)1 : (bit0 < 0 ? (uint8_t)(bitmap[i] != 0) : (uint8_t)((bitmap[b >> 3] >> (b & 7)) & 1));
+    }
+}
+__global__ void k_arrow_lengths(int64_t n, const int64_t *__restrict__ off, const uint8_t *__restrict__ valid,
+                                unsigned long long *__restrict__ stats) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long len = 0, empty = 0;
+    if (i < n) {
+        len = (unsigned long long)(off[i + 1] - off[i]);
+        empty = (valid[i] && len == 0) ? 1ull : 0ull;
+    }
+    // wave maximum / or, one atomic per wave
+    for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long a = __shfl_xor(len, o), e = __shfl_xor(empty, o);
+        len = a > len ? a : len;
+        empty |= e;
+    }
+    if ((threadIdx.x & 63) == 0 && (len || empty)) {
+        atomicMax(&stats[0], len);
+        if (empty) atomicOr(&stats[1], 1ull);
+    }
+}
+
+// FNV-style 64-bit digest of a byte range, order-dependent (the replication tests compare two contexts'
+// encoded tables): each thread folds its 8-byte words, then the per-thread digests are combined in
+// thread order on the host.
+__global__ void k_digest(const uint64_t *__restrict__ w, int64_t n_words, uint64_t *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t T = (int64_t)gridDim.x * blockDim.x;
+    uint64_t h = 1469598103934665603ull ^ (uint64_t)t;
+    for (int64_t i = t; i < n_words; i += T) h = (h ^ (w[i] + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1))) * 1099511628211ull;
+    out[t] = h;
+}
+
+static int digest(spk_ctx *ctx, const void *p, int64_t bytes, uint64_t &acc) {
+    const int64_t nw = bytes / 8;
+    constexpr int G = 256, B = 256;
+    DevBuf<uint64_t> d;
+    SPK_TRY(d.alloc((size_t)G * B));
+    k_digest<<<G, B, 0, ctx->stream>>>(reinterpret_cast<const uint64_t *>(p), nw, d.p);
+    SPK_HIP(hipGetLastError());
+    std::vector<uint64_t> h((size_t)G * B);
+    SPK_HIP(hipMemcpyAsync(h.data(), d.p, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<uint8_t> tail((size_t)(bytes - nw * 8));
+    if (!tail.empty())
+        SPK_HIP(hipMemcpyAsync(tail.data(), static_cast<const uint8_t *>(p) + nw * 8, tail.size(), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    for (uint64_t x : h) acc = (acc ^ x) * 1099511628211ull;
+    for (uint8_t x : tail) acc = (acc ^ x) * 1099511628211ull;
+    acc = (acc ^ (uint64_t)bytes) * 1099511628211ull;
+    return SPK_OK;
+}
+
 extern "C" {
 
 int spk_raw_utf8(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const uint8_t *data, const uint8_t *valid) {
@@ -363,6 +426,88 @@ int spk_raw_utf8(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const
     if (nbytes) SPK_HIP(hipMemcpyAsync(r->bytes.p, data, (size_t)nbytes, hipMemcpyHostToDevice, ctx->stream));
     if (n) SPK_HIP(hipMemcpyAsync(r->valid.p, valid, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    return SPK_OK;
+}
+
+int spk_raw_utf8_arrow(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const uint8_t *data,
+                       const uint8_t *validity, int64_t validity_bit_offset, int on_device) {
+    SPK_REQUIRE(ctx && offsets && data && n >= 0 && n < (int64_t)INT32_MAX && validity_bit_offset >= -1, SPK_E_INVALID,
+                "spk_raw_utf8_arrow: bad args");
+    SPK_HIP(hipSetDevice(ctx->device));
+    int64_t ends[2] = {0, 0};  // offsets[0], offsets[n]
+    if (on_device) {
+        SPK_HIP(hipMemcpyAsync(&ends[0], offsets, 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipMemcpyAsync(&ends[1], offsets + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+    } else {
+        ends[0] = offsets[0];
+        ends[1] = offsets[n];
+    }
+    SPK_REQUIRE(ends[0] >= 0 && ends[1] >= ends[0], SPK_E_INVALID, "spk_raw_utf8_arrow: offsets out of order");
+    RawCol *r = nullptr;
+    SPK_TRY(new_raw(ctx, raw, &r));
+    r->kind = RAW_UTF8;
+    r->n = n;
+    const int64_t nbytes = ends[1] - ends[0];
+    SPK_TRY(r->off.alloc((size_t)n + 1));
+    SPK_TRY(r->bytes.alloc((size_t)nbytes + 1));
+    SPK_TRY(r->valid.alloc((size_t)n + 1));
+    const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    SPK_HIP(hipMemcpyAsync(r->off.p, offsets, (size_t)(n + 1) * 8, kind, ctx->stream));
+    if (nbytes) SPK_HIP(hipMemcpyAsync(r->bytes.p, data + ends[0], (size_t)nbytes, kind, ctx->stream));
+    DevBuf<uint8_t> bm;
+    const uint8_t *d_bm = nullptr;
+    if (validity && n) {
+        const int64_t nb = validity_bit_offset < 0 ? n : (validity_bit_offset + n + 7) / 8;
+        if (on_device) {
+            d_bm = validity;
+        } else {
+            SPK_TRY(bm.alloc((size_t)nb));
+            SPK_HIP(hipMemcpyAsync(bm.p, validity, (size_t)nb, hipMemcpyHostToDevice, ctx->stream));
+            d_bm = bm.p;
+        }
+    }
+    DevBuf<unsigned long long> st;
+    SPK_TRY(st.alloc(2));
+    SPK_HIP(hipMemsetAsync(st.p, 0, 16, ctx->stream));
+    k_arrow_rebase<<<grid(n + 1), 256, 0, ctx->stream>>>(n, r->off.p, ends[0], d_bm, validity_bit_offset, r->valid.p);
+    if (n) k_arrow_lengths<<<grid(n), 256, 0, ctx->stream>>>(n, r->off.p, r->valid.p, st.p);
+    SPK_HIP(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    SPK_HIP(hipMemcpyAsync(h, st.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    r->max_len = (int64_t)h[0];
+    r->has_empty = h[1] != 0;
+    return SPK_OK;
+}
+
+int spk_table_digest(spk_ctx *ctx, int side, uint64_t *out) {
+    SPK_REQUIRE(ctx && out && (side == 0 || side == 1), SPK_E_INVALID, "spk_table_digest: bad args");
+    SPK_HIP(hipSetDevice(ctx->device));
+    Table &t = ctx->table[side];
+    SPK_REQUIRE(t.n >= 0, SPK_E_STATE, "spk_table_digest: table not created");
+    uint64_t acc = 1469598103934665603ull ^ (uint64_t)t.n;
+    if (t.perm.p) SPK_TRY(digest(ctx, t.perm.p, t.n * 4, acc));
+    if (t.rank.p) SPK_TRY(digest(ctx, t.rank.p, t.n * 8, acc));
+    for (const Column *c : t.cols) {
+        if (!c || c->kind == COL_NONE) continue;
+        acc = (acc ^ (uint64_t)c->kind) * 1099511628211ull;
+        if (c->kind == COL_STR) {
+            // units: up to the last row's end (the buffer's padding past it is not part of the encoding)
+            SPK_TRY(digest(ctx, c->meta.p, t.n * (int64_t)sizeof(RecMeta), acc));
+            SPK_TRY(digest(ctx, c->units.p, (int64_t)c->units.n * 2, acc));
+            if (c->planes.p) SPK_TRY(digest(ctx, c->planes.p, t.n * N_PLANES * 8, acc));
+            if (c->planes_hi.p) SPK_TRY(digest(ctx, c->planes_hi.p, t.n * N_PLANES * 8, acc));
+            acc = (acc ^ (uint64_t)c->n_ids) * 1099511628211ull;
+        } else {
+            SPK_TRY(digest(ctx, c->val.p, t.n * 8, acc));
+            SPK_TRY(digest(ctx, c->valid.p, t.n, acc));
+        }
+    }
+    for (int w = 0; w < 2; ++w)
+        for (size_t r = 0; r < t.key[w].size(); ++r)
+            if (t.key[w][r] && t.key[w][r]->p) SPK_TRY(digest(ctx, t.key[w][r]->p, t.n * 8, acc));
+    *out = acc;
     return SPK_OK;
 }
 

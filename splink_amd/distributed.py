@@ -96,3 +96,58 @@ def barrier():
     dist = _dist()
     if dist is not None and dist.get_world_size() > 1:
         dist.barrier()
+
+
+def allgather_utf8_rows(arr, force: bool = False):
+    """Replicated ingest of one string column (the records are uploaded once and replicated
+    over the ranks instead of every rank decoding the whole table from host memory): rank g hands over
+    rows [g n / G, (g + 1) n / G) of the Arrow array, the ranks all-gather them -- RCCL over xGMI under
+    `nccl` (device tensors), host tensors under `gloo` -- and every rank gets the whole column back.
+
+    Returns (n, offsets, data, valid, on_device): int64 offsets [n + 1] from 0, the bytes, one validity byte
+    per row; torch device tensors when on_device, else numpy arrays (Context.raw_utf8_device / _arrow)."""
+    import numpy as np
+    import torch
+    from . import table as T
+    dist = _dist()
+    assert dist is not None and (dist.get_world_size() > 1 or force)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = len(arr)
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    off, data, bitmap, bit0 = T.arrow_views(arr.slice(lo, hi - lo))
+    o = (off - off[0]).astype(np.int64)
+    d = data[off[0]:off[-1]] if off[-1] > off[0] else np.zeros(0, np.uint8)
+    if bitmap is None:
+        v = np.ones(hi - lo, dtype=np.uint8)
+    else:
+        bits = np.unpackbits(bitmap, bitorder="little")
+        v = bits[bit0: bit0 + (hi - lo)].astype(np.uint8)
+    on_device = dist.get_backend() != "gloo"
+    dev = torch.device(f"cuda:{torch.cuda.current_device()}") if on_device else torch.device("cpu")
+    rows = [n * (g + 1) // world - n * g // world for g in range(world)]
+    sz = torch.tensor([len(d)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, sz)
+    sizes = [int(x.item()) for x in sizes]
+    mb, mr = max(max(sizes), 1), max(rows)
+
+    def gather(x, pad_to, dtype):
+        t = torch.zeros(pad_to, dtype=dtype, device=dev)
+        if len(x):
+            t[:len(x)] = torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+        parts = [torch.empty(pad_to, dtype=dtype, device=dev) for _ in range(world)]
+        dist.all_gather(parts, t)
+        return parts
+
+    dp = gather(d, mb, torch.uint8)
+    op = gather(o[:-1], mr, torch.int64)
+    vp = gather(v, mr, torch.uint8)
+    base = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    offsets = torch.cat([op[g][:rows[g]] + int(base[g]) for g in range(world)] +
+                        [torch.tensor([int(base[-1])], dtype=torch.int64, device=dev)])
+    data_all = torch.cat([dp[g][:sizes[g]] for g in range(world)] + [torch.zeros(1, dtype=torch.uint8, device=dev)])
+    valid = torch.cat([vp[g][:rows[g]] for g in range(world)] + [torch.zeros(1, dtype=torch.uint8, device=dev)])
+    if on_device:
+        torch.cuda.synchronize(dev)  # the context reads them on its own stream
+        return n, offsets, data_all, valid, True
+    return n, offsets.numpy(), data_all.numpy(), valid.numpy(), False

@@ -91,7 +91,7 @@ class Job:
     order (materialised on demand, for output columns and checks)."""
 
     def __init__(self, link_type: str, tables: List[pd.DataFrame], unique_id_col: str, device: int,
-                 shard=(0, 1), cluster: bool = True):
+                 shard=(0, 1), cluster: bool = True, replicate: bool = False):
         self.link_type = link_type
         self.cluster = cluster
         self.inputs = [t.reset_index(drop=True) for t in tables]
@@ -119,6 +119,10 @@ class Job:
         self.code_meta = None
         self.timings = {}
         self.force_reduce = False  # tests: the multi-GPU EM path (histogram -> all-reduce -> finalize) at one rank
+        # ranks of a sharded job upload 1/G of each string column and all-gather the rest (tests: force it at
+        # one rank with force_replicate)
+        self.force_replicate = bool(replicate)
+        self.replicate_ingest = self.reduces_across_ranks() or self.force_replicate
         self._set_rank()
 
     @classmethod
@@ -164,12 +168,27 @@ class Job:
         return len(self._raw)
 
     def raw_utf8(self, side: int, name: str) -> int:
-        """Raw string column (input row order) on the device, uploaded once."""
+        """Raw string column (input row order) on the device, uploaded once.  Arrow columns hand over their
+        buffers as they are (no host copy; rebasing and the validity bitmap are handled on the device).  A
+        rank of a sharded job (replicate_ingest) uploads only its slice of the rows and gets the rest from
+        the other ranks (distributed.allgather_utf8_rows): one host upload of the records per job, not per
+        rank."""
         key = (side, name, "utf8")
         if key not in self._raw:
-            off, data, valid = T.arrow_utf8(self.inputs[side][name])
             rid = self._new_raw()
-            self.ctx.raw_utf8(rid, off, data, valid)
+            arr = T.arrow_large_utf8(self.inputs[side][name])
+            if arr is not None and self.replicate_ingest:
+                n, off, data, valid, on_dev = D.allgather_utf8_rows(arr, force=self.force_replicate)
+                if on_dev:
+                    self.ctx.raw_utf8_device(rid, n, off.data_ptr(), data.data_ptr(), valid.data_ptr())
+                else:
+                    self.ctx.raw_utf8_arrow(rid, n, off, data, valid, -1)
+            elif arr is not None:
+                off, data, bitmap, bit0 = T.arrow_views(arr)
+                self.ctx.raw_utf8_arrow(rid, len(arr), off, data, bitmap, bit0)
+            else:
+                off, data, valid = T.arrow_utf8(self.inputs[side][name])
+                self.ctx.raw_utf8(rid, off, data, valid)
             self._raw[key] = rid
         return self._raw[key]
 

@@ -118,6 +118,28 @@ def arrow_utf8(series: pd.Series):
     return encode_utf8(series)
 
 
+def arrow_large_utf8(series: pd.Series):
+    """The Arrow large_string array behind a string column (one chunk), or None for other columns."""
+    if pa is None:
+        return None
+    arr = getattr(series.array, "_pa_array", None)
+    if arr is None or not (pa.types.is_large_string(arr.type) or pa.types.is_string(arr.type)):
+        return None
+    arr = arr.combine_chunks() if isinstance(arr, pa.ChunkedArray) else arr
+    return arr.cast(pa.large_string()) if pa.types.is_string(arr.type) else arr
+
+
+def arrow_views(arr):
+    """Zero-copy numpy views of a large_string array's buffers: (offsets int64[n+1] (any base), data
+    uint8, validity bitmap uint8 or None, bit offset of row 0 in it)."""
+    n = len(arr)
+    bufs = arr.buffers()
+    off = np.frombuffer(bufs[1], dtype=np.int64)[arr.offset: arr.offset + n + 1]
+    data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None and bufs[2].size else np.zeros(1, np.uint8)
+    bitmap = np.frombuffer(bufs[0], dtype=np.uint8) if (bufs[0] is not None and arr.null_count) else None
+    return off, data, bitmap, int(arr.offset)
+
+
 def numeric_key_bits(series: pd.Series):
     """(int64 values, valid) whose bit patterns are equal iff the numbers are: int64 columns as they
     are, float columns as canonical float64 bits (-0.0 -> 0.0); NaN is NULL."""

@@ -24,7 +24,9 @@ ITERS = 5
 
 
 def records():
-    return make_records(20000, seed=23, surname_vocab=500, first_vocab=300, city_vocab=80)[["unique_id"] + COLS]
+    # Arrow-backed string columns: a sharded rank uploads its slice of each and all-gathers the rest
+    return make_records(20000, seed=23, surname_vocab=500, first_vocab=300, city_vocab=80,
+                        arrow=True)[["unique_id"] + COLS]
 
 
 def run(shard, want_job=False):
@@ -41,7 +43,8 @@ def run(shard, want_job=False):
         lam, rows = m_step_rows(stats, names, nlev)
         params._update_params(lam, rows)
     out = {"n_pairs": int(job.n_pairs), "lambda": params.params["λ"],
-           "pi": [[list(m), list(u)] for m, u in params._level_probabilities()]}
+           "pi": [[list(m), list(u)] for m, u in params._level_probabilities()],
+           "replicated_ingest": bool(job.replicate_ingest), "table_digest": int(job.ctx.table_digest(0))}
     if want_job:
         return out, job, initial, nlev
     return out

@@ -153,3 +153,41 @@ def test_two_rank_gloo_tf_tables(tmp_path):
         want = np.full(50, np.iinfo(np.int32).min, dtype=np.int32)
         np.maximum.at(want, ids, np.frexp(mpv)[1].astype(np.int32))
         assert np.array_equal(x["scale"], want)
+
+
+def _gather_rank_main(rank, world, port, out_dir):
+    """Replicated ingest (distributed.allgather_utf8_rows): each rank hands over its slice of the rows."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from splink_amd import distributed as D
+    arr = _gather_input()
+    n, off, data, valid, on_dev = D.allgather_utf8_rows(arr)
+    assert not on_dev
+    np.savez(os.path.join(out_dir, f"g{rank}.npz"), n=n, off=off, data=data, valid=valid)
+    dist.destroy_process_group()
+
+
+def _gather_input():
+    import pyarrow as pa
+    vals = ["ann", None, "", "bérénice", "o'brien", None, "z" * 300, "x"] * 251 + ["last"]
+    return pa.array(["pad"] * 7 + vals, type=pa.large_string()).slice(7)  # a sliced array: offsets past 0
+
+
+def test_two_rank_gloo_replicated_ingest(tmp_path):
+    """Every rank of a two-rank job gets the whole column (offsets from 0, bytes, one validity byte per
+    row) from the slices the ranks uploaded, identical to the column itself."""
+    from splink_amd import table as T
+    world = 2
+    mp.start_processes(_gather_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    arr = _gather_input()
+    off, data, bitmap, bit0 = T.arrow_views(arr)
+    want_off = off - off[0]
+    want_data = data[off[0]:off[-1]]
+    want_valid = np.array([v is not None for v in arr.to_pylist()], dtype=np.uint8)
+    for k in range(world):
+        x = np.load(tmp_path / f"g{k}.npz")
+        assert int(x["n"]) == len(arr)
+        assert np.array_equal(x["off"], want_off)
+        assert np.array_equal(x["data"][:len(want_data)], want_data)
+        assert np.array_equal(x["valid"][:len(arr)], want_valid)

@@ -112,3 +112,29 @@ def test_nccl_stream_ordered_em_matches_single_gpu(nccl_group):
         assert np.array_equal(s, hist_a[i], equal_nan=True), i
         pb._update_params(*m_step_rows(s, names, nlev))
     assert pa.params["λ"] == pb.params["λ"]
+
+
+def test_nccl_replicated_ingest_matches_local(nccl_group):
+    """The replicated ingest's RCCL path (device all-gather of the rank's row slices, then the device copy
+    into the raw columns) at world size 1: the encoded table (permutation, ranks, every comparison column,
+    blocking keys) is byte-identical to a local ingest, and so are the pairs and comparison vectors."""
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.session import AmdSession
+    from splink_amd.synthetic import cfg_settings, make_records
+    df = make_records(30000, seed=33, surname_vocab=600, first_vocab=400, city_vocab=100,
+                      arrow=True)[["unique_id"] + COLS]
+    st = Params(cfg_settings(2), AmdSession(0)).settings
+    jobs = []
+    for rep in (False, True):
+        job = Job("dedupe_only", [df], "unique_id", 0, replicate=rep)
+        assert job.replicate_ingest == rep
+        job.block(st["blocking_rules"])
+        job.gammas(st)
+        jobs.append(job)
+    a, b = jobs
+    assert a.ctx.table_digest(0) == b.ctx.table_digest(0)
+    la, ra = a.pair_rows()
+    lb, rb = b.pair_rows()
+    assert np.array_equal(la, lb) and np.array_equal(ra, rb)
+    assert np.array_equal(a.gammas_host(), b.gammas_host())

@@ -857,6 +857,10 @@ def test_sharded_ranks_match_oracle(amd, tmp_path):
             assert all(rel_close(a, b) for a, b in zip(m, m_o[k])), (k, m, m_o[k])
             assert all(rel_close(a, b) for a, b in zip(u, u_o[k]))
         assert rk["lambda"] == single["lambda"] and rk["pi"] == single["pi"]
+        # each rank uploaded half of every string column and gathered the rest from the other rank: its
+        # encoded table is byte-identical to the single process's local ingest
+        assert rk["replicated_ingest"] and not single["replicated_ingest"]
+        assert rk["table_digest"] == single["table_digest"]
 
 
 def test_sharded_link_tf_matches_reference(amd, tmp_path):
