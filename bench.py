@@ -20,6 +20,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 import warnings
@@ -335,6 +336,42 @@ def em_streaming(job, names, nlev, params, reps, iters=10):
             "em_restream_pairs_per_s": P / (h / 1e3)}
 
 
+def lev_scan_cells(a: str, b: str, cut: int) -> int:
+    """DP cells the exact pass's bit-parallel scan updates for one listed cell of rows <= 64 units (a host
+    restatement of spk_strsim.h lev_rows_planes_np / myers_plane_text[_lazy]): common prefix and suffix
+    stripped, the longer remainder is the pattern (m rows) and the scan runs over the shorter one (n text
+    units), one word-step per text unit of 32 rows (m <= 32; the lazy scan also up to its switch unit
+    J0 = 31 - cut, taken per cell here, per wave in the kernel) or 64 rows, stopping after the first
+    fourth unit j whose bound D[m][j + 1] - (n - 1 - j) exceeds cut.  Equal strings (decided before any
+    scan) and a side that strips to empty count 0."""
+    la, lb = len(a), len(b)
+    mn = min(la, lb)
+    pre = 0
+    while pre < mn and a[pre] == b[pre]:
+        pre += 1
+    suf = 0
+    while suf < mn - pre and a[la - 1 - suf] == b[lb - 1 - suf]:
+        suf += 1
+    ra, rb = a[pre:la - suf], b[pre:lb - suf]
+    if not ra or not rb:
+        return 0
+    pat, txt = (ra, rb) if len(ra) >= len(rb) else (rb, ra)
+    m, n = len(pat), len(txt)
+    wide = m > 32
+    j0 = (31 - cut if cut < 31 else 0) if wide else n
+    col = list(range(m + 1))  # D[i][0]
+    cells = 0
+    for j in range(n):
+        cells += 64 if (wide and j >= j0) else 32
+        prev, col[0] = col[0], j + 1
+        for i in range(1, m + 1):
+            cur = min(col[i] + 1, col[i - 1] + 1, prev + (pat[i - 1] != txt[j]))
+            prev, col[i] = col[i], cur
+        if (j & 3) == 3 and col[m] - (n - 1 - j) > cut:
+            break
+    return cells
+
+
 def string_rates(job, st, pairs, g_ms):
     """Rates of the string work in the last γ pass (Levenshtein GCUPS, JW comparisons/s).
 
@@ -350,23 +387,46 @@ def string_rates(job, st, pairs, g_ms):
     exact = job.ctx.gammas_exact_counts(len(names))
     xms = job.ctx.gammas_exact_ms(len(names))
     lev, n_jw, n_lev = {}, 0, 0
+    rng = np.random.Generator(np.random.PCG64(7))
     for k, c in enumerate(st["comparison_columns"]):
         expr = (c.get("case_expression") or "").lower()
         if "levenshtein" in expr:
             n_lev += 1
-            ln = t[c["col_name"]].str.len().fillna(0).to_numpy(np.int64)
+            vals = t[c["col_name"]]
+            ln = vals.str.len().fillna(0).to_numpy(np.int64)
             items = job.ctx.gammas_exact_list(k, int(exact[k]))
-            cells = int(np.dot(ln[l[items]], ln[r[items]]))
-            lev[c["col_name"]] = {"exact_cells": int(exact[k]), "dp_cells": cells, "exact_pass_ms": xms[k],
-                                  "gcups": cells / (xms[k] / 1e3) / 1e9 if xms[k] > 0 else None,
-                                  "exact_cells_per_s": exact[k] / (xms[k] / 1e3) if xms[k] > 0 else None}
+            nominal = int(np.dot(ln[l[items]], ln[r[items]]))
+            # cells the scans actually update, from a host restatement of the scan over a random sample of
+            # the listed cells (rows <= 64 units: the exact pass's own; longer rows go to the 128-bit pass)
+            thr = [float(x) for x in re.findall(r"<=\s*([0-9.]+)", expr)] or [0.0]
+            sample = rng.choice(len(items), size=min(2000, len(items)), replace=False) if len(items) else []
+            tot = cnt = 0
+            for i in sample:
+                a, b = vals.iat[int(l[items[i]])], vals.iat[int(r[items[i]])]
+                if a is None or b is None or max(len(a), len(b)) > 64:
+                    continue
+                cut = max(int(np.floor(x * (len(a) + len(b)) / 2.0)) + 1 for x in thr)
+                tot += lev_scan_cells(a, b, cut)
+                cnt += 1
+            scanned = tot / cnt * len(items) if cnt else None
+            sec_x = xms[k] / 1e3 if xms[k] > 0 else None
+            lev[c["col_name"]] = {"exact_cells": int(exact[k]), "exact_pass_ms": xms[k],
+                                  "dp_cells_nominal": nominal,
+                                  "gcups_nominal": nominal / sec_x / 1e9 if sec_x else None,
+                                  "dp_cells_scanned_est": scanned,
+                                  "gcups_scanned": scanned / sec_x / 1e9 if (sec_x and scanned) else None,
+                                  "scan_sample": {"cells": int(cnt), "rows_le_64_units_of": int(len(sample))},
+                                  "exact_cells_per_s": exact[k] / sec_x if sec_x else None}
         elif "jaro_winkler" in expr:
             n_jw += 1
     K = len(st["comparison_columns"])
     return {"comparisons_per_s": pairs * K / sec, "jw_comparisons_per_s": pairs * n_jw / sec,
             "lev_comparisons_per_s": pairs * n_lev / sec, "levenshtein_exact_pass": lev,
-            "note": "comparisons/s: all pairs x columns over the whole γ pass; levenshtein_exact_pass.gcups: DP "
-                    "cells (len_l x len_r) of the exactly evaluated cells over that launch's HIP-event time"}
+            "note": "comparisons/s: all pairs x columns over the whole γ pass; levenshtein_exact_pass: "
+                    "gcups_scanned = DP cells the bit-parallel scans update (word-steps x word width after the "
+                    "prefix / suffix strip and the early exit, bench.lev_scan_cells over a 2000-cell sample, "
+                    "extrapolated to the list) over that launch's HIP-event time; gcups_nominal = len_l x len_r "
+                    "of the same cells (the work a full DP would do)"}
 
 
 def cpu_baseline(job, df, st, seconds, col_names):

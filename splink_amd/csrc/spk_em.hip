@@ -96,6 +96,9 @@ constexpr int HL_THREADS = 1024;
 constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS (gfx950), capped by the device attribute
 constexpr int HL_UNROLL = 4;
 constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups per group
+#ifndef SPK_EM_ATOMIC_ROW
+#define SPK_EM_ATOMIC_ROW 0  // 1: one-level reduction through agent-scope atomics into one row (A/B)
+#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
                                                         unsigned int *__restrict__ ticket, double *__restrict__ mpat,
                                                         double *__restrict__ llpat, double *__restrict__ cpat,
                                                         double *__restrict__ out, unsigned long long *__restrict__ out_hist,
-                                                        int fence) {
+                                                        int fence, uint32_t *__restrict__ arow) {
     extern __shared__ uint32_t sh[];
     __shared__ bool s_last;
     const int n_pat = A0.n_pat;
@@ -477,6 +480,26 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         }
         __syncthreads();
     };
+    if (arow) {
+        // One-level alternative (SPK_EM_ATOMIC_ROW): every workgroup adds its counts into one global row with
+        // agent-scope integer atomics (exact, so their order does not matter), drains them, takes the
+        // ticket; the last one reads that row and zeroes it for the next launch.
+        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < R; ++k) c += sh[b * R + ((k + b) & (R - 1))];
+            if (c) __hip_atomic_fetch_add(arow + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (!arrive(ticket, (unsigned int)(G - 1))) return;
+        uint32_t *s1 = sh;
+        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
+            s1[b] = __hip_atomic_load(arow + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            arow[b] = 0u;
+        }
+        __syncthreads();
+    } else {
     // this workgroup's row straight from its counters (a quad of bins per lane, 16-byte sc1 stores)
     {
         const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
@@ -521,6 +544,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     EM_STAMP(5);
 #endif
     sum_rows(part2, NG);
+    }  // two-level reduction
     EM_STAMP(6);
     // thread t owns bins p = t, t + HL_THREADS, ... (the same mapping as em_finalize_block's loop, so
     // the count it parks in cpat is read back by the thread that wrote it)
@@ -664,16 +688,16 @@ static int64_t lane_grid(spk_ctx *ctx) {
         if (ctx->code_bytes == 2)                                                                                \
             k_em_iter<uint16_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
                 reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
-                ctx->em_fence ? 1 : 0);                                                                          \
+                ctx->em_fence ? 1 : 0, arow);                                                                    \
         else                                                                                                     \
             k_em_iter<uint32_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
                 reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
-                ctx->em_fence ? 1 : 0);                                                                          \
+                ctx->em_fence ? 1 : 0, arow);                                                                    \
         break;
 
 // The padded accumulation histogram and the ticket of k_em_iter: zero between launches (the last workgroup
 // resets them), zeroed here only when (re)allocated.
-static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket) {
+static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket, uint32_t **arow) {
     // k_em_iter: one count row per workgroup (<= n_cu), then one per group of EM_GROUP workgroups;
     // tickets [final | per group]
     const int64_t n_groups = ((int64_t)ctx->n_cu + EM_GROUP - 1) / EM_GROUP;
@@ -685,6 +709,15 @@ static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket) {
     }
     *acc = ctx->hist_part.p;
     *ticket = ctx->em_ticket.p;
+    *arow = nullptr;
+    if (SPK_EM_ATOMIC_ROW) {  // the one-level reduction's row: zero between launches (the last workgroup resets it)
+        const size_t ps = (size_t)part_stride(ctx->n_patterns);
+        if (!ctx->em_row.p || ctx->em_row.n < ps) {
+            SPK_TRY(ctx->em_row.alloc(ps));
+            SPK_HIP(hipMemsetAsync(ctx->em_row.p, 0, ps * 4, ctx->stream));
+        }
+        *arow = ctx->em_row.p;
+    }
     return SPK_OK;
 }
 
@@ -707,7 +740,8 @@ static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
         const size_t sh = (size_t)n_pat * R * 4;
         uint32_t *acc = nullptr;
         unsigned int *ticket = nullptr;
-        SPK_TRY(em_accumulator(ctx, &acc, &ticket));
+        uint32_t *arow = nullptr;
+        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow));
         double *mpat = nullptr, *llpat = nullptr, *cpat = nullptr, *out = nullptr;
         switch (R) {
             SPK_EM_ITER(64, false)
@@ -831,7 +865,8 @@ static int enqueue_em(spk_ctx *ctx) {
         uint32_t *acc = nullptr;
         unsigned long long *h = nullptr;
         unsigned int *ticket = nullptr;
-        SPK_TRY(em_accumulator(ctx, &acc, &ticket));
+        uint32_t *arow = nullptr;
+        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow));
         const int64_t P = ctx->n_pairs;
         const int64_t g = lane_grid(ctx);
         const size_t sh = std::max<size_t>((size_t)n_pat * R * 4, sizeof(PatArgs));

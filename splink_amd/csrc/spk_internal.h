@@ -302,6 +302,7 @@ struct spk_ctx {
     spk::DevBuf<double> mpat, llpat, cpat, stats, mu;  // per pattern: mp, ln(...), count; statistics; m / u
     spk::DevBuf<uint32_t> hist_part;    // k_em_iter's per-workgroup pattern counts (rows of part_stride)
     spk::DevBuf<unsigned int> em_ticket;  // its last-workgroup ticket (kept zero between launches)
+    spk::DevBuf<uint32_t> em_row;         // its one-level reduction row (SPK_EM_ATOMIC_ROW; kept zero)
     double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;
     int n_cu = 256;                   // compute units of the device (grid sizing)
