@@ -30,7 +30,8 @@ struct FCommon {
     uint32_t in;           // byte offset of the field inside its 16-byte chunk (0 or 8)
     int32_t ci;            // index of that chunk in a row (its plane in a staged tile)
     uint32_t stride;       // code stride of the column
-    int32_t k;             // comparison column (work list)
+    int32_t k;             // comparison column
+    int32_t ws;            // its work-list slot
     int32_t null_level;
     int64_t imp_lo, imp_hi;  // pairs whose level the blocking key implies (SimpleCol.imp_lo / imp_hi)
     uint32_t imp_add;        // (eq_level + 1) * stride
@@ -169,7 +170,7 @@ __device__ __attribute__((always_inline)) inline void append(const FiltArgs &A, 
     unsigned int base = 0;
     if (lane == 0) base = atomicAdd(cnt, total);
     base = __shfl(base, 0);
-    int32_t *list = A.work + (int64_t)c.k * A.P + r0;
+    int32_t *list = A.work + (int64_t)c.ws * A.P + r0;
     const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
@@ -714,6 +715,7 @@ static void common(const SimpleCol &s, const GammaArgs &A, int off, FCommon &c) 
     c.ci = off >> 4;
     c.stride = (uint32_t)s.stride;
     c.k = s.k;
+    c.ws = A.wslot[s.k];
     c.null_level = s.null_level;
     c.imp_lo = s.imp_lo;
     c.imp_hi = s.imp_hi;

@@ -111,7 +111,8 @@ struct GammaArgs {
     const int64_t *stride;
     void *codes;                  // packed code per pair: uint16 (code16) or uint32
     int code16;
-    int32_t *work;                // [K][P] pair indices per column needing the exact pass, by region
+    int32_t *work;                // [slots][P] pair indices per column needing the exact pass, by region
+    int32_t wslot[MAX_SIMPLE];    // column k's work-list slot (columns whose filter can leave cells undecided)
     unsigned int *region_count;   // [K][n_regions] list length of each region
     int64_t region_len;           // pair ordinals per region (one filter workgroup each)
     int n_regions;
@@ -250,7 +251,7 @@ __device__ inline Region my_region(const GammaArgs &A) {
 }
 
 __device__ inline int32_t *region_list(const GammaArgs &A, int k, const Region &r) {
-    return A.work + (int64_t)k * A.P + r.r0;
+    return A.work + (int64_t)A.wslot[k] * A.P + r.r0;
 }
 
 template <class SC>

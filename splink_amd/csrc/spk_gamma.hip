@@ -1859,7 +1859,17 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     // the filter's work lists and the exact passes hold pair ordinals as int32
     SPK_REQUIRE(P <= (int64_t)INT32_MAX, SPK_E_LIMIT,
                 "spk_gammas: more than 2^31-1 pairs in one context (shard the pair set over more ranks)");
-    SPK_TRY(ctx->work.alloc((size_t)K * (size_t)P + 1));
+    // work lists only for the columns whose filter can leave cells undecided (a dictionary-id equality
+    // or numeric column never does): one slot of P pair indices each
+    std::vector<int32_t> wslot(K, 0);
+    int n_wslots = 0;
+    for (int k = 0; k < K; ++k) {
+        bool may = true;
+        for (const SimpleCol &sc : simple)
+            if (sc.k == k && (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids))) may = false;
+        wslot[k] = may ? n_wslots++ : 0;
+    }
+    SPK_TRY(ctx->work.alloc((size_t)std::max(n_wslots, 1) * (size_t)P + 1));
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
     // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
     // 20 regions (256-thread workgroups) per CU: four rounds of the 5 resident workgroups a CU holds
@@ -1905,6 +1915,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.codes = ctx->codes.p;
     A.code16 = ctx->code_bytes == 2;
     A.work = ctx->work.p;
+    for (int k = 0; k < K; ++k) A.wslot[k] = wslot[k];
     A.region_count = ctx->region_count.p;
     A.region_len = region_len;
     A.n_regions = n_regions;
