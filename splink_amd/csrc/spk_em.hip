@@ -96,6 +96,9 @@ constexpr int HL_THREADS = 1024;
 constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS (gfx950), capped by the device attribute
 constexpr int HL_UNROLL = 4;
 constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups per group
+#ifndef SPK_EM_PRE
+#define SPK_EM_PRE 0  // 1: workgroup 0 evaluates the E-step per pattern during the streaming (A/B)
+#endif
 #ifndef SPK_EM_ATOMIC_ROW
 #define SPK_EM_ATOMIC_ROW 0  // 1: one-level reduction through agent-scope atomics into one row (A/B)
 #endif
@@ -230,7 +233,8 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
 
 template <class Count>
 __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restrict__ mpat, double *__restrict__ llpat,
-                                  double *__restrict__ cpat, double *__restrict__ out, double *s_tab) {
+                                  double *__restrict__ cpat, double *__restrict__ out, double *s_tab,
+                                  bool pre = false) {
     const bool lds = s_tab != nullptr && A.n_pat <= EF_LDS_PAT;  // block-uniform
     double *tc = lds ? s_tab : cpat, *tm = lds ? s_tab + A.n_pat : mpat, *tl = lds ? s_tab + 2 * A.n_pat : llpat;
     __shared__ double s_rr[PA_MAXK];  // 1 / (L_k + 1): the digits' reciprocals, once per launch
@@ -238,6 +242,17 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
     __syncthreads();
     for (int p = threadIdx.x; p < A.n_pat; p += blockDim.x) {
         const unsigned long long c = count(p);
+        if (pre) {  // E-step per pattern already in mpat / llpat (k_em_iter's workgroup 0)
+            const double mp = mpat[p], ll = llpat[p];
+            if (lds) {
+                tc[p] = (double)c;
+                tm[p] = mp;
+                tl[p] = ll;
+            } else {
+                cpat[p] = (double)c;
+            }
+            continue;
+        }
         // mixed-radix digits, then the reference's left-associative products (pattern_mp)
         double num = A.lambda, den = A.one_minus;
         int q = p;
@@ -371,6 +386,23 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     const unsigned long long t_start = wall_clock64();
     if (blockIdx.x == 0) EM_STAMP(0);
 #endif
+    // SPK_EM_PRE: workgroup 0 evaluates the E-step of every pattern (it needs only the parameters) while
+    // the others stream the codes, and streams none itself; its write-through stores are published with
+    // its count row, so the last workgroup reads mp / ln per pattern instead of computing them.
+    const bool pre = FIN && SPK_EM_PRE && gridDim.x > 1;
+    if (pre && blockIdx.x == 0) {
+        PatArgs *sA = reinterpret_cast<PatArgs *>(sh);
+        const PatArgs &A = stage_args(A0, sA);
+        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
+            double ll;
+            const double mp = pattern_mp(A, p, &ll);
+            __hip_atomic_store(reinterpret_cast<unsigned long long *>(mpat) + p,
+                               (unsigned long long)__double_as_longlong(mp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<unsigned long long *>(llpat) + p,
+                               (unsigned long long)__double_as_longlong(ll), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    }
     for (int b = threadIdx.x; b < n_pat * R; b += HL_THREADS) sh[b] = 0;
     __syncthreads();
     constexpr int VEC = 16 / sizeof(CodeT);
@@ -378,8 +410,8 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     const uint32_t copy = threadIdx.x & (R - 1);
     const u32x4 *cv = reinterpret_cast<const u32x4 *>(codes);
     const int64_t n_vec = P / VEC;
-    const int64_t stride = (int64_t)gridDim.x * HL_THREADS;
-    int64_t v = (int64_t)blockIdx.x * HL_THREADS + threadIdx.x;
+    const int64_t stride = (int64_t)(gridDim.x - (pre ? 1 : 0)) * HL_THREADS;
+    int64_t v = (pre && blockIdx.x == 0) ? n_vec : (int64_t)(blockIdx.x - (pre ? 1 : 0)) * HL_THREADS + threadIdx.x;
     auto count_word = [&](uint32_t w) {
 #pragma unroll
         for (int j = 0; j < 32 / BITS; ++j) {
@@ -422,7 +454,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         count_word(x.z);
         count_word(x.w);
     }
-    if (blockIdx.x == 0)  // tail (P not a multiple of VEC)
+    if (blockIdx.x == (pre ? 1u : 0u))  // tail (P not a multiple of VEC)
         for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
     __syncthreads();
     // Two-level last-arriver reduction of the workgroups' count rows (exact integers, so the order of
@@ -562,7 +594,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         const bool room = ((sizeof(PatArgs) + 7) / 8 + 3 * (size_t)n_pat) * 8 <= (size_t)n_pat * R * 4;
         EM_STAMP(7);
         em_finalize_block(A, [&](int p) { return (unsigned long long)cpat[p]; }, mpat, llpat, cpat, out,
-                          room ? tab : nullptr);
+                          room ? tab : nullptr, pre);
     }
     EM_STAMP(9);
     if (threadIdx.x == 0) atomicExch(ticket, 0u);
