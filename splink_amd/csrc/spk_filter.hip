@@ -300,7 +300,34 @@ __device__ __attribute__((always_inline)) inline void ev_lev(const FLev &L, cons
     Chain ch[FP];
 #pragma unroll
     for (int u = 0; u < FP; ++u) ch[u] = Chain(L.lv_else);
-    for (int i = 0; i < L.n; ++i) {  // wave-uniform: the tests unequal strings can still pass
+    // The templates' shape (levenshtein_3 / _4: one or two ratio tests with threshold tables) with the
+    // test parameters at constant indices: read once, not per test through a dynamic kernel-argument
+    // index (a dependent scalar load per test and pair group).
+    bool fast = (L.n == 1 || L.n == 2) && L.kind[0] == LK_RATIO && L.a[0] >= 0 &&
+                (L.n == 1 || (L.kind[1] == LK_RATIO && L.a[1] >= 0));
+    if (fast) {
+        bool narrow = true;
+#pragma unroll
+        for (int u = 0; u < FP; ++u) narrow = narrow && S[u] < THR_S;
+        fast = !__any(!narrow);
+    }
+    if (fast) {
+        const int a0 = L.a[0], lv0 = L.level[0];
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            const int th = s_thr[a0 + S[u]];
+            ch[u].fold(hi[u] <= th ? KT : (lo[u] > th ? KF : KU), lv0);
+        }
+        if (L.n == 2) {
+            const int a1 = L.a[1], lv1 = L.level[1];
+#pragma unroll
+            for (int u = 0; u < FP; ++u) {
+                const int th = s_thr[a1 + S[u]];
+                ch[u].fold(hi[u] <= th ? KT : (lo[u] > th ? KF : KU), lv1);
+            }
+        }
+    }
+    for (int i = 0; i < (fast ? 0 : L.n); ++i) {  // wave-uniform: the tests unequal strings can still pass
         const int kind = L.kind[i], A_ = L.a[i], lv = L.level[i];
         if (kind == LK_RATIO) {
             // integer thresholds from the table when len_l + len_r < THR_S, else the fp64 bound with one
