@@ -908,6 +908,8 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     return SPK_OK;
 }
 
+int filter_chunk_pairs() { return F_THREADS * SPK_F_NPL; }
+
 int launch_chunk_plan(hipStream_t stream, const GammaArgs &A, const int32_t *vpl, const int32_t *vpr, int64_t va,
                       int64_t vb, int4 *plan, int cpr) {
     if (A.n_regions <= 0 || A.P <= 0) return SPK_OK;

@@ -342,7 +342,8 @@ int launch_chunk_plan(hipStream_t stream, const GammaArgs &A, const int32_t *vpl
 #ifndef SPK_F_TILE_KB
 #define SPK_F_TILE_KB 19
 #endif
-constexpr int filter_chunk_pairs() { return F_THREADS * SPK_F_NPL; }
+// Pairs per filter chunk (defined in spk_filter.hip, so a build with other SPK_F_* options stays consistent).
+int filter_chunk_pairs();
 // Columns of each class the filter kernel handles (more go to the interpreter).
 constexpr int FJ_MAX = 4, FL_MAX = 3, FE_MAX = 6, FN_MAX = 4;
 
