@@ -280,11 +280,15 @@ __device__ __attribute__((always_inline)) inline int sketch_inter_ub_bf(uint64_t
     const uint32_t gt = (aH & ~bH) | (~(aH ^ bH) & aL & ~bL);
     const uint32_t mL = (aL & ~gt) | (bL & gt), mH = (aH & ~gt) | (bH & gt);
     const uint32_t both_sat = aL & aH & bL & bH, rest = ~both_sat;
+    const int lmn = la < lb ? la : lb;
+    if (!__any(both_sat != 0u)) {  // wave-uniform: no bucket saturated on both sides (rest = all ones)
+        const int inter = __builtin_popcount(mL) + 2 * __builtin_popcount(mH);
+        return inter < lmn ? inter : lmn;
+    }
     int inter = __builtin_popcount(mL & rest) + 2 * __builtin_popcount(mH & rest);
     const int ra = la - (__builtin_popcount(aL & rest) + 2 * __builtin_popcount(aH & rest));
     const int rb = lb - (__builtin_popcount(bL & rest) + 2 * __builtin_popcount(bH & rest));
     inter += both_sat ? (ra < rb ? ra : rb) : 0;
-    const int lmn = la < lb ? la : lb;
     return inter < lmn ? inter : lmn;
 }
 
