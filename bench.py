@@ -405,7 +405,9 @@ def string_rates(job, st, pairs, g_ms):
                 a, b = vals.iat[int(l[items[i]])], vals.iat[int(r[items[i]])]
                 if a is None or b is None or max(len(a), len(b)) > 64:
                     continue
-                cut = max(int(np.floor(x * (len(a) + len(b)) / 2.0)) + 1 for x in thr)
+                # simple_lev_cut: one unit over the largest passing distance (ratio tests: t x mean length)
+                ratio = "length(" in expr
+                cut = max(int(np.floor(x * (len(a) + len(b)) / 2.0 if ratio else x)) + 1 for x in thr)
                 tot += lev_scan_cells(a, b, cut)
                 cnt += 1
             scanned = tot / cnt * len(items) if cnt else None

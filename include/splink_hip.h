@@ -105,6 +105,9 @@ int spk_raw_utf8_arrow(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets,
  * metadata / bit-planes / values, blocking keys): two contexts that ingested the same rows by
  * different routes (local upload, or rows gathered from other ranks) give the same digest. */
 int spk_table_digest(spk_ctx *ctx, int side, uint64_t *out);
+/* Free a raw column's device buffers (its keys and decoded columns stay; using it again is SPK_E_STATE
+ * until it is uploaded again under the same index). */
+int spk_raw_release(spk_ctx *ctx, int raw);
 /* 8-byte values compared as bit patterns (int64 ids, canonical float64 bits, host-computed key ids). */
 int spk_raw_i64(spk_ctx *ctx, int raw, int64_t n, const int64_t *values, const uint8_t *valid);
 /* One equality term of a blocking rule: l-side column `raw_l` (table 0) = r-side column `raw_r` (the

@@ -50,7 +50,7 @@ EXPORTS = [
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
-    "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_table_digest",
+    "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_table_digest", "spk_raw_release",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
     "spk_em_finalize_start", "spk_gammas_exact_ms",
 ]
@@ -213,6 +213,9 @@ class Context:
         check(self._lib.spk_raw_utf8_arrow(self._h, ctypes.c_int(raw), ctypes.c_int64(n), ctypes.c_void_p(d_offsets),
                                            ctypes.c_void_p(d_data), ctypes.c_void_p(d_valid_bytes),
                                            ctypes.c_int64(-1), ctypes.c_int(1)), "spk_raw_utf8_arrow")
+
+    def raw_release(self, raw: int):
+        check(self._lib.spk_raw_release(self._h, ctypes.c_int(raw)), "spk_raw_release")
 
     def table_digest(self, side: int) -> int:
         out = ctypes.c_uint64(0)

@@ -292,6 +292,7 @@ static int hashed_ids(spk_ctx *ctx, const HashSeg &s0, const HashSeg &s1, DevBuf
 static int seg_of(spk_ctx *ctx, int raw, int64_t want_rows, int substr_start, int substr_len, HashSeg *out) {
     SPK_REQUIRE(raw >= 0 && raw < (int)ctx->raw.size() && ctx->raw[raw], SPK_E_INVALID, "unknown raw column");
     RawCol *r = ctx->raw[raw];
+    SPK_REQUIRE(!r->released, SPK_E_STATE, "raw column released (spk_raw_release): upload it again");
     SPK_REQUIRE(r->n == want_rows, SPK_E_INVALID, "raw column length does not match the table");
     SPK_REQUIRE(r->kind == RAW_UTF8 || substr_len < 0, SPK_E_INVALID,
                 "substr of a non-string raw column");
@@ -508,6 +509,22 @@ int spk_table_digest(spk_ctx *ctx, int side, uint64_t *out) {
         for (size_t r = 0; r < t.key[w].size(); ++r)
             if (t.key[w][r] && t.key[w][r]->p) SPK_TRY(digest(ctx, t.key[w][r]->p, t.n * 8, acc));
     *out = acc;
+    return SPK_OK;
+}
+
+// Free a raw column's device buffers once everything derived from it exists (keys, decoded comparison
+// columns): its serial stays, so the blocking-key / column provenance checks still see it.
+int spk_raw_release(spk_ctx *ctx, int raw) {
+    SPK_REQUIRE(ctx && raw >= 0 && raw < (int)ctx->raw.size() && ctx->raw[raw], SPK_E_INVALID,
+                "spk_raw_release: unknown raw column");
+    SPK_HIP(hipSetDevice(ctx->device));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));  // no queued kernel reads it any more
+    RawCol *r = ctx->raw[raw];
+    r->off.release();
+    r->bytes.release();
+    r->i64.release();
+    r->valid.release();
+    r->released = true;
     return SPK_OK;
 }
 

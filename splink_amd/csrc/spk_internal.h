@@ -171,6 +171,7 @@ struct RawCol {
     DevBuf<uint8_t> bytes;   // RAW_UTF8
     DevBuf<int64_t> i64;     // RAW_I64: values (compared as 8-byte patterns)
     DevBuf<uint8_t> valid;   // 1 = non-NULL
+    bool released = false;   // spk_raw_release: buffers freed, serial kept
 };
 
 struct Table {

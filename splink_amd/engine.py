@@ -368,8 +368,17 @@ class Job:
             cache[key] = (prog, args)
         return cache[key]
 
+    def release_raw_strings(self):
+        """Free the device copies of the input string columns once the comparison columns are decoded from
+        them and the blocking keys built (at 100M records ~20 GB of UTF-8 bytes and offsets); a later
+        block() or a new comparison column uploads what it needs again."""
+        for key in [k for k in self._raw if len(k) == 3 and k[2] == "utf8"]:
+            self.ctx.raw_release(self._raw.pop(key))
+
     def gammas(self, settings, token=None) -> CompiledComparisons:
         prog, args = self._compiled(settings)
+        if self.n_pairs > 0:
+            self.release_raw_strings()
         self.ctx.gammas_native(args)
         self.codes_token = token if token is not None else object()
         self.code_meta = (prog.gamma_names, prog.n_levels)

@@ -1,5 +1,6 @@
-"""bench.string_rates on a stub job (host logic only, no GPU): DP cells (len_l·len_r) of the cells in each
-Levenshtein column's exact list over that launch's time, comparisons per second over the γ-pass time."""
+"""bench.string_rates on a stub job (host logic only, no GPU): DP cells of the cells in each Levenshtein
+column's exact list (nominal len_l·len_r, and the word-steps x word width the scans update) over that
+launch's time, comparisons per second over the γ-pass time."""
 import os
 import sys
 
@@ -42,9 +43,23 @@ def test_string_rates_counts_dp_cells_and_rates():
     out = bench.string_rates(_StubJob(t, l, r), st, len(l), g_ms=2.0)
     lev = out["levenshtein_exact_pass"]["email"]
     # listed pairs 1 (rows 0, 3: 3 x 3 code points) and 3 (rows 2, 3: 4 x 3)
-    assert lev["dp_cells"] == 21 and lev["exact_cells"] == 2
-    assert np.isclose(lev["gcups"], 21 / 0.5e-3 / 1e9)
+    assert lev["dp_cells_nominal"] == 21 and lev["exact_cells"] == 2
+    assert np.isclose(lev["gcups_nominal"], 21 / 0.5e-3 / 1e9)
+    # the scans: no common prefix / suffix, 3 text units each (shorter side), 32-bit words, no early exit
+    assert lev["dp_cells_scanned_est"] == 2 * 3 * 32
+    assert np.isclose(lev["gcups_scanned"], 192 / 0.5e-3 / 1e9)
     assert np.isclose(lev["exact_cells_per_s"], 2 / 0.5e-3)
     assert np.isclose(out["comparisons_per_s"], 4 * 2 / 2e-3)
     assert np.isclose(out["jw_comparisons_per_s"], 4 / 2e-3)
     assert np.isclose(out["lev_comparisons_per_s"], 4 / 2e-3)
+
+
+def test_lev_scan_cells_early_exit_and_strip():
+    # equal strings and a side that strips to nothing: no scan
+    assert bench.lev_scan_cells("abc", "abc", 2) == 0
+    assert bench.lev_scan_cells("abc", "abcd", 2) == 0
+    # common prefix and suffix stripped: "x" vs "yz" -> one text unit, 32 rows
+    assert bench.lev_scan_cells("abxcd", "abyzcd", 2) == 32
+    # dissimilar 40 vs 40 units at cut 3: the bound passes cut at the first tested unit (j = 3) -> 4 steps, the
+    # wide pattern (40 > 32 rows) still in its 32-bit phase (J0 = 31 - 3 = 28)
+    assert bench.lev_scan_cells("a" * 40, "b" * 40, 3) == 4 * 32
