@@ -590,8 +590,11 @@ __device__ __attribute__((always_inline)) inline void stage_chunk(const FiltArgs
 // gathering them from the image with one texture-addressed load per pair, field and side.  Software
 // pipeline, one barrier per chunk: chunk k+1's tile (the other buffer) and pair rows are in flight while
 // chunk k is evaluated.  A chunk whose rows do not fit the tile gathers from the image.
+// The arguments live in device memory (FiltArgs is ~2.8 KB and indexed per column at run time: as a kernel
+// argument, some builds copied it to scratch per lane, 2776 B/lane); uniform reads become scalar loads.
 template <int NPL, int FP, int MINW, bool C32>
-__global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
+__global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs *__restrict__ Ap) {
+    const FiltArgs &A = *Ap;
     __shared__ unsigned int s_cnt[N_FCOLS + FJ_MAX];  // work-list lengths: per column slot, then JW gap EQs
     extern __shared__ uint4 s_dyn[];                  // tiles 0 and 1 (cap x nck each), then A.thr
     const int64_t tile_n = (int64_t)A.cap * A.nck;
@@ -843,7 +846,7 @@ static void make_num(const SimpleCol &s, const GammaArgs &A, FNum &N) {
 }
 
 int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::vector<SimpleCol> &simple,
-                           int64_t region_lo, int64_t region_hi, const int4 *plan, int cpr) {
+                           int64_t region_lo, int64_t region_hi, const int4 *plan, int cpr, FilterArgSlot &slot) {
     if (region_hi <= region_lo || simple.empty()) return SPK_OK;
     SPK_REQUIRE(A.img_rows0 <= IMG_MAX_ROWS && A.img_rows1 <= IMG_MAX_ROWS, SPK_E_LIMIT,
                 "spk_gammas: more than 2^27 rows in one table (row-image planes are limited to 2^31 bytes)");
@@ -902,8 +905,19 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     F.rows1 = A.img_rows1;
     const unsigned g = (unsigned)(region_hi - region_lo);
     const size_t shm = (size_t)2 * F.cap * F.nck * 16 + (size_t)A.n_thr * sizeof(int16_t);
-    if (A.code16) k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, false><<<g, F_THREADS, shm, stream>>>(F);
-    else k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, true><<<g, F_THREADS, shm, stream>>>(F);
+    // upload the arguments only when they changed (every pass of an EM run launches the same ones)
+    if (!slot.dev || slot.host.size() != sizeof(F) || std::memcmp(slot.host.data(), &F, sizeof(F)) != 0) {
+        if (!slot.dev) {
+            void *p = nullptr;
+            SPK_HIP(hipMalloc(&p, sizeof(FiltArgs)));
+            slot.dev = p;
+        }
+        slot.host.assign(reinterpret_cast<const uint8_t *>(&F), reinterpret_cast<const uint8_t *>(&F) + sizeof(F));
+        SPK_HIP(hipMemcpyAsync(slot.dev, slot.host.data(), sizeof(F), hipMemcpyHostToDevice, stream));
+    }
+    const FiltArgs *dF = static_cast<const FiltArgs *>(slot.dev);
+    if (A.code16) k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, false><<<g, F_THREADS, shm, stream>>>(dF);
+    else k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, true><<<g, F_THREADS, shm, stream>>>(dF);
     SPK_HIP(hipGetLastError());
     return SPK_OK;
 }

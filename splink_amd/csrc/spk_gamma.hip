@@ -1464,6 +1464,7 @@ struct GammaPlan {
     std::vector<char> slow_skipped;  // columns whose slow-list kernels this call did not launch
     int K = 0, n_regions = 0, n_info = 0, n_cnt = 0, n_all = 0;
     int64_t g_exact = 1, max_units = 1;
+    FilterArgSlot fargs[3];  // the filter launches' device argument copies (table, view, table)
 };
 }  // namespace spk
 
@@ -1996,16 +1997,16 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
                                           vb > va ? ctx->pvr.p - ctx->pv_base : nullptr, va, vb, ctx->fplan.p, cpr));
                 ctx->fplan_key = pkey;
             }
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va, ctx->fplan.p, cpr));
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va, ctx->fplan.p, cpr, G.fargs[0]));
             if (vb > va) {
                 GammaArgs VA = A;
                 VA.pl = ctx->pvl.p - ctx->pv_base;  // pl[p] = view position of pair p (p >= pv_base)
                 VA.pr = ctx->pvr.p - ctx->pv_base;
                 VA.img0 = V.img0;
                 VA.img1 = V.img1;
-                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb, ctx->fplan.p, cpr));
+                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb, ctx->fplan.p, cpr, G.fargs[1]));
             }
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions, ctx->fplan.p, cpr));
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions, ctx->fplan.p, cpr, G.fargs[2]));
         }
         if (A.n_complex) {
             k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);

@@ -215,10 +215,11 @@ def test_tf_sums_use_the_scores_not_a_later_em_iteration(amd):
 
 
 def test_tf_sums_keep_tiny_match_probabilities(amd):
-    """Per-value Σmp (term_frequencies.py:49-65) when every pair scores far below 2^-260 (mp ~ 1e-290 and
-    subnormal): the sums keep their relative precision (1e-12 against a host sum), so adj_lambda stays
-    the small positive mean the reference computes instead of 0 (parameters as tests/test_spark.py:130-160's
-    tiny m, pushed further)."""
+    """Per-value Σmp (term_frequencies.py:49-65) when every pair scores far below 2^-260 (mp ~ 1e-160): the
+    sums keep their relative precision (1e-12 against a host sum), so adj_lambda stays the small positive
+    mean the reference computes instead of 0 (parameters as tests/test_spark.py:130-160's tiny m, pushed
+    further).  The m values stay >= 1e-33: the E-step's 35-decimal literal (expectation_step.py:212) turns
+    anything below 1e-35 into 0."""
     import pandas as pd
     from splink_amd.engine import Job
     from splink_amd.params import Params
@@ -231,14 +232,14 @@ def test_tf_sums_keep_tiny_match_probabilities(amd):
     job.gammas(st)
     tiny = []
     for k, (m, u) in enumerate(params._level_probabilities()):
-        tiny.append(([1e-60 * (j + 1) * (k + 1) for j in range(len(m))], list(u)))
+        tiny.append(([1e-33 * (j + 1) * (k + 1) for j in range(len(m))], list(u)))
     codes, _ = pd.factorize(job.tables[0]["surname"], use_na_sentinel=True)
     codes = codes.astype(np.int64)
     n = int(codes.max()) + 1
     l, r = job.pair_rows()
     for lam in (1e-3, 0.2):
         mp = job.score(lam, tiny)
-        assert np.nanmax(mp) < 1e-250 and np.nanmin(mp) > 0.0
+        assert np.nanmax(mp) < 1e-100 and np.nanmin(mp) > 0.0
         s, c = job.ctx.tf_accumulate(n, codes, codes)  # host value ids: the same scale and sum kernels
         ok = (codes[l] >= 0) & (codes[l] == codes[r]) & ~np.isnan(mp)
         want = np.bincount(codes[l][ok], weights=mp[ok], minlength=n)
