@@ -239,7 +239,8 @@ def test_tf_sums_keep_tiny_match_probabilities(amd):
     l, r = job.pair_rows()
     for lam in (1e-3, 0.2):
         mp = job.score(lam, tiny)
-        assert np.nanmax(mp) < 1e-100 and np.nanmin(mp) > 0.0
+        # patterns with most columns null keep a single m/u factor (mp up to ~1e-34); the bulk is ~1e-160
+        assert np.nanmax(mp) < 1e-30 and np.nanmedian(mp) < 1e-100 and np.nanmin(mp) > 0.0
         s, c = job.ctx.tf_accumulate(n, codes, codes)  # host value ids: the same scale and sum kernels
         ok = (codes[l] >= 0) & (codes[l] == codes[r]) & ~np.isnan(mp)
         want = np.bincount(codes[l][ok], weights=mp[ok], minlength=n)
