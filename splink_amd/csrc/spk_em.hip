@@ -97,10 +97,10 @@ constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LD
 constexpr int HL_UNROLL = 4;
 constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups per group
 #ifndef SPK_EM_PRE
-#define SPK_EM_PRE 0  // 1: workgroup 0 evaluates the E-step per pattern during the streaming (A/B)
+#define SPK_EM_PRE 1  // 1: workgroup 0 evaluates the E-step per pattern during the streaming (A/B)
 #endif
 #ifndef SPK_EM_ATOMIC_ROW
-#define SPK_EM_ATOMIC_ROW 0  // 1: one-level reduction through agent-scope atomics into one row (A/B)
+#define SPK_EM_ATOMIC_ROW 1  // 1: one-level reduction through agent-scope atomics into one row (A/B)
 #endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

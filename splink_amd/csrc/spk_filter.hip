@@ -28,14 +28,13 @@ enum LevKind : int32_t { LK_GE = 0, LK_LE = 1, LK_EXACT = 2, LK_RATIO = 3 };
 struct FCommon {
     int64_t p0, p1;        // byte offset of the chunk plane holding the column's field, side 0 / side 1
     uint32_t in;           // byte offset of the field inside its 16-byte chunk (0 or 8)
-    int32_t ci;            // index of that chunk in a row (its plane in a staged tile)
     uint32_t stride;       // code stride of the column
-    int32_t k;             // comparison column
-    int32_t ws;            // its work-list slot
+    int32_t k;             // comparison column (work list)
     int32_t null_level;
     int64_t imp_lo, imp_hi;  // pairs whose level the blocking key implies (SimpleCol.imp_lo / imp_hi)
     uint32_t imp_add;        // (eq_level + 1) * stride
     int32_t und_same;        // equal keys without dictionary ids: the exact pass compares the units
+    int ws;
 };
 
 struct FEq {
@@ -46,7 +45,6 @@ struct FEq {
 struct FJw {
     FCommon c;
     int64_t h0, h1;  // planes of the four head units (low 8 bytes of the next chunk)
-    int32_t hci;     // the head chunk's index in a row
     int32_t lv_one, lv_zero, lv_bound;
     float cf;        // undecided iff the fp32 upper bound >= cf (+inf: never)
     // An equality column whose 8-byte field fills the high half of the head chunk (layout_image puts
@@ -82,13 +80,6 @@ struct FiltArgs {
     const int16_t *thr;
     int n_thr;
     int nj, nl, ne, nn;
-    // LDS staging (k_filter): a chunk's rows are copied into one of two tiles of `cap` rows x `nck`
-    // 16-byte chunks (chunk-major, like the image), then its pairs read their fields from the tile.
-    // plan[region][k] = {lo, hi} of the l-side and r-side rows of chunk k of the region (k_chunk_plan).
-    int nck, cap;
-    const int4 *plan;
-    int cpr;  // chunks per region
-    int64_t rows0, rows1;  // image rows (staging clamps the last 64-row block to them)
     FJw jw[FJ_MAX];
     FLev lev[FL_MAX];
     FEq eq[FE_MAX];
@@ -96,57 +87,32 @@ struct FiltArgs {
 };
 static_assert(sizeof(FiltArgs) <= 4096, "kernel argument size");
 
-// Where a lane's FP pairs read their fields: from the global row image by 32-bit byte offsets (ox / oy =
-// row x 16) through one buffer descriptor per side (ST = false), or from the LDS tile a chunk staged
-// (ST = true: ox / oy = the rows' indices in the tile, field plane ci at ci x cap).
-struct Tile {
-    const uint4 *t;
-    int cap;
-};
-
-template <int FP, bool ST>
-__device__ __attribute__((always_inline)) inline void load16(const FiltArgs &A, const Tile &T, int ci, int64_t p0,
-                                                             int64_t p1, const uint32_t (&ox)[FP],
-                                                             const uint32_t (&oy)[FP], uint4 (&a)[FP], uint4 (&b)[FP]) {
-    if constexpr (ST) {
-        const uint4 *t = T.t + ci * T.cap;
+// Loads of one field of FP pairs' rows (ox / oy = row x 16) from the planes of a column.
+template <int FP>
+__device__ __attribute__((always_inline)) inline void load16(const FiltArgs &A, int64_t p0, int64_t p1,
+                                                             const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
+                                                             uint4 (&a)[FP], uint4 (&b)[FP]) {
+    const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
 #pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            a[u] = t[ox[u]];
-            b[u] = t[oy[u]];
-        }
-    } else {
-        const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r0, ox[u], 0, 0);
-            const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(r1, oy[u], 0, 0);
-            a[u] = make_uint4(x.x, x.y, x.z, x.w);
-            b[u] = make_uint4(y.x, y.y, y.z, y.w);
-        }
+    for (int u = 0; u < FP; ++u) {
+        const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r0, ox[u], 0, 0);
+        const u32x4_t y = __builtin_amdgcn_raw_buffer_load_b128(r1, oy[u], 0, 0);
+        a[u] = make_uint4(x.x, x.y, x.z, x.w);
+        b[u] = make_uint4(y.x, y.y, y.z, y.w);
     }
 }
 
-template <int FP, bool ST>
-__device__ __attribute__((always_inline)) inline void load8(const FiltArgs &A, const Tile &T, int ci, int64_t p0,
-                                                            int64_t p1, uint32_t in, const uint32_t (&ox)[FP],
-                                                            const uint32_t (&oy)[FP], uint2 (&a)[FP], uint2 (&b)[FP]) {
-    if constexpr (ST) {
-        const uint2 *t = reinterpret_cast<const uint2 *>(T.t + ci * T.cap) + (in >> 3);
+template <int FP>
+__device__ __attribute__((always_inline)) inline void load8(const FiltArgs &A, int64_t p0, int64_t p1, uint32_t in,
+                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
+                                                            uint2 (&a)[FP], uint2 (&b)[FP]) {
+    const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
 #pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            a[u] = t[2 * ox[u]];
-            b[u] = t[2 * oy[u]];
-        }
-    } else {
-        const __amdgpu_buffer_rsrc_t r0 = image_rsrc(A.img0 + p0, A.plane0), r1 = image_rsrc(A.img1 + p1, A.plane1);
-#pragma unroll
-        for (int u = 0; u < FP; ++u) {
-            const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(r0, ox[u] + in, 0, 0);
-            const u32x2_t y = __builtin_amdgcn_raw_buffer_load_b64(r1, oy[u] + in, 0, 0);
-            a[u] = make_uint2(x.x, x.y);
-            b[u] = make_uint2(y.x, y.y);
-        }
+    for (int u = 0; u < FP; ++u) {
+        const u32x2_t x = __builtin_amdgcn_raw_buffer_load_b64(r0, ox[u] + in, 0, 0);
+        const u32x2_t y = __builtin_amdgcn_raw_buffer_load_b64(r1, oy[u] + in, 0, 0);
+        a[u] = make_uint2(x.x, x.y);
+        b[u] = make_uint2(y.x, y.y);
     }
 }
 
@@ -155,9 +121,6 @@ template <int FP>
 __device__ __attribute__((always_inline)) inline void append(const FiltArgs &A, const FCommon &c, int64_t r0,
                                                              unsigned int *cnt, const bool (&und)[FP],
                                                              const uint32_t (&p)[FP]) {
-#ifdef SPK_DIAG_NO_APPEND  // timing diagnostic only (wrong results): no work-list appends
-    return;
-#endif
     unsigned long long m[FP];
     unsigned int total = 0;
 #pragma unroll
@@ -192,16 +155,15 @@ struct JwData {
     uint4 a[FP], b[FP];
     uint4 qa[FP], qb[FP];  // head chunk: head units in .x / .y, the gap EQ field (if any) in .z / .w
 };
-template <int FP, bool ST>
-__device__ __attribute__((always_inline)) inline void ld_jw(const FiltArgs &A, const Tile &T, const FJw &J,
-                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
-                                                            JwData<FP> &d) {
-    load16<FP, ST>(A, T, J.c.ci, J.c.p0, J.c.p1, ox, oy, d.a, d.b);
+template <int FP>
+__device__ __attribute__((always_inline)) inline void ld_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
+                                                            const uint32_t (&oy)[FP], JwData<FP> &d) {
+    load16<FP>(A, J.c.p0, J.c.p1, ox, oy, d.a, d.b);
     if (J.geq) {  // kernel-argument (wave-uniform) branch
-        load16<FP, ST>(A, T, J.hci, J.h0, J.h1, ox, oy, d.qa, d.qb);
+        load16<FP>(A, J.h0, J.h1, ox, oy, d.qa, d.qb);
     } else {
         uint2 ha[FP], hb[FP];
-        load8<FP, ST>(A, T, J.hci, J.h0, J.h1, 0, ox, oy, ha, hb);
+        load8<FP>(A, J.h0, J.h1, 0, ox, oy, ha, hb);
 #pragma unroll
         for (int u = 0; u < FP; ++u) {
             d.qa[u] = make_uint4(ha[u].x, ha[u].y, 0u, 0u);
@@ -262,6 +224,14 @@ __device__ __attribute__((always_inline)) inline void ev_jw(const FJw &J, const 
         const int level = nul[u] ? J.c.null_level : lv;
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * J.c.stride;
     }
+}
+template <int FP>
+__device__ __attribute__((always_inline)) inline void f_jw(const FiltArgs &A, const FJw &J, const uint32_t (&ox)[FP],
+                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
+                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
+    JwData<FP> d;
+    ld_jw<FP>(A, J, ox, oy, d);
+    ev_jw<FP>(J, d, act, acc, und);
 }
 
 // ---- Levenshtein template column ---------------------------------------------------------------------
@@ -374,6 +344,15 @@ __device__ __attribute__((always_inline)) inline void ev_lev(const FLev &L, cons
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * L.c.stride;
     }
 }
+template <int FP>
+__device__ __attribute__((always_inline)) inline void f_lev(const FiltArgs &A, const FLev &L, const int16_t *s_thr,
+                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
+                                                            const bool (&act)[FP], uint32_t (&acc)[FP],
+                                                            bool (&und)[FP]) {
+    Data16<FP> d;
+    load16<FP>(A, L.c.p0, L.c.p1, ox, oy, d.a, d.b);
+    ev_lev<FP>(L, s_thr, d, act, acc, und);
+}
 
 // ---- strict-equality template column -----------------------------------------------------------------
 template <int FP>
@@ -394,14 +373,21 @@ __device__ __attribute__((always_inline)) inline void ev_eq(const FEq &E, const 
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * E.c.stride;
     }
 }
+template <int FP>
+__device__ __attribute__((always_inline)) inline void f_eq(const FiltArgs &A, const FEq &E, const uint32_t (&ox)[FP],
+                                                           const uint32_t (&oy)[FP], const bool (&act)[FP],
+                                                           uint32_t (&acc)[FP], bool (&und)[FP]) {
+    Data8<FP> d;
+    load8<FP>(A, E.c.p0, E.c.p1, E.c.in, ox, oy, d.a, d.b);
+    ev_eq<FP>(E, d, act, acc, und);
+}
 
 // ---- numeric template column --------------------------------------------------------------------------
-template <int FP, bool ST>
-__device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, const Tile &T, const FNum &N,
-                                                            const uint32_t (&ox)[FP], const uint32_t (&oy)[FP],
-                                                            uint32_t (&acc)[FP]) {
+template <int FP>
+__device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, const FNum &N, const uint32_t (&ox)[FP],
+                                                            const uint32_t (&oy)[FP], uint32_t (&acc)[FP]) {
     uint4 a[FP], b[FP];
-    load16<FP, ST>(A, T, N.c.ci, N.c.p0, N.c.p1, ox, oy, a, b);
+    load16<FP>(A, N.c.p0, N.c.p1, ox, oy, a, b);
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
         const int level = simple_num(N, a[u].z != 0, bits_to_double(a[u].x, a[u].y), b[u].z != 0,
@@ -412,318 +398,123 @@ __device__ __attribute__((always_inline)) inline void f_num(const FiltArgs &A, c
 
 constexpr int N_FCOLS = FJ_MAX + FL_MAX + FE_MAX + FN_MAX;
 
-// The columns of FP pairs per lane (pairs base + u * 64 + lane, u < FP, those below `end`): per column
-// the FP pairs' field loads (tile or global image), their evaluation, one wave-aggregated append of the
-// undecided cells; then the codes.
-template <int FP, bool ST, bool C32>
-__device__ __attribute__((always_inline)) inline void eval_pairs(const FiltArgs &A, const Tile &T,
-                                                                 const int16_t *s_thr, unsigned int *s_cnt,
-                                                                 int64_t r0, uint32_t base, uint32_t end,
-                                                                 const uint32_t (&ox)[FP], const uint32_t (&oy)[FP]) {
-    constexpr int SPAN = 64 * FP;
+// One workgroup per region of consecutive pair ordinals; each lane takes FP pairs per iteration (the
+// next iteration's pair rows are in flight meanwhile).  Per column: the FP pairs' field loads, then
+// their evaluation, then one wave-aggregated append of the undecided cells.
+template <int FP, int MINW, bool C32>
+__global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
+    __shared__ unsigned int s_cnt[N_FCOLS + FJ_MAX];  // work-list lengths: per column slot, then JW gap EQs
+    extern __shared__ int16_t s_thr[];  // A.thr (dynamic LDS: n_thr entries)
+    if (threadIdx.x < N_FCOLS + FJ_MAX) s_cnt[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
+    __syncthreads();
     const int lane = threadIdx.x & 63;
-    uint32_t p[FP], acc[FP];
-    bool act[FP], und[FP];
+    const int64_t r0 = (int64_t)(A.region_base + blockIdx.x) * A.region_len;
+    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
+    constexpr int SPAN = 64 * FP;
+    constexpr int STEP = (F_THREADS / 64) * SPAN;
+    const uint32_t end = (uint32_t)r1;
+    uint32_t base = (uint32_t)r0 + (uint32_t)(threadIdx.x >> 6) * SPAN;
+    int32_t nx[FP], ny[FP];
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
-        p[u] = base + u * 64 + lane;
-        act[u] = p[u] < end;
-        acc[u] = 0;
+        const uint32_t q = base + u * 64 + lane;
+        nx[u] = q < end ? A.pl[q] : 0;  // inactive lanes read row 0 harmlessly
+        ny[u] = q < end ? A.pr[q] : 0;
     }
+    for (; base < end; base += STEP) {  // wave-uniform
+        uint32_t p[FP], ox[FP], oy[FP], acc[FP];
+        bool act[FP], und[FP];
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            p[u] = base + u * 64 + lane;
+            act[u] = p[u] < end;
+            ox[u] = (uint32_t)nx[u] << 4;
+            oy[u] = (uint32_t)ny[u] << 4;
+            acc[u] = 0;
+            const uint32_t q = p[u] + STEP;
+            nx[u] = q < end ? A.pl[q] : 0;
+            ny[u] = q < end ? A.pr[q] : 0;
+        }
 #pragma unroll 1
-    for (int j = 0; j < A.nj; ++j) {
-        const FJw &J = A.jw[j];
-#ifdef SPK_DIAG_SKIP_JW  // timing diagnostic only (wrong results)
-        break;
-#endif
-        const bool ji = implied(J.c, base, SPAN);
-        const bool gi = J.geq && implied(J.ge.c, base, SPAN);
-        if (ji) {
+        for (int j = 0; j < A.nj; ++j) {
+            const FJw &J = A.jw[j];
+            const bool ji = implied(J.c, base, SPAN);
+            const bool gi = J.geq && implied(J.ge.c, base, SPAN);
+            if (ji) {
 #pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
-        }
-        if (gi) {
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
+            }
+            if (gi) {
 #pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
-        }
-        if (ji) {
-            if (J.geq && !gi) {  // only the gap EQ field is needed
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
+            }
+            if (ji) {
+                if (J.geq && !gi) {  // only the gap EQ field is needed
+                    f_eq<FP>(A, J.ge, ox, oy, act, acc, und);
+                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+                }
+                continue;
+            }
+            JwData<FP> d;
+            ld_jw<FP>(A, J, ox, oy, d);
+            ev_jw<FP>(J, d, act, acc, und);
+            append<FP>(A, J.c, r0, &s_cnt[j], und, p);
+            if (J.geq && !gi) {
                 Data8<FP> e;
-                load8<FP, ST>(A, T, J.ge.c.ci, J.ge.c.p0, J.ge.c.p1, J.ge.c.in, ox, oy, e.a, e.b);
+#pragma unroll
+                for (int u = 0; u < FP; ++u) {
+                    e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
+                    e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
+                }
                 ev_eq<FP>(J.ge, e, act, acc, und);
                 if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
             }
-            continue;
         }
-        JwData<FP> d;
-        ld_jw<FP, ST>(A, T, J, ox, oy, d);
-        ev_jw<FP>(J, d, act, acc, und);
-        append<FP>(A, J.c, r0, &s_cnt[j], und, p);
-        if (J.geq && !gi) {
-            Data8<FP> e;
+#pragma unroll 1
+        for (int j = 0; j < A.nl; ++j) {
+            const FLev &L = A.lev[j];
+            if (implied(L.c, base, SPAN)) {
 #pragma unroll
-            for (int u = 0; u < FP; ++u) {
-                e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
-                e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? L.c.imp_add : 0u;
+                continue;
             }
-            ev_eq<FP>(J.ge, e, act, acc, und);
-            if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+            f_lev<FP>(A, L, s_thr, ox, oy, act, acc, und);
+            append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
         }
-    }
 #pragma unroll 1
-    for (int j = 0; j < A.nl; ++j) {
-        const FLev &L = A.lev[j];
-#ifdef SPK_DIAG_SKIP_LEV  // timing diagnostic only (wrong results)
-        break;
-#endif
-        if (implied(L.c, base, SPAN)) {
+        for (int j = 0; j < A.ne; ++j) {
+            const FEq &E = A.eq[j];
+            if (implied(E.c, base, SPAN)) {
 #pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? L.c.imp_add : 0u;
-            continue;
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? E.c.imp_add : 0u;
+                continue;
+            }
+            f_eq<FP>(A, E, ox, oy, act, acc, und);
+            if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
         }
-        Data16<FP> d;
-        load16<FP, ST>(A, T, L.c.ci, L.c.p0, L.c.p1, ox, oy, d.a, d.b);
-        ev_lev<FP>(L, s_thr, d, act, acc, und);
-        append<FP>(A, L.c, r0, &s_cnt[FJ_MAX + j], und, p);
-    }
 #pragma unroll 1
-    for (int j = 0; j < A.ne; ++j) {
-        const FEq &E = A.eq[j];
-        if (implied(E.c, base, SPAN)) {
-#pragma unroll
-            for (int u = 0; u < FP; ++u) acc[u] += act[u] ? E.c.imp_add : 0u;
-            continue;
+        for (int j = 0; j < A.nn; ++j) {
+            f_num<FP>(A, A.num[j], ox, oy, acc);
         }
-        Data8<FP> d;
-        load8<FP, ST>(A, T, E.c.ci, E.c.p0, E.c.p1, E.c.in, ox, oy, d.a, d.b);
-        ev_eq<FP>(E, d, act, acc, und);
-        if (E.c.und_same) append<FP>(A, E.c, r0, &s_cnt[FJ_MAX + FL_MAX + j], und, p);
-    }
-#pragma unroll 1
-    for (int j = 0; j < A.nn; ++j) f_num<FP, ST>(A, T, A.num[j], ox, oy, acc);
-#pragma unroll
-    for (int u = 0; u < FP; ++u) {
-        if (!act[u]) continue;
-        if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
-        else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
-    }
-}
-
-// A wave's NPL pairs per lane of a chunk, FP at a time.
-template <int NPL, int FP, bool ST, bool C32>
-__device__ __attribute__((always_inline)) inline void eval_chunk(const FiltArgs &A, const Tile &T,
-                                                                 const int16_t *s_thr, unsigned int *s_cnt,
-                                                                 int64_t r0, uint32_t wb, uint32_t we,
-                                                                 const uint32_t (&ox)[NPL], const uint32_t (&oy)[NPL]) {
-    static_assert(NPL % FP == 0, "pairs per lane");
-#pragma unroll
-    for (int i0 = 0; i0 < NPL; i0 += FP) {
-        const uint32_t base = wb + i0 * 64;
-        if (base >= we) break;  // wave-uniform
-        uint32_t gx[FP], gy[FP];
 #pragma unroll
         for (int u = 0; u < FP; ++u) {
-            gx[u] = ox[i0 + u];
-            gy[u] = oy[i0 + u];
+            if (!act[u]) continue;
+            if (C32) static_cast<uint32_t *>(A.codes)[p[u]] = acc[u];
+            else static_cast<uint16_t *>(A.codes)[p[u]] = (uint16_t)acc[u];
         }
-        eval_pairs<FP, ST, C32>(A, T, s_thr, s_cnt, r0, base, we, gx, gy);
-    }
-}
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void gbl_void_t;
-
-// LDS-DMA of rows [lo, lo + span) of one side's image into tile rows [dst, dst + span) (every 16-byte
-// chunk of the row, chunk-major): one global_load_lds_dwordx4 moves 64 consecutive rows of one chunk
-// plane (the destination is the wave's base + lane x 16).  Waves take the (plane, 64-row block) pieces
-// in turn.  Source rows past the image are clamped (their tile slots are never read).
-__device__ __attribute__((always_inline)) inline void stage_dma(const FiltArgs &A, uint4 *tile, const uint8_t *img,
-                                                                int64_t rows, int32_t lo, int span, int dst) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int nb = (span + 63) >> 6;
-    const uint4 *src = reinterpret_cast<const uint4 *>(img);
-    for (int piece = wv; piece < nb * A.nck; piece += F_THREADS / 64) {  // wave-uniform
-        const int c = piece / nb, b = piece - c * nb;
-        int64_t row = (int64_t)lo + b * 64 + lane;
-        row = row < rows ? row : rows - 1;
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + (int64_t)c * rows + row),
-                                         (lds_void_t *)(tile + c * A.cap + dst + b * 64), 16, 0, 0);
-    }
-}
-
-// What a chunk's plan entry says: stage (the rows fit the tile) and where its rows sit in the tile.
-struct ChunkTile {
-    bool staged, merged;
-    int32_t lo, loL, loR;
-    int span, spanL, spanR;
-};
-__device__ __attribute__((always_inline)) inline ChunkTile chunk_tile(const FiltArgs &A, int4 m) {
-    ChunkTile t;
-    const int32_t loL = m.x, hiL = m.y, loR = m.z, hiR = m.w;
-    t.loL = loL;
-    t.loR = loR;
-    t.merged = A.img0 == A.img1 && loR <= hiL + 1 && loL <= hiR + 1;
-    t.spanL = hiL - loL + 1;
-    t.spanR = hiR - loR + 1;
-    t.lo = loL < loR ? loL : loR;
-    const int64_t span = t.merged ? (int64_t)(hiL > hiR ? hiL : hiR) - t.lo + 1 : (int64_t)t.spanL + t.spanR;
-    // the r range starts on a 64-row boundary of the tile (whole DMA pieces)
-    const int64_t need = t.merged ? span : (((int64_t)t.spanL + 63) & ~63) + t.spanR;
-    t.staged = hiL >= 0 && need <= A.cap;
-    t.span = (int)span;
-    return t;
-}
-__device__ __attribute__((always_inline)) inline void stage_chunk(const FiltArgs &A, uint4 *tile, const ChunkTile &t) {
-    if (t.merged) {
-        stage_dma(A, tile, A.img0, A.rows0, t.lo, t.span, 0);
-    } else {
-        stage_dma(A, tile, A.img0, A.rows0, t.loL, t.spanL, 0);
-        stage_dma(A, tile, A.img1, A.rows1, t.loR, t.spanR, (t.spanL + 63) & ~63);
-    }
-}
-
-// One workgroup per region of consecutive pair ordinals, walked in chunks of F_THREADS x NPL pairs (wave
-// w takes the chunk's w-th quarter, NPL pairs per lane).  Candidate pairs are within-block cross
-// products (blocking.py:145-158), so a chunk's pairs touch few rows, each of them many times: the
-// workgroup copies those rows' image rows into an LDS tile once (LDS-DMA: consecutive rows are
-// consecutive in a chunk plane) and every pair then reads its two rows' fields from the tile instead of
-// gathering them from the image with one texture-addressed load per pair, field and side.  Software
-// pipeline, one barrier per chunk: chunk k+1's tile (the other buffer) and pair rows are in flight while
-// chunk k is evaluated.  A chunk whose rows do not fit the tile gathers from the image.
-// The arguments live in device memory (FiltArgs is ~2.8 KB and indexed per column at run time: as a kernel
-// argument, some builds copied it to scratch per lane, 2776 B/lane); uniform reads become scalar loads.
-template <int NPL, int FP, int MINW, bool C32>
-__global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs *__restrict__ Ap) {
-    const FiltArgs &A = *Ap;
-    __shared__ unsigned int s_cnt[N_FCOLS + FJ_MAX];  // work-list lengths: per column slot, then JW gap EQs
-    extern __shared__ uint4 s_dyn[];                  // tiles 0 and 1 (cap x nck each), then A.thr
-    const int64_t tile_n = (int64_t)A.cap * A.nck;
-    int16_t *s_thr = reinterpret_cast<int16_t *>(s_dyn + 2 * tile_n);
-    if (threadIdx.x < N_FCOLS + FJ_MAX) s_cnt[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < A.n_thr; i += F_THREADS) s_thr[i] = A.thr[i];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t region = (int64_t)A.region_base + blockIdx.x;
-    const int64_t r0 = region * A.region_len;
-    const int64_t r1 = r0 + A.region_len < A.P ? r0 + A.region_len : A.P;
-    constexpr int WCH = 64 * NPL, CH = (F_THREADS / 64) * WCH;
-    const int nch = r1 > r0 ? (int)((r1 - r0 + CH - 1) / CH) : 0;
-    const int4 *plan = A.plan + region * A.cpr;
-    auto wave_range = [&](int k, uint32_t &wb, uint32_t &we) {
-        const int64_t c0 = r0 + (int64_t)k * CH, c1 = c0 + CH < r1 ? c0 + CH : r1;
-        wb = (uint32_t)c0 + (uint32_t)(wv * WCH);
-        we = (int64_t)wb + WCH < c1 ? wb + WCH : (uint32_t)(c1 > (int64_t)wb ? c1 : wb);
-    };
-    auto load_pairs = [&](uint32_t wb, uint32_t we, int32_t (&x)[NPL], int32_t (&y)[NPL]) {
-#pragma unroll
-        for (int u = 0; u < NPL; ++u) {
-            const uint32_t q = wb + u * 64 + lane;
-            x[u] = q < we ? A.pl[q] : 0;
-            y[u] = q < we ? A.pr[q] : 0;
-        }
-    };
-    int32_t x[NPL], y[NPL];
-    uint32_t wb = 0, we = 0;
-    ChunkTile t{};
-    if (nch > 0) {
-        wave_range(0, wb, we);
-        load_pairs(wb, we, x, y);
-        t = chunk_tile(A, plan[0]);
-        if (t.staged) stage_chunk(A, s_dyn, t);
-    }
-    for (int k = 0; k < nch; ++k) {  // workgroup-uniform
-        // chunk k's tile and pair rows have landed; every wave is done with chunk k - 1 (the other tile)
-        __syncthreads();
-        int32_t nx[NPL], ny[NPL];
-        uint32_t nwb = 0, nwe = 0;
-        ChunkTile nt{};
-        if (k + 1 < nch) {
-            wave_range(k + 1, nwb, nwe);
-            nt = chunk_tile(A, plan[k + 1]);
-            if (nt.staged) stage_chunk(A, s_dyn + ((k + 1) & 1) * tile_n, nt);
-            load_pairs(nwb, nwe, nx, ny);
-        }
-        if (t.staged) {
-            const Tile T{s_dyn + (k & 1) * tile_n, A.cap};
-            const int32_t bx = t.merged ? t.lo : t.loL;
-            const int32_t by = t.merged ? t.lo : t.loR - ((t.spanL + 63) & ~63);
-            uint32_t ox[NPL], oy[NPL];
-#pragma unroll
-            for (int u = 0; u < NPL; ++u) {
-                const bool on = wb + u * 64 + lane < we;
-                ox[u] = on ? (uint32_t)(x[u] - bx) : 0u;
-                oy[u] = on ? (uint32_t)(y[u] - by) : 0u;
-            }
-            eval_chunk<NPL, FP, true, C32>(A, T, s_thr, s_cnt, r0, wb, we, ox, oy);
-        } else {
-            const Tile T{s_dyn, A.cap};
-            uint32_t ox[NPL], oy[NPL];
-#pragma unroll
-            for (int u = 0; u < NPL; ++u) {
-                ox[u] = (uint32_t)x[u] << 4;
-                oy[u] = (uint32_t)y[u] << 4;
-            }
-            eval_chunk<NPL, FP, false, C32>(A, T, s_thr, s_cnt, r0, wb, we, ox, oy);
-        }
-#pragma unroll
-        for (int u = 0; u < NPL; ++u) {
-            x[u] = nx[u];
-            y[u] = ny[u];
-        }
-        wb = nwb;
-        we = nwe;
-        t = nt;
     }
     __syncthreads();
     const int64_t slot = A.region_base + blockIdx.x;
-    const int tt = threadIdx.x;
-    if (tt < A.nj) A.region_count[(int64_t)A.jw[tt].c.k * A.n_regions + slot] = s_cnt[tt];
-    else if (tt >= FJ_MAX && tt < FJ_MAX + A.nl) A.region_count[(int64_t)A.lev[tt - FJ_MAX].c.k * A.n_regions + slot] = s_cnt[tt];
-    else if (tt >= FJ_MAX + FL_MAX && tt < FJ_MAX + FL_MAX + A.ne)
-        A.region_count[(int64_t)A.eq[tt - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[tt];
-    else if (tt >= FJ_MAX + FL_MAX + FE_MAX && tt < FJ_MAX + FL_MAX + FE_MAX + A.nn)
-        A.region_count[(int64_t)A.num[tt - FJ_MAX - FL_MAX - FE_MAX].c.k * A.n_regions + slot] = 0;
-    else if (tt >= N_FCOLS && tt < N_FCOLS + A.nj && A.jw[tt - N_FCOLS].geq)
-        A.region_count[(int64_t)A.jw[tt - N_FCOLS].ge.c.k * A.n_regions + slot] = s_cnt[tt];
-}
-
-// The filter's chunk plan: for chunk k of region g (pairs [g L + k CH, ...) of the region's L), the lo / hi
-// row of each side ({INT32_MAX, -1} for an empty side).  Rows are A.pl / A.pr, or the view positions for
-// regions [va, vb) (vpl / vpr, rule 1's view launch).  Once per pair set.
-__global__ __launch_bounds__(256) void k_chunk_plan(const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
-                                                    const int32_t *__restrict__ vpl, const int32_t *__restrict__ vpr,
-                                                    int64_t va, int64_t vb, int64_t P, int64_t region_len, int cpr,
-                                                    int ch, int4 *__restrict__ plan) {
-    const int64_t g = blockIdx.x;
-    const int64_t region = g / cpr, k = g - region * cpr;
-    const bool view = region >= va && region < vb;
-    const int32_t *L = view ? vpl : pl, *R = view ? vpr : pr;
-    const int64_t r0 = region * region_len, r1 = r0 + region_len < P ? r0 + region_len : P;
-    const int64_t c0 = r0 + k * ch, c1 = c0 + ch < r1 ? c0 + ch : r1;
-    int32_t loL = INT32_MAX, hiL = -1, loR = INT32_MAX, hiR = -1;
-    for (int64_t q = c0 + threadIdx.x; q < c1; q += 256) {
-        const int32_t a = L[q], b = R[q];
-        loL = a < loL ? a : loL;
-        hiL = a > hiL ? a : hiL;
-        loR = b < loR ? b : loR;
-        hiR = b > hiR ? b : hiR;
-    }
-    __shared__ int32_t s[4][256];
-    s[0][threadIdx.x] = loL;
-    s[1][threadIdx.x] = hiL;
-    s[2][threadIdx.x] = loR;
-    s[3][threadIdx.x] = hiR;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            const int i = threadIdx.x, j = threadIdx.x + o;
-            s[0][i] = s[0][j] < s[0][i] ? s[0][j] : s[0][i];
-            s[1][i] = s[1][j] > s[1][i] ? s[1][j] : s[1][i];
-            s[2][i] = s[2][j] < s[2][i] ? s[2][j] : s[2][i];
-            s[3][i] = s[3][j] > s[3][i] ? s[3][j] : s[3][i];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) plan[g] = make_int4(s[0][0], s[1][0], s[2][0], s[3][0]);
+    const int t = threadIdx.x;
+    if (t < A.nj) A.region_count[(int64_t)A.jw[t].c.k * A.n_regions + slot] = s_cnt[t];
+    else if (t >= FJ_MAX && t < FJ_MAX + A.nl) A.region_count[(int64_t)A.lev[t - FJ_MAX].c.k * A.n_regions + slot] = s_cnt[t];
+    else if (t >= FJ_MAX + FL_MAX && t < FJ_MAX + FL_MAX + A.ne)
+        A.region_count[(int64_t)A.eq[t - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[t];
+    else if (t >= FJ_MAX + FL_MAX + FE_MAX && t < FJ_MAX + FL_MAX + FE_MAX + A.nn)
+        A.region_count[(int64_t)A.num[t - FJ_MAX - FL_MAX - FE_MAX].c.k * A.n_regions + slot] = 0;
+    else if (t >= N_FCOLS && t < N_FCOLS + A.nj && A.jw[t - N_FCOLS].geq)
+        A.region_count[(int64_t)A.jw[t - N_FCOLS].ge.c.k * A.n_regions + slot] = s_cnt[t];
 }
 
 // ---- host: the per-column decision constants --------------------------------------------------------------
@@ -742,7 +533,6 @@ static void common(const SimpleCol &s, const GammaArgs &A, int off, FCommon &c) 
     c.p0 = (int64_t)(off >> 4) * A.img_rows0 * 16;
     c.p1 = (int64_t)(off >> 4) * A.img_rows1 * 16;
     c.in = (uint32_t)(off & 15);
-    c.ci = off >> 4;
     c.stride = (uint32_t)s.stride;
     c.k = s.k;
     c.ws = A.wslot[s.k];
@@ -764,7 +554,6 @@ static void make_jw(const SimpleCol &s, const GammaArgs &A, FJw &J) {
     common(s, A, s.off, J.c);
     J.h0 = (int64_t)(s.off2 >> 4) * A.img_rows0 * 16;
     J.h1 = (int64_t)(s.off2 >> 4) * A.img_rows1 * 16;
-    J.hci = s.off2 >> 4;
     auto first_pass = [&](double v) {
         for (int i = 0; i < s.n_tests; ++i)
             if (hcmp(v, s.t[i], s.cmp[i])) return s.level[i];
@@ -846,7 +635,7 @@ static void make_num(const SimpleCol &s, const GammaArgs &A, FNum &N) {
 }
 
 int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::vector<SimpleCol> &simple,
-                           int64_t region_lo, int64_t region_hi, const int4 *plan, int cpr, FilterArgSlot &slot) {
+                           int64_t region_lo, int64_t region_hi) {
     if (region_hi <= region_lo || simple.empty()) return SPK_OK;
     SPK_REQUIRE(A.img_rows0 <= IMG_MAX_ROWS && A.img_rows1 <= IMG_MAX_ROWS, SPK_E_LIMIT,
                 "spk_gammas: more than 2^27 rows in one table (row-image planes are limited to 2^31 bytes)");
@@ -894,43 +683,13 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
         SPK_REQUIRE(F.ne < FE_MAX, SPK_E_INVALID, "filter: EQ slots");
         make_eq(s, A, F.eq[F.ne++]);
     }
-    // the staging tiles: two of SPK_F_TILE_KB KiB of rows each (cfg2's 80-byte rows: 192 rows), so that
-    // SPK_F_MINW workgroups fit a CU's 160 KiB of LDS
-    F.nck = (int)(A.img_stride / 16);
-    SPK_REQUIRE(F.nck >= 1 && F.nck * 16 <= IMG_MAX, SPK_E_INVALID, "filter: image stride");
-    F.cap = (int)((int64_t)SPK_F_TILE_KB * 1024 / (F.nck * 16)) / 64 * 64;
-    F.plan = plan;
-    F.cpr = cpr;
-    F.rows0 = A.img_rows0;
-    F.rows1 = A.img_rows1;
     const unsigned g = (unsigned)(region_hi - region_lo);
-    const size_t shm = (size_t)2 * F.cap * F.nck * 16 + (size_t)A.n_thr * sizeof(int16_t);
-    // upload the arguments only when they changed (every pass of an EM run launches the same ones)
-    if (!slot.dev || slot.host.size() != sizeof(F) || std::memcmp(slot.host.data(), &F, sizeof(F)) != 0) {
-        if (!slot.dev) {
-            void *p = nullptr;
-            SPK_HIP(hipMalloc(&p, sizeof(FiltArgs)));
-            slot.dev = p;
-        }
-        slot.host.assign(reinterpret_cast<const uint8_t *>(&F), reinterpret_cast<const uint8_t *>(&F) + sizeof(F));
-        SPK_HIP(hipMemcpyAsync(slot.dev, slot.host.data(), sizeof(F), hipMemcpyHostToDevice, stream));
-    }
-    const FiltArgs *dF = static_cast<const FiltArgs *>(slot.dev);
-    if (A.code16) k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, false><<<g, F_THREADS, shm, stream>>>(dF);
-    else k_filter<SPK_F_NPL, SPK_F_FP, SPK_F_MINW, true><<<g, F_THREADS, shm, stream>>>(dF);
-    SPK_HIP(hipGetLastError());
-    return SPK_OK;
-}
-
-int filter_chunk_pairs() { return F_THREADS * SPK_F_NPL; }
-
-int launch_chunk_plan(hipStream_t stream, const GammaArgs &A, const int32_t *vpl, const int32_t *vpr, int64_t va,
-                      int64_t vb, int4 *plan, int cpr) {
-    if (A.n_regions <= 0 || A.P <= 0) return SPK_OK;
-    k_chunk_plan<<<(unsigned)((int64_t)A.n_regions * cpr), 256, 0, stream>>>(A.pl, A.pr, vpl, vpr, va, vb, A.P, A.region_len,
-                                                                           cpr, filter_chunk_pairs(), plan);
+    const size_t shm = (size_t)A.n_thr * sizeof(int16_t);
+    if (A.code16) k_filter<3, 5, false><<<g, F_THREADS, shm, stream>>>(F);
+    else k_filter<3, 5, true><<<g, F_THREADS, shm, stream>>>(F);
     SPK_HIP(hipGetLastError());
     return SPK_OK;
 }
 
 }  // namespace spk
+

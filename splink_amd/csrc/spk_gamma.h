@@ -325,37 +325,8 @@ __device__ inline void wave_append_batch(int32_t *list, unsigned int *count, con
 // Filter regions [region_lo, region_hi) of A's pair range over the simple columns (every one of class
 // SC_EQ / SC_JW / SC_LEV / SC_NUM, laid out in A's row image), `shm` bytes of LDS for the threshold
 // tables.  Writes each pair's code over those columns, their work lists and region counts.
-// plan / cpr: the chunk plan of the pair set (launch_chunk_plan, cpr chunks per region).  slot: the device
-// copy of the launch's arguments (re-uploaded when they change; the caller keeps one per launch site).
-struct FilterArgSlot {
-    void *dev = nullptr;
-    std::vector<uint8_t> host;
-    ~FilterArgSlot() {
-        if (dev) (void)hipFree(dev);
-    }
-};
 int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::vector<SimpleCol> &simple,
-                           int64_t region_lo, int64_t region_hi, const int4 *plan, int cpr, FilterArgSlot &slot);
-// The filter's chunk plan (row range of each side per chunk of filter_chunk_pairs() pairs); regions
-// [va, vb) read view positions (vpl / vpr indexed by pair ordinal).
-int launch_chunk_plan(hipStream_t stream, const GammaArgs &A, const int32_t *vpl, const int32_t *vpr, int64_t va,
-                      int64_t vb, int4 *plan, int cpr);
-// Filter kernel shape (build options for A/B runs): pairs per lane per chunk, pairs per lane evaluated at
-// once, waves per SIMD, LDS tile KiB per workgroup.
-#ifndef SPK_F_NPL
-#define SPK_F_NPL 4
-#endif
-#ifndef SPK_F_FP
-#define SPK_F_FP 2
-#endif
-#ifndef SPK_F_MINW
-#define SPK_F_MINW 4
-#endif
-#ifndef SPK_F_TILE_KB
-#define SPK_F_TILE_KB 19
-#endif
-// Pairs per filter chunk (defined in spk_filter.hip, so a build with other SPK_F_* options stays consistent).
-int filter_chunk_pairs();
+                           int64_t region_lo, int64_t region_hi);
 // Columns of each class the filter kernel handles (more go to the interpreter).
 constexpr int FJ_MAX = 4, FL_MAX = 3, FE_MAX = 6, FN_MAX = 4;
 

@@ -1464,7 +1464,6 @@ struct GammaPlan {
     std::vector<char> slow_skipped;  // columns whose slow-list kernels this call did not launch
     int K = 0, n_regions = 0, n_info = 0, n_cnt = 0, n_all = 0;
     int64_t g_exact = 1, max_units = 1;
-    FilterArgSlot fargs[3];  // the filter launches' device argument copies (table, view, table)
 };
 }  // namespace spk
 
@@ -1972,11 +1971,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         // 31.1 to 22.8 ms (profiles/archive/r2_ab_views.log).
         bool have_view = false;
         const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
-        // The filter stages each chunk's rows in LDS, which pays only when they are a short contiguous range:
-        // rule 1's blocks are contiguous in its view order, so its view image is built whenever there is a
-        // view (use_views 1; 2 forces view launches even for the interpreter, 0 never).
-        (void)big;
-        if (ctx->use_views == 1 || ctx->use_views == 2) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
+        if ((ctx->use_views == 1 && big) || ctx->use_views == 2) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
         if (have_view) {  // regions [i L, min((i + 1) L, P)) inside [V.lo, V.hi)
             va = std::min<int64_t>(n_regions, (V.lo + region_len - 1) / region_len);
             vb = V.hi >= P ? n_regions : std::min<int64_t>(n_regions, V.hi / region_len);
@@ -1987,26 +1982,16 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         if (simple.empty())
             SPK_HIP(hipMemsetAsync(ctx->codes.p, 0, (size_t)P * ctx->code_bytes, ctx->stream));
         if (!simple.empty()) {
-            // the filter's chunk plan (row ranges per chunk), rebuilt when the pairs or the regions change
-            const int ch = filter_chunk_pairs();
-            const int cpr = (int)((region_len + ch - 1) / ch);
-            const std::vector<int64_t> pkey = {(int64_t)ctx->pairs_epoch, P, n_regions, region_len, va, vb, ch};
-            if (!ctx->fplan.p || ctx->fplan_key != pkey) {
-                SPK_TRY(ctx->fplan.alloc((size_t)n_regions * cpr));
-                SPK_TRY(launch_chunk_plan(ctx->stream, A, vb > va ? ctx->pvl.p - ctx->pv_base : nullptr,
-                                          vb > va ? ctx->pvr.p - ctx->pv_base : nullptr, va, vb, ctx->fplan.p, cpr));
-                ctx->fplan_key = pkey;
-            }
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va, ctx->fplan.p, cpr, G.fargs[0]));
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va));
             if (vb > va) {
                 GammaArgs VA = A;
                 VA.pl = ctx->pvl.p - ctx->pv_base;  // pl[p] = view position of pair p (p >= pv_base)
                 VA.pr = ctx->pvr.p - ctx->pv_base;
                 VA.img0 = V.img0;
                 VA.img1 = V.img1;
-                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb, ctx->fplan.p, cpr, G.fargs[1]));
+                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb));
             }
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions, ctx->fplan.p, cpr, G.fargs[2]));
+            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions));
         }
         if (A.n_complex) {
             k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);

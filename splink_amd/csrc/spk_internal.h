@@ -295,8 +295,6 @@ struct spk_ctx {
     bool slow_force_skip = false;  // tests: leave every slow-list launch to settle_gammas
     uint64_t slow_key_pairs = 0, slow_key_tables = 0;
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
-    spk::DevBuf<int4> fplan;                 // the filter's chunk plan (spk_filter.hip k_chunk_plan)
-    std::vector<int64_t> fplan_key;
 
     // EM state
     spk::DevBuf<uint64_t> hist;

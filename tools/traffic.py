@@ -34,13 +34,13 @@ import re
 # the list against the sources' launch sites, so a renamed or new kernel cannot drop out of the group.
 GAMMA_KERNELS = ("k_build_image", "k_view_image", "k_filter", "k_gamma_filter", "k_gamma_exact",
                  "k_gamma_exact_simple", "k_gamma_slow", "k_gamma_slow_lev", "k_gamma_rest", "k_gamma_huge",
-                 "k_compact", "k_prefix", "k_chunk_plan")
+                 "k_compact", "k_prefix")
 # launched from the same sources by other entry points (spk_gammas_load / _copy, the bulk UDFs)
 NOT_GAMMA_KERNELS = ("k_codes_from_gammas", "k_gammas_from_codes", "k_udf", "k_udf_huge")
 GAMMA = re.compile(r"\b(?:spk::)?(" + "|".join(GAMMA_KERNELS) + r")\b")
 EM = re.compile(r"k_hist|k_em_iter|k_em_finalize")
 # built once per table / pair-set change, not per call: reported beside the per-call traffic
-GAMMA_ONCE = re.compile(r"\b(?:spk::)?(k_build_image|k_view_image|k_chunk_plan)\b")
+GAMMA_ONCE = re.compile(r"\b(?:spk::)?(k_build_image|k_view_image)\b")
 
 
 def gamma_traffic(per_kernel_avg_kib, calls):
