@@ -6,7 +6,7 @@ LIBS=${1:-}; RX=${2:-k_filter}
 B="python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --em-scale 0"
 for lib in A $LIBS; do
   if [ $lib == A ]; then unset SPLINK_AMD_LIB; else export SPLINK_AMD_LIB=$GRAFT_REPO_ROOT/splink_amd/$lib; fi
-  timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d gpurun_out/pmcq_$lib -o run -- $B > gpurun_out/pmcq_$lib.log 2>&1 || exit 1
+  timeout -s KILL 200 rocprofv3 --pmc ${COUNTERS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD} --kernel-trace --output-format csv -d gpurun_out/pmcq_$lib -o run -- $B > gpurun_out/pmcq_$lib.log 2>&1 || exit 1
   python - <<PY
 import csv, glob, re, collections
 v = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter(); dur = collections.defaultdict(float)
