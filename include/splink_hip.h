@@ -101,6 +101,11 @@ int spk_raw_utf8(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const
  * copied device to device.  Rebasing, validity expansion and the length scan run on the device. */
 int spk_raw_utf8_arrow(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets, const uint8_t *data,
                        const uint8_t *validity, int64_t validity_bit_offset, int on_device);
+/* A chunked Arrow column (pyarrow ChunkedArray: one call instead of a host-side combine_chunks copy):
+ * chunk c has rows[c] rows, its own offsets (any base), data and validity (bit_offsets[c] as above, -1 for
+ * one byte per row; validity[c] NULL = no NULLs).  The chunks' rows are concatenated in order. */
+int spk_raw_utf8_arrow_chunks(spk_ctx *ctx, int raw, int n_chunks, const int64_t *rows, const int64_t *const *offsets,
+                              const uint8_t *const *data, const uint8_t *const *validity, const int64_t *bit_offsets);
 /* 64-bit digest of a table's encoded device form (row permutation, ranks, every comparison column's
  * metadata / bit-planes / values, blocking keys): two contexts that ingested the same rows by
  * different routes (local upload, or rows gathered from other ranks) give the same digest. */

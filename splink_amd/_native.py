@@ -50,7 +50,7 @@ EXPORTS = [
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
-    "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_table_digest", "spk_raw_release",
+    "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_raw_utf8_arrow_chunks", "spk_table_digest", "spk_raw_release",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
     "spk_em_finalize_start", "spk_gammas_exact_ms",
 ]
@@ -207,6 +207,18 @@ class Context:
         check(self._lib.spk_raw_utf8_arrow(self._h, ctypes.c_int(raw), ctypes.c_int64(n), _ptr(offsets), _ptr(data),
                                            _ptr(bitmap), ctypes.c_int64(bit_offset), ctypes.c_int(0)),
               "spk_raw_utf8_arrow")
+
+    def raw_utf8_arrow_chunks(self, raw, views, rows):
+        """A chunked Arrow column: views[c] = arrow_views(chunk c) (offsets, data, bitmap or None, bit offset),
+        rows[c] its row count; the chunks' rows are concatenated on the device."""
+        nc = len(views)
+        c_rows = (ctypes.c_int64 * nc)(*[int(r) for r in rows])
+        c_off = (ctypes.c_void_p * nc)(*[_ptr(v[0]).value for v in views])
+        c_data = (ctypes.c_void_p * nc)(*[_ptr(v[1]).value for v in views])
+        c_valid = (ctypes.c_void_p * nc)(*[_ptr(v[2]).value if v[2] is not None else None for v in views])
+        c_bit = (ctypes.c_int64 * nc)(*[int(v[3]) if v[2] is not None else 0 for v in views])
+        check(self._lib.spk_raw_utf8_arrow_chunks(self._h, ctypes.c_int(raw), ctypes.c_int(nc), c_rows, c_off, c_data,
+                                                  c_valid, c_bit), "spk_raw_utf8_arrow_chunks")
 
     def raw_utf8_device(self, raw, n, d_offsets, d_data, d_valid_bytes):
         """The same from device buffers (int pointers: offsets int64[n+1], data, one validity byte per row)."""

@@ -453,9 +453,13 @@ int spk_raw_utf8_arrow(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets,
     SPK_TRY(r->off.alloc((size_t)n + 1));
     SPK_TRY(r->bytes.alloc((size_t)nbytes + 1));
     SPK_TRY(r->valid.alloc((size_t)n + 1));
-    const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    SPK_HIP(hipMemcpyAsync(r->off.p, offsets, (size_t)(n + 1) * 8, kind, ctx->stream));
-    if (nbytes) SPK_HIP(hipMemcpyAsync(r->bytes.p, data + ends[0], (size_t)nbytes, kind, ctx->stream));
+    if (on_device) {
+        SPK_HIP(hipMemcpyAsync(r->off.p, offsets, (size_t)(n + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        if (nbytes) SPK_HIP(hipMemcpyAsync(r->bytes.p, data + ends[0], (size_t)nbytes, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        SPK_HIP(hipMemcpyAsync(r->off.p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (nbytes) SPK_HIP(hipMemcpyAsync(r->bytes.p, data + ends[0], (size_t)nbytes, hipMemcpyHostToDevice, ctx->stream));
+    }
     DevBuf<uint8_t> bm;
     const uint8_t *d_bm = nullptr;
     if (validity && n) {
@@ -472,6 +476,63 @@ int spk_raw_utf8_arrow(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets,
     SPK_TRY(st.alloc(2));
     SPK_HIP(hipMemsetAsync(st.p, 0, 16, ctx->stream));
     k_arrow_rebase<<<grid(n + 1), 256, 0, ctx->stream>>>(n, r->off.p, ends[0], d_bm, validity_bit_offset, r->valid.p);
+    if (n) k_arrow_lengths<<<grid(n), 256, 0, ctx->stream>>>(n, r->off.p, r->valid.p, st.p);
+    SPK_HIP(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    SPK_HIP(hipMemcpyAsync(h, st.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    r->max_len = (int64_t)h[0];
+    r->has_empty = h[1] != 0;
+    return SPK_OK;
+}
+
+int spk_raw_utf8_arrow_chunks(spk_ctx *ctx, int raw, int n_chunks, const int64_t *rows, const int64_t *const *offsets,
+                              const uint8_t *const *data, const uint8_t *const *validity, const int64_t *bit_offsets) {
+    SPK_REQUIRE(ctx && n_chunks >= 1 && rows && offsets && data && validity && bit_offsets, SPK_E_INVALID,
+                "spk_raw_utf8_arrow_chunks: bad args");
+    int64_t n = 0, nbytes = 0;
+    for (int c = 0; c < n_chunks; ++c) {
+        SPK_REQUIRE(rows[c] >= 0 && offsets[c] && data[c] && bit_offsets[c] >= -1, SPK_E_INVALID,
+                    "spk_raw_utf8_arrow_chunks: bad chunk");
+        SPK_REQUIRE(offsets[c][0] >= 0 && offsets[c][rows[c]] >= offsets[c][0], SPK_E_INVALID,
+                    "spk_raw_utf8_arrow_chunks: offsets out of order");
+        n += rows[c];
+        nbytes += offsets[c][rows[c]] - offsets[c][0];
+    }
+    SPK_REQUIRE(n < (int64_t)INT32_MAX, SPK_E_LIMIT, "spk_raw_utf8_arrow_chunks: more than 2^31-1 rows");
+    SPK_HIP(hipSetDevice(ctx->device));
+    RawCol *r = nullptr;
+    SPK_TRY(new_raw(ctx, raw, &r));
+    r->kind = RAW_UTF8;
+    r->n = n;
+    SPK_TRY(r->off.alloc((size_t)n + 1));
+    SPK_TRY(r->bytes.alloc((size_t)nbytes + 1));
+    SPK_TRY(r->valid.alloc((size_t)n + 1));
+    // chunk c's rows go to [row0, row0 + rows[c]) and its bytes to [byte0, ...): its offsets are copied as
+    // they are and rebased on the device by (first offset - byte0); the next chunk's copy overwrites the
+    // shared end offset with the same value
+    std::vector<DevBuf<uint8_t>> bms((size_t)n_chunks);
+    int64_t row0 = 0, byte0 = 0;
+    for (int c = 0; c < n_chunks; ++c) {
+        const int64_t m = rows[c], first = offsets[c][0], len = offsets[c][m] - first;
+        SPK_HIP(hipMemcpyAsync(r->off.p + row0, offsets[c], (size_t)(m + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (len) SPK_HIP(hipMemcpyAsync(r->bytes.p + byte0, data[c] + first, (size_t)len, hipMemcpyHostToDevice, ctx->stream));
+        const uint8_t *d_bm = nullptr;
+        if (validity[c] && m) {
+            const int64_t nb = bit_offsets[c] < 0 ? m : (bit_offsets[c] + m + 7) / 8;
+            SPK_TRY(bms[c].alloc((size_t)nb));
+            SPK_HIP(hipMemcpyAsync(bms[c].p, validity[c], (size_t)nb, hipMemcpyHostToDevice, ctx->stream));
+            d_bm = bms[c].p;
+        }
+        k_arrow_rebase<<<grid(m + 1), 256, 0, ctx->stream>>>(m, r->off.p + row0, first - byte0, d_bm, bit_offsets[c],
+                                                            r->valid.p + row0);
+        SPK_HIP(hipGetLastError());
+        row0 += m;
+        byte0 += len;
+    }
+    DevBuf<unsigned long long> st;
+    SPK_TRY(st.alloc(2));
+    SPK_HIP(hipMemsetAsync(st.p, 0, 16, ctx->stream));
     if (n) k_arrow_lengths<<<grid(n), 256, 0, ctx->stream>>>(n, r->off.p, r->valid.p, st.p);
     SPK_HIP(hipGetLastError());
     unsigned long long h[2] = {0, 0};

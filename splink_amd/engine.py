@@ -176,6 +176,12 @@ class Job:
         key = (side, name, "utf8")
         if key not in self._raw:
             rid = self._new_raw()
+            chunks = None if self.replicate_ingest else T.arrow_large_utf8_chunks(self.inputs[side][name])
+            if chunks is not None and len(chunks) > 1:
+                # a chunked column: each chunk's buffers as they are, no host-side combine copy
+                self.ctx.raw_utf8_arrow_chunks(rid, [T.arrow_views(c) for c in chunks], [len(c) for c in chunks])
+                self._raw[key] = rid
+                return rid
             arr = T.arrow_large_utf8(self.inputs[side][name])
             if arr is not None and self.replicate_ingest:
                 n, off, data, valid, on_dev = D.allgather_utf8_rows(arr, force=self.force_replicate)
@@ -241,8 +247,14 @@ class Job:
         if form == "str":
             # decoded on the device through the row permutation; dictionary ids computed there, in one
             # id space for both sides (string equality = one integer compare)
+            import time
+            t0 = time.perf_counter()
             raws = [self.raw_utf8(side, name) for side in sides]
+            t1 = time.perf_counter()
             self.ctx.table_add_raw_utf8(idx, raws[0], raws[1] if len(raws) > 1 else -1)
+            t2 = time.perf_counter()
+            self.timings["raw_upload_s"] = self.timings.get("raw_upload_s", 0.0) + (t1 - t0)
+            self.timings["column_encode_s"] = self.timings.get("column_encode_s", 0.0) + (t2 - t1)
         else:
             for side in sides:
                 vals, valid = T.encode_float64(self.inputs[side][name])

@@ -129,6 +129,18 @@ def arrow_large_utf8(series: pd.Series):
     return arr.cast(pa.large_string()) if pa.types.is_string(arr.type) else arr
 
 
+def arrow_large_utf8_chunks(series: pd.Series):
+    """The chunks of the Arrow string array behind a column, each as large_string (no combine: a chunked
+    column is uploaded chunk by chunk), or None for other columns."""
+    if pa is None:
+        return None
+    arr = getattr(series.array, "_pa_array", None)
+    if arr is None or not (pa.types.is_large_string(arr.type) or pa.types.is_string(arr.type)):
+        return None
+    chunks = arr.chunks if isinstance(arr, pa.ChunkedArray) else [arr]
+    return [c.cast(pa.large_string()) if pa.types.is_string(c.type) else c for c in chunks]
+
+
 def arrow_views(arr):
     """Zero-copy numpy views of a large_string array's buffers: (offsets int64[n+1] (any base), data
     uint8, validity bitmap uint8 or None, bit offset of row 0 in it)."""

@@ -25,6 +25,21 @@ def golden():
     return load_golden
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """GPU runs: torch's HIP runtime starts before the library's, as in bench.py.  torch ships its own
+    HIP / HSA runtime; with the library's already up, torch found no device (tests/test_gpu_dist.py run
+    after tests/test_gpu_edge.py), while this order serves both (the -m gpu suite, bench.py)."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
+    yield
+
+
 @pytest.fixture
 def heartbeat(request):
     """For tests that run for minutes in one call (the per-GPU-share scale tests): a progress line on the

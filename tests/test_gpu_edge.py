@@ -248,3 +248,38 @@ def test_tf_sums_keep_tiny_match_probabilities(amd):
         has = c > 0
         assert has.sum() > 50 and (s[has] > 0.0).all()
         assert np.allclose(s, want, rtol=1e-12, atol=0.0)
+
+
+def test_chunked_arrow_ingest_matches_combined(amd):
+    """A string column handed over as a multi-chunk Arrow array (spk_raw_utf8_arrow_chunks: no host-side
+    combine) encodes to the same device table as the combined column: uneven chunks, sliced chunks (a
+    nonzero first offset and validity bit offset), NULLs and empty strings; pairs and comparison vectors
+    equal too."""
+    import pyarrow as pa
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    cols = ["first_name", "surname", "dob", "city", "email"]
+    df = make_records(30_000, seed=44, surname_vocab=500, arrow=True)[["unique_id"] + cols].copy()
+    df.loc[5, "email"] = ""
+    chunked = df.copy()
+    cuts = [0, 1, 7, 4000, 4001, 17_333, 30_000]
+    for c in ("first_name", "surname", "city", "email"):
+        whole = pa.array(df[c].array._pa_array.to_pylist(), type=pa.large_string())
+        padded = pa.concat_arrays([pa.array(["x", None, "yz"], type=pa.large_string()), whole])
+        parts = [padded.slice(3 + a, b - a) for a, b in zip(cuts[:-1], cuts[1:])]
+        chunked[c] = pd.Series(pd.arrays.ArrowExtensionArray(pa.chunked_array(parts)), index=df.index)
+    assert chunked["email"].array._pa_array.num_chunks == len(cuts) - 1
+    st = Params(cfg_settings(2), amd).settings
+    jobs = []
+    for frame_ in (df, chunked):
+        job = Job("dedupe_only", [frame_], "unique_id", 0)
+        job.block(st["blocking_rules"])
+        job.gammas(st)
+        jobs.append(job)
+    a, b = jobs
+    assert a.ctx.table_digest(0) == b.ctx.table_digest(0)
+    la, ra = a.pair_rows()
+    lb, rb = b.pair_rows()
+    assert np.array_equal(la, lb) and np.array_equal(ra, rb)
+    assert np.array_equal(a.gammas_host(), b.gammas_host())

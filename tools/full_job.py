@@ -174,7 +174,7 @@ def main():
                      f"{' | '.join('(' + r + ')' for r in st['blocking_rules'])}, {len(COLS)} columns, "
                      f"pair-ordinal shard {shard}/{n_shards}"),
         "records": a.records, "candidates_total": int(job.n_candidates), "pairs_this_gpu": int(P),
-        "iterations": a.iters, "wall_s": wall, "job_wall_s": total,
+        "iterations": a.iters, "wall_s": wall, "job_wall_s": total, "job_timings_s": dict(job.timings),
         "device_ms": {"block": block_dev, "gamma_pass_first": gamma_dev, "gamma_pass": gamma_warm,
                       "em_per_iter_mean": float(np.mean(em_dev)), "score": score_dev},
         "exact_cells_per_column": exact_cells,
