@@ -96,6 +96,10 @@ constexpr int HL_THREADS = 1024;
 constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS (gfx950), capped by the device attribute
 constexpr int HL_UNROLL = 4;
 constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups per group
+#ifndef SPK_EM_NHOT
+#define SPK_EM_NHOT 2
+#endif
+constexpr int EM_NHOT = SPK_EM_NHOT;  // patterns k_em_iter counts in registers
 #ifndef SPK_EM_PRE
 #define SPK_EM_PRE 1  // 1: workgroup 0 evaluates the E-step per pattern during the streaming (A/B)
 #endif
@@ -378,7 +382,8 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
                                                         unsigned int *__restrict__ ticket, double *__restrict__ mpat,
                                                         double *__restrict__ llpat, double *__restrict__ cpat,
                                                         double *__restrict__ out, unsigned long long *__restrict__ out_hist,
-                                                        int fence, uint32_t *__restrict__ arow) {
+                                                        int fence, uint32_t *__restrict__ arow,
+                                                        int32_t *__restrict__ hot, int refresh) {
     extern __shared__ uint32_t sh[];
     __shared__ bool s_last;
     const int n_pat = A0.n_pat;
@@ -412,11 +417,28 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     const int64_t n_vec = P / VEC;
     const int64_t stride = (int64_t)(gridDim.x - (pre ? 1 : 0)) * HL_THREADS;
     int64_t v = (pre && blockIdx.x == 0) ? n_vec : (int64_t)(blockIdx.x - (pre ? 1 : 0)) * HL_THREADS + threadIdx.x;
+    // The EM_NHOT most frequent patterns of the codes (found by an earlier launch's last workgroup; -1 = none)
+    // are counted in registers: candidate pairs are mostly non-matches that share a few patterns, and with
+    // few lane copies (R = 8 for cfg5's 2,160 patterns) their equal codes in a wave serialise on one LDS
+    // counter.  Any pair of values counts exactly; they only decide which codes skip the LDS atomics.
+    uint32_t hc[EM_NHOT], hn[EM_NHOT];
+#pragma unroll
+    for (int q = 0; q < EM_NHOT; ++q) {
+        hc[q] = (uint32_t)hot[q];
+        hn[q] = 0;
+    }
     auto count_word = [&](uint32_t w) {
 #pragma unroll
         for (int j = 0; j < 32 / BITS; ++j) {
             const uint32_t c = BITS == 32 ? w : ((w >> (BITS * j)) & ((1u << BITS) - 1u));
-            atomicAdd(&sh[c * R + copy], 1u);
+            bool done = false;
+#pragma unroll
+            for (int q = 0; q < EM_NHOT; ++q) {
+                const bool m = c == hc[q];
+                hn[q] += m ? 1u : 0u;
+                done = done || m;
+            }
+            if (!done) atomicAdd(&sh[c * R + copy], 1u);
         }
     };
     // software-pipelined 16-byte nontemporal loads, 2 x HL_UNROLL in flight per lane (k_hist_lanes)
@@ -456,6 +478,13 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     }
     if (blockIdx.x == (pre ? 1u : 0u))  // tail (P not a multiple of VEC)
         for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
+    // the register counts of the hot patterns: one LDS add per wave
+#pragma unroll
+    for (int q = 0; q < EM_NHOT; ++q) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) hn[q] += __shfl_xor(hn[q], off);
+        if ((threadIdx.x & 63) == 0 && hn[q]) atomicAdd(&sh[hc[q] * R], hn[q]);
+    }
     __syncthreads();
     // Two-level last-arriver reduction of the workgroups' count rows (exact integers, so the order of
     // the additions does not matter).  Each row is stored write-through (sc1, 16 B per lane) and drained
@@ -585,6 +614,35 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         const unsigned long long c = sp1[p];
         if (FIN) cpat[p] = (double)c;
         else out_hist[p] = c;
+    }
+    if (refresh) {  // the EM_NHOT most frequent patterns (ties: the lower one) for the next launches
+        __shared__ unsigned long long s_best[HL_THREADS / 64];
+        __shared__ uint32_t s_top[EM_NHOT];
+        for (int r = 0; r < EM_NHOT; ++r) {
+            unsigned long long best = 0;
+            for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
+                bool taken = false;
+                for (int q = 0; q < r; ++q) taken = taken || (uint32_t)p == s_top[q];
+                if (taken) continue;
+                const unsigned long long v = ((unsigned long long)sp1[p] << 32) | (0xFFFFFFFFull - (uint32_t)p);
+                best = v > best ? v : best;
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long o = __shfl_xor(best, off);
+                best = o > best ? o : best;
+            }
+            if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long b = 0;
+                for (int w = 0; w < HL_THREADS / 64; ++w) b = s_best[w] > b ? s_best[w] : b;
+                const uint32_t pb = (b >> 32) ? (uint32_t)(0xFFFFFFFFull - (b & 0xFFFFFFFFull)) : 0xFFFFFFFFu;
+                hot[r] = (int32_t)pb;
+                s_top[r] = pb;
+            }
+            __syncthreads();
+        }
     }
     if (FIN) {
         __syncthreads();  // the partials' LDS is reused for the staged arguments and the pattern table
@@ -720,16 +778,17 @@ static int64_t lane_grid(spk_ctx *ctx) {
         if (ctx->code_bytes == 2)                                                                                \
             k_em_iter<uint16_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
                 reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
-                ctx->em_fence ? 1 : 0, arow);                                                                    \
+                ctx->em_fence ? 1 : 0, arow, hot, refresh);                                                      \
         else                                                                                                     \
             k_em_iter<uint32_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
                 reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
-                ctx->em_fence ? 1 : 0, arow);                                                                    \
+                ctx->em_fence ? 1 : 0, arow, hot, refresh);                                                      \
         break;
 
 // The padded accumulation histogram and the ticket of k_em_iter: zero between launches (the last workgroup
 // resets them), zeroed here only when (re)allocated.
-static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket, uint32_t **arow) {
+static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket, uint32_t **arow, int32_t **hot,
+                          int *refresh) {
     // k_em_iter: one count row per workgroup (<= n_cu), then one per group of EM_GROUP workgroups;
     // tickets [final | per group]
     const int64_t n_groups = ((int64_t)ctx->n_cu + EM_GROUP - 1) / EM_GROUP;
@@ -750,6 +809,19 @@ static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket, u
         }
         *arow = ctx->em_row.p;
     }
+    // the hot patterns: found again (by the launch's last workgroup) when the pair set or the pattern
+    // space changed; the codes of repeated comparison passes over the same pairs keep them
+    if (!ctx->em_hot.p) {
+        SPK_TRY(ctx->em_hot.alloc(EM_NHOT));
+        SPK_HIP(hipMemsetAsync(ctx->em_hot.p, 0xFF, EM_NHOT * sizeof(int32_t), ctx->stream));
+    }
+    const std::vector<int64_t> key = {(int64_t)ctx->pairs_epoch, ctx->n_pairs, ctx->n_patterns, ctx->code_bytes};
+#ifndef SPK_EM_HOT
+#define SPK_EM_HOT 1  // 0: no register-counted patterns (A/B)
+#endif
+    *refresh = SPK_EM_HOT && ctx->em_hot_key != key;
+    ctx->em_hot_key = key;
+    *hot = ctx->em_hot.p;
     return SPK_OK;
 }
 
@@ -773,7 +845,9 @@ static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
         uint32_t *acc = nullptr;
         unsigned int *ticket = nullptr;
         uint32_t *arow = nullptr;
-        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow));
+        int32_t *hot = nullptr;
+        int refresh = 0;
+        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow, &hot, &refresh));
         double *mpat = nullptr, *llpat = nullptr, *cpat = nullptr, *out = nullptr;
         switch (R) {
             SPK_EM_ITER(64, false)
@@ -898,7 +972,9 @@ static int enqueue_em(spk_ctx *ctx) {
         unsigned long long *h = nullptr;
         unsigned int *ticket = nullptr;
         uint32_t *arow = nullptr;
-        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow));
+        int32_t *hot = nullptr;
+        int refresh = 0;
+        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow, &hot, &refresh));
         const int64_t P = ctx->n_pairs;
         const int64_t g = lane_grid(ctx);
         const size_t sh = std::max<size_t>((size_t)n_pat * R * 4, sizeof(PatArgs));

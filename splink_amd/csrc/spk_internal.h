@@ -302,6 +302,8 @@ struct spk_ctx {
     spk::DevBuf<uint32_t> hist_part;    // k_em_iter's per-workgroup pattern counts (rows of part_stride)
     spk::DevBuf<unsigned int> em_ticket;  // its last-workgroup ticket (kept zero between launches)
     spk::DevBuf<uint32_t> em_row;         // its one-level reduction row (SPK_EM_ATOMIC_ROW; kept zero)
+    spk::DevBuf<int32_t> em_hot;          // its register-counted patterns (-1: none yet)
+    std::vector<int64_t> em_hot_key;      // the pair set / pattern space they were found for
     double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;
     int n_cu = 256;                   // compute units of the device (grid sizing)
