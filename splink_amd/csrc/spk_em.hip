@@ -100,6 +100,10 @@ constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups p
 #define SPK_EM_NHOT 2
 #endif
 constexpr int EM_NHOT = SPK_EM_NHOT;  // patterns k_em_iter counts in registers
+#ifndef SPK_EM_AROWS
+#define SPK_EM_AROWS 4
+#endif
+constexpr int EM_AROWS = SPK_EM_AROWS;  // the one-level reduction's rows
 #ifndef SPK_EM_PRE
 #define SPK_EM_PRE 1  // 1: workgroup 0 evaluates the E-step per pattern during the streaming (A/B)
 #endif
@@ -297,7 +301,43 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
     // round trips.  Deterministic: the same tree whatever the counts.
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n_waves = blockDim.x >> 6;
     const int half = lane >> 5, l32 = lane & 31;
-    for (int s0 = 2 * wave; s0 <= A.n_slots; s0 += 2 * n_waves) {  // wave-uniform
+#ifndef SPK_EM_TOTALS_WAVES
+#define SPK_EM_TOTALS_WAVES 1
+#endif
+    // The totals slot (0) sums every pattern, the column slots a 1 / radix share: with spare waves (slots
+    // 1 .. n_slots two per wave) the totals are split over them -- a strided share per wave, a 64-lane
+    // fixed tree, the waves' partials added in wave order -- instead of 32 lanes walking the whole table.
+    const int col_waves = (A.n_slots + 1) / 2, spare = n_waves - col_waves;
+    const bool split = SPK_EM_TOTALS_WAVES && spare >= 2;  // block-uniform
+    __shared__ double s_tot[16][6];
+    if (split && wave >= col_waves) {
+        const int sw = wave - col_waves;
+        double v[6] = {0, 0, 0, 0, 0, 0};
+        for (int p = sw * 64 + lane; p < A.n_pat; p += spare * 64) {
+            const double c = tc[p], mp = tm[p], ll = tl[p];
+            if (c == 0.0) continue;
+            v[0] += c;
+            if (!isnan(mp)) {
+                v[1] += c;
+                v[2] += c * mp;
+                v[3] += c * (1.0 - mp);
+            }
+            if (!isnan(ll)) {
+                v[5] += c;
+                v[4] += c * ll;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const double r = row_sum16(v[q]);
+            v[q] = (readlane_d(r, 0) + readlane_d(r, 16)) + (readlane_d(r, 32) + readlane_d(r, 48));
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) s_tot[sw][q] = v[q];
+    }
+    for (int s0 = split ? 1 + 2 * wave : 2 * wave; s0 <= A.n_slots && (!split || wave < col_waves);
+         s0 += split ? 2 * col_waves : 2 * n_waves) {  // wave-uniform
         const int slot = s0 + half;
         double v[6] = {0, 0, 0, 0, 0, 0};  // rows, non-null rows, Σmp, Σ(1-mp), Σ ln, non-null ln rows
         if (slot <= A.n_slots) {
@@ -348,6 +388,20 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
                 o[2] = v[2];
                 o[3] = v[3];
             }
+        }
+    }
+    if (split) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double v[6] = {0, 0, 0, 0, 0, 0};
+            for (int w = 0; w < spare; ++w)
+#pragma unroll
+                for (int q = 0; q < 6; ++q) v[q] += s_tot[w][q];
+            out[0] = v[2];
+            out[1] = v[0];
+            out[2] = v[1];
+            out[3] = v[4];
+            out[4] = v[5];
         }
     }
     if (lds) {
@@ -542,24 +596,53 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         __syncthreads();
     };
     if (arow) {
-        // One-level alternative (SPK_EM_ATOMIC_ROW): every workgroup adds its counts into one global row with
-        // agent-scope integer atomics (exact, so their order does not matter), drains them, takes the
-        // ticket; the last one reads that row and zeroes it for the next launch.
+#ifdef SPK_EM_STAMPS
+        const unsigned long long t_streamed = wall_clock64();
+#endif
+        // One-level alternative (SPK_EM_ATOMIC_ROW): every workgroup adds its counts into one of EM_AROWS
+        // global rows (workgroup mod EM_AROWS: 64 workgroups per row at 4 rows instead of all 256
+        // contending on each bin; 1 / 4 / 8 / 16 rows measured 38.9 / 37.7 / 38.1 / 38.8 us at cfg2) with agent-scope integer atomics (exact, so their order does not matter), drains them,
+        // takes the ticket; the last one sums the rows in row order and zeroes them for the next launch.
+        const int64_t ps_a = part_stride(n_pat);
+        uint32_t *my_row = arow + (int64_t)(blockIdx.x % EM_AROWS) * ps_a;
         for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
             uint32_t c = 0;
 #pragma unroll
             for (int k = 0; k < R; ++k) c += sh[b * R + ((k + b) & (R - 1))];
-            if (c) __hip_atomic_fetch_add(arow + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c) __hip_atomic_fetch_add(my_row + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#ifdef SPK_EM_STAMPS
+        const unsigned long long t_added = wall_clock64();
+#endif
         if (!arrive(ticket, (unsigned int)(G - 1))) return;
+#ifdef SPK_EM_STAMPS
+        if (threadIdx.x == 0) {  // the last arriver: its start, end of streaming, row adds drained, ticket
+            g_em_stamps[1] = t_start;
+            g_em_stamps[2] = t_streamed;
+            g_em_stamps[3] = t_added;
+            g_em_stamps[4] = t_added;
+        }
+        EM_STAMP(5);
+#endif
         uint32_t *s1 = sh;
+        const int nr = G < EM_AROWS ? G : EM_AROWS;
+        // every row's bin first (independent loads in flight together), then the zeroing stores: a store
+        // behind each load to the same address serialised the round trips
         for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
-            s1[b] = __hip_atomic_load(arow + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            arow[b] = 0u;
+            uint32_t v[EM_AROWS];
+#pragma unroll
+            for (int r = 0; r < EM_AROWS; ++r)
+                v[r] = r < nr ? __hip_atomic_load(arow + r * ps_a + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            uint32_t c = 0;
+#pragma unroll
+            for (int r = 0; r < EM_AROWS; ++r) c += v[r];
+            s1[b] = c;
         }
         __syncthreads();
+        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS)
+            for (int r = 0; r < nr; ++r) arow[r * ps_a + b] = 0u;
     } else {
     // this workgroup's row straight from its counters (a quad of bins per lane, 16-byte sc1 stores)
     {
@@ -802,7 +885,7 @@ static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket, u
     *ticket = ctx->em_ticket.p;
     *arow = nullptr;
     if (SPK_EM_ATOMIC_ROW) {  // the one-level reduction's row: zero between launches (the last workgroup resets it)
-        const size_t ps = (size_t)part_stride(ctx->n_patterns);
+        const size_t ps = (size_t)part_stride(ctx->n_patterns) * EM_AROWS;
         if (!ctx->em_row.p || ctx->em_row.n < ps) {
             SPK_TRY(ctx->em_row.alloc(ps));
             SPK_HIP(hipMemsetAsync(ctx->em_row.p, 0, ps * 4, ctx->stream));

@@ -283,3 +283,48 @@ def test_chunked_arrow_ingest_matches_combined(amd):
     lb, rb = b.pair_rows()
     assert np.array_equal(la, lb) and np.array_equal(ra, rb)
     assert np.array_equal(a.gammas_host(), b.gammas_host())
+
+
+def test_tf_adjusted_tiny_mp_link_only_matches_oracle(amd):
+    """tf adjustment (term_frequencies.py:49-117) on a link_only frame whose match probabilities are all
+    tiny: the m probabilities follow the reference's tiny_numbers case (tests/test_spark.py:137-150,
+    m = 5.9e-25 for a level) on every column, so mp per pair sits far below 2^-260.  The per-value sums
+    keep their relative precision (per-value scale + fixed-point limbs), so every pair's
+    tf_adjusted_match_prob equals oracle.tf_adjust_codes over host-factorised surnames at 1e-9; an
+    exponent-blind fixed point would give adj_lambda = 0 and a different tf_adjusted_match_prob."""
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    from splink_amd.term_frequencies import _bayes_pair
+    import oracle as orc
+    df = make_records(40_000, seed=45, surname_vocab=700)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
+    a, b = df.iloc[:20_000].reset_index(drop=True), df.iloc[20_000:].reset_index(drop=True)
+    settings = cfg_settings(2)
+    settings["link_type"] = "link_only"
+    for c in settings["comparison_columns"]:
+        if c["col_name"] == "surname":
+            c["term_frequency_adjustments"] = True
+    params = Params(settings, amd)
+    st = params.settings
+    job = Job("link_only", [a, b], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    tiny = [([5.9380419956766985e-25 * (j + 1) for j in range(len(m))], list(u)) for m, u in params._level_probabilities()]
+    lam = 0.4
+    mp = job.score(lam, tiny)
+    assert np.nanmax(mp) < 1e-20 and np.nanmedian(mp) < 1e-78 and np.nanmin(mp) > 0.0
+    col = job._col_index[("surname", "str")]
+    n_values = job.ctx.tf_column_values(col)
+    sums, counts = job.ctx.tf_accumulate_column(col, n_values)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
+    has = counts > 0
+    assert has.sum() > 50 and (adj_lambda[has] > 0.0).all()
+    table = _bayes_pair(adj_lambda, float(1 - lam))
+    tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
+    l, r = job.pair_rows()
+    vl = job.inputs[0]["surname"] if job.perm[0] is None else job.inputs[0]["surname"].take(np.asarray(job.perm[0])).reset_index(drop=True)
+    vr = job.inputs[1]["surname"] if job.perm[1] is None else job.inputs[1]["surname"].take(np.asarray(job.perm[1])).reset_index(drop=True)
+    codes, _ = pd.factorize(pd.concat([vl, vr], ignore_index=True), use_na_sentinel=True)
+    want, _ = orc.tf_adjust_codes(codes[:len(vl)][l], codes[len(vl):][r], mp, lam)
+    assert np.allclose(tf_mp, want, rtol=1e-9, atol=0, equal_nan=True)

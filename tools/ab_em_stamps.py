@@ -46,7 +46,7 @@ for it in range(12):
         t = out.astype(np.int64)
         rows.append([(t[i] - t[0]) / 100.0 for i in range(10)])  # us from block 0's start
 r = np.median(np.array(rows), axis=0)
-names_ = ["block0 start", "final wg start", "own row published", "group complete", "group row published",
+names_ = ["block0 start", "final wg start", "own row published / streamed", "group complete / row adds", "group row published",
           "all groups in", "group rows summed", "args staged", "E-step per pattern", "M-step sums"]
 print(f"pairs {job.n_pairs}: k_em_iter stages (median of {len(rows)}, us since block 0 started)")
 for nm, x in zip(names_, r):
