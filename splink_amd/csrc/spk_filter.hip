@@ -40,6 +40,7 @@ struct FCommon {
 struct FEq {
     FCommon c;
     int32_t lv_same, lv_diff;
+    int32_t eq4;  // a 4-byte id field (SimpleCol.eq4): compare the ids, all ones = NULL
 };
 
 struct FJw {
@@ -47,10 +48,11 @@ struct FJw {
     int64_t h0, h1;  // planes of the four head units (low 8 bytes of the next chunk)
     int32_t lv_one, lv_zero, lv_bound;
     float cf;        // undecided iff the fp32 upper bound >= cf (+inf: never)
-    // An equality column whose 8-byte field fills the high half of the head chunk (layout_image puts
-    // EQ fields in those gaps): one 16-byte load per side serves both, instead of two 8-byte loads.
-    int32_t geq;
-    FEq ge;
+    // Equality columns in the high half of the head chunk (layout_image puts EQ fields in those gaps:
+    // one 8-byte field, or two 4-byte id fields): one 16-byte load per side serves them all, instead
+    // of separate loads.  ge[q].c.in = 8 or 12 says which half.
+    int32_t geq;  // gap equality columns (0 .. 2)
+    FEq ge[2];
 };
 
 struct FLev {
@@ -373,6 +375,34 @@ __device__ __attribute__((always_inline)) inline void ev_eq(const FEq &E, const 
         acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * E.c.stride;
     }
 }
+// A gap equality column from the high half (z, w) of the head chunks: the 8-byte field, or the 4-byte id at
+// byte 8 (z) or 12 (w) of the chunk.
+template <int FP>
+__device__ __attribute__((always_inline)) inline void ev_gap_eq(const FEq &E, const uint2 (&ha)[FP], const uint2 (&hb)[FP],
+                                                                const bool (&act)[FP], uint32_t (&acc)[FP],
+                                                                bool (&und)[FP]) {
+    if (E.eq4) {  // kernel-argument (wave-uniform) branch
+        const bool hi = E.c.in == 12;
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
+            const uint32_t a = hi ? ha[u].y : ha[u].x, b = hi ? hb[u].y : hb[u].x;
+            const bool nul = a == 0xFFFFFFFFu || b == 0xFFFFFFFFu;
+            und[u] = false;  // ids: equal ids are equal strings
+            const int level = nul ? E.c.null_level : (a == b ? E.lv_same : E.lv_diff);
+            acc[u] += (uint32_t)(level + 1) * E.c.stride;
+        }
+        (void)act;
+        return;
+    }
+    Data8<FP> d;
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+        d.a[u] = ha[u];
+        d.b[u] = hb[u];
+    }
+    ev_eq<FP>(E, d, act, acc, und);
+}
+
 template <int FP>
 __device__ __attribute__((always_inline)) inline void f_eq(const FiltArgs &A, const FEq &E, const uint32_t (&ox)[FP],
                                                            const uint32_t (&oy)[FP], const bool (&act)[FP],
@@ -440,35 +470,42 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
         for (int j = 0; j < A.nj; ++j) {
             const FJw &J = A.jw[j];
             const bool ji = implied(J.c, base, SPAN);
-            const bool gi = J.geq && implied(J.ge.c, base, SPAN);
+            bool gi[2] = {false, false}, gneed = false;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                gi[q] = q < J.geq && implied(J.ge[q].c, base, SPAN);
+                gneed = gneed || (q < J.geq && !gi[q]);
+            }
             if (ji) {
 #pragma unroll
                 for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.c.imp_add : 0u;
             }
-            if (gi) {
 #pragma unroll
-                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge.c.imp_add : 0u;
+            for (int q = 0; q < 2; ++q) {
+                if (!gi[q]) continue;
+#pragma unroll
+                for (int u = 0; u < FP; ++u) acc[u] += act[u] ? J.ge[q].c.imp_add : 0u;
             }
+            uint2 ga[FP], gb[FP];  // the head chunks' high halves: the gap equality fields
             if (ji) {
-                if (J.geq && !gi) {  // only the gap EQ field is needed
-                    f_eq<FP>(A, J.ge, ox, oy, act, acc, und);
-                    if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
-                }
-                continue;
-            }
-            JwData<FP> d;
-            ld_jw<FP>(A, J, ox, oy, d);
-            ev_jw<FP>(J, d, act, acc, und);
-            append<FP>(A, J.c, r0, &s_cnt[j], und, p);
-            if (J.geq && !gi) {
-                Data8<FP> e;
+                if (!gneed) continue;
+                load8<FP>(A, J.h0, J.h1, 8, ox, oy, ga, gb);  // only the gap fields are needed
+            } else {
+                JwData<FP> d;
+                ld_jw<FP>(A, J, ox, oy, d);
+                ev_jw<FP>(J, d, act, acc, und);
+                append<FP>(A, J.c, r0, &s_cnt[j], und, p);
 #pragma unroll
                 for (int u = 0; u < FP; ++u) {
-                    e.a[u] = make_uint2(d.qa[u].z, d.qa[u].w);
-                    e.b[u] = make_uint2(d.qb[u].z, d.qb[u].w);
+                    ga[u] = make_uint2(d.qa[u].z, d.qa[u].w);
+                    gb[u] = make_uint2(d.qb[u].z, d.qb[u].w);
                 }
-                ev_eq<FP>(J.ge, e, act, acc, und);
-                if (J.ge.c.und_same) append<FP>(A, J.ge.c, r0, &s_cnt[N_FCOLS + j], und, p);
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (q >= J.geq || gi[q]) continue;
+                ev_gap_eq<FP>(J.ge[q], ga, gb, act, acc, und);
+                if (J.ge[q].c.und_same) append<FP>(A, J.ge[q].c, r0, &s_cnt[N_FCOLS + j], und, p);
             }
         }
 #pragma unroll 1
@@ -513,8 +550,12 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
         A.region_count[(int64_t)A.eq[t - FJ_MAX - FL_MAX].c.k * A.n_regions + slot] = s_cnt[t];
     else if (t >= FJ_MAX + FL_MAX + FE_MAX && t < FJ_MAX + FL_MAX + FE_MAX + A.nn)
         A.region_count[(int64_t)A.num[t - FJ_MAX - FL_MAX - FE_MAX].c.k * A.n_regions + slot] = 0;
-    else if (t >= N_FCOLS && t < N_FCOLS + A.nj && A.jw[t - N_FCOLS].geq)
-        A.region_count[(int64_t)A.jw[t - N_FCOLS].ge.c.k * A.n_regions + slot] = s_cnt[t];
+    else if (t >= N_FCOLS && t < N_FCOLS + A.nj && A.jw[t - N_FCOLS].geq) {
+        // a gap with two id fields appends nothing (ids); an 8-byte field is alone in its gap
+        const FJw &J = A.jw[t - N_FCOLS];
+        A.region_count[(int64_t)J.ge[0].c.k * A.n_regions + slot] = s_cnt[t];
+        if (J.geq > 1) A.region_count[(int64_t)J.ge[1].c.k * A.n_regions + slot] = 0;
+    }
 }
 
 // ---- host: the per-column decision constants --------------------------------------------------------------
@@ -619,6 +660,7 @@ static void make_eq(const SimpleCol &s, const GammaArgs &A, FEq &E) {
     common(s, A, s.off, E.c);
     E.lv_same = eq_chain(s, true);
     E.lv_diff = eq_chain(s, false);
+    E.eq4 = s.eq4;
 }
 
 static void make_num(const SimpleCol &s, const GammaArgs &A, FNum &N) {
@@ -672,14 +714,16 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     }
     for (const SimpleCol &s : simple) {
         if (s.cls != SC_EQ) continue;
-        int host = -1;  // a JW slot whose head chunk's high half is this column's field
+        int host = -1;  // a JW slot whose head chunk's high half holds this column's field
         for (int j = 0; j < F.nj && host < 0; ++j)
-            if (!F.jw[j].geq && (jw_off2[j] & 15) == 0 && s.off == jw_off2[j] + 8) host = j;
+            if (F.jw[j].geq < 2 && (jw_off2[j] & 15) == 0 && s.off >= jw_off2[j] + 8 && s.off < jw_off2[j] + 16 &&
+                (s.eq4 || s.off == jw_off2[j] + 8))
+                host = j;
         if (host >= 0) {
-            F.jw[host].geq = 1;
-            make_eq(s, A, F.jw[host].ge);
+            make_eq(s, A, F.jw[host].ge[F.jw[host].geq++]);
             continue;
         }
+        SPK_REQUIRE(!s.eq4, SPK_E_INVALID, "filter: a 4-byte equality field outside a JW gap");
         SPK_REQUIRE(F.ne < FE_MAX, SPK_E_INVALID, "filter: EQ slots");
         make_eq(s, A, F.eq[F.ne++]);
     }

@@ -41,6 +41,7 @@ struct SimpleCol {
     int32_t off;      // byte offset of the column's fields in a row-image row
     int32_t off2;     // SC_JW: offset of the four head units
     int32_t has_ids;  // both sides carry dictionary ids (equal keys = equal strings)
+    int32_t eq4;      // SC_EQ with ids in half of a JW gap: a 4-byte field, the id or 0xFFFFFFFF (NULL)
     // Per-test decision parameters, precomputed on the host (prepare_tests) so the filter decides
     // every test with compares and selects only -- no divergent branches:
     int32_t tflag[MAX_TESTS];  // TF_* bits

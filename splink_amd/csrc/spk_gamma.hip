@@ -403,6 +403,10 @@ __global__ void k_build_image(int64_t n, const ColDesc *__restrict__ cols, const
             const int lcp = meta_cplen(m) < LEN_SAT ? meta_cplen(m) : LEN_SAT;
             lens = (uint32_t)l16 | ((uint32_t)lcp << 16);
         }
+        if (sc.eq4) {  // half of a JW gap: the id alone (NULL = all ones; ids are dense, < 2^32 - 1)
+            *reinterpret_cast<uint32_t *>(img + img_at(rows_img, row, sc.off)) = m.len16 < 0 ? 0xFFFFFFFFu : m.key;
+            continue;
+        }
         *reinterpret_cast<uint2 *>(img + img_at(rows_img, row, sc.off)) = make_uint2(m.key, lens);
         if (sc.cls != SC_EQ) *reinterpret_cast<uint64_t *>(img + img_at(rows_img, row, sc.off + 8)) = m.sketch;
         if (sc.cls == SC_JW) *reinterpret_cast<uint64_t *>(img + img_at(rows_img, row, sc.off2)) = m.head;
@@ -1249,7 +1253,9 @@ static int32_t simple_class(const SimpleCol &s) {
 
 // Row-image offsets; returns the row stride (a multiple of 16), 0 when nothing uses the image.
 // JW fields take 24 B at a 16-byte boundary (key, lens, sketch; head units at off + 16, the low half
-// of the next chunk), LEV / NUM 16 B at a boundary, EQ 8 B in the gaps JW leaves, then at the end.
+// of the next chunk), LEV / NUM 16 B at a boundary, EQ in the 8-byte gaps JW leaves (an EQ column with
+// dictionary ids takes 4 B there -- its id, two to a gap, so one head-chunk load serves a JW column and
+// two equality columns -- one without ids the whole gap), then 8 B each at the end.
 // Columns that do not fit in IMG_MAX bytes, or past the filter kernel's slots of their class
 // (FJ_MAX ...), go to the interpreter (SC_NONE).
 static int64_t layout_image(std::vector<SimpleCol> &simple) {
@@ -1279,28 +1285,36 @@ static int64_t layout_image(std::vector<SimpleCol> &simple) {
         s.off = (int32_t)off;
         off += 16;
     }
-    size_t g = 0;
-    for (SimpleCol &s : simple) {
-        if (s.cls != SC_EQ) continue;
-        if (ne == FE_MAX) {
-            s.cls = SC_NONE;
-            continue;
-        }
-        if (g < gaps.size()) {
-            s.off = (int32_t)gaps[g++];
+    std::vector<int> used(gaps.size(), 0);  // 4-byte halves taken in each gap
+    for (SimpleCol &s : simple) s.eq4 = 0;
+    for (int pass = 0; pass < 2; ++pass) {  // ids first (half gaps), then the others (whole gaps)
+        for (SimpleCol &s : simple) {
+            if (s.cls != SC_EQ || (pass == 0) != (s.has_ids != 0)) continue;
+            if (ne == FE_MAX) {
+                s.cls = SC_NONE;
+                continue;
+            }
+            size_t g = 0;
+            const int need = pass == 0 ? 1 : 2;
+            while (g < gaps.size() && used[g] + need > 2) ++g;
+            if (g < gaps.size()) {
+                s.off = (int32_t)(gaps[g] + 4 * used[g]);
+                s.eq4 = pass == 0 ? 1 : 0;
+                used[g] += need;
+                ++ne;
+                continue;
+            }
+            if (off + 8 > IMG_MAX) {
+                s.cls = SC_NONE;
+                continue;
+            }
             ++ne;
-            continue;
+            s.off = (int32_t)off;
+            off += 8;
         }
-        if (off + 8 > IMG_MAX) {
-            s.cls = SC_NONE;
-            continue;
-        }
-        ++ne;
-        s.off = (int32_t)off;
-        off += 8;
     }
     int64_t end = off;
-    if (g < gaps.size() && gaps.back() + 8 == off) end = off - 8;  // trailing unused JW gap
+    if (!gaps.empty() && used.back() == 0 && gaps.back() + 8 == off) end = off - 8;  // trailing unused JW gap
     return (end + 15) & ~(int64_t)15;
 }
 
@@ -1379,6 +1393,7 @@ static int build_images(spk_ctx *ctx, Table &t0, Table &t1, GammaArgs &A, int64_
             key.push_back(sc.col);
             key.push_back(sc.off);
             key.push_back(sc.off2);
+            key.push_back(sc.eq4);
         }
         const bool fresh = ctx->img[s].p && ctx->img_key[s] == key;
         SPK_TRY(ctx->img[s].alloc((size_t)(t.n + 1) * (size_t)stride));
