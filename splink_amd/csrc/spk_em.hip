@@ -347,16 +347,23 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
                 for (kk = 0; kk < A.K && r > A.nlev[kk]; ++kk) r -= A.nlev[kk] + 1;
                 vv = r - 1;
             }
-            // the slot's patterns directly: digit vv + 1 of column kk, p = a·(st·radix) + (vv + 1)·st + b
+            // the slot's patterns directly: digit vv + 1 of column kk, p = a·(st·radix) + (vv + 1)·st + b with
+            // t = a·st + b stepping by 32 in integers (t = l32 + 32 i), two patterns' loads in flight per
+            // step, added in the same order as one at a time
             const int st = kk >= 0 ? A.stride[kk] : 1, radix = kk >= 0 ? A.nlev[kk] + 1 : 1;
             const int n_sel = A.n_pat / radix, base = kk >= 0 ? (vv + 1) * st : 0;
-            const double rst = 1.0 / (double)st;
-            for (int t = l32; t < n_sel; t += 32) {
-                int b;
-                const int a = kk >= 0 ? udiv_uniform(t, st, rst, b) : 0;
-                const int p = kk >= 0 ? a * (st * radix) + base + b : t;
-                const double c = tc[p], mp = tm[p], ll = tl[p];
-                if (c == 0.0) continue;
+            const int q32 = 32 / st, r32 = 32 - q32 * st, span = st * radix;
+            int a = l32 / st, b = l32 - (l32 / st) * st;
+            auto step = [&]() {
+                a += q32;
+                b += r32;
+                if (b >= st) {
+                    b -= st;
+                    ++a;
+                }
+            };
+            auto add = [&](double c, double mp, double ll) {
+                if (c == 0.0) return;
                 v[0] += c;
                 if (!isnan(mp)) {
                     v[1] += c;
@@ -367,6 +374,22 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
                     v[5] += c;
                     v[4] += c * ll;
                 }
+            };
+            for (int t = l32; t < n_sel; t += 64) {
+                const int p1 = kk >= 0 ? a * span + base + b : t;
+                step();
+                const bool two = t + 32 < n_sel;
+                const int p2 = kk >= 0 ? a * span + base + b : t + 32;
+                step();
+                const double c1 = tc[p1], m1 = tm[p1], l1 = tl[p1];
+                double c2 = 0.0, m2 = 0.0, l2 = 0.0;
+                if (two) {
+                    c2 = tc[p2];
+                    m2 = tm[p2];
+                    l2 = tl[p2];
+                }
+                add(c1, m1, l1);
+                if (two) add(c2, m2, l2);
             }
         }
 #pragma unroll
