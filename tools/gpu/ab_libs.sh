@@ -23,7 +23,7 @@ for rep in 1 2; do
     timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --em-scale 0 ${BENCH_ARGS:-} > gpurun_out/ablib_$tag.json 2>/dev/null || exit 1
     python -c "
 import json; d=json.load(open('gpurun_out/ablib_$tag.json')); b=d['breakdown_ms']
-print('$lib', 'ms/step %.4f' % d['ms_per_step'], 'gamma %.4f' % b['gamma'], 'em %.4f' % (b['em_hist'] + b['em_final']), d.get('block_tiles', ''))" >> gpurun_out/ablibs.log
+print('$lib', 'ms/step %.4f' % d['ms_per_step'], 'gamma %.4f' % b['gamma'], 'em %.4f' % (b['em_hist'] + b['em_final']), 'em@scale %.3f' % d['em_at_scale']['em_iteration']['frac'] if d.get('em_at_scale') else '')" >> gpurun_out/ablibs.log
   done
 done
 cat gpurun_out/ablibs.log
