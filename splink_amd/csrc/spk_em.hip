@@ -97,7 +97,7 @@ constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LD
 constexpr int HL_UNROLL = 4;
 constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups per group
 #ifndef SPK_EM_NHOT
-#define SPK_EM_NHOT 2
+#define SPK_EM_NHOT 1  // cfg5 at 368 M pairs: 1 -> 0.65 of HBM peak, 2 -> 0.58, 3 -> 0.43, 4 -> 0.33 (profiles/r4_ab_em_nhot_cfg5.log)
 #endif
 constexpr int EM_NHOT = SPK_EM_NHOT;  // patterns k_em_iter counts in registers
 #ifndef SPK_EM_AROWS
@@ -497,7 +497,8 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     // The EM_NHOT most frequent patterns of the codes (found by an earlier launch's last workgroup; -1 = none)
     // are counted in registers: candidate pairs are mostly non-matches that share a few patterns, and with
     // few lane copies (R = 8 for cfg5's 2,160 patterns) their equal codes in a wave serialise on one LDS
-    // counter.  Any pair of values counts exactly; they only decide which codes skip the LDS atomics.
+    // counter.  Any values count exactly; they only decide which codes skip the LDS atomics.  The first is
+    // not counted at all (its bin is derived after the reduction), the others in registers.
     uint32_t hc[EM_NHOT], hn[EM_NHOT];
 #pragma unroll
     for (int q = 0; q < EM_NHOT; ++q) {
@@ -515,9 +516,10 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
                 atomicAdd(&sh[c * R + copy], 1u);
                 continue;
             }
-            bool done = false;
+            // hot pattern 0 is not counted at all: the last workgroup sets its bin to P minus the others
+            bool done = c == hc[0];
 #pragma unroll
-            for (int q = 0; q < EM_NHOT; ++q) {
+            for (int q = 1; q < EM_NHOT; ++q) {
                 const bool m = c == hc[q];
                 hn[q] += m ? 1u : 0u;
                 done = done || m;
@@ -564,7 +566,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
     // the register counts of the hot patterns: one LDS add per wave
 #pragma unroll
-    for (int q = 0; q < (HOT ? EM_NHOT : 0); ++q) {
+    for (int q = 1; q < (HOT ? EM_NHOT : 0); ++q) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) hn[q] += __shfl_xor(hn[q], off);
         if ((threadIdx.x & 63) == 0 && hn[q]) atomicAdd(&sh[hc[q] * R], hn[q]);
@@ -719,6 +721,21 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
 #endif
     sum_rows(part2, NG);
     }  // two-level reduction
+    if (HOT && hc[0] < (uint32_t)n_pat) {  // hot pattern 0's bin: P minus every other bin (exact, P < 2^32)
+        __shared__ uint32_t s_rest[HL_THREADS / 64];
+        uint32_t s = 0;
+        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) s += (uint32_t)p == hc[0] ? 0u : sh[p];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        if ((threadIdx.x & 63) == 0) s_rest[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < HL_THREADS / 64; ++w) t += s_rest[w];
+            sh[hc[0]] = (uint32_t)P - t;
+        }
+        __syncthreads();
+    }
     EM_STAMP(6);
     // thread t owns bins p = t, t + HL_THREADS, ... (the same mapping as em_finalize_block's loop, so
     // the count it parks in cpat is read back by the thread that wrote it)
