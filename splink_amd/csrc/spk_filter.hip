@@ -729,8 +729,14 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     }
     const unsigned g = (unsigned)(region_hi - region_lo);
     const size_t shm = (size_t)A.n_thr * sizeof(int16_t);
-    if (A.code16) k_filter<3, 5, false><<<g, F_THREADS, shm, stream>>>(F);
-    else k_filter<3, 5, true><<<g, F_THREADS, shm, stream>>>(F);
+#ifndef SPK_F_FP
+#define SPK_F_FP 3  // pairs per lane per step
+#endif
+#ifndef SPK_F_MINW
+#define SPK_F_MINW 5  // waves per SIMD the register budget is sized for
+#endif
+    if (A.code16) k_filter<SPK_F_FP, SPK_F_MINW, false><<<g, F_THREADS, shm, stream>>>(F);
+    else k_filter<SPK_F_FP, SPK_F_MINW, true><<<g, F_THREADS, shm, stream>>>(F);
     SPK_HIP(hipGetLastError());
     return SPK_OK;
 }
