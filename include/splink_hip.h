@@ -32,7 +32,7 @@ extern "C" {
 #define SPK_E_HIP (-2)     /* HIP runtime failure */
 #define SPK_E_OOM (-3)     /* device allocation failed */
 #define SPK_E_STATE (-4)   /* call out of order (e.g. gammas before pairs) */
-#define SPK_E_LIMIT (-5)   /* input beyond a supported limit (e.g. 2^31 pairs in one context) */
+#define SPK_E_LIMIT (-5)   /* input beyond a supported limit (e.g. 2^31 rows in one table) */
 
 #define SPK_LINK_DEDUPE 0        /* "dedupe_only"     */
 #define SPK_LINK_ONLY 1          /* "link_only"       */
@@ -254,6 +254,14 @@ int spk_gammas_implied_pairs(spk_ctx *ctx, int64_t *out, int n);
  * took as template columns. */
 int spk_gammas_set_simple(spk_ctx *ctx, int on);
 int spk_gammas_simple_count(spk_ctx *ctx, int *out);
+/* Ordinal windows.  The reference joins and projects any number of pairs (blocking.py:95-160,
+ * gammas.py:65-89); spk_gammas runs a pair set of more than ~2^31 pairs as consecutive windows of equal
+ * size (the exact passes' work lists hold window-relative int32 ordinals), so one context takes any pair
+ * count its device memory holds.  spk_gammas_set_window caps the window at `pairs` (0 = default, just under
+ * 2^31; smaller windows give identical codes -- for testing); spk_gammas_windows: windows the last
+ * spk_gammas ran. */
+int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs);
+int spk_gammas_windows(spk_ctx *ctx, int64_t *out);
 /* Filter regions (workgroups) the last spk_gammas ran over the second rule's view-ordered image. */
 int spk_gammas_view_regions(spk_ctx *ctx, int64_t *out);
 

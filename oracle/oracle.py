@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import re
 import sqlite3
 import subprocess
 
@@ -53,6 +54,8 @@ def _lib():
     lib.orc_em_stats.restype = ctypes.c_int
     lib.orc_score.restype = None
     lib.orc_log_likelihood.restype = None
+    lib.orc_em_stats_weighted.restype = ctypes.c_int
+    lib.orc_pattern_codes.restype = None
     _LIB = lib
     return lib
 
@@ -232,6 +235,66 @@ def m_step(stats, nlev):
     return lam, m_new, u_new
 
 
+def pattern_codes(gam, nlev, hist=None, want_codes=True):
+    """Mixed-radix pattern index per comparison vector (Σ (γ_k + 1) Π_{j<k} (L_j + 1)); counts are ADDED
+    to `hist` (int64 [Π (L_k + 1)]) when given, so chunks of a large pair set accumulate."""
+    gam = np.ascontiguousarray(gam, dtype=np.int8)
+    nlev = np.ascontiguousarray(nlev, dtype=np.int32)
+    n_pat = int(np.prod(nlev.astype(np.int64) + 1))
+    out = np.empty(gam.shape[0], dtype=np.int32) if want_codes else None
+    _lib().orc_pattern_codes(ctypes.c_int(len(nlev)), nlev.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(gam.shape[0]),
+                             gam.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(n_pat),
+                             None if out is None else out.ctypes.data_as(ctypes.c_void_p),
+                             None if hist is None else hist.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def patterns_of(nlev):
+    """Every comparison vector of the pattern space, row p = the vector whose pattern index is p."""
+    nlev = [int(x) for x in nlev]
+    n_pat = int(np.prod([L + 1 for L in nlev]))
+    idx = np.arange(n_pat, dtype=np.int64)
+    cols = []
+    for L in nlev:
+        cols.append((idx % (L + 1)) - 1)
+        idx //= L + 1
+    return np.stack(cols, axis=1).astype(np.int8)
+
+
+def em_stats_hist(hist, nlev, lam, m, u):
+    """em_stats over a pattern histogram (distinct comparison vectors with their pair counts)."""
+    nlev = np.ascontiguousarray(nlev, dtype=np.int32)
+    hist = np.asarray(hist, dtype=np.int64)
+    pats = patterns_of(nlev)
+    nz = np.nonzero(hist)[0]
+    g = np.ascontiguousarray(pats[nz])
+    w = np.ascontiguousarray(hist[nz])
+    mq = np.array([quantise(x) for row in m for x in row], dtype=np.float64)
+    uq = np.array([quantise(x) for row in u for x in row], dtype=np.float64)
+    out = np.zeros(3 + 4 * int(np.sum(nlev + 1)), dtype=np.float64)
+    _lib().orc_em_stats_weighted(ctypes.c_int(len(nlev)), nlev.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(len(nz)),
+                                 g.ctypes.data_as(ctypes.c_void_p), w.ctypes.data_as(ctypes.c_void_p),
+                                 ctypes.c_double(float(repr(lam))), ctypes.c_double(float(repr(1 - lam))),
+                                 mq.ctypes.data_as(ctypes.c_void_p), uq.ctypes.data_as(ctypes.c_void_p),
+                                 out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def em_iterate_hist(hist, nlev, lam, m, u, max_iterations, em_convergence):
+    """em_iterate on a pattern histogram; the final mp is returned per pattern index (NaN = NULL)."""
+    history = []
+    for _ in range(max_iterations):
+        stats = em_stats_hist(hist, nlev, lam, m, u)
+        new_lam, new_m, new_u = m_step(stats, nlev)
+        old = [x for row in m for x in row] + [x for row in u for x in row]
+        new = [x for row in new_m for x in row] + [x for row in new_u for x in row]
+        lam, m, u = new_lam, new_m, new_u
+        history.append((lam, [list(r) for r in m], [list(r) for r in u]))
+        if all(abs(a - b) < em_convergence for a, b in zip(new, old)):  # params.py:316-336
+            break
+    return history, score(patterns_of(nlev), nlev, lam, m, u)
+
+
 def em_iterate(gam, nlev, lam, m, u, max_iterations, em_convergence):
     """iterate.py:37-63 on a gamma matrix; returns (history of (λ, m, u) after each M-step, final mp)."""
     history = []
@@ -259,11 +322,141 @@ def _lev(a, b):
     return None if v is None else float(v)
 
 
+# Spark built-ins over one record (Apache Spark 2.3/2.4, unpinned: SURVEY.md §2.2 N3), restated for sqlite,
+# whose own lower / upper are ASCII-only, whose concat() skips NULLs and whose CAST accepts '12abc' as 12.
+def _s(v):
+    """Spark's implicit cast to string of a sqlite value (strings and integers only in the tests)."""
+    if v is None or isinstance(v, str):
+        return v
+    if isinstance(v, int):
+        return str(v)
+    raise ValueError(f"oracle: no Java rendering for {v!r}")
+
+
+def _spark_lower(v):
+    v = _s(v)
+    return None if v is None else v.lower()  # Java String.toLowerCase; non-ASCII: parity unpinned
+
+
+def _spark_upper(v):
+    v = _s(v)
+    return None if v is None else v.upper()
+
+
+def _spark_trim(v, how="both"):
+    v = _s(v)
+    if v is None:
+        return None
+    while how in ("both", "left") and v.startswith(" "):  # UTF8String.trim: U+0020 only
+        v = v[1:]
+    while how in ("both", "right") and v.endswith(" "):
+        v = v[:-1]
+    return v
+
+
+def _spark_concat(*args):
+    parts = [_s(a) for a in args]
+    return None if any(p is None for p in parts) else "".join(parts)
+
+
+def _spark_concat_ws(sep, *args):
+    if sep is None:
+        return None
+    return _s(sep).join(p for p in (_s(a) for a in args) if p is not None)
+
+
+def _spark_to_integral(v, bits):
+    """cast(x as int / bigint / smallint / tinyint) (UTF8String.toInt / toLong, Spark 2.4)."""
+    if v is None:
+        return None
+    if isinstance(v, float):
+        if v != v:
+            return 0
+        lim = 2 ** (bits - 1)
+        return lim - 1 if v >= lim else (-lim if v < -lim else int(v))
+    if isinstance(v, int):
+        return v
+    m = re.fullmatch(r"([+-]?)([0-9]*)(\.[0-9]*)?", v)
+    if not m or v in ("", "+", "-"):
+        return None
+    x = int(m.group(2) or "0") * (-1 if m.group(1) == "-" else 1)
+    lim = 2 ** (bits - 1)
+    return x if -lim <= x < lim else None
+
+
+def _spark_to_double(v):
+    """cast(x as double): java.lang.Double.parseDouble of the string (Spark 2.4); NULL when it throws."""
+    if v is None or isinstance(v, (int, float)):
+        return None if v is None else float(v)
+    t = v.strip("".join(chr(c) for c in range(33)))
+    m = re.fullmatch(r"([+-]?)(NaN|Infinity|(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?)[fFdD]?", t)
+    if not m:
+        h = re.fullmatch(r"([+-]?)0[xX]([0-9a-fA-F]*)\.?([0-9a-fA-F]*)[pP]([+-]?[0-9]+)[fFdD]?", t)
+        if not h or not (h.group(2) or h.group(3)):
+            return None
+        x = (int((h.group(2) or "0") + h.group(3), 16) / 16 ** len(h.group(3))) * 2.0 ** int(h.group(4))
+        return -x if h.group(1) == "-" else x
+    if m.group(2) in ("NaN", "Infinity") and t[-1] in "fFdD":
+        return None
+    if m.group(2) == "NaN":
+        return None  # the device keeps NaN as NULL in numeric columns: parity unpinned for it
+    body = m.group(2)
+    x = float("inf") if body == "Infinity" else float(body)
+    return -x if m.group(1) == "-" else x
+
+
+_CASTS = {"int": lambda v: _spark_to_integral(v, 32), "integer": lambda v: _spark_to_integral(v, 32),
+          "bigint": lambda v: _spark_to_integral(v, 64), "long": lambda v: _spark_to_integral(v, 64),
+          "smallint": lambda v: _spark_to_integral(v, 16), "tinyint": lambda v: _spark_to_integral(v, 8),
+          "double": _spark_to_double, "string": _s}
+
+
+def rewrite_casts(expr):
+    """CAST(x AS t) -> spark_cast_t(x) (sqlite's CAST has other semantics)."""
+    out, i = [], 0
+    low = expr.lower()
+    while True:
+        j = low.find("cast(", i)
+        if j < 0 or (j > 0 and (low[j - 1].isalnum() or low[j - 1] == "_")):
+            if j < 0:
+                out.append(expr[i:])
+                return "".join(out)
+            out.append(expr[i:j + 5])
+            i = j + 5
+            continue
+        out.append(expr[i:j])
+        depth, k, as_at = 0, j + 4, -1
+        while True:
+            c = expr[k]
+            if c == "(":
+                depth += 1
+            elif c == ")":
+                depth -= 1
+                if depth == 0:
+                    break
+            elif c == "'":
+                k = expr.index("'", k + 1)
+            elif depth == 1 and low.startswith(" as ", k):
+                as_at = k
+            k += 1
+        inner, typ = expr[j + 5:as_at], expr[as_at + 4:k].strip().lower()
+        out.append(f"spark_cast_{typ}({rewrite_casts(inner)})")
+        i = k + 1
+
+
 def connect():
     con = sqlite3.connect(":memory:")
     con.create_function("jaro_winkler_sim", 2, jaro_winkler, deterministic=True)
     con.create_function("levenshtein", 2, _lev, deterministic=True)
     con.create_function("length", 1, _length, deterministic=True)
+    for name, fn in (("lower", _spark_lower), ("lcase", _spark_lower), ("upper", _spark_upper),
+                     ("ucase", _spark_upper), ("trim", _spark_trim),
+                     ("ltrim", lambda v: _spark_trim(v, "left")), ("rtrim", lambda v: _spark_trim(v, "right"))):
+        con.create_function(name, 1, fn, deterministic=True)
+    con.create_function("concat", -1, _spark_concat, deterministic=True)
+    con.create_function("concat_ws", -1, _spark_concat_ws, deterministic=True)
+    for t, fn in _CASTS.items():
+        con.create_function(f"spark_cast_{t}", 1, fn, deterministic=True)
     return con
 
 
@@ -321,7 +514,7 @@ def sql_gammas(cmp_df, case_expressions):
     cmp_df.to_sql("cmp", con, index=False)
     out = np.empty((len(cmp_df), len(case_expressions)), dtype=np.int8)
     for k, expr in enumerate(case_expressions):
-        e = _strip_alias(expr)
+        e = rewrite_casts(_strip_alias(expr))
         vals = [r[0] for r in con.execute(f"select {e} from cmp").fetchall()]
         out[:, k] = np.array([-99 if v is None else v for v in vals], dtype=np.int64)
     return out

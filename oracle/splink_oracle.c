@@ -244,10 +244,11 @@ static inline void neu_add(double *s, double *c, double x)
     *s = t;
 }
 
-int orc_em_stats(int K, const int *nlev, int64_t P, const int8_t *gam, double lambda, double one_minus,
-                 const double *m, const double *u, double *stats, int n_threads_hint)
+/* weight (optional, NULL = 1 per row): rows of `gam` stand for that many pairs each (distinct comparison
+ * vectors with their counts, orc_pattern_hist), each term entering the sums as weight x value. */
+static int em_stats_impl(int K, const int *nlev, int64_t P, const int8_t *gam, const int64_t *weight, double lambda,
+                         double one_minus, const double *m, const double *u, double *stats)
 {
-    (void)n_threads_hint;
     int lvl_off[64];
     int n_slots = 0;
     for (int k = 0; k < K; k++) { lvl_off[k] = n_slots; n_slots += nlev[k] + 1; }
@@ -268,17 +269,18 @@ int orc_em_stats(int K, const int *nlev, int64_t P, const int8_t *gam, double la
 #pragma omp for schedule(static)
         for (int64_t p = 0; p < P; p++) {
             const int8_t *g = gam + p * K;
+            const double w = weight ? (double)weight[p] : 1.0;
             double mp = 0.0;
             int ok = mp_one(K, g, lvl_off, lambda, one_minus, m, u, &mp);
-            loc[1] += 1.0;  /* counts stay exact in doubles (< 2^53) */
-            if (ok) { neu_add(&loc[0], &cmp[0], mp); loc[2] += 1.0; }
+            loc[1] += w;  /* counts stay exact in doubles (< 2^53) */
+            if (ok) { neu_add(&loc[0], &cmp[0], w * mp); loc[2] += w; }
             for (int k = 0; k < K; k++) {
                 const int o = 3 + 4 * (lvl_off[k] + g[k] + 1);
-                loc[o] += 1.0;
+                loc[o] += w;
                 if (ok) {
-                    loc[o + 1] += 1.0;
-                    neu_add(&loc[o + 2], &cmp[o + 2], mp);
-                    neu_add(&loc[o + 3], &cmp[o + 3], 1.0 - mp);
+                    loc[o + 1] += w;
+                    neu_add(&loc[o + 2], &cmp[o + 2], w * mp);
+                    neu_add(&loc[o + 3], &cmp[o + 3], w * (1.0 - mp));
                 }
             }
         }
@@ -294,6 +296,57 @@ int orc_em_stats(int K, const int *nlev, int64_t P, const int8_t *gam, double la
     }
     free(part);
     return n_stats;
+}
+
+int orc_em_stats(int K, const int *nlev, int64_t P, const int8_t *gam, double lambda, double one_minus,
+                 const double *m, const double *u, double *stats, int n_threads_hint)
+{
+    (void)n_threads_hint;
+    return em_stats_impl(K, nlev, P, gam, NULL, lambda, one_minus, m, u, stats);
+}
+
+/* The same statistics from distinct comparison vectors and their pair counts. */
+int orc_em_stats_weighted(int K, const int *nlev, int64_t n, const int8_t *gam, const int64_t *count,
+                          double lambda, double one_minus, const double *m, const double *u, double *stats)
+{
+    return em_stats_impl(K, nlev, n, gam, count, lambda, one_minus, m, u, stats);
+}
+
+/* Mixed-radix pattern index of each comparison vector, code = Σ_k (γ_k + 1) · Π_{j<k} (L_j + 1) (the
+ * packing the device uses; computed here from the γ columns alone), and its histogram (hist may be NULL;
+ * out may be NULL).  hist is ADDED to (callers accumulate chunks). */
+void orc_pattern_codes(int K, const int *nlev, int64_t P, const int8_t *gam, int64_t n_pat, int32_t *out,
+                       int64_t *hist)
+{
+    int64_t stride[64];
+    int64_t s = 1;
+    for (int k = 0; k < K; k++) { stride[k] = s; s *= nlev[k] + 1; }
+    int nt = 1;
+#ifdef _OPENMP
+    nt = omp_get_max_threads();
+#endif
+    int64_t *part = hist ? (int64_t *)calloc((size_t)nt * (size_t)n_pat, sizeof(int64_t)) : NULL;
+#pragma omp parallel
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        int64_t *h = part ? part + (size_t)tid * (size_t)n_pat : NULL;
+#pragma omp for schedule(static)
+        for (int64_t p = 0; p < P; p++) {
+            const int8_t *g = gam + p * K;
+            int64_t c = 0;
+            for (int k = 0; k < K; k++) c += (int64_t)(g[k] + 1) * stride[k];
+            if (out) out[p] = (int32_t)c;
+            if (h) h[c] += 1;
+        }
+    }
+    if (part) {
+        for (int t = 0; t < nt; t++)
+            for (int64_t i = 0; i < n_pat; i++) hist[i] += part[(size_t)t * (size_t)n_pat + i];
+        free(part);
+    }
 }
 
 /* Log-likelihood of the parameters (expectation_step.py:224-272): Σ over pairs of

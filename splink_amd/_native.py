@@ -52,7 +52,7 @@ EXPORTS = [
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
     "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_raw_utf8_arrow_chunks", "spk_table_digest", "spk_raw_release",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
-    "spk_em_finalize_start", "spk_gammas_exact_ms",
+    "spk_em_finalize_start", "spk_gammas_exact_ms", "spk_gammas_set_window", "spk_gammas_windows",
 ]
 TF_LIMBS = 14  # SPK_TF_LIMBS
 
@@ -377,6 +377,15 @@ class Context:
         """1 / True: template-shaped columns through the filter kernel, 0: every column through the interpreter;
         + 10: rule 1's pairs never read the view-ordered image, + 20: always (tests)."""
         check(self._lib.spk_gammas_set_simple(self._h, ctypes.c_int(int(mode))), "spk_gammas_set_simple")
+
+    def gammas_set_window(self, pairs: int):
+        """Cap spk_gammas' ordinal windows at `pairs` (0 = default, just under 2^31; for testing)."""
+        check(self._lib.spk_gammas_set_window(self._h, ctypes.c_int64(int(pairs))), "spk_gammas_set_window")
+
+    def gammas_windows(self) -> int:
+        n = ctypes.c_int64(0)
+        check(self._lib.spk_gammas_windows(self._h, ctypes.byref(n)), "spk_gammas_windows")
+        return n.value
 
     def lds_per_block(self) -> int:
         n = ctypes.c_int(0)

@@ -4,7 +4,9 @@
   case_statements.py:62-277 or user-written) becomes a column program: WHEN branches whose
   predicates are RPN sequences of leaf tests (IS NULL, =, jaro_winkler_sim(..) cmp t,
   levenshtein(..)/((length(..)+length(..))/2) cmp t, abs(a-b) cmp t, abs(a-b)/abs(max) cmp t,
-  substr / ifnull operands) combined with Kleene AND / OR / NOT.
+  substr / ifnull operands) combined with Kleene AND / OR / NOT.  An operand may be a Spark built-in
+  over ONE record's columns (lower / upper / trim / ltrim / rtrim / concat / concat_ws / cast, nested,
+  with substr / ifnull inside): a derived column (derived.py) evaluated once per row at ingest.
 * Blocking rules (blocking.py:95-160): conjunctions of equalities between an l-side and an
   r-side key expression (a column, optionally under substr / lower / upper / trim).
 
@@ -18,6 +20,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
+from . import derived as D
 from .sqlexpr import Bin, Case, Col, Func, IsNull, Lit, Un, conjuncts, parse
 
 KLEENE_CONST = {False: 0, True: 1, None: 2}
@@ -50,6 +53,8 @@ class CompiledComparisons:
     n_levels: List[int]
     gamma_names: List[str]
     columns: List[Tuple[str, str]]   # (canonical name, form) the device tables must hold
+    # derived columns (derived.py): name -> side-neutral expression of one record, evaluated once per row
+    derived: Dict[str, object] = field(default_factory=dict)
 
     def native_operands(self, column_index: Dict[Tuple[str, str], int]):
         arr = np.zeros(len(self.operands), dtype=N.OPERAND_DTYPE)
@@ -98,6 +103,7 @@ class _ProgramBuilder:
         self.instrs: List[tuple] = []
         self.whens: List[Tuple[int, int, int]] = []
         self.columns: Dict[Tuple[str, str], None] = {}
+        self.derived: Dict[str, object] = {}
 
     # ---- operands -----------------------------------------------------------------------------
     def _column_ref(self, node: Col):
@@ -127,6 +133,8 @@ class _ProgramBuilder:
                 raise ValueError(f"{node.name}() is supported with a column and a literal default")
             default = node.args[1].value
             node = node.args[0]
+        if D.is_derived(node):
+            return self._derived_operand(node, form_hint, substr, default)
         if isinstance(node, Lit):
             if substr is not None:
                 raise ValueError("substr() of a literal is not supported")
@@ -150,6 +158,40 @@ class _ProgramBuilder:
                 spec["num"] = float(default)
                 spec["has_num_default"] = True
                 spec["form"] = "num"
+            else:
+                raise ValueError(f"unsupported ifnull default {default!r}")
+        o = OperandSpec(**spec)
+        self.columns[(o.name, o.form)] = None
+        return o
+
+    def _derived_neutral(self, node):
+        neutral, side = D.neutralise(node, self._column_ref)
+        if side is None:
+            raise ValueError(f"{D.render_any(node)} in a case_expression references no <col>_l / <col>_r column")
+        return neutral, side
+
+    def _derived_operand(self, node, form_hint, substr, default) -> OperandSpec:
+        """A Spark built-in over one record's columns (lower / upper / trim / concat / cast ...): a derived
+        column evaluated once per row at ingest (derived.py), read by the pair kernels like an input column.
+        When the comparison needs the other form, Spark's implicit cast is folded into the expression."""
+        neutral, side = self._derived_neutral(node)
+        form = D.form_of(neutral, self.schema.form)
+        want = "str" if substr is not None else (form_hint or form)
+        if default is not None:
+            want = "str" if isinstance(default, str) else "num"
+        if want != form:
+            neutral = Func("cast", (neutral, Lit("string" if want == "str" else "double")))
+            form = want
+        name = D.render(neutral)
+        self.derived[name] = neutral
+        spec = dict(kind="col", side=side, name=name, form=form, substr=substr)
+        if default is not None:
+            if isinstance(default, str):
+                spec["lit"] = default
+                self._lit(default)
+            elif isinstance(default, (int, float)) and not isinstance(default, bool):
+                spec["num"] = float(default)
+                spec["has_num_default"] = True
             else:
                 raise ValueError(f"unsupported ifnull default {default!r}")
         o = OperandSpec(**spec)
@@ -222,8 +264,12 @@ class _ProgramBuilder:
             inner = node
             if isinstance(inner, Func) and inner.name in ("substr", "substring"):
                 return "str"
+            if D.is_derived(inner):
+                return D.form_of(self._derived_neutral(inner)[0], self.schema.form)
             if isinstance(inner, Func):
                 inner = inner.args[0]
+                if D.is_derived(inner):
+                    return D.form_of(self._derived_neutral(inner)[0], self.schema.form)
             if isinstance(inner, Lit):
                 return "str" if isinstance(inner.value, str) else "num"
             name, _ = self._column_ref(inner)
@@ -258,7 +304,7 @@ def _classify(node):
         ad = _strip_abs_diff(node)
         if ad:
             return ("absdiff", ad[0], ad[1])
-        if node.name in ("substr", "substring", "ifnull", "coalesce", "nvl"):
+        if node.name in ("substr", "substring", "ifnull", "coalesce", "nvl") or D.is_derived(node):
             return ("operand",)
         raise ValueError(f"unsupported function {node.name}() in case_expression")
     if isinstance(node, Bin) and node.op == "/":
@@ -294,6 +340,75 @@ def _level(node, num_levels, what):
     return v
 
 
+_NULL_EXACT = ("lower", "lcase", "upper", "ucase", "trim", "ltrim", "rtrim")
+
+
+def _null_exact_of(node):
+    """(F, column) when node = F(<column>) for a chain F of lower / upper / trim functions: F(x) is NULL
+    exactly when x is (Spark's string functions of one argument)."""
+    chain = []
+    while isinstance(node, Func) and node.name in _NULL_EXACT and len(node.args) == 1:
+        chain.append(node.name)
+        node = node.args[0]
+    return (tuple(chain), node) if chain and isinstance(node, Col) else None
+
+
+def _guard_on_derived(tree: Case) -> Case:
+    """`WHEN x_l IS NULL OR x_r IS NULL` followed by tests that read x only as F(x_l) / F(x_r), for one
+    null-exact chain F (lower / upper / trim ...): the guard is rewritten onto F(x_l) / F(x_r) (the same
+    truth value for every row), so the column keeps the templates' shape over the derived column and
+    runs through the filter kernel (spk_gammas classify_simple) instead of the interpreter."""
+    if not tree.whens:
+        return tree
+    cond, val = tree.whens[0]
+    if not (isinstance(cond, Bin) and cond.op == "or" and isinstance(cond.a, IsNull) and isinstance(cond.b, IsNull)
+            and not cond.a.negated and not cond.b.negated and isinstance(cond.a.a, Col) and isinstance(cond.b.a, Col)):
+        return tree
+    xs = {cond.a.a, cond.b.a}
+    found = set()
+    ok = [True]
+
+    def walk(n):
+        if isinstance(n, Col):
+            if n in xs:
+                ok[0] = False  # a bare reference to x
+            return
+        ne = _null_exact_of(n)
+        if ne is not None and ne[1] in xs:
+            found.add(ne[0])
+            return
+        if isinstance(n, Func):
+            for a in n.args:
+                walk(a)
+        elif isinstance(n, Bin):
+            walk(n.a)
+            walk(n.b)
+        elif isinstance(n, Un):
+            walk(n.a)
+        elif isinstance(n, IsNull):
+            walk(n.a)
+        elif isinstance(n, Case):
+            for c, v in n.whens:
+                walk(c)
+                walk(v)
+            if n.else_ is not None:
+                walk(n.else_)
+
+    for c, v in tree.whens[1:]:
+        walk(c)
+    if not ok[0] or len(found) != 1:
+        return tree
+    chain = found.pop()
+
+    def wrap(col):
+        for name in reversed(chain):
+            col = Func(name, (col,))
+        return col
+
+    guard = Bin("or", IsNull(wrap(cond.a.a)), IsNull(wrap(cond.b.a)))
+    return Case(((guard, val),) + tuple(tree.whens[1:]), tree.else_)
+
+
 def compile_comparisons(settings: dict, schema: Schema) -> CompiledComparisons:
     b = _ProgramBuilder(schema)
     programs, names, n_levels = [], [], []
@@ -303,6 +418,7 @@ def compile_comparisons(settings: dict, schema: Schema) -> CompiledComparisons:
         tree = parse(col["case_expression"])
         if not isinstance(tree, Case):
             raise ValueError(f"case_expression for {name} is not a CASE expression")
+        tree = _guard_on_derived(tree)
         first_when = len(b.whens)
         for cond, val in tree.whens:
             start = len(b.instrs)
@@ -321,7 +437,8 @@ def compile_comparisons(settings: dict, schema: Schema) -> CompiledComparisons:
     wf = np.array([w[0] for w in b.whens], dtype=np.int32)
     wn = np.array([w[1] for w in b.whens], dtype=np.int32)
     wl = np.array([w[2] for w in b.whens], dtype=np.int32)
-    return CompiledComparisons(prog, wf, wn, wl, instrs, b.operands, b.literals, n_levels, names, list(b.columns))
+    return CompiledComparisons(prog, wf, wn, wl, instrs, b.operands, b.literals, n_levels, names, list(b.columns),
+                               dict(b.derived))
 
 
 # ---------------------------------------------------------------------------------------------

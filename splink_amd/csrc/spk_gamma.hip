@@ -1692,14 +1692,15 @@ static int settle_info(spk_ctx *ctx, bool *fixed) {
     }
     int64_t n_slow = 0, n_huge = 0, max_huge = 0;
     ctx->last_exact.assign((size_t)K, 0);
+    const bool carry = (int)ctx->exact_carry.size() == K;  // earlier windows of the same call
     for (int k = 0; k < K; ++k) {
-        ctx->last_exact[k] = ctx->h_info[K + k];
+        ctx->last_exact[k] = ctx->h_info[K + k] + (carry ? ctx->exact_carry[k] : 0);
         n_slow += h_slow[k];
         n_huge += h_slow[2 * K + k];
         max_huge = std::max<int64_t>(max_huge, h_slow[2 * K + k]);
     }
     ctx->last_xbase.assign(ctx->h_info, ctx->h_info + K);
-    ctx->last_deferred = n_slow;
+    ctx->last_deferred = n_slow + ctx->deferred_carry;
     if (n_huge) {  // cells with a string longer than SLOW_LIMIT units (none in the benchmark configs)
         Scratch S;
         DevBuf<uint8_t> scratch;
@@ -1871,11 +1872,16 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     uint8_t *base = ctx->prog_blob.p;
     auto at = [&](auto *&dst, size_t off) { dst = reinterpret_cast<std::remove_reference_t<decltype(dst)>>(base + off); };
     const int64_t P = ctx->n_pairs;
-    // the filter's work lists and the exact passes hold pair ordinals as int32
-    SPK_REQUIRE(P <= (int64_t)INT32_MAX, SPK_E_LIMIT,
-                "spk_gammas: more than 2^31-1 pairs in one context (shard the pair set over more ranks)");
+    // Ordinal windows: the filter's work lists and the exact / slow passes hold window-relative pair
+    // ordinals as int32 (and the filter walks them in uint32), so a pair set of more than ~2^31 pairs runs
+    // as consecutive windows of equal size.  Every window but the last is settled (list overflow, skipped
+    // slow lists, huge cells) before the next one reuses the lists; the last is left pending as usual.
+    const int64_t WMAX = ((int64_t)1 << 31) - ((int64_t)1 << 22);
+    const int64_t wcap = ctx->gamma_window > 0 ? std::min<int64_t>(ctx->gamma_window, WMAX) : WMAX;
+    const int64_t n_win = std::max<int64_t>(1, (P + wcap - 1) / wcap);
+    const int64_t W = n_win == 1 ? P : ((P + n_win - 1) / n_win + 63) / 64 * 64;  // pairs per window (the last: rest)
     // work lists only for the columns whose filter can leave cells undecided (a dictionary-id equality
-    // or numeric column never does): one slot of P pair indices each
+    // or numeric column never does): one slot of W pair indices each
     std::vector<int32_t> wslot(K, 0);
     int n_wslots = 0;
     for (int k = 0; k < K; ++k) {
@@ -1884,25 +1890,26 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             if (sc.k == k && (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids))) may = false;
         wslot[k] = may ? n_wslots++ : 0;
     }
-    SPK_TRY(ctx->work.alloc((size_t)std::max(n_wslots, 1) * (size_t)P + 1));
+    SPK_TRY(ctx->work.alloc((size_t)std::max(n_wslots, 1) * (size_t)W + 1));
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
     // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
     // 20 regions (256-thread workgroups) per CU: four rounds of the 5 resident workgroups a CU holds
     // at the filter's 96-VGPR cap, so the regions' uneven work evens out (measured best of 1280 ..
     // 20480 on MI355X: 5120 regions 1.76 ms vs 2048 regions 1.86 ms for the cfg2 pass)
     const int64_t max_regions = 20 * (int64_t)ctx->n_cu;
-    const int n_regions = (int)std::max<int64_t>(1, std::min<int64_t>(max_regions, (P + F_THREADS - 1) / F_THREADS));
-    const int64_t region_len = ((P + n_regions - 1) / n_regions + 63) / 64 * 64;
+    auto regions_of = [&](int64_t pw) {
+        return (int)std::max<int64_t>(1, std::min<int64_t>(max_regions, (pw + F_THREADS - 1) / F_THREADS));
+    };
+    const int n_regions_max = regions_of(W);
     // every (column, region) count is written by the filter launch that covers the region: no memset
-    SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions));
+    SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions_max));
     // One device info block, read back with one copy: xinfo (k_prefix: list bases and counts, overflow,
-    // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed here.
+    // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed per window.
     const int n_info = 2 * K + 2;
     const int n_cnt = (3 * K + 1) / 2;  // int64 slots of the 3K uint32 list lengths
     const int n_all = n_info + n_cnt + 2;  // + the error word and k_prefix's completion counter
     SPK_TRY(ctx->xinfo.alloc((size_t)n_all));
     SPK_TRY(ctx->pinned_info((size_t)n_all));
-    SPK_HIP(hipMemsetAsync(ctx->xinfo.p + n_info, 0, (size_t)(n_cnt + 2) * 8, ctx->stream));
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -1932,8 +1939,6 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     A.work = ctx->work.p;
     for (int k = 0; k < K; ++k) A.wslot[k] = wslot[k];
     A.region_count = ctx->region_count.p;
-    A.region_len = region_len;
-    A.n_regions = n_regions;
     A.slow_count = reinterpret_cast<unsigned int *>(ctx->xinfo.p + n_info);
     A.n_simple = (int)simple.size();
     A.n_complex = (int)complex_k.size();
@@ -1957,11 +1962,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     for (int k = 0; k < K; ++k)
         G.huge_in_slow[k] = (G.may_exact[k] && G.simple_of[k] >= 0 && simple[G.simple_of[k]].cls == SC_LEV) ? 1 : 0;
     G.K = K;
-    G.n_regions = n_regions;
     G.n_info = n_info;
     G.n_cnt = n_cnt;
     G.n_all = n_all;
-    G.g_exact = std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ctx->n_cu, (P + X_THREADS - 1) / X_THREADS));
     // every string a program can meet is a row of a loaded string column (UTF-8 bytes bound its UTF-16
     // units), a substring of one, or a literal: the huge pass's scratch per lane
     G.max_units = 1;
@@ -1969,13 +1972,15 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         for (const Column *c : t->cols)
             if (c && c->kind == COL_STR) G.max_units = std::max<int64_t>(G.max_units, c->max_bytes);
     for (int i = 0; i < n_lits; ++i) G.max_units = std::max<int64_t>(G.max_units, llen[i]);
-    SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions + 1)));
-    const int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(P, 1 << 16));
+    SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions_max + 1)));
 
+    ctx->exact_carry.clear();
+    ctx->deferred_carry = 0;
+    ctx->last_windows = n_win;
     SPK_TRY(ctx->begin(K_GAMMA));
     // row images and rule-view images: kernels only when a table, the column layout or the pairs changed
     ViewLaunch V{};
-    int64_t va = n_regions, vb = n_regions;  // regions over rule 1's view-ordered image: [va, vb)
+    bool have_view = false;
     ctx->last_view_regions = 0;
     if (P > 0) {
         SPK_TRY(build_images(ctx, t0, t1, A, img_stride, simple));
@@ -1984,37 +1989,72 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         // outgrows the caches: at 1M rows (80 MB, held by the 256 MB Infinity Cache) the second launch's
         // tail cost 4 % (1.41 vs 1.34 ms, cfg2); at 20M rows (1.6 GB) the view launch took the pass from
         // 31.1 to 22.8 ms (profiles/archive/r2_ab_views.log).
-        bool have_view = false;
         const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
         if ((ctx->use_views == 1 && big) || ctx->use_views == 2) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
-        if (have_view) {  // regions [i L, min((i + 1) L, P)) inside [V.lo, V.hi)
-            va = std::min<int64_t>(n_regions, (V.lo + region_len - 1) / region_len);
-            vb = V.hi >= P ? n_regions : std::min<int64_t>(n_regions, V.hi / region_len);
-            vb = std::max<int64_t>(va, vb);
-        }
-        ctx->last_view_regions = vb - va;
-        // the filter pass (the interpreter's columns add to the codes the template filter sets)
-        if (simple.empty())
-            SPK_HIP(hipMemsetAsync(ctx->codes.p, 0, (size_t)P * ctx->code_bytes, ctx->stream));
-        if (!simple.empty()) {
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, 0, va));
-            if (vb > va) {
-                GammaArgs VA = A;
-                VA.pl = ctx->pvl.p - ctx->pv_base;  // pl[p] = view position of pair p (p >= pv_base)
-                VA.pr = ctx->pvr.p - ctx->pv_base;
-                VA.img0 = V.img0;
-                VA.img1 = V.img1;
-                SPK_TRY(launch_template_filter(ctx->stream, VA, simple, va, vb));
-            }
-            SPK_TRY(launch_template_filter(ctx->stream, A, simple, vb, n_regions));
-        }
-        if (A.n_complex) {
-            k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(A);
-            SPK_HIP(hipGetLastError());
-        }
     }
-    G.A = A;
-    SPK_TRY(enqueue_phase(ctx, G, cap, /*skip=*/true));
+    for (int64_t w = 0; w < n_win; ++w) {
+        const int64_t b = w * W, Pw = std::min<int64_t>(W, P - b);
+        const int n_regions = regions_of(Pw);
+        const int64_t region_len = ((Pw + n_regions - 1) / n_regions + 63) / 64 * 64;
+        GammaArgs AW = A;  // the window [b, b + Pw) as a pair set of its own
+        AW.pl = ctx->pl.p + b;
+        AW.pr = ctx->pr.p + b;
+        AW.P = Pw;
+        AW.codes = ctx->codes.p + b * ctx->code_bytes;
+        AW.region_len = region_len;
+        AW.n_regions = n_regions;
+        std::vector<SimpleCol> sw = simple;  // implied ranges relative to the window
+        for (SimpleCol &sc : sw) {
+            sc.imp_lo = std::min<int64_t>(std::max<int64_t>(sc.imp_lo - b, 0), Pw);
+            sc.imp_hi = std::min<int64_t>(std::max<int64_t>(sc.imp_hi - b, 0), Pw);
+            if (sc.imp_hi <= sc.imp_lo) sc.imp_lo = sc.imp_hi = 0;
+        }
+        G.n_regions = n_regions;
+        G.g_exact = std::max<int64_t>(1, std::min<int64_t>(8 * (int64_t)ctx->n_cu, (Pw + X_THREADS - 1) / X_THREADS));
+        SPK_HIP(hipMemsetAsync(ctx->xinfo.p + n_info, 0, (size_t)(n_cnt + 2) * 8, ctx->stream));
+        int64_t va = n_regions, vb = n_regions;  // regions over rule 1's view-ordered image: [va, vb)
+        if (Pw > 0) {
+            if (have_view) {  // regions [i L, min((i + 1) L, Pw)) inside the window's part of [V.lo, V.hi)
+                const int64_t lo = std::min<int64_t>(std::max<int64_t>(V.lo - b, 0), Pw);
+                const int64_t hi = std::min<int64_t>(std::max<int64_t>(V.hi - b, 0), Pw);
+                va = std::min<int64_t>(n_regions, (lo + region_len - 1) / region_len);
+                vb = hi >= Pw ? n_regions : std::min<int64_t>(n_regions, hi / region_len);
+                vb = hi > lo ? std::max<int64_t>(va, vb) : va;
+            }
+            ctx->last_view_regions += vb - va;
+            // the filter pass (the interpreter's columns add to the codes the template filter sets)
+            if (sw.empty())
+                SPK_HIP(hipMemsetAsync(AW.codes, 0, (size_t)Pw * ctx->code_bytes, ctx->stream));
+            if (!sw.empty()) {
+                SPK_TRY(launch_template_filter(ctx->stream, AW, sw, 0, va));
+                if (vb > va) {
+                    GammaArgs VA = AW;
+                    VA.pl = ctx->pvl.p - ctx->pv_base + b;  // pl[p] = view position of pair b + p (>= pv_base)
+                    VA.pr = ctx->pvr.p - ctx->pv_base + b;
+                    VA.img0 = V.img0;
+                    VA.img1 = V.img1;
+                    SPK_TRY(launch_template_filter(ctx->stream, VA, sw, va, vb));
+                }
+                SPK_TRY(launch_template_filter(ctx->stream, AW, sw, vb, n_regions));
+            }
+            if (AW.n_complex) {
+                k_gamma_filter<<<(unsigned)n_regions, F_THREADS, 0, ctx->stream>>>(AW);
+                SPK_HIP(hipGetLastError());
+            }
+        }
+        G.A = AW;
+        const int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(Pw, 1 << 16));
+        SPK_TRY(enqueue_phase(ctx, G, cap, /*skip=*/true));
+        if (w + 1 == n_win) break;
+        // settle this window before the next one reuses the lists
+        SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+        ctx->gamma_pending = true;
+        ctx->codes_valid = true;
+        SPK_TRY(settle_info(ctx, nullptr));
+        ctx->exact_carry = ctx->last_exact;
+        ctx->deferred_carry = ctx->last_deferred;
+    }
     SPK_TRY(ctx->end(K_GAMMA));
     SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
@@ -2286,5 +2326,17 @@ extern "C" int spk_gammas_view_regions(spk_ctx *ctx, int64_t *out) {
 extern "C" int spk_gammas_simple_count(spk_ctx *ctx, int *out) {
     SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
     *out = ctx->last_simple;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs) {
+    SPK_REQUIRE(ctx && pairs >= 0, SPK_E_INVALID, "spk_gammas_set_window: bad args");
+    ctx->gamma_window = pairs;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_windows(spk_ctx *ctx, int64_t *out) {
+    SPK_REQUIRE(ctx && out, SPK_E_INVALID, "spk_gammas_windows: bad args");
+    *out = ctx->last_windows;
     return SPK_OK;
 }

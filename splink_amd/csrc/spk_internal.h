@@ -253,6 +253,13 @@ struct spk_ctx {
                                       // image outgrows the caches, 2 always (tests)
     int64_t last_view_regions = 0;    // filter regions the last spk_gammas ran as a view launch
     int last_simple = 0;
+    // ordinal windows: spk_gammas runs the filter / exact / slow passes over windows of at most this many
+    // pairs (0: the default, just under 2^31 -- the work lists hold window-relative int32 ordinals); each
+    // window but the last is settled before the next one reuses the lists
+    int64_t gamma_window = 0;
+    int64_t last_windows = 0;             // windows the last spk_gammas ran
+    std::vector<int64_t> exact_carry;     // exact-pass cells of the windows settled before the last one
+    int64_t deferred_carry = 0;           // their slow-list cells
 
     // comparison-vector work buffers (reused across calls)
     spk::DevBuf<int32_t> work;

@@ -110,6 +110,7 @@ class Job:
         self.schema = Schema(forms)
         self._col_index = {}
         self._raw = {}
+        self._next_raw = 0  # raw-column ids only go up: a released id is never handed out again
         for side, t in enumerate(self.inputs):
             self.ctx.table_create(side, len(t), 8)
         self.n_pairs = 0
@@ -165,7 +166,12 @@ class Job:
         return self._host_cols[key]
 
     def _new_raw(self) -> int:
-        return len(self._raw)
+        """A fresh raw-column index.  Released columns leave _raw (release_raw_strings), so len(_raw) could
+        name an index a live column still holds (spk_raw_* replaces whatever is there): ids come from a
+        counter instead."""
+        rid = self._next_raw
+        self._next_raw += 1
+        return rid
 
     def raw_utf8(self, side: int, name: str) -> int:
         """Raw string column (input row order) on the device, uploaded once.  Arrow columns hand over their
@@ -263,6 +269,21 @@ class Job:
                 self.ctx.table_add_float64(side, idx, vals, valid)
         self._col_index[key] = idx
         return idx
+
+    def add_derived(self, name: str, node):
+        """A derived column (derived.py: a Spark built-in over one record's columns in a case_expression),
+        evaluated once per row of each input table at ingest and added to the inputs under its canonical
+        name, so it goes to the device and into the comparison programs like an input column."""
+        from . import derived as D
+        sides = [0, 1] if self.link_type == "link_only" else [0]
+        form = D.form_of(node, self.schema.form)
+        for side in sides:
+            if name in self.inputs[side].columns:
+                continue
+            self.inputs[side][name] = D.evaluate(node, self.inputs[side], form)
+            self._views.pop(side, None)
+        self.schema.forms[name] = form
+        self.schema._lower[name.lower()] = name
 
     # ---- blocking ----------------------------------------------------------------------------------
     def _key_values(self, t: pd.DataFrame, kexpr):
@@ -373,6 +394,8 @@ class Job:
         cache = self.__dict__.setdefault("_prog_cache", {})
         if key not in cache:
             prog = compile_comparisons(settings, self.schema)
+            for name, node in prog.derived.items():
+                self.add_derived(name, node)
             index = {k: self.column_index(*k) for k in prog.columns}
             lit_off, lit_bytes = prog.literal_buffers()
             args = N.Context.gammas_args(prog.programs, prog.when_first, prog.when_n, prog.when_level, prog.instrs,

@@ -15,7 +15,7 @@ Grammar (precedence low -> high):
     mul      := unary ((* | / | %) unary)*
     unary    := - unary | primary
     primary  := number | 'string' | TRUE | FALSE | NULL | CASE ... END
-              | name ( args ) | name[.name] | ( expr )
+              | CAST ( expr AS type ) | name ( args ) | name[.name] | ( expr )
 """
 from __future__ import annotations
 
@@ -220,6 +220,14 @@ class _Parser:
             self.expect("op", ")")
             return e
         if kind == "id":
+            if val.lower() == "cast" and self.peek()[0] == "op" and self.peek()[1] == "(":
+                # CAST(expr AS type): Func("cast", (expr, Lit(type)))
+                self.take()
+                e = self.parse_expr()
+                self.expect("kw", "as")
+                typ = self.expect("id")[1].lower()
+                self.expect("op", ")")
+                return Func("cast", (e, Lit(typ)))
             if self.accept("op", "("):
                 args = []
                 if not self.accept("op", ")"):

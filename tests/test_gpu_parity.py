@@ -610,6 +610,21 @@ def test_em_histogram_kernels_agree(amd, n_levels):
         ctx.em_set_lane_histogram(mode)
         stats.append(ctx.em_iteration(lam, 1.0 - lam, m, u, n_stats))
     assert np.array_equal(stats[0], stats[1])
+    # ... and equal to the per-pair oracle: with fewer than 64 lane copies (>= 641 patterns) k_em_iter counts
+    # the most frequent pattern as P minus every other bin, so a stray or missing code would shift counts into
+    # it; P is odd, past the last 16-byte vector
+    ms, us, at = [], [], 0
+    for L in n_levels:
+        ms.append(m[at:at + L])
+        us.append(u[at:at + L])
+        at += L
+    want = orc.em_stats(g, n_levels, lam, ms, us)
+    got = stats[0]
+    assert got[1] == want[1] == P and got[2] == want[2]
+    assert np.allclose(got[[0]], want[[0]], rtol=1e-12, atol=0)
+    assert np.array_equal(got[5::4], want[3::4]) and np.array_equal(got[6::4], want[4::4])  # counts
+    assert np.allclose(got[7::4], want[5::4], rtol=1e-11, atol=1e-300)
+    assert np.allclose(got[8::4], want[6::4], rtol=1e-11, atol=1e-300)
 
 
 def _mutate(rng, s, k, alpha):

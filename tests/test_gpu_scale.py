@@ -168,24 +168,91 @@ def check_shard(job, params, cols, iters, sample=2_000_000):
     return mp, l, r
 
 
-def test_cfg4_shard_full_size(amd, heartbeat):
+def check_shard_streamed(job, params, cols, iters, sample=2_000_000, chunk=1 << 27):
+    """check_shard for a pair set too large to hold on the host a few times over (more than 2^31 pairs):
+    the comparison vectors are read back chunk by chunk.  A strided sample of `sample` pairs is bit-exact
+    against oracle.template_gammas; the oracle's pattern histogram of every pair's comparison vector
+    (oracle.pattern_codes: the γ columns as the device decodes them, counted on the host) drives
+    `iters` EM iterations of oracle.em_iterate_hist, checked against the device at 1e-9 after every
+    M-step; every pair's match_probability is checked against the oracle's mp of its comparison vector."""
+    from splink_amd.engine import m_step_rows
+    specs = SPECS[:len(cols)]
+    names, nlev = job.code_meta
+    K, P = len(names), job.n_pairs
+    step = max(1, P // sample)
+    hist = np.zeros(int(np.prod([L + 1 for L in nlev])), dtype=np.int64)
+    sl, sr, sg = [], [], []
+    for c0 in range(0, P, chunk):
+        n = min(chunk, P - c0)
+        g = job.ctx.gammas_copy(K, c0, n)
+        orc.pattern_codes(g, nlev, hist, want_codes=False)
+        loc = np.arange((-c0) % step, n, step)  # global ordinals k * step
+        l, r = job.ctx.pairs_copy(c0, n)
+        sl.append(l[loc])
+        sr.append(r[loc])
+        sg.append(g[loc])
+        del g, l, r
+    assert int(hist.sum()) == P
+    sl, sr, sg = np.concatenate(sl), np.concatenate(sr), np.concatenate(sg)
+    assert len(sl) == (P + step - 1) // step
+    rows, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
+    sub = rows_of(job, 0, rows)
+    ocols = [orc.StrCol(sub[c].tolist()) for c in cols]
+    ref = orc.template_gammas(specs, ocols, ocols, inv[:len(sl)].astype(np.int32), inv[len(sl):].astype(np.int32))
+    del ocols, sub
+    bad = np.nonzero((sg != ref).any(axis=1))[0]
+    assert len(bad) == 0, (len(bad), bad[:5] * step)
+    lam0, lp0 = params.params["λ"], params._level_probabilities()
+    hist_o, mpat_o = orc.em_iterate_hist(hist, nlev, lam0, [m for m, _ in lp0], [u for _, u in lp0], iters, 1e-300)
+    assert len(hist_o) == iters
+    for lam_o, m_o, u_o in hist_o:
+        stats = job.em_stats(params.params["λ"], params._level_probabilities())
+        new_lambda, rows_ = m_step_rows(stats, names, nlev)
+        params._update_params(new_lambda, rows_)
+        assert rel_close(params.params["λ"], lam_o)
+        for k, (m, u) in enumerate(params._level_probabilities()):
+            assert all(rel_close(a, b) for a, b in zip(m, m_o[k])), (k, m, m_o[k])
+            assert all(rel_close(a, b) for a, b in zip(u, u_o[k])), (k, u, u_o[k])
+    lam = params.params["λ"]
+    m_t, u_t = job.flat_tables(params._level_probabilities())
+    for c0 in range(0, P, chunk):
+        n = min(chunk, P - c0)
+        mp = job.ctx.score(float(lam), float(1 - lam), m_t, u_t, c0, n)
+        want = mpat_o[orc.pattern_codes(job.ctx.gammas_copy(K, c0, n), nlev)]
+        assert np.allclose(mp, want, rtol=1e-9, atol=0, equal_nan=True), c0
+
+
+@pytest.fixture(scope="module")
+def cfg4_records():
+    from splink_amd.synthetic import make_records
+    return make_records(20_000_000, surname_vocab=300_000, arrow=True)[["unique_id"] + COLS]
+
+
+@pytest.mark.parametrize("shard", [(0, 8), (0, 2)], ids=["0of8", "0of2"])
+def test_cfg4_shard_full_size(amd, heartbeat, cfg4_records, shard):
     """BASELINE configs[3] at one GPU's share: a 20M-record dedupe (blocking surname | dob: 6.2e9 candidate
-    ordinals, past 2^31) whose ordinal space is split over 8 GPUs; this process is rank 0 and generates only
-    its slice (~770M pairs), as each rank of the 8-GPU job does (blocking.py:95-160, int64 ordinals).  A
-    strided sample of 2M comparison vectors is bit-exact against oracle.template_gammas, and 10 EM
-    iterations of λ / m / u plus every pair's match_probability agree with oracle.em_iterate at 1e-9."""
+    ordinals, past 2^31) whose ordinal space is split over 8 (or 2) GPUs; this process is rank 0 and
+    generates only its slice, as each rank of the multi-GPU job does (blocking.py:95-160, int64 ordinals).
+    0of8: ~770M pairs; a strided sample of 2M comparison vectors is bit-exact against
+    oracle.template_gammas, and 10 EM iterations of λ / m / u plus every pair's match_probability agree
+    with oracle.em_iterate at 1e-9.  0of2: ~3.1e9 pairs in ONE context (the 2-GPU split of BASELINE's
+    "2/4/8 GPUs"), past 2^31, so the comparison pass runs as ordinal windows (spk_gammas_windows >= 2);
+    checked by check_shard_streamed (the same sample, the oracle's EM on the host-counted pattern
+    histogram of every pair, every match_probability)."""
     from splink_amd.engine import Job
     from splink_amd.params import Params
-    from splink_amd.synthetic import cfg_settings, make_records
-    df = make_records(20_000_000, surname_vocab=300_000, arrow=True)[["unique_id"] + COLS]
+    from splink_amd.synthetic import cfg_settings
     params = Params(cfg_settings(4, max_iterations=10), amd)
     st = params.settings
-    job = Job("dedupe_only", [df], "unique_id", 0, shard=(0, 8))
-    del df
+    job = Job("dedupe_only", [cfg4_records], "unique_id", 0, shard=shard)
     job.block(st["blocking_rules"])
     assert job.n_candidates > 2 ** 31 and job.n_pairs > 500_000_000
     job.gammas(st)
-    check_shard(job, params, COLS, 10)
+    if shard[1] == 8:
+        check_shard(job, params, COLS, 10)
+        return
+    assert job.n_pairs > 2 ** 31 and job.ctx.gammas_windows() >= 2
+    check_shard_streamed(job, params, COLS, 10)
 
 
 CFG5_RULES = ["l.surname = r.surname", "l.dob = r.dob and l.city = r.city"]

@@ -1,0 +1,147 @@
+"""Ordinal windows of spk_gammas and other regressions of the context's bookkeeping (through the C ABI).
+
+The reference joins and projects any number of pairs (blocking.py:95-160, gammas.py:65-89); the device
+pass runs a pair set of more than ~2^31 pairs as consecutive ordinal windows (include/splink_hip.h,
+spk_gammas_set_window).  Here the window is forced small so that many windows run over a few million
+pairs, and every comparison vector must equal the one-window pass and the oracle: windows that split a
+blocking rule, the implied-level ranges, the rule-1 view launch, the interpreter path and a link_only job.
+The pass over more than 2^31 real pairs is tests/test_gpu_scale.py::test_cfg4_shard_full_size[0of2].
+"""
+import numpy as np
+import pytest
+
+import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+COLS = ["first_name", "surname", "dob", "city", "email"]
+SPECS = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3])]
+
+
+@pytest.fixture(scope="module")
+def amd():
+    from splink_amd import AmdSession, _native
+    if _native.device_count() == 0:
+        pytest.fail("no HIP device visible: the -m gpu tests need an MI355X")
+    return AmdSession(0)
+
+
+def _records(n, seed):
+    from splink_amd.synthetic import make_records
+    return make_records(n, seed=seed, surname_vocab=max(n // 40, 50), first_vocab=300,
+                        city_vocab=60)[["unique_id"] + COLS]
+
+
+@pytest.fixture(scope="module")
+def dedupe_job(amd):
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import cfg_settings
+    st = complete_settings_dict(cfg_settings(2), amd)
+    job = Job("dedupe_only", [_records(60000, 41)], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    ref = job.gammas_host()
+    table = job.tables[0]
+    l, r = job.pair_rows()
+    cols = [orc.StrCol(table[c].tolist()) for c in COLS]
+    assert (ref == orc.template_gammas(SPECS, cols, cols, l, r)).all()
+    return job, st, ref
+
+
+@pytest.mark.parametrize("size", ["tiny", "odd", "fifth"])
+@pytest.mark.parametrize("mode", [1, 21, 0])  # filter, filter + forced rule-1 view launch, interpreter
+def test_windows_give_identical_codes(dedupe_job, size, mode):
+    job, st, ref = dedupe_job
+    P = job.n_pairs
+    window = {"tiny": 1000, "odd": 4096 + 17, "fifth": P // 5 + 1}[size]
+    assert P > 4 * window  # several windows, and rule 1's pairs start inside one of them
+    job.ctx.gammas_set_simple(mode)
+    job.ctx.gammas_set_window(0)
+    job.gammas(st)
+    one = job.gammas_host()
+    exact_one = job.ctx.gammas_exact_counts(len(COLS))
+    job.ctx.gammas_set_window(window)
+    try:
+        job.gammas(st)
+        got = job.gammas_host()
+        n_win = job.ctx.gammas_windows()
+        exact = job.ctx.gammas_exact_counts(len(COLS))
+        # the E+M launch over codes written window by window
+        lam, m, u = 0.2, [], []
+        for L in job.code_meta[1]:
+            pm = np.linspace(1.0, 3.0, L)
+            m += list(pm / pm.sum())
+            u += list(pm[::-1] / pm.sum())
+        n_stats = 5 + 4 * sum(L + 1 for L in job.code_meta[1])
+        stats_w = job.ctx.em_iteration(lam, 1 - lam, m, u, n_stats)
+    finally:
+        job.ctx.gammas_set_window(0)
+        job.ctx.gammas_set_simple(1)
+    assert n_win == -(-P // window) and n_win >= 4
+    assert (one == ref).all() and (got == ref).all(), np.nonzero((got != ref).any(axis=1))[0][:10]
+    assert exact == exact_one  # the filter decides each cell alone: the same cells reach the exact passes
+    job.gammas(st)
+    stats_1 = job.ctx.em_iteration(lam, 1 - lam, m, u, n_stats)
+    assert np.array_equal(stats_w, stats_1)
+
+
+def test_windows_link_only(amd):
+    """link_only (two tables, asymmetric sides) with three rules, windows of 3000 pairs."""
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import cfg_settings
+    df = _records(30000, 43)
+    st = cfg_settings(2)
+    st["link_type"] = "link_only"
+    st["blocking_rules"] = ["l.surname = r.surname", "l.dob = r.dob", "l.email = r.email"]
+    st = complete_settings_dict(st, amd)
+    inputs = [df.iloc[:15000].reset_index(drop=True), df.iloc[15000:].reset_index(drop=True)]
+    job = Job("link_only", inputs, "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.ctx.gammas_set_window(3000)
+    try:
+        job.gammas(st)
+        got = job.gammas_host()
+        assert job.ctx.gammas_windows() >= 4
+    finally:
+        job.ctx.gammas_set_window(0)
+    l, r = job.pair_rows()
+    tl, tr = job.tables[0], job.r_table()
+    ref = orc.template_gammas(SPECS, [orc.StrCol(tl[c].tolist()) for c in COLS],
+                              [orc.StrCol(tr[c].tolist()) for c in COLS], l, r)
+    assert (got == ref).all()
+
+
+def test_new_column_after_raw_release(amd):
+    """gammas() releases the raw string columns; a later upload (a new comparison column, a
+    new blocking pass) must get a fresh raw id, never one a live raw column (uid, numeric or host key)
+    still holds.  Re-blocking on the same job and adding a comparison column both stay oracle-exact."""
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import _lev3, cfg_settings
+    df = _records(8000, 47)
+    df["email2"] = df["email"]
+    st = complete_settings_dict(cfg_settings(2), amd)
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    # a host-keyed rule (lower()) uploads an int64 key column next to the uid and the string columns
+    rules = ["lower(l.surname) = lower(r.surname)", "l.dob = r.dob"]
+    job.block(rules)
+    job.gammas(st)  # releases the raw string columns
+    st2 = complete_settings_dict(cfg_settings(2), amd)
+    st2["comparison_columns"].append({"col_name": "email2", "num_levels": 3, "case_expression": _lev3("email2")})
+    st2 = complete_settings_dict(st2, amd)
+    job.gammas(st2)  # a new string column: new raw ids after the released ones
+    job.block(rules)  # re-block: the key and uid columns must still be the ones uploaded
+    job.gammas(st2)
+    got = job.gammas_host()
+    table = job.tables[0]
+    l, r = job.pair_rows()
+    cols = [orc.StrCol(table[c].tolist()) for c in COLS + ["email2"]]
+    specs = SPECS + [("lev", 3, [0.3])]
+    assert (got == orc.template_gammas(specs, cols, cols, l, r)).all()
+    sn = table["surname"].str.lower().to_numpy()
+    dob = table["dob"].to_numpy()
+    uid = table["unique_id"].to_numpy()
+    ok = ((sn[l] == sn[r]) & (table["surname"].notna().to_numpy()[l])) | (dob[l] == dob[r])
+    assert ok.all() and (uid[l] < uid[r]).all()

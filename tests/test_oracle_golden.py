@@ -197,3 +197,28 @@ def test_edge_cases(case):
         assert len(lls) == len(g["log_likelihood"])
         for a, b in zip(lls, g["log_likelihood"]):
             assert rel_close(a, b), (a, b)
+
+
+def test_histogram_em_equals_per_pair_em():
+    """oracle.em_iterate_hist (the EM check of the >2^31-pair GPU test: the pattern histogram of every
+    pair's comparison vector) gives the per-pair oracle's λ / m / u and match probabilities, NULL levels
+    and unobserved patterns included."""
+    rng = np.random.Generator(np.random.PCG64(3))
+    nlev = [3, 3, 2, 2, 3]
+    P = 300_001
+    gam = np.stack([np.where(rng.random(P) < 0.6, 0, rng.integers(-1, L, P)) for L in nlev], 1).astype(np.int8)
+    lam = 0.05
+    m = [[0.1, 0.2, 0.7], [0.1, 0.3, 0.6], [0.2, 0.8], [0.3, 0.7], [0.05, 0.15, 0.8]]
+    u = [[0.8, 0.15, 0.05], [0.7, 0.2, 0.1], [0.9, 0.1], [0.85, 0.15], [0.9, 0.08, 0.02]]
+    h1, mp1 = orc.em_iterate(gam, nlev, lam, m, u, 6, 1e-300)
+    hist = np.zeros(int(np.prod([L + 1 for L in nlev])), dtype=np.int64)
+    codes = orc.pattern_codes(gam[:P // 2], nlev, hist)  # two chunks accumulate into one histogram
+    codes = np.concatenate([codes, orc.pattern_codes(gam[P // 2:], nlev, hist)])
+    assert hist.sum() == P and (np.bincount(codes, minlength=len(hist)) == hist).all()
+    h2, mpat = orc.em_iterate_hist(hist, nlev, lam, m, u, 6, 1e-300)
+    assert len(h1) == len(h2) == 6
+    for (l1, m1, u1), (l2, m2, u2) in zip(h1, h2):
+        assert rel_close(l1, l2)
+        for a, b in zip(sum(m1, []) + sum(u1, []), sum(m2, []) + sum(u2, [])):
+            assert rel_close(a, b)
+    assert np.allclose(mp1, mpat[codes], rtol=1e-12, atol=0, equal_nan=True)
