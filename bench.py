@@ -40,6 +40,9 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r4_pmc_kernels.json")
 COLS = ["first_name", "surname", "dob", "city", "email"]
 WORKLOADS = {2: "cfg2: synthetic person-record dedupe, 1M x sqrt(N) records, blocking surname|dob, "
                 "5 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3)",
+             4: "cfg4: synthetic person-record dedupe of 20M records (fixed: strong scaling), blocking surname|dob "
+                "(~6.2e9 candidate pairs, BASELINE.md cfg4 note), 5 comparison columns (JW-3 x2, exact-2 x2, "
+                "Levenshtein-3), pair ordinals sharded over the ranks",
              5: "cfg5 columns at cfg2 size: synthetic person-record dedupe, 1M x sqrt(N) records, blocking "
                 "surname|dob, 6 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3, free-text address "
                 "30-128 chars Levenshtein-4)"}
@@ -55,8 +58,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--records", type=int, default=1_000_000, help="records at N=1 (scaled by sqrt(N))")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
-                    help="2: the headline workload; 5: + free-text address Levenshtein-4 (cfg5's columns at cfg2's size)")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
+                    help="2: the headline workload; 4: BASELINE configs[3], a 20M-record dedupe sharded over the "
+                         "ranks (strong scaling); 5: + free-text address Levenshtein-4 (cfg5's columns at cfg2's size)")
+    ap.add_argument("--share", type=str, default=None,
+                    help="k/n: run rank k's share of an n-rank job on this one GPU (e.g. --config 4 --share 0/8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--em-scale", type=int, default=8,
@@ -81,19 +87,30 @@ def main():
     from splink_amd.session import AmdSession
     from splink_amd.synthetic import cfg_settings, make_records
 
-    n_records = int(round(args.records * math.sqrt(world)))
+    shard = (rank, world)
+    if args.share:
+        k, n = (int(x) for x in args.share.split("/"))
+        assert world == 1 and 0 <= k < n, "--share runs one rank's share on one GPU"
+        shard = (k, n)
     t0 = time.time()
     cols = COLS + (["address"] if args.config == 5 else [])
-    # Arrow-backed string columns: the columnar form a Spark / Arrow source hands over (values identical
-    # to the object-column records; spk_raw_utf8 takes their buffers without a per-row pass)
-    df = make_records(n_records, surname_vocab=15000, with_address=args.config == 5, arrow=True)[["unique_id"] + cols]
+    if args.config == 4:
+        # the job's size does not grow with N: its ordinal space is split over the ranks (strong scaling)
+        from splink_amd.synthetic import make_records_parallel
+        n_records = 20_000_000
+        df = make_records_parallel(n_records, 16, 16, surname_vocab=300_000)[["unique_id"] + cols]
+    else:
+        n_records = int(round(args.records * math.sqrt(world)))
+        # Arrow-backed string columns: the columnar form a Spark / Arrow source hands over (values identical
+        # to the object-column records; spk_raw_utf8 takes their buffers without a per-row pass)
+        df = make_records(n_records, surname_vocab=15000, with_address=args.config == 5, arrow=True)[["unique_id"] + cols]
     log(f"[rank {rank}] generated {n_records} records in {time.time() - t0:.1f}s")
 
     settings = cfg_settings(args.config, max_iterations=10)
     params = Params(settings, AmdSession(local))
     st = params.settings
 
-    job = Job("dedupe_only", [df], "unique_id", local, shard=(rank, world))
+    job = Job("dedupe_only", [df], "unique_id", local, shard=shard)
     job.ctx.enable_timing(True)
     t0 = time.time()
     job.block(st["blocking_rules"])
@@ -251,10 +268,11 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(job, df, st, args.cpu_seconds, cols)
 
-    rates = string_rates(job, st, local_pairs, g_ms) if world == 1 else None
+    # (cfg4: billions of pairs per GPU -- already the scale of the E/M row, and too many to copy to the host)
+    rates = string_rates(job, st, local_pairs, g_ms) if (world == 1 and args.config != 4) else None
 
     em_scale = None
-    if world == 1 and args.em_scale > 0:
+    if world == 1 and args.em_scale > 0 and args.config != 4:
         em_scale = em_streaming(job, names, nlev, params, args.em_scale)
 
     out = {
@@ -266,12 +284,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == 4 else "weak",
         "vs_baseline": None,
         "dtype": "fp64",
         "data": "synthetic",
         "config": {"workload": WORKLOADS[args.config],
                    "records": n_records, "candidate_pairs": total_pairs, "comparison_columns": len(cols),
+                   "candidate_ordinals_total": job.n_candidates, "shard": list(shard),
+                   "comparison_windows": job.ctx.gammas_windows(),
                    "parallelism": f"pair-ordinal shards x{world}, RCCL all-reduce of pattern histogram"},
         "roofline": roofline,
         "roofline_em": em_roofline,
@@ -437,7 +457,8 @@ def cpu_baseline(job, df, st, seconds, col_names):
     import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    l, r = job.pair_rows()
+    n_max = min(job.n_pairs, 50_000_000)
+    l, r = job.ctx.pairs_copy(0, n_max)  # a prefix of the pairs is all the sample needs
     t = job.tables[0]  # pair rows index the job's (blocking-key clustered) table
     cols = [orc.StrCol(t[c].tolist()) for c in col_names]
     specs = [("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88]), ("eq", 2, []), ("eq", 2, []), ("lev", 3, [0.3]),

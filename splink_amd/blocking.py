@@ -41,10 +41,28 @@ def _tables(settings, df_l, df_r, df):
 
 
 def _block(settings, spark, df_l, df_r, df, rules):
-    job = Job(settings["link_type"], _tables(settings, df_l, df_r, df), settings["unique_id_column_name"],
-              session_device(spark), shard=distributed_shard())
+    tables = _tables(settings, df_l, df_r, df)
+    # comparison-only string columns start their upload at once, behind the unique-id ranks and the blocking
+    # work (Job.prefetch_strings)
+    job = Job(settings["link_type"], tables, settings["unique_id_column_name"], session_device(spark),
+              shard=distributed_shard(), prefetch=_comparison_only_columns(settings, rules, tables[0].columns))
     job.block(list(rules))
     return ComparisonFrame(job, settings)
+
+
+def _comparison_only_columns(settings, rules, columns):
+    """Input columns the comparison columns read that no blocking rule mentions (those are uploaded by the
+    blocking pass itself, which must not wait behind a prefetch)."""
+    import re
+    used = set(re.findall(r"[a-z_][a-z_0-9]*", " ".join(rules).lower()))
+    by_lower = {str(c).lower(): c for c in columns}
+    out = []
+    for c in settings["comparison_columns"]:
+        for name in ([c["col_name"]] if "col_name" in c else []) + list(c.get("custom_columns_used", [])):
+            canon = by_lower.get(str(name).lower())
+            if canon is not None and canon.lower() not in used and canon not in out:
+                out.append(canon)
+    return out
 
 
 @check_types

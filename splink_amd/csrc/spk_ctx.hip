@@ -432,6 +432,7 @@ int spk_table_add_utf8(spk_ctx *ctx, int side, int col, const int64_t *offsets, 
     if (nbytes) SPK_HIP(hipMemcpyAsync(d_bytes.p, data, (size_t)nbytes, hipMemcpyHostToDevice, ctx->stream));
     if (n) SPK_HIP(hipMemcpyAsync(d_valid.p, valid, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
     SPK_HIP(hipMemsetAsync(c->units.p, 0, (size_t)(nbytes + 3 * n + 16) * 2, ctx->stream));
+    c->units_len = nbytes + 3 * n + 16;
     SPK_HIP(hipMemcpyAsync(d_off8.p, offsets, (size_t)(n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
     if (n) {
         int bs = 256;

@@ -85,31 +85,27 @@ __global__ __launch_bounds__(H_THREADS) void k_hist(const CodeT *__restrict__ co
     }
 }
 
-// Histogram with lane-private LDS counters, for pattern spaces with n_pat x 4 copies x 4 B <= 80 KiB.  Counter
-// (bin, copy) lives at word bin * R + copy with copy = lane % R, R = 64 / 32 / 16 / 8 / 4 copies:
-// with R = 64 every lane of a wave hits its own bank (64 x 4-byte banks) whatever the codes are, so
-// one code costs one conflict-free `ds_add_u32` and a couple of VALU ops -- no ballots, no
-// serialisation on the few dominant patterns.  Smaller R (larger pattern spaces) admits at most
-// 64 / R lanes per bank.  Waves of a workgroup share the copies (atomics; different instructions
-// never bank-conflict).  Codes are streamed as 16-byte vectors, four loads in flight per lane.
+// Histogram with lane-private LDS counters.  Counter (bin, copy) lives at word bin * R + copy with copy =
+// lane % R, R = 64 / 32 / 16 / 8 / 4 copies: with R = 64 every lane of a wave hits its own bank (64 x
+// 4-byte banks) whatever the codes are, so one code costs one conflict-free `ds_add_u32` and a couple of
+// VALU ops -- no ballots, no serialisation on the few dominant patterns.  Smaller R (larger pattern spaces)
+// admits 64 / R lanes per counter, and equal codes among them serialise on it.  Waves of a workgroup
+// share the copies (atomics; different instructions never bank-conflict).  Codes are streamed as 16-byte
+// vectors, four loads in flight per lane.
+//
+// Two tiers (R < 64, when the LDS left over holds them): the EM_TIER most frequent patterns of the pair set
+// (found by the launch that first counts it) get 64 lane-private copies each, every other pattern its R
+// copies; an LDS map (pattern -> first counter word, one uint16 per pattern) sends each code to its
+// counters.  Candidate pairs are mostly non-matches sharing a few hundred patterns, so nearly every code
+// lands on a conflict-free counter while the pattern space stays in LDS (cfg5: 2,880 patterns, R = 8,
+// 256 hot patterns x 64 copies + 2,880 x 8 = 153 KiB).  Any map counts exactly; it only decides which
+// counters a code uses.
 constexpr int HL_THREADS = 1024;
 constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS (gfx950), capped by the device attribute
+constexpr int HL_STATIC_LDS = 2048;       // k_em_iter's static LDS (finalize scratch), kept out of the plan
 constexpr int HL_UNROLL = 4;
-constexpr int EM_GROUP = 16;  // k_em_iter's first reduction level: workgroups per group
-#ifndef SPK_EM_NHOT
-#define SPK_EM_NHOT 1  // cfg5 at 368 M pairs: 1 -> 0.65 of HBM peak, 2 -> 0.58, 3 -> 0.43, 4 -> 0.33 (profiles/r4_ab_em_nhot_cfg5.log)
-#endif
-constexpr int EM_NHOT = SPK_EM_NHOT;  // patterns k_em_iter counts in registers
-#ifndef SPK_EM_AROWS
-#define SPK_EM_AROWS 4
-#endif
-constexpr int EM_AROWS = SPK_EM_AROWS;  // the one-level reduction's rows
-#ifndef SPK_EM_PRE
-#define SPK_EM_PRE 1  // 1: workgroup 0 evaluates the E-step per pattern during the streaming (A/B)
-#endif
-#ifndef SPK_EM_ATOMIC_ROW
-#define SPK_EM_ATOMIC_ROW 1  // 1: one-level reduction through agent-scope atomics into one row (A/B)
-#endif
+constexpr int EM_TIER = 256;              // hot patterns at most (64 copies each)
+constexpr int EM_AROWS = 4;               // the one-level reduction's rows (workgroup mod EM_AROWS)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -301,14 +297,11 @@ __device__ void em_finalize_block(const PatArgs &A, Count count, double *__restr
     // round trips.  Deterministic: the same tree whatever the counts.
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n_waves = blockDim.x >> 6;
     const int half = lane >> 5, l32 = lane & 31;
-#ifndef SPK_EM_TOTALS_WAVES
-#define SPK_EM_TOTALS_WAVES 1
-#endif
     // The totals slot (0) sums every pattern, the column slots a 1 / radix share: with spare waves (slots
     // 1 .. n_slots two per wave) the totals are split over them -- a strided share per wave, a 64-lane
     // fixed tree, the waves' partials added in wave order -- instead of 32 lanes walking the whole table.
     const int col_waves = (A.n_slots + 1) / 2, spare = n_waves - col_waves;
-    const bool split = SPK_EM_TOTALS_WAVES && spare >= 2;  // block-uniform
+    const bool split = spare >= 2;  // block-uniform
     __shared__ double s_tot[16][6];
     if (split && wave >= col_waves) {
         const int sw = wave - col_waves;
@@ -446,32 +439,35 @@ __global__ __launch_bounds__(EF_THREADS) void k_em_finalize(PatArgs A0, const un
     em_finalize_block(A, [&](int p) { return hist[p]; }, mpat, llpat, cpat, out, s_tab);
 }
 
-// Histogram of the codes with lane-private LDS counters (as k_hist_lanes); each workgroup writes its
-// counts as one row of `part` (plain whole-line stores; device-scope atomics into one histogram cost
-// 15-25 us per cfg2 iteration: every workgroup's adds to a bin serialise at the memory side).  The
-// workgroup that finishes last (device-scope ticket, release / acquire fences) sums the rows in a fixed
-// order -- exact integers -- and either (FIN) runs the E-step and M-step sums, one launch per EM
-// iteration, or writes the plain histogram to out_hist (multi-GPU: the caller all-reduces it).
+// One EM iteration (FIN) or one histogram (!FIN) over the codes with the lane-private counters above.  Each
+// workgroup sums its counters per pattern and adds them into one of EM_AROWS global rows with agent-scope
+// integer atomics (exact, so their order does not matter), drains them and takes a ticket; the last one sums
+// the rows in row order, zeroes them for the next launch, and either (FIN) runs the E-step and the M-step sums
+// -- one launch per EM iteration -- or writes the plain histogram to out_hist (multi-GPU: the caller
+// all-reduces it).  Workgroup 0 of a FIN launch streams nothing: it evaluates mp and ln(...) per pattern from
+// the parameters while the others stream (published with its ticket), so the finishing workgroup only runs
+// the M-step sums.  TIER: the two-tier counters, with the map gmap (pattern -> first counter word; hot
+// patterns [0, hb) in 64-copy slots, the others at hb + p * R); `refresh` makes the last workgroup rank the
+// patterns by count and write the map the next launches use.
 __host__ __device__ inline int64_t part_stride(int64_t n_pat) { return (n_pat + 31) / 32 * 32; }  // whole 128-B lines
-template <typename CodeT, int R, bool FIN>
+template <typename CodeT, int R, bool FIN, bool TIER>
 __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict__ codes, int64_t P, PatArgs A0,
-                                                        uint32_t *__restrict__ part,
                                                         unsigned int *__restrict__ ticket, double *__restrict__ mpat,
                                                         double *__restrict__ llpat, double *__restrict__ cpat,
                                                         double *__restrict__ out, unsigned long long *__restrict__ out_hist,
                                                         int fence, uint32_t *__restrict__ arow,
-                                                        int32_t *__restrict__ hot, int refresh) {
+                                                        uint16_t *__restrict__ gmap, int32_t *__restrict__ ghot, int hb,
+                                                        int refresh, int lds_bytes) {
     extern __shared__ uint32_t sh[];
     __shared__ bool s_last;
     const int n_pat = A0.n_pat;
+    const int n_cnt = (TIER ? hb : 0) + n_pat * R;  // counter words; the map follows them
+    uint16_t *smap = reinterpret_cast<uint16_t *>(sh + n_cnt);
 #ifdef SPK_EM_STAMPS
     const unsigned long long t_start = wall_clock64();
     if (blockIdx.x == 0) EM_STAMP(0);
 #endif
-    // SPK_EM_PRE: workgroup 0 evaluates the E-step of every pattern (it needs only the parameters) while
-    // the others stream the codes, and streams none itself; its write-through stores are published with
-    // its count row, so the last workgroup reads mp / ln per pattern instead of computing them.
-    const bool pre = FIN && SPK_EM_PRE && gridDim.x > 1;
+    const bool pre = FIN && gridDim.x > 1;
     if (pre && blockIdx.x == 0) {
         PatArgs *sA = reinterpret_cast<PatArgs *>(sh);
         const PatArgs &A = stage_args(A0, sA);
@@ -485,49 +481,36 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         }
         __syncthreads();
     }
-    for (int b = threadIdx.x; b < n_pat * R; b += HL_THREADS) sh[b] = 0;
+    for (int b = threadIdx.x; b < n_cnt; b += HL_THREADS) sh[b] = 0;
+    if (TIER)
+        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) smap[b] = gmap[b];
+    // TIER: the most frequent pattern (rank 0 of the last ranking; -1 none) is not counted at all -- half or
+    // more of the codes skip the atomic -- and the last workgroup sets its bin to P minus every other bin
+    // (exact: every one of the P codes is streamed once and is < n_pat; P < 2^32 on this path)
+    const uint32_t hot0 = TIER ? (uint32_t)ghot[0] : 0xFFFFFFFFu;
     __syncthreads();
     constexpr int VEC = 16 / sizeof(CodeT);
     constexpr int BITS = 8 * sizeof(CodeT);
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t copy = threadIdx.x & (R - 1);
     const u32x4 *cv = reinterpret_cast<const u32x4 *>(codes);
     const int64_t n_vec = P / VEC;
     const int64_t stride = (int64_t)(gridDim.x - (pre ? 1 : 0)) * HL_THREADS;
     int64_t v = (pre && blockIdx.x == 0) ? n_vec : (int64_t)(blockIdx.x - (pre ? 1 : 0)) * HL_THREADS + threadIdx.x;
-    // The EM_NHOT most frequent patterns of the codes (found by an earlier launch's last workgroup; -1 = none)
-    // are counted in registers: candidate pairs are mostly non-matches that share a few patterns, and with
-    // few lane copies (R = 8 for cfg5's 2,160 patterns) their equal codes in a wave serialise on one LDS
-    // counter.  Any values count exactly; they only decide which codes skip the LDS atomics.  The first is
-    // not counted at all (its bin is derived after the reduction), the others in registers.
-    uint32_t hc[EM_NHOT], hn[EM_NHOT];
-#pragma unroll
-    for (int q = 0; q < EM_NHOT; ++q) {
-        hc[q] = (uint32_t)hot[q];
-        hn[q] = 0;
-    }
-    // Only with fewer than 64 copies: with one copy per lane no two lanes share a counter, and the compares
-    // would cost an issue-bound loop ~20 % (cfg2: 0.121 -> 0.147 ms at 368 M pairs).
-    constexpr bool HOT = R < 64;
-    auto count_word = [&](uint32_t w) {
-#pragma unroll
-        for (int j = 0; j < 32 / BITS; ++j) {
-            const uint32_t c = BITS == 32 ? w : ((w >> (BITS * j)) & ((1u << BITS) - 1u));
-            if (!HOT) {
-                atomicAdd(&sh[c * R + copy], 1u);
-                continue;
-            }
-            // hot pattern 0 is not counted at all: the last workgroup sets its bin to P minus the others
-            bool done = c == hc[0];
-#pragma unroll
-            for (int q = 1; q < EM_NHOT; ++q) {
-                const bool m = c == hc[q];
-                hn[q] += m ? 1u : 0u;
-                done = done || m;
-            }
-            if (!done) atomicAdd(&sh[c * R + copy], 1u);
+    auto count_code = [&](uint32_t c) {
+        if (TIER) {
+            if (c == hot0) return;
+            const uint32_t b = smap[c];
+            atomicAdd(&sh[b + (b < (uint32_t)hb ? lane : copy)], 1u);
+        } else {
+            atomicAdd(&sh[c * R + copy], 1u);
         }
     };
-    // software-pipelined 16-byte nontemporal loads, 2 x HL_UNROLL in flight per lane (k_hist_lanes)
+    auto count_word = [&](uint32_t w) {
+#pragma unroll
+        for (int j = 0; j < 32 / BITS; ++j) count_code(BITS == 32 ? w : ((w >> (BITS * j)) & ((1u << BITS) - 1u)));
+    };
+    // software-pipelined 16-byte nontemporal loads, 2 x HL_UNROLL in flight per lane
     const int64_t step = HL_UNROLL * stride;
     bool have = v + (HL_UNROLL - 1) * stride < n_vec;
     u32x4 w[HL_UNROLL];
@@ -563,38 +546,16 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         count_word(x.w);
     }
     if (blockIdx.x == (pre ? 1u : 0u))  // tail (P not a multiple of VEC)
-        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) atomicAdd(&sh[(uint32_t)codes[p] * R + copy], 1u);
-    // the register counts of the hot patterns: one LDS add per wave
-#pragma unroll
-    for (int q = 1; q < (HOT ? EM_NHOT : 0); ++q) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) hn[q] += __shfl_xor(hn[q], off);
-        if ((threadIdx.x & 63) == 0 && hn[q]) atomicAdd(&sh[hc[q] * R], hn[q]);
-    }
+        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) count_code((uint32_t)codes[p]);
     __syncthreads();
-    // Two-level last-arriver reduction of the workgroups' count rows (exact integers, so the order of
-    // the additions does not matter).  Each row is stored write-through (sc1, 16 B per lane) and drained
-    // by every storing wave, then one lane's ticket atomic: no release fence (its L2 write-back costs
-    // 1.7 us or more per workgroup; MI355X_MICROARCH.md visibility table, cdna_hip_programming.md G16 R1).
-    // The last of each group of EM_GROUP workgroups sums the group's rows into a group row; the last
-    // group sums those.  One workgroup summing all G rows was bound by one CU's load bandwidth (590 KB
-    // for cfg2's 576 patterns, ~15 us of a 60 us iteration).
-    const int64_t ps = part_stride(n_pat);
-    const int Q = (int)(ps / 4);  // quads of 4 bins per row (the row's padding bins are zero)
-    const int G = (int)gridDim.x;
-    const int NG = (G + EM_GROUP - 1) / EM_GROUP;
-    const int grp = (int)blockIdx.x / EM_GROUP;
-    const int gsz = G - grp * EM_GROUP < EM_GROUP ? G - grp * EM_GROUP : EM_GROUP;
-    uint32_t *part2 = part + (int64_t)G * ps;  // group rows follow the workgroup rows
-    auto publish = [&](uint32_t *row, const u32x4 *vals_lds) {
-        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void *)row, (short)0, (int)(ps * 4), 0x00020000);
-        for (int q = threadIdx.x; q < Q; q += HL_THREADS) __builtin_amdgcn_raw_buffer_store_b128(vals_lds[q], prs, q * 16, 0, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
-        __syncthreads();
-    };
+#ifdef SPK_EM_STAMPS
+    const unsigned long long t_streamed = wall_clock64();
+#endif
     // fence != 0 (spk_em_set_lane_histogram mode 2): an agent-scope release fence before each ticket, the
     // ordering the HSA memory model itself guarantees (after the barrier it is cumulative over the
-    // workgroup's stores); the A/B test checks both forms give the same statistics
+    // workgroup's atomics); the A/B test checks both forms give the same statistics.  Default: the row adds
+    // are device-scope atomics performed at L2, drained (s_waitcnt) before the ticket atomic, which gfx950
+    // orders behind them (MI355X_MICROARCH.md visibility table, cdna_hip_programming.md G16 R1).
     auto arrive = [&](unsigned int *t, unsigned int last) {  // true in the last arriver (whole workgroup)
         if (threadIdx.x == 0) {
             if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -607,179 +568,102 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         __syncthreads();
         return true;
     };
-    // rows [r0, r0 + n) summed per quad into LDS (up to 16 loads in flight per thread)
-    u32x4 *sq = reinterpret_cast<u32x4 *>(sh);
-    auto sum_rows = [&](const uint32_t *rows, int n) {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(rows);
-        for (int q = threadIdx.x; q < Q; q += HL_THREADS) {
-            u32x4 a[16];
+    const int G = (int)gridDim.x;
+    const int64_t ps = part_stride(n_pat);
+    uint32_t *my_row = arow + (int64_t)(blockIdx.x % EM_AROWS) * ps;
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
+        uint32_t c = 0;
+        if (TIER) {
+            const uint32_t base = smap[b];
+            if (base < (uint32_t)hb) {
+#pragma unroll 8
+                for (int k = 0; k < 64; ++k) c += sh[base + ((k + b) & 63)];  // rotate: spread banks
+            } else {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) a[j] = u32x4{0u, 0u, 0u, 0u};
-            for (int b = 0; b < n; b += 16)
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (b + j < n) a[j] += src[(int64_t)(b + j) * (ps / 4) + q];
-#pragma unroll
-            for (int w = 8; w > 0; w >>= 1)
-#pragma unroll
-                for (int j = 0; j < w; ++j) a[j] += a[j + w];
-            sq[q] = a[0];
-        }
-        __syncthreads();
-    };
-    if (arow) {
-#ifdef SPK_EM_STAMPS
-        const unsigned long long t_streamed = wall_clock64();
-#endif
-        // One-level alternative (SPK_EM_ATOMIC_ROW): every workgroup adds its counts into one of EM_AROWS
-        // global rows (workgroup mod EM_AROWS: 64 workgroups per row at 4 rows instead of all 256
-        // contending on each bin; 1 / 4 / 8 / 16 rows measured 38.9 / 37.7 / 38.1 / 38.8 us at cfg2) with agent-scope integer atomics (exact, so their order does not matter), drains them,
-        // takes the ticket; the last one sums the rows in row order and zeroes them for the next launch.
-        const int64_t ps_a = part_stride(n_pat);
-        uint32_t *my_row = arow + (int64_t)(blockIdx.x % EM_AROWS) * ps_a;
-        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
-            uint32_t c = 0;
+                for (int k = 0; k < R; ++k) c += sh[base + ((k + b) & (R - 1))];
+            }
+        } else {
 #pragma unroll
             for (int k = 0; k < R; ++k) c += sh[b * R + ((k + b) & (R - 1))];
-            if (c) __hip_atomic_fetch_add(my_row + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-#ifdef SPK_EM_STAMPS
-        const unsigned long long t_added = wall_clock64();
-#endif
-        if (!arrive(ticket, (unsigned int)(G - 1))) return;
-#ifdef SPK_EM_STAMPS
-        if (threadIdx.x == 0) {  // the last arriver: its start, end of streaming, row adds drained, ticket
-            g_em_stamps[1] = t_start;
-            g_em_stamps[2] = t_streamed;
-            g_em_stamps[3] = t_added;
-            g_em_stamps[4] = t_added;
-        }
-        EM_STAMP(5);
-#endif
-        uint32_t *s1 = sh;
-        const int nr = G < EM_AROWS ? G : EM_AROWS;
-        // every row's bin first (independent loads in flight together), then the zeroing stores: a store
-        // behind each load to the same address serialised the round trips
-        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
-            uint32_t v[EM_AROWS];
-#pragma unroll
-            for (int r = 0; r < EM_AROWS; ++r)
-                v[r] = r < nr ? __hip_atomic_load(arow + r * ps_a + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            uint32_t c = 0;
-#pragma unroll
-            for (int r = 0; r < EM_AROWS; ++r) c += v[r];
-            s1[b] = c;
-        }
-        __syncthreads();
-        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS)
-            for (int r = 0; r < nr; ++r) arow[r * ps_a + b] = 0u;
-    } else {
-    // this workgroup's row straight from its counters (a quad of bins per lane, 16-byte sc1 stores)
-    {
-        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(part + (int64_t)blockIdx.x * ps), (short)0, (int)(ps * 4), 0x00020000);
-        for (int q = threadIdx.x; q < Q; q += HL_THREADS) {
-            u32x4 v;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int b = 4 * q + j;
-                uint32_t s = 0;
-                if (b < n_pat)
-#pragma unroll
-                    for (int c = 0; c < R; ++c) s += sh[b * R + ((c + b) & (R - 1))];  // rotate: spread banks
-                v[j] = s;
-            }
-            __builtin_amdgcn_raw_buffer_store_b128(v, prs, q * 16, 0, 16);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
-        __syncthreads();
+        if (c) __hip_atomic_fetch_add(my_row + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 #ifdef SPK_EM_STAMPS
-    const unsigned long long t_pub = wall_clock64();
+    const unsigned long long t_added = wall_clock64();
 #endif
-    if (!arrive(ticket + 1 + grp, (unsigned int)(gsz - 1))) return;
-    if (threadIdx.x == 0) atomicExch(ticket + 1 + grp, 0u);  // ready for the next launch
+    if (!arrive(ticket, (unsigned int)(G - 1))) return;
 #ifdef SPK_EM_STAMPS
-    const unsigned long long t_g0 = wall_clock64();
-#endif
-    sum_rows(part + (int64_t)grp * EM_GROUP * ps, gsz);
-    publish(part2 + (int64_t)grp * ps, sq);
-#ifdef SPK_EM_STAMPS
-    const unsigned long long t_g1 = wall_clock64();
-#endif
-    if (!arrive(ticket, (unsigned int)(NG - 1))) return;
-#ifdef SPK_EM_STAMPS
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // the last arriver: its start, end of streaming, row adds drained, ticket
         g_em_stamps[1] = t_start;
-        g_em_stamps[2] = t_pub;
-        g_em_stamps[3] = t_g0;
-        g_em_stamps[4] = t_g1;
+        g_em_stamps[2] = t_streamed;
+        g_em_stamps[3] = t_added;
+        g_em_stamps[4] = t_added;
     }
     EM_STAMP(5);
 #endif
-    sum_rows(part2, NG);
-    }  // two-level reduction
-    if (HOT && hc[0] < (uint32_t)n_pat) {  // hot pattern 0's bin: P minus every other bin (exact, P < 2^32)
-        __shared__ uint32_t s_rest[HL_THREADS / 64];
-        uint32_t s = 0;
-        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) s += (uint32_t)p == hc[0] ? 0u : sh[p];
+    uint32_t *s1 = sh;  // per-pattern counts from here on
+    const int nr = G < EM_AROWS ? G : EM_AROWS;
+    // every row's bin first (independent loads in flight together), then the zeroing stores: a store
+    // behind each load to the same address serialised the round trips
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
+        uint32_t vr[EM_AROWS];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        if ((threadIdx.x & 63) == 0) s_rest[threadIdx.x >> 6] = s;
+        for (int r = 0; r < EM_AROWS; ++r)
+            vr[r] = r < nr ? __hip_atomic_load(arow + r * ps + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < EM_AROWS; ++r) c += vr[r];
+        s1[b] = c;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS)
+        for (int r = 0; r < nr; ++r) arow[r * ps + b] = 0u;
+    if (TIER && hot0 < (uint32_t)n_pat) {  // the uncounted pattern's bin: P minus every other bin
+        __shared__ uint32_t s_rest[HL_THREADS / 64];
+        uint32_t t = 0;
+        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) t += (uint32_t)p == hot0 ? 0u : s1[p];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if ((threadIdx.x & 63) == 0) s_rest[threadIdx.x >> 6] = t;
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t t = 0;
-            for (int w = 0; w < HL_THREADS / 64; ++w) t += s_rest[w];
-            sh[hc[0]] = (uint32_t)P - t;
+            uint32_t rest = 0;
+            for (int w = 0; w < HL_THREADS / 64; ++w) rest += s_rest[w];
+            s1[hot0] = (uint32_t)P - rest;
         }
         __syncthreads();
     }
     EM_STAMP(6);
     // thread t owns bins p = t, t + HL_THREADS, ... (the same mapping as em_finalize_block's loop, so
     // the count it parks in cpat is read back by the thread that wrote it)
-    const uint32_t *sp1 = reinterpret_cast<const uint32_t *>(sh);
     for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
-        const unsigned long long c = sp1[p];
+        const unsigned long long c = s1[p];
         if (FIN) cpat[p] = (double)c;
         else out_hist[p] = c;
     }
-    if (refresh) {  // the EM_NHOT most frequent patterns (ties: the lower one) for the next launches
-        __shared__ unsigned long long s_best[HL_THREADS / 64];
-        __shared__ uint32_t s_top[EM_NHOT];
-        for (int r = 0; r < EM_NHOT; ++r) {
-            unsigned long long best = 0;
-            for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
-                bool taken = false;
-                for (int q = 0; q < r; ++q) taken = taken || (uint32_t)p == s_top[q];
-                if (taken) continue;
-                const unsigned long long v = ((unsigned long long)sp1[p] << 32) | (0xFFFFFFFFull - (uint32_t)p);
-                best = v > best ? v : best;
+    if (TIER && refresh) {
+        // the next launches' map: pattern p's rank by (count desc, index asc); the hb / 64 first with a
+        // nonzero count get 64-copy slots (rank x 64), the others their R copies at hb + p x R
+        const int M = hb / 64;
+        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
+            const uint32_t cp = s1[p];
+            int rank = 0;
+            for (int q = 0; q < n_pat; ++q) {
+                const uint32_t cq = s1[q];
+                rank += (cq > cp || (cq == cp && q < p)) ? 1 : 0;
             }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const unsigned long long o = __shfl_xor(best, off);
-                best = o > best ? o : best;
-            }
-            if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                unsigned long long b = 0;
-                for (int w = 0; w < HL_THREADS / 64; ++w) b = s_best[w] > b ? s_best[w] : b;
-                const uint32_t pb = (b >> 32) ? (uint32_t)(0xFFFFFFFFull - (b & 0xFFFFFFFFull)) : 0xFFFFFFFFu;
-                hot[r] = (int32_t)pb;
-                s_top[r] = pb;
-            }
-            __syncthreads();
+            gmap[p] = (uint16_t)((rank < M && cp > 0) ? rank * 64 : hb + p * R);
+            if (rank == 0) ghot[0] = cp > 0 ? p : -1;
         }
     }
     if (FIN) {
-        __syncthreads();  // the partials' LDS is reused for the staged arguments and the pattern table
+        __syncthreads();  // the counts' LDS is reused for the staged arguments and the pattern table
         PatArgs *sA = reinterpret_cast<PatArgs *>(sh);
         const PatArgs &A = stage_args(A0, sA);
         double *tab = reinterpret_cast<double *>(sh) + (sizeof(PatArgs) + 7) / 8;
-        const bool room = ((sizeof(PatArgs) + 7) / 8 + 3 * (size_t)n_pat) * 8 <= (size_t)n_pat * R * 4;
+        const bool room = ((sizeof(PatArgs) + 7) / 8 + 3 * (size_t)n_pat) * 8 <= (size_t)lds_bytes;
         EM_STAMP(7);
         em_finalize_block(A, [&](int p) { return (unsigned long long)cpat[p]; }, mpat, llpat, cpat, out,
                           room ? tab : nullptr, pre);
@@ -788,22 +672,20 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
+__global__ void k_em_map_init(int n_pat, int hb, int R, uint16_t *__restrict__ gmap, int32_t *__restrict__ ghot) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n_pat) gmap[p] = (uint16_t)(hb + p * R);  // every pattern in the cold tier until ranked
+    if (p == 0) ghot[0] = -1;
+}
+
 // Final E-step: mp[i] = mpat[code[i]] for pairs [start, start + n).  Each lane turns two codes into
 // one 16-byte store of two doubles, so a wave instruction writes 1 KiB contiguous (the 8 B/pair of
 // output is the dominant stream); the per-pattern table sits in LDS when it fits.  Plain stores:
 // 0.704 ms against 0.757 with nontemporal ones over 368M pairs (65 % of HBM peak).  The odd pair at
 // either end (when start or start + n is odd) is written by lane 0 of block 0.
-#ifndef SPK_SC_THREADS
-#define SPK_SC_THREADS 256
-#endif
-#ifndef SPK_SC_UNROLL
-#define SPK_SC_UNROLL 4
-#endif
-#ifndef SPK_SC_WG_PER_CU
-#define SPK_SC_WG_PER_CU 8
-#endif
-constexpr int SC_THREADS = SPK_SC_THREADS;
-constexpr int SC_UNROLL = SPK_SC_UNROLL;
+constexpr int SC_THREADS = 256;
+constexpr int SC_UNROLL = 4;
+constexpr int SC_WG_PER_CU = 8;  // grid-stride over at most this many workgroups per CU
 constexpr int SC_LDS_PAT = 4096;
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
@@ -888,13 +770,35 @@ static int pat_args(spk_ctx *ctx, double lambda, double one_minus, const double 
 using namespace spk;
 
 
-// Lane-private copies of the counters that fit the LDS budget (R = 64 .. 4), 0 when none fits.  k_em_iter
-// sums its count rows in uint32: 2^32 or more pairs in one context take the k_hist path (uint64 counters).
-static int lane_copies(spk_ctx *ctx) {
+// The LDS plan of k_em_iter: R lane-private copies per pattern (64 .. 4) and, with R < 64, hb counter words
+// of 64-copy slots for the most frequent patterns (hb = 64 x M, M <= EM_TIER) when they fit next to the map.
+// R = 0: no lane path (the pattern space exceeds the LDS, or 2^32 or more pairs: k_em_iter sums its rows in
+// uint32); those take k_hist (uint64 counters) + k_em_finalize.
+struct LanePlan {
+    int R = 0, hb = 0;
+    size_t bytes = 0;  // dynamic LDS of the launch
+};
+
+static LanePlan lane_plan(spk_ctx *ctx) {
+    LanePlan L;
+    const int64_t n_pat = ctx->n_patterns;
+    const int64_t budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block) - HL_STATIC_LDS;
     int R = 64;
-    const int64_t lds_budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block);
-    while (R >= 4 && ctx->n_patterns * R * 4 > lds_budget) R >>= 1;
-    return (R >= 4 && ctx->hist_lanes && ctx->n_pairs < (int64_t)UINT32_MAX) ? R : 0;
+    while (R >= 4 && n_pat * R * 4 > budget) R >>= 1;
+    if (R < 4 || !ctx->hist_lanes || ctx->n_pairs >= (int64_t)UINT32_MAX) return L;
+    L.R = R;
+    int64_t bytes = n_pat * R * 4;
+    if (R < 64) {
+        const int64_t map = (n_pat * 2 + 15) / 16 * 16;
+        int64_t M = EM_TIER;
+        while (M >= 16 && bytes + map + M * 64 * 4 > budget) M >>= 1;
+        if (M >= 16 && (M * 64 + n_pat * R) < 65536) {  // map entries are uint16 word offsets
+            L.hb = (int)(M * 64);
+            bytes += map + M * 64 * 4;
+        }
+    }
+    L.bytes = (size_t)std::max<int64_t>(bytes, (int64_t)sizeof(PatArgs));
+    return L;
 }
 
 // Grid of the lane-histogram launches: one 1024-thread workgroup per CU.
@@ -903,55 +807,82 @@ static int64_t lane_grid(spk_ctx *ctx) {
     return std::max<int64_t>(1, std::min<int64_t>(ctx->n_cu, (vecs + HL_THREADS - 1) / HL_THREADS));
 }
 
-#define SPK_EM_ITER(RR, FIN)                                                                                      \
-    case RR:                                                                                                     \
-        if (ctx->code_bytes == 2)                                                                                \
-            k_em_iter<uint16_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
-                reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
-                ctx->em_fence ? 1 : 0, arow, hot, refresh);                                                      \
-        else                                                                                                     \
-            k_em_iter<uint32_t, RR, FIN><<<(unsigned)g, HL_THREADS, sh, ctx->stream>>>(                         \
-                reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, acc, ticket, mpat, llpat, cpat, out, h, \
-                ctx->em_fence ? 1 : 0, arow, hot, refresh);                                                      \
-        break;
+// The reduction rows and the ticket of k_em_iter (zero between launches: the last workgroup resets them,
+// zeroed here only when allocated) and the two-tier map, ranked again (by the launch's last workgroup) when
+// the pair set, the pattern space or the plan changed; repeated comparison passes over the same pairs keep it.
+struct EmState {
+    unsigned int *ticket = nullptr;
+    uint32_t *arow = nullptr;
+    uint16_t *gmap = nullptr;
+    int32_t *ghot = nullptr;
+    int refresh = 0;
+};
 
-// The padded accumulation histogram and the ticket of k_em_iter: zero between launches (the last workgroup
-// resets them), zeroed here only when (re)allocated.
-static int em_accumulator(spk_ctx *ctx, uint32_t **acc, unsigned int **ticket, uint32_t **arow, int32_t **hot,
-                          int *refresh) {
-    // k_em_iter: one count row per workgroup (<= n_cu), then one per group of EM_GROUP workgroups;
-    // tickets [final | per group]
-    const int64_t n_groups = ((int64_t)ctx->n_cu + EM_GROUP - 1) / EM_GROUP;
-    const size_t need = (size_t)part_stride(ctx->n_patterns) * (size_t)(ctx->n_cu + n_groups);
-    SPK_TRY(ctx->hist_part.alloc(need));
-    if (!ctx->em_ticket.p || ctx->em_ticket.n < (size_t)(1 + n_groups)) {
-        SPK_TRY(ctx->em_ticket.alloc((size_t)(1 + n_groups)));
-        SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, (size_t)(1 + n_groups) * 4, ctx->stream));
+static int em_state(spk_ctx *ctx, const LanePlan &L, EmState &S) {
+    if (!ctx->em_ticket.p) {
+        SPK_TRY(ctx->em_ticket.alloc(1));
+        SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, 4, ctx->stream));
     }
-    *acc = ctx->hist_part.p;
-    *ticket = ctx->em_ticket.p;
-    *arow = nullptr;
-    if (SPK_EM_ATOMIC_ROW) {  // the one-level reduction's row: zero between launches (the last workgroup resets it)
-        const size_t ps = (size_t)part_stride(ctx->n_patterns) * EM_AROWS;
-        if (!ctx->em_row.p || ctx->em_row.n < ps) {
-            SPK_TRY(ctx->em_row.alloc(ps));
-            SPK_HIP(hipMemsetAsync(ctx->em_row.p, 0, ps * 4, ctx->stream));
+    const size_t ps = (size_t)part_stride(ctx->n_patterns) * EM_AROWS;
+    if (!ctx->em_row.p || ctx->em_row.n < ps) {
+        SPK_TRY(ctx->em_row.alloc(ps));
+        SPK_HIP(hipMemsetAsync(ctx->em_row.p, 0, ps * 4, ctx->stream));
+    }
+    S.ticket = ctx->em_ticket.p;
+    S.arow = ctx->em_row.p;
+    if (L.hb) {
+        const std::vector<int64_t> key = {(int64_t)ctx->pairs_epoch, ctx->n_pairs, ctx->n_patterns, ctx->code_bytes,
+                                          L.R, L.hb};
+        if (ctx->em_map_key != key || !ctx->em_map.p) {
+            SPK_TRY(ctx->em_map.alloc((size_t)ctx->n_patterns));
+            SPK_TRY(ctx->em_hot.alloc(1));
+            k_em_map_init<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(
+                (int)ctx->n_patterns, L.hb, L.R, ctx->em_map.p, ctx->em_hot.p);
+            SPK_HIP(hipGetLastError());
+            ctx->em_map_key = key;
+            S.refresh = 1;
         }
-        *arow = ctx->em_row.p;
+        S.gmap = ctx->em_map.p;
+        S.ghot = ctx->em_hot.p;
     }
-    // the hot patterns: found again (by the launch's last workgroup) when the pair set or the pattern
-    // space changed; the codes of repeated comparison passes over the same pairs keep them
-    if (!ctx->em_hot.p) {
-        SPK_TRY(ctx->em_hot.alloc(EM_NHOT));
-        SPK_HIP(hipMemsetAsync(ctx->em_hot.p, 0xFF, EM_NHOT * sizeof(int32_t), ctx->stream));
+    return SPK_OK;
+}
+
+template <int R, bool FIN>
+static void launch_em_iter(spk_ctx *ctx, const LanePlan &L, const EmState &S, int64_t g, const PatArgs &A,
+                           double *mpat, double *llpat, double *cpat, double *out, unsigned long long *h) {
+    const int64_t P = ctx->n_pairs;
+    const int fence = ctx->em_fence ? 1 : 0;
+    const unsigned grid = (unsigned)g;
+    if (ctx->code_bytes == 2) {
+        const auto *c = reinterpret_cast<const uint16_t *>(ctx->codes.p);
+        if (L.hb) k_em_iter<uint16_t, R, FIN, true><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, S.gmap, S.ghot, L.hb, S.refresh, (int)L.bytes);
+        else k_em_iter<uint16_t, R, FIN, false><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, nullptr, nullptr, 0, 0, (int)L.bytes);
+    } else {
+        const auto *c = reinterpret_cast<const uint32_t *>(ctx->codes.p);
+        if (L.hb) k_em_iter<uint32_t, R, FIN, true><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, S.gmap, S.ghot, L.hb, S.refresh, (int)L.bytes);
+        else k_em_iter<uint32_t, R, FIN, false><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, nullptr, nullptr, 0, 0, (int)L.bytes);
     }
-    const std::vector<int64_t> key = {(int64_t)ctx->pairs_epoch, ctx->n_pairs, ctx->n_patterns, ctx->code_bytes};
-#ifndef SPK_EM_HOT
-#define SPK_EM_HOT 1  // 0: no register-counted patterns (A/B)
-#endif
-    *refresh = SPK_EM_HOT && ctx->em_hot_key != key;
-    ctx->em_hot_key = key;
-    *hot = ctx->em_hot.p;
+}
+
+template <bool FIN>
+static int launch_em_lanes(spk_ctx *ctx, const LanePlan &L, const PatArgs &A, double *mpat, double *llpat,
+                           double *cpat, double *out, unsigned long long *h) {
+    EmState S;
+    SPK_TRY(em_state(ctx, L, S));
+    const int64_t g = lane_grid(ctx);
+    switch (L.R) {
+        case 64: launch_em_iter<64, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        case 32: launch_em_iter<32, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        case 16: launch_em_iter<16, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        case 8: launch_em_iter<8, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        default: launch_em_iter<4, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+    }
+    SPK_HIP(hipGetLastError());
     return SPK_OK;
 }
 
@@ -965,27 +896,12 @@ static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     }
     const int64_t P = ctx->n_pairs;
     const int vec = 16 / ctx->code_bytes;
-    const int R = lane_copies(ctx);
+    const LanePlan L = lane_plan(ctx);
     SPK_TRY(ctx->begin(K_EMHIST));
-    if (R) {
+    if (L.R) {
         PatArgs A{};
         A.n_pat = (int)n_pat;
-        const int64_t g = lane_grid(ctx);
-        const size_t sh = (size_t)n_pat * R * 4;
-        uint32_t *acc = nullptr;
-        unsigned int *ticket = nullptr;
-        uint32_t *arow = nullptr;
-        int32_t *hot = nullptr;
-        int refresh = 0;
-        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow, &hot, &refresh));
-        double *mpat = nullptr, *llpat = nullptr, *cpat = nullptr, *out = nullptr;
-        switch (R) {
-            SPK_EM_ITER(64, false)
-            SPK_EM_ITER(32, false)
-            SPK_EM_ITER(16, false)
-            SPK_EM_ITER(8, false)
-            SPK_EM_ITER(4, false)
-        }
+        SPK_TRY(launch_em_lanes<false>(ctx, L, A, nullptr, nullptr, nullptr, nullptr, h));
     } else {
         SPK_HIP(hipMemsetAsync(h, 0, (size_t)n_pat * 8, ctx->stream));
         int64_t blocks = (P / vec + H_THREADS - 1) / H_THREADS;
@@ -1088,8 +1004,8 @@ static int enqueue_em(spk_ctx *ctx) {
     const int n_stats = ctx->em_n_stats;
     SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_iteration: n_stats mismatch");
     SPK_TRY(em_buffers(ctx, n_stats));
-    const int R = lane_copies(ctx);
-    if (!R) {
+    const LanePlan L = lane_plan(ctx);
+    if (!L.R) {
         SPK_TRY(enqueue_histogram(ctx, nullptr));
         SPK_TRY(ctx->begin(K_EMFIN));
         k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, reinterpret_cast<const unsigned long long *>(ctx->hist.p),
@@ -1097,27 +1013,8 @@ static int enqueue_em(spk_ctx *ctx) {
         SPK_HIP(hipGetLastError());
         SPK_TRY(ctx->end(K_EMFIN));
     } else {
-        const int64_t n_pat = ctx->n_patterns;
-        uint32_t *acc = nullptr;
-        unsigned long long *h = nullptr;
-        unsigned int *ticket = nullptr;
-        uint32_t *arow = nullptr;
-        int32_t *hot = nullptr;
-        int refresh = 0;
-        SPK_TRY(em_accumulator(ctx, &acc, &ticket, &arow, &hot, &refresh));
-        const int64_t P = ctx->n_pairs;
-        const int64_t g = lane_grid(ctx);
-        const size_t sh = std::max<size_t>((size_t)n_pat * R * 4, sizeof(PatArgs));
-        double *mpat = ctx->mpat.p, *llpat = ctx->llpat.p, *cpat = ctx->cpat.p, *out = ctx->stats.p;
         SPK_TRY(ctx->begin(K_EMHIST));
-        switch (R) {
-            SPK_EM_ITER(64, true)
-            SPK_EM_ITER(32, true)
-            SPK_EM_ITER(16, true)
-            SPK_EM_ITER(8, true)
-            SPK_EM_ITER(4, true)
-        }
-        SPK_HIP(hipGetLastError());
+        SPK_TRY(launch_em_lanes<true>(ctx, L, A, ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p, nullptr));
         SPK_TRY(ctx->end(K_EMHIST));
         ctx->ev_used[0][K_EMFIN] = ctx->ev_used[1][K_EMFIN] = false;  // one launch: the E-step is inside it
     }
@@ -1211,7 +1108,6 @@ extern "C" int spk_em_iteration(spk_ctx *ctx, double lambda, double one_minus, c
     return spk_em_iteration_wait(ctx, out_stats, n_stats);
 }
 
-#undef SPK_EM_ITER
 extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const double *m, const double *u,
                          int64_t start, int64_t count, double *out_mp) {
     SPK_REQUIRE(ctx && m && u, SPK_E_INVALID, "spk_score: null arg");
@@ -1227,9 +1123,10 @@ extern "C" int spk_score(spk_ctx *ctx, double lambda, double one_minus, const do
     k_pattern_mp<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(A, ctx->mpat_score.p, nullptr);
     SPK_HIP(hipGetLastError());
     ctx->mpat_valid = true;
+    ++ctx->score_seq;
     if (count) {
         int64_t g = (count / 2 + SC_THREADS - 1) / SC_THREADS;
-        if (g > SPK_SC_WG_PER_CU * (int64_t)ctx->n_cu) g = SPK_SC_WG_PER_CU * (int64_t)ctx->n_cu;  // grid-stride
+        if (g > SC_WG_PER_CU * (int64_t)ctx->n_cu) g = SC_WG_PER_CU * (int64_t)ctx->n_cu;  // grid-stride
         if (g < 1) g = 1;
         const int np = (int)ctx->n_patterns;
         const bool lds = ctx->n_patterns <= SC_LDS_PAT;  // LDS table: 0.795 ms vs 0.828 from L1 (368M pairs)

@@ -729,14 +729,11 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     }
     const unsigned g = (unsigned)(region_hi - region_lo);
     const size_t shm = (size_t)A.n_thr * sizeof(int16_t);
-#ifndef SPK_F_FP
-#define SPK_F_FP 3  // pairs per lane per step
-#endif
-#ifndef SPK_F_MINW
-#define SPK_F_MINW 5  // waves per SIMD the register budget is sized for
-#endif
-    if (A.code16) k_filter<SPK_F_FP, SPK_F_MINW, false><<<g, F_THREADS, shm, stream>>>(F);
-    else k_filter<SPK_F_FP, SPK_F_MINW, true><<<g, F_THREADS, shm, stream>>>(F);
+    // 3 pairs per lane per step at a register budget for 5 waves per SIMD (94 VGPRs): the best point of the
+    // round-4 sweep (<2,6> / <4,4> slower, <3,6> / <2,8> spill: profiles/r4_ab_filter_occupancy.log)
+    constexpr int FP = 3, MINW = 5;
+    if (A.code16) k_filter<FP, MINW, false><<<g, F_THREADS, shm, stream>>>(F);
+    else k_filter<FP, MINW, true><<<g, F_THREADS, shm, stream>>>(F);
     SPK_HIP(hipGetLastError());
     return SPK_OK;
 }

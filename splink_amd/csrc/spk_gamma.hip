@@ -764,10 +764,10 @@ __device__ inline int lev_work_bin(int la, int lb) {
 
 // Counting sort of the workgroup's (key, item) by key through LDS: one LDS atomic per lane, a
 // LEV_BINS exclusive scan in wave 0 (three bins per lane), one scatter and one gather.  Three barriers.
-__device__ inline void lev_sort_items(int key, bool &have, int32_t &p, int32_t &x, int32_t &y) {
+__device__ inline void lev_sort_items(int &key, bool &have, int32_t &p, int32_t &x, int32_t &y) {
     __shared__ unsigned int s_bin[LEV_BINS];
     __shared__ int32_t s_p[X_THREADS], s_x[X_THREADS], s_y[X_THREADS];
-    __shared__ uint8_t s_have[X_THREADS];
+    __shared__ uint8_t s_have[X_THREADS], s_key[X_THREADS];
     const int t = threadIdx.x;
     if (t < LEV_BINS) s_bin[t] = 0;
     __syncthreads();
@@ -793,11 +793,13 @@ __device__ inline void lev_sort_items(int key, bool &have, int32_t &p, int32_t &
     s_x[pos] = x;
     s_y[pos] = y;
     s_have[pos] = have ? 1 : 0;
+    s_key[pos] = (uint8_t)key;
     __syncthreads();
     p = s_p[t];
     x = s_x[t];
     y = s_y[t];
     have = s_have[t] != 0;
+    key = s_key[t];
 }
 
 constexpr int LEV_WAVES = 5;
@@ -887,7 +889,11 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         }
         if (regroup) lev_sort_items(key, have, p, x, y);
         bool to_slow = false;
-        if (have) {
+        if (have && regroup && key >= 128) {
+            // a row past 64 units (work bins 128 +): no 64-bit planes, the 128-bit slow pass takes the cell --
+            // straight to its list, without loading the rows' planes and records first
+            to_slow = true;
+        } else if (have) {
             int level = 0;
             int st;
             if constexpr (MODE == X_LEV) st = lev_cell(sc, s_c0, s_c1, x, y, level);
@@ -1496,10 +1502,8 @@ static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
         const bool lev = si >= 0 && G.simple[si].cls == SC_LEV;
         const ColSet one_k{1, {k, 0, 0, 0}};
         if (lev) {
-#ifndef SPK_SLOWLEV_WG_PER_CU
-#define SPK_SLOWLEV_WG_PER_CU 8  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU fit at once
-#endif
-            const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SPK_SLOWLEV_WG_PER_CU * ctx->n_cu));
+            constexpr int SLOWLEV_WG_PER_CU = 8;  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU at once
+            const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SLOWLEV_WG_PER_CU * ctx->n_cu));
             k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
             k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
         } else {
@@ -1533,12 +1537,10 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
     const std::vector<SimpleCol> &simple = G.simple;
     // Jaro-Winkler template columns: compact every list, then one exact launch over all of them
     // JW exact launches: a JW cell is one short latency-bound evaluation, and the kernel holds 3 waves per
-    // SIMD, so a grid of 8 workgroups per CU ran in rounds of dispatch latency; SPK_JW_WG_PER_CU per
-    // column keeps it near one resident round with the grid-stride loop's prefetch
-#ifndef SPK_JW_WG_PER_CU
-#define SPK_JW_WG_PER_CU 8
-#endif
-    const int64_t g_jw = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SPK_JW_WG_PER_CU * ctx->n_cu));
+    // SIMD, so a grid of 8 workgroups per CU ran in rounds of dispatch latency; JW_WG_PER_CU per column
+    // keeps it near one resident round with the grid-stride loop's prefetch
+    constexpr int JW_WG_PER_CU = 8;
+    const int64_t g_jw = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)JW_WG_PER_CU * ctx->n_cu));
     ExactCols jw{};
     jw.g = (int)g_jw;
     ColSet jk{};
@@ -1585,10 +1587,8 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
             one.n = 1;
             // one resident round: the grid-stride loop gives every block a fixed share of the list, so a
             // grid larger than what fits at once (LEV_WAVES per SIMD) runs a second, partly empty round
-#ifndef SPK_LEV_WG_PER_CU
-#define SPK_LEV_WG_PER_CU 8
-#endif
-            const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SPK_LEV_WG_PER_CU * ctx->n_cu));
+            constexpr int LEV_WG_PER_CU = 8;
+            const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)LEV_WG_PER_CU * ctx->n_cu));
             one.g = (int)g_lev;
             one.si[0] = si;
             one.k[0] = simple[si].k;

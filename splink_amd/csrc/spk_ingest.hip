@@ -555,9 +555,10 @@ int spk_table_digest(spk_ctx *ctx, int side, uint64_t *out) {
         if (!c || c->kind == COL_NONE) continue;
         acc = (acc ^ (uint64_t)c->kind) * 1099511628211ull;
         if (c->kind == COL_STR) {
-            // units: up to the last row's end (the buffer's padding past it is not part of the encoding)
+            // units: the zeroed extent the last decode wrote (a reused buffer's capacity past it is not part of
+            // the encoding)
             SPK_TRY(digest(ctx, c->meta.p, t.n * (int64_t)sizeof(RecMeta), acc));
-            SPK_TRY(digest(ctx, c->units.p, (int64_t)c->units.n * 2, acc));
+            SPK_TRY(digest(ctx, c->units.p, c->units_len * 2, acc));
             if (c->planes.p) SPK_TRY(digest(ctx, c->planes.p, t.n * N_PLANES * 8, acc));
             if (c->planes_hi.p) SPK_TRY(digest(ctx, c->planes_hi.p, t.n * N_PLANES * 8, acc));
             acc = (acc ^ (uint64_t)c->n_ids) * 1099511628211ull;
@@ -822,6 +823,7 @@ int spk_table_add_raw_utf8(spk_ctx *ctx, int col, int raw0, int raw1) {
         if (long_rows) SPK_TRY(c->planes_hi.alloc((size_t)(n + 1) * N_PLANES));
         else c->planes_hi.release();
         SPK_HIP(hipMemsetAsync(c->units.p, 0, (size_t)(nbytes + 3 * n + 16) * 2, ctx->stream));
+        c->units_len = nbytes + 3 * n + 16;
         SPK_TRY(launch_utf8_decode(ctx, n, off8.p, r->off.p, perm, r->bytes.p, r->valid.p, c, long_rows,
                                    ids.p + (side == 0 ? 0 : s0.n)));
         SPK_HIP(hipStreamSynchronize(ctx->stream));

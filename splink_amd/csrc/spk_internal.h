@@ -135,6 +135,7 @@ struct DevBuf {
 struct Column {
     ColKind kind = COL_NONE;
     DevBuf<uint16_t> units;
+    int64_t units_len = 0;  // units written by the last decode (zeroed first); the buffer may be larger (reused)
     DevBuf<RecMeta> meta;
     DevBuf<uint64_t> planes;
     DevBuf<uint64_t> planes_hi;  // allocated only when some row has more than 64 UTF-8 bytes
@@ -306,11 +307,11 @@ struct spk_ctx {
     // EM state
     spk::DevBuf<uint64_t> hist;
     spk::DevBuf<double> mpat, llpat, cpat, stats, mu;  // per pattern: mp, ln(...), count; statistics; m / u
-    spk::DevBuf<uint32_t> hist_part;    // k_em_iter's per-workgroup pattern counts (rows of part_stride)
-    spk::DevBuf<unsigned int> em_ticket;  // its last-workgroup ticket (kept zero between launches)
-    spk::DevBuf<uint32_t> em_row;         // its one-level reduction row (SPK_EM_ATOMIC_ROW; kept zero)
-    spk::DevBuf<int32_t> em_hot;          // its register-counted patterns (-1: none yet)
-    std::vector<int64_t> em_hot_key;      // the pair set / pattern space they were found for
+    spk::DevBuf<unsigned int> em_ticket;  // k_em_iter's last-workgroup ticket (kept zero between launches)
+    spk::DevBuf<uint32_t> em_row;         // its reduction rows (kept zero between launches)
+    spk::DevBuf<uint16_t> em_map;         // its two-tier map: pattern -> first counter word (spk_em.hip)
+    spk::DevBuf<int32_t> em_hot;          // the pattern it does not count (rank 0 of the map; -1 none)
+    std::vector<int64_t> em_map_key;      // the pair set / pattern space / LDS plan the map was ranked for
     double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;
     int n_cu = 256;                   // compute units of the device (grid sizing)
@@ -338,6 +339,11 @@ struct spk_ctx {
         if (gplan && gplan_free) gplan_free(gplan);
     }
     bool mpat_valid = false;  // mpat_score holds the mp per pattern of the current codes' last spk_score
+    uint64_t score_seq = 0;   // spk_score calls so far (the tf runs depend on their mp per pattern)
+    // the (value, pattern) runs of the last tf scale pass over a device-id column, reused by its sum pass
+    spk::DevBuf<unsigned long long> tf_uniq;
+    spk::DevBuf<unsigned int> tf_runs, tf_nruns;
+    std::vector<int64_t> tf_key;
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
     bool em_fence = false;   // k_em_iter: release fence before each ticket (spk_em_set_lane_histogram mode 2)
 

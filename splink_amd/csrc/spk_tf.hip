@@ -112,17 +112,40 @@ __global__ void k_tf_runs(const unsigned long long *__restrict__ keys, const uns
 // The runs of (value, pattern) keys of the current pairs, value ids per row on the device (d0 side 0, d1
 // side 1), chunk by chunk: scale pass (acc null: each value's scale into d_scale) or sum pass (the counts
 // and the scaled fixed-point sums at the given d_scale).
+// key (optional): what the runs depend on (pair set, codes, scores, value ids).  With a key and one chunk,
+// the runs stay in the context after the scale pass, and a sum pass with the same key reuses them instead of
+// building and sorting the keys again (the tf adjustment's two passes then cost one sort); the sum pass
+// releases them.
 static int tf_pass(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int *d_scale,
-                   unsigned long long *acc, unsigned long long *cnt) {
+                   unsigned long long *acc, unsigned long long *cnt, const std::vector<int64_t> *key = nullptr) {
     SPK_REQUIRE(ctx->mpat_valid && ctx->mpat_score.p, SPK_E_STATE, "tf: run spk_score first (mp per pattern)");
     SPK_REQUIRE(n_values < ((int64_t)1 << 31), SPK_E_LIMIT, "tf: more than 2^31 distinct values");
     const int64_t P = ctx->n_pairs;
     // the sort and the run counts work on uint32 lengths: chunks of at most 2^30 pairs
     const int64_t CH = (int64_t)1 << 30;
-    DevBuf<unsigned long long> k_in, k_out, uniq;
-    DevBuf<unsigned int> runs, n_runs;
-    DevBuf<uint8_t> tmp;
+    const bool cache = key != nullptr && P <= CH;
     const int64_t cap = std::min<int64_t>(std::max<int64_t>(P, 1), CH);
+    if (cache && ctx->tf_key == *key && ctx->tf_uniq.p) {  // the runs of the scale pass
+        const unsigned g = (unsigned)((cap + 255) / 256);
+        if (acc) k_tf_runs<<<g, 256, 0, ctx->stream>>>(ctx->tf_uniq.p, ctx->tf_runs.p, ctx->tf_nruns.p, ctx->mpat_score.p,
+                                                       d_scale, acc, cnt);
+        else k_tf_scale<<<g, 256, 0, ctx->stream>>>(ctx->tf_uniq.p, ctx->tf_nruns.p, ctx->mpat_score.p, d_scale);
+        SPK_HIP(hipGetLastError());
+        if (acc) {
+            SPK_HIP(hipStreamSynchronize(ctx->stream));
+            ctx->tf_uniq.release();
+            ctx->tf_runs.release();
+            ctx->tf_key.clear();
+        }
+        return SPK_OK;
+    }
+    DevBuf<unsigned long long> k_in, k_out, uniq_l;
+    DevBuf<unsigned int> runs_l, n_runs_l;
+    DevBuf<uint8_t> tmp;
+    DevBuf<unsigned long long> &uniq = cache ? ctx->tf_uniq : uniq_l;
+    DevBuf<unsigned int> &runs = cache ? ctx->tf_runs : runs_l;
+    DevBuf<unsigned int> &n_runs = cache ? ctx->tf_nruns : n_runs_l;
+    if (cache) ctx->tf_key.clear();
     SPK_TRY(k_in.alloc((size_t)cap));
     SPK_TRY(k_out.alloc((size_t)cap));
     SPK_TRY(uniq.alloc((size_t)cap));
@@ -150,6 +173,15 @@ static int tf_pass(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int6
         else k_tf_scale<<<g, 256, 0, ctx->stream>>>(uniq.p, n_runs.p, ctx->mpat_score.p, d_scale);
         SPK_HIP(hipGetLastError());
     }
+    if (cache) {
+        SPK_HIP(hipStreamSynchronize(ctx->stream));  // the locals (keys, sort scratch) are freed on return
+        if (acc) {
+            ctx->tf_uniq.release();
+            ctx->tf_runs.release();
+        } else {
+            ctx->tf_key = *key;
+        }
+    }
     return SPK_OK;
 }
 
@@ -159,11 +191,12 @@ __global__ void k_fill_i32(int64_t n, int v, int *__restrict__ out) {
 }
 
 // Per-value scales of this context's pairs (TF_NO_SCALE: no positive term).
-static int tf_scales(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int32_t *out_scale) {
+static int tf_scales(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, int32_t *out_scale,
+                     const std::vector<int64_t> *key = nullptr) {
     DevBuf<int> sc;
     SPK_TRY(sc.alloc((size_t)n_values + 1));
     k_fill_i32<<<(unsigned)((n_values + 256) / 256), 256, 0, ctx->stream>>>(n_values + 1, TF_NO_SCALE, sc.p);
-    SPK_TRY(tf_pass(ctx, n_values, d0, d1, sc.p, nullptr, nullptr));
+    SPK_TRY(tf_pass(ctx, n_values, d0, d1, sc.p, nullptr, nullptr, key));
     if (n_values) SPK_HIP(hipMemcpyAsync(out_scale, sc.p, (size_t)n_values * 4, hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     return SPK_OK;
@@ -171,7 +204,7 @@ static int tf_scales(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const in
 
 // Exact per-value sums at the given scales (every rank's scales all-reduced with MAX).
 static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int64_t *d1, const int32_t *scale,
-                    int64_t *out_limbs, int64_t *out_count) {
+                    int64_t *out_limbs, int64_t *out_count, const std::vector<int64_t> *key = nullptr) {
     DevBuf<unsigned long long> acc, cnt;
     DevBuf<int> sc;
     SPK_TRY(acc.alloc((size_t)n_values * TF_LIMBS + 1));
@@ -180,7 +213,7 @@ static int tf_exact(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int
     SPK_HIP(hipMemsetAsync(acc.p, 0, ((size_t)n_values * TF_LIMBS + 1) * 8, ctx->stream));
     SPK_HIP(hipMemsetAsync(cnt.p, 0, ((size_t)n_values + 1) * 8, ctx->stream));
     if (n_values) SPK_HIP(hipMemcpyAsync(sc.p, scale, (size_t)n_values * 4, hipMemcpyHostToDevice, ctx->stream));
-    SPK_TRY(tf_pass(ctx, n_values, d0, d1, sc.p, acc.p, cnt.p));
+    SPK_TRY(tf_pass(ctx, n_values, d0, d1, sc.p, acc.p, cnt.p, key));
     if (n_values) {
         SPK_HIP(hipMemcpyAsync(out_limbs, acc.p, (size_t)n_values * TF_LIMBS * 8, hipMemcpyDeviceToHost, ctx->stream));
         SPK_HIP(hipMemcpyAsync(out_count, cnt.p, (size_t)n_values * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -292,6 +325,11 @@ static int tf_column_ids(spk_ctx *ctx, int col, int64_t n_values, TfIds &I) {
     I.p1 = &t1 != &t0 ? I.d1.p : I.d0.p;
     return SPK_OK;
 }
+// What the runs of a device-id tf column depend on (tf_pass's cache key).
+static std::vector<int64_t> tf_column_key(spk_ctx *ctx, int col, int64_t n_values) {
+    return {(int64_t)ctx->pairs_epoch, (int64_t)ctx->gamma_seq, (int64_t)ctx->score_seq,
+            (int64_t)ctx->table[0].version, (int64_t)ctx->side_table(1).version, col, n_values};
+}
 static int tf_ready(spk_ctx *ctx, const char *what) {
     SPK_REQUIRE(ctx->pairs_valid && ctx->codes_valid, SPK_E_STATE, std::string(what) + ": run spk_score first");
     SPK_HIP(hipSetDevice(ctx->device));
@@ -313,7 +351,8 @@ extern "C" int spk_tf_scales_column(spk_ctx *ctx, int col, int64_t n_values, int
     SPK_TRY(tf_ready(ctx, "spk_tf_scales_column"));
     TfIds I;
     SPK_TRY(tf_column_ids(ctx, col, n_values, I));
-    return tf_scales(ctx, n_values, I.p0, I.p1, out_scale);
+    const std::vector<int64_t> key = tf_column_key(ctx, col, n_values);
+    return tf_scales(ctx, n_values, I.p0, I.p1, out_scale, &key);
 }
 
 extern "C" int spk_tf_accumulate_exact(spk_ctx *ctx, int64_t n_values, const int64_t *ids_side0, const int64_t *ids_side1,
@@ -333,7 +372,8 @@ extern "C" int spk_tf_accumulate_column_exact(spk_ctx *ctx, int col, int64_t n_v
     SPK_TRY(tf_ready(ctx, "spk_tf_accumulate_column_exact"));
     TfIds I;
     SPK_TRY(tf_column_ids(ctx, col, n_values, I));
-    return tf_exact(ctx, n_values, I.p0, I.p1, scale, out_limbs, out_count);
+    const std::vector<int64_t> key = tf_column_key(ctx, col, n_values);
+    return tf_exact(ctx, n_values, I.p0, I.p1, scale, out_limbs, out_count, &key);
 }
 
 // The double forms: the exact sums of this context's pairs at its own scales, converted (the values the

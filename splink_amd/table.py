@@ -184,7 +184,9 @@ def encode_float64(series: pd.Series):
         vals = pd.to_numeric(pd.Series([None if is_null_scalar(v) else v for v in series.tolist()], dtype=object),
                              errors="coerce").astype(np.float64).to_numpy()
     valid = (~np.isnan(vals)).astype(np.uint8)
-    return np.nan_to_num(vals, nan=0.0), valid
+    # NaN = NULL (value 0); +-Infinity stay infinite (np.nan_to_num would clamp them to +-DBL_MAX, and then
+    # Infinity - Infinity would compare as 0 instead of NaN)
+    return np.where(valid.astype(bool), vals, 0.0), valid
 
 
 def factorize_joint(parts):

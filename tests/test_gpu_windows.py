@@ -145,3 +145,31 @@ def test_new_column_after_raw_release(amd):
     uid = table["unique_id"].to_numpy()
     ok = ((sn[l] == sn[r]) & (table["surname"].notna().to_numpy()[l])) | (dob[l] == dob[r])
     assert ok.all() and (uid[l] < uid[r]).all()
+
+
+@pytest.mark.parametrize("chunked", [False, True])
+def test_prefetched_columns_match_direct_upload(amd, chunked):
+    """Job(prefetch=...) uploads comparison-only string columns from a background thread while the uid
+    ranks and blocking run; the adopted device columns (spk_raw_utf8_arrow, on_device) must give the same
+    encoded table (spk_table_digest) and comparison vectors as the direct upload -- Arrow chunks with sliced
+    offsets and validity bitmaps included."""
+    import pandas as pd
+    import pyarrow as pa
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import cfg_settings
+    df = _records(20000, 53)
+    for c in COLS:  # Arrow-backed; chunked: several chunks, the later ones sliced (nonzero offset base)
+        vals = pa.array(df[c].tolist(), type=pa.large_string())
+        parts = [vals.slice(0, 7000), vals.slice(7000, 6000), vals.slice(13000)] if chunked else [vals]
+        df[c] = pd.Series(pd.arrays.ArrowExtensionArray(pa.chunked_array(parts)))
+    st = complete_settings_dict(cfg_settings(2), amd)
+    out = []
+    for pre in (None, ["first_name", "email", "city"]):
+        job = Job("dedupe_only", [df], "unique_id", 0, prefetch=pre)
+        job.block(st["blocking_rules"])
+        job.gammas(st)
+        out.append((job.ctx.table_digest(0), job.gammas_host(), job.timings.get("prefetch_wait_s")))
+    assert out[1][2] is not None  # the prefetched columns were adopted
+    assert out[0][0] == out[1][0]
+    assert (out[0][1] == out[1][1]).all()

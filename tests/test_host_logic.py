@@ -226,3 +226,13 @@ def test_derived_values_match_oracle_functions():
                 assert got == want_n, (e, [(g, w) for g, w in zip(got, want_n) if g != w][:5])
             else:
                 assert got == want, (e, [(g, w) for g, w in zip(got, want) if g != w][:5])
+
+
+def test_float64_encoding_keeps_infinities():
+    """Numeric columns go to the device as fp64 + validity: NaN / None are NULL, +-Infinity stay infinite
+    (Spark doubles; abs(Infinity - Infinity) is NaN, so `< t` is false, not true as for clamped values)."""
+    import pandas as pd
+    from splink_amd.table import encode_float64
+    vals, valid = encode_float64(pd.Series([1.5, float("inf"), -float("inf"), float("nan"), None]))
+    assert valid.tolist() == [1, 1, 1, 0, 0]
+    assert vals[1] == float("inf") and vals[2] == -float("inf") and vals[3] == 0.0

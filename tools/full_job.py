@@ -67,6 +67,8 @@ def main():
                     help="generate the records as this many independent chunks over one vocabulary, in parallel "
                          "(synthetic.make_records_parallel; 0 = the serial make_records)")
     ap.add_argument("--workers", type=int, default=16)
+    ap.add_argument("--no-prefetch", dest="prefetch", action="store_false",
+                    help="upload the comparison-only columns in the first comparison call (no background prefetch)")
     a = ap.parse_args()
     global COLS, SPECS
     if a.config == 5:  # + the free-text address column, Levenshtein-4 (cfg5's columns)
@@ -117,7 +119,10 @@ def main():
     wall = {}
     t_job = time.perf_counter()
     t = time.perf_counter()
-    job = Job(st["link_type"], inputs, "unique_id", 0, shard=(shard, n_shards))
+    from splink_amd.blocking import _comparison_only_columns
+    # the comparison-only columns upload in the background while the uid ranks and blocking run
+    pre = _comparison_only_columns(st, st["blocking_rules"], inputs[0].columns) if a.prefetch else None
+    job = Job(st["link_type"], inputs, "unique_id", 0, shard=(shard, n_shards), prefetch=pre)
     job.ctx.enable_timing(True)
     wall["job_setup_incl_uid_rank"] = time.perf_counter() - t
     t = time.perf_counter()

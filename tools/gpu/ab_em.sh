@@ -7,9 +7,10 @@ LIBS=${1:-}
 for cfg in 2 5; do
   for lib in A $LIBS; do
     if [ $lib == A ]; then unset SPLINK_AMD_LIB; else export SPLINK_AMD_LIB=$GRAFT_REPO_ROOT/splink_amd/$lib; fi
-    timeout -k 10 300 python -u bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline --em-scale 8 > gpurun_out/abem_${cfg}_$lib.json 2>/dev/null || exit 1
+    tag=${lib//\//_}
+    timeout -k 10 300 python -u bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline --em-scale 8 > gpurun_out/abem_${cfg}_$tag.json 2>/dev/null || exit 1
     python -c "
-import json; d=json.load(open('gpurun_out/abem_${cfg}_$lib.json')); b=d['breakdown_ms']; s=d.get('em_at_scale') or {}
+import json; d=json.load(open('gpurun_out/abem_${cfg}_$tag.json')); b=d['breakdown_ms']; s=d.get('em_at_scale') or {}
 e=s.get('em_iteration', {})
 print('cfg$cfg $lib', 'ms/step %.4f' % d['ms_per_step'], 'em %.4f' % b['em_hist'], 'at-scale em %.4f ms frac %.3f' % (e.get('avg_launch_ms', -1), e.get('frac', -1)), 'pairs', s.get('pairs'))" >> gpurun_out/abem.log
   done
