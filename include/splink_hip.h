@@ -262,6 +262,14 @@ int spk_gammas_simple_count(spk_ctx *ctx, int *out);
  * spk_gammas ran. */
 int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs);
 int spk_gammas_windows(spk_ctx *ctx, int64_t *out);
+/* Levenshtein exact pass kernel (same codes either way; for A/B tests): 1 = lane refill (default: a lane that
+ * finishes its cell takes the next one of its wave's range), 0 = one cell per lane per wave round. */
+int spk_gammas_set_lev_kernel(spk_ctx *ctx, int mode);
+/* Two-phase Levenshtein passes (same codes; tuning / A/B): the first phase scans at most `cap` text units per
+ * cell, the cells it leaves go to a second, uncapped phase.  exact_cap applies to the exact pass of free-text
+ * columns (rows past 64 units), slow_cap to the slow pass (rows of 65..128 units); 0 = one uncapped pass;
+ * multiples of 4. */
+int spk_gammas_set_lev_caps(spk_ctx *ctx, int exact_cap, int slow_cap);
 /* Filter regions (workgroups) the last spk_gammas ran over the second rule's view-ordered image. */
 int spk_gammas_view_regions(spk_ctx *ctx, int64_t *out);
 
@@ -297,10 +305,11 @@ int spk_em_iteration_wait(spk_ctx *ctx, double *out_stats, int n_stats);
  * with a caller buffer it returns once the histogram is final.  Callers sharding pairs over GPUs
  * all-reduce it (exact integer sum), then spk_em_finalize. */
 int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist);
-/* Histogram kernel choice (same result): 1 = lane-private LDS counters when the pattern space fits
- * (default), 0 = wave-ballot aggregation into one LDS histogram, 2 = as 1 with an agent-scope release
- * fence before each last-arriver ticket (the memory model's own ordering; 1 relies on gfx950's
- * write-through stores).  For testing and measurement. */
+/* Histogram kernel choice (same result): 1 = lane-private LDS counters when the pattern space fits, with an
+ * agent-scope release fence before each last-arriver ticket (default: the memory model's own ordering; it
+ * measured within 1 us of the unfenced form on MI355X, tools/ab_em_fence.py), 0 = wave-ballot aggregation
+ * into one LDS histogram, 2 = as 1 without the fence (relies on gfx950 draining the row atomics before the
+ * ticket).  For testing and measurement. */
 int spk_em_set_lane_histogram(spk_ctx *ctx, int on);
 /* E-step per pattern with the reference's literal arithmetic, then the M-step sums:
  * out_stats (host) = [Σmp, rows, non-null rows, Σ ln(λΠm + (1-λ)Πu), non-null ln rows] + per column k,

@@ -89,22 +89,19 @@ __global__ __launch_bounds__(H_THREADS) void k_hist(const CodeT *__restrict__ co
 // lane % R, R = 64 / 32 / 16 / 8 / 4 copies: with R = 64 every lane of a wave hits its own bank (64 x
 // 4-byte banks) whatever the codes are, so one code costs one conflict-free `ds_add_u32` and a couple of
 // VALU ops -- no ballots, no serialisation on the few dominant patterns.  Smaller R (larger pattern spaces)
-// admits 64 / R lanes per counter, and equal codes among them serialise on it.  Waves of a workgroup
-// share the copies (atomics; different instructions never bank-conflict).  Codes are streamed as 16-byte
-// vectors, four loads in flight per lane.
+// admits 64 / R lanes per counter, and equal codes among them serialise on it; there (R < 64) the most
+// frequent pattern of the pair set (found by the launch that first counts it) is not counted at all: its
+// bin is P minus every other bin, and the half or more of the codes that carry it skip the atomic.  Waves
+// of a workgroup share the copies (atomics; different instructions never bank-conflict).  Codes are
+// streamed as 16-byte vectors, four loads in flight per lane.
 //
-// Two tiers (R < 64, when the LDS left over holds them): the EM_TIER most frequent patterns of the pair set
-// (found by the launch that first counts it) get 64 lane-private copies each, every other pattern its R
-// copies; an LDS map (pattern -> first counter word, one uint16 per pattern) sends each code to its
-// counters.  Candidate pairs are mostly non-matches sharing a few hundred patterns, so nearly every code
-// lands on a conflict-free counter while the pattern space stays in LDS (cfg5: 2,880 patterns, R = 8,
-// 256 hot patterns x 64 copies + 2,880 x 8 = 153 KiB).  Any map counts exactly; it only decides which
-// counters a code uses.
+// Measured and not kept (round 5): two tiers for R < 64 -- the 256 most frequent patterns in 64-copy slots,
+// the others in R copies, an LDS map pattern -> counters -- with and without the uncounted top pattern:
+// the map read per code cost more than the conflicts it removed (cfg5 codes tiled to 368 M pairs: 0.177 ms
+// against 0.142; the real 100M-record share: 0.768 against 0.598 ms per iteration; profiles/r5_ab_em_tiers.log).
 constexpr int HL_THREADS = 1024;
 constexpr int HL_LDS_BYTES = 160 * 1024;  // one workgroup per CU, all of its LDS (gfx950), capped by the device attribute
-constexpr int HL_STATIC_LDS = 2048;       // k_em_iter's static LDS (finalize scratch), kept out of the plan
 constexpr int HL_UNROLL = 4;
-constexpr int EM_TIER = 256;              // hot patterns at most (64 copies each)
 constexpr int EM_AROWS = 4;               // the one-level reduction's rows (workgroup mod EM_AROWS)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -446,23 +443,21 @@ __global__ __launch_bounds__(EF_THREADS) void k_em_finalize(PatArgs A0, const un
 // -- one launch per EM iteration -- or writes the plain histogram to out_hist (multi-GPU: the caller
 // all-reduces it).  Workgroup 0 of a FIN launch streams nothing: it evaluates mp and ln(...) per pattern from
 // the parameters while the others stream (published with its ticket), so the finishing workgroup only runs
-// the M-step sums.  TIER: the two-tier counters, with the map gmap (pattern -> first counter word; hot
-// patterns [0, hb) in 64-copy slots, the others at hb + p * R); `refresh` makes the last workgroup rank the
-// patterns by count and write the map the next launches use.
+// the M-step sums.  R < 64: ghot[0] is the pattern not counted (-1: none yet); `refresh` makes the last
+// workgroup write the most frequent pattern there for the next launches.
 __host__ __device__ inline int64_t part_stride(int64_t n_pat) { return (n_pat + 31) / 32 * 32; }  // whole 128-B lines
-template <typename CodeT, int R, bool FIN, bool TIER>
+template <typename CodeT, int R, bool FIN>
 __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict__ codes, int64_t P, PatArgs A0,
                                                         unsigned int *__restrict__ ticket, double *__restrict__ mpat,
                                                         double *__restrict__ llpat, double *__restrict__ cpat,
                                                         double *__restrict__ out, unsigned long long *__restrict__ out_hist,
                                                         int fence, uint32_t *__restrict__ arow,
-                                                        uint16_t *__restrict__ gmap, int32_t *__restrict__ ghot, int hb,
-                                                        int refresh, int lds_bytes) {
+                                                        int32_t *__restrict__ ghot, int refresh, int lds_bytes) {
     extern __shared__ uint32_t sh[];
     __shared__ bool s_last;
     const int n_pat = A0.n_pat;
-    const int n_cnt = (TIER ? hb : 0) + n_pat * R;  // counter words; the map follows them
-    uint16_t *smap = reinterpret_cast<uint16_t *>(sh + n_cnt);
+    const int n_cnt = n_pat * R;  // counter words
+    constexpr bool HOT = R < 64;
 #ifdef SPK_EM_STAMPS
     const unsigned long long t_start = wall_clock64();
     if (blockIdx.x == 0) EM_STAMP(0);
@@ -482,29 +477,22 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         __syncthreads();
     }
     for (int b = threadIdx.x; b < n_cnt; b += HL_THREADS) sh[b] = 0;
-    if (TIER)
-        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) smap[b] = gmap[b];
-    // TIER: the most frequent pattern (rank 0 of the last ranking; -1 none) is not counted at all -- half or
-    // more of the codes skip the atomic -- and the last workgroup sets its bin to P minus every other bin
-    // (exact: every one of the P codes is streamed once and is < n_pat; P < 2^32 on this path)
-    const uint32_t hot0 = TIER ? (uint32_t)ghot[0] : 0xFFFFFFFFu;
+    // HOT: the most frequent pattern (-1: none yet) is not counted at all and the last workgroup sets its bin
+    // to P minus every other bin (exact: every one of the P codes is streamed once and is < n_pat; P < 2^32 on
+    // this path).  With R = 64 the compare would only cost issue slots in an issue-bound loop (cfg2 0.121 ->
+    // 0.147 ms at 368 M pairs when it ran there).
+    const uint32_t hot0 = HOT ? (uint32_t)ghot[0] : 0xFFFFFFFFu;
     __syncthreads();
     constexpr int VEC = 16 / sizeof(CodeT);
     constexpr int BITS = 8 * sizeof(CodeT);
-    const uint32_t lane = threadIdx.x & 63;
     const uint32_t copy = threadIdx.x & (R - 1);
     const u32x4 *cv = reinterpret_cast<const u32x4 *>(codes);
     const int64_t n_vec = P / VEC;
     const int64_t stride = (int64_t)(gridDim.x - (pre ? 1 : 0)) * HL_THREADS;
     int64_t v = (pre && blockIdx.x == 0) ? n_vec : (int64_t)(blockIdx.x - (pre ? 1 : 0)) * HL_THREADS + threadIdx.x;
     auto count_code = [&](uint32_t c) {
-        if (TIER) {
-            if (c == hot0) return;
-            const uint32_t b = smap[c];
-            atomicAdd(&sh[b + (b < (uint32_t)hb ? lane : copy)], 1u);
-        } else {
-            atomicAdd(&sh[c * R + copy], 1u);
-        }
+        if (HOT && c == hot0) return;
+        atomicAdd(&sh[c * R + copy], 1u);
     };
     auto count_word = [&](uint32_t w) {
 #pragma unroll
@@ -551,11 +539,13 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
 #ifdef SPK_EM_STAMPS
     const unsigned long long t_streamed = wall_clock64();
 #endif
-    // fence != 0 (spk_em_set_lane_histogram mode 2): an agent-scope release fence before each ticket, the
-    // ordering the HSA memory model itself guarantees (after the barrier it is cumulative over the
-    // workgroup's atomics); the A/B test checks both forms give the same statistics.  Default: the row adds
-    // are device-scope atomics performed at L2, drained (s_waitcnt) before the ticket atomic, which gfx950
-    // orders behind them (MI355X_MICROARCH.md visibility table, cdna_hip_programming.md G16 R1).
+    // fence != 0 (default): an agent-scope release fence before each ticket, the ordering the HSA memory model
+    // itself guarantees (after the barrier it is cumulative over the workgroup's atomics).  It cost nothing
+    // measurable on MI355X (tools/ab_em_fence.py: E+M launch 121.1 vs 121.7 us at cfg2 x8, 82.2 vs 82.2 us at
+    // cfg5 x4, medians of 20, identical statistics).  fence == 0 (spk_em_set_lane_histogram mode 2, A/B
+    // only): the row adds are device-scope atomics performed at L2, drained (s_waitcnt) before the ticket
+    // atomic, which gfx950 orders behind them (MI355X_MICROARCH.md visibility table, cdna_hip_programming.md
+    // G16 R1); the A/B test checks both forms give the same statistics.
     auto arrive = [&](unsigned int *t, unsigned int last) {  // true in the last arriver (whole workgroup)
         if (threadIdx.x == 0) {
             if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -573,19 +563,8 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     uint32_t *my_row = arow + (int64_t)(blockIdx.x % EM_AROWS) * ps;
     for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
         uint32_t c = 0;
-        if (TIER) {
-            const uint32_t base = smap[b];
-            if (base < (uint32_t)hb) {
-#pragma unroll 8
-                for (int k = 0; k < 64; ++k) c += sh[base + ((k + b) & 63)];  // rotate: spread banks
-            } else {
 #pragma unroll
-                for (int k = 0; k < R; ++k) c += sh[base + ((k + b) & (R - 1))];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < R; ++k) c += sh[b * R + ((k + b) & (R - 1))];
-        }
+        for (int k = 0; k < R; ++k) c += sh[b * R + ((k + b) & (R - 1))];  // rotate: spread banks
         if (c) __hip_atomic_fetch_add(my_row + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -620,7 +599,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     __syncthreads();
     for (int b = threadIdx.x; b < n_pat; b += HL_THREADS)
         for (int r = 0; r < nr; ++r) arow[r * ps + b] = 0u;
-    if (TIER && hot0 < (uint32_t)n_pat) {  // the uncounted pattern's bin: P minus every other bin
+    if (HOT && hot0 < (uint32_t)n_pat) {  // the uncounted pattern's bin: P minus every other bin
         __shared__ uint32_t s_rest[HL_THREADS / 64];
         uint32_t t = 0;
         for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) t += (uint32_t)p == hot0 ? 0u : s1[p];
@@ -643,19 +622,24 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         if (FIN) cpat[p] = (double)c;
         else out_hist[p] = c;
     }
-    if (TIER && refresh) {
-        // the next launches' map: pattern p's rank by (count desc, index asc); the hb / 64 first with a
-        // nonzero count get 64-copy slots (rank x 64), the others their R copies at hb + p x R
-        const int M = hb / 64;
+    if (HOT && refresh) {  // the most frequent pattern (ties: the lower one) for the next launches
+        __shared__ unsigned long long s_best[HL_THREADS / 64];
+        unsigned long long best = 0;
         for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
-            const uint32_t cp = s1[p];
-            int rank = 0;
-            for (int q = 0; q < n_pat; ++q) {
-                const uint32_t cq = s1[q];
-                rank += (cq > cp || (cq == cp && q < p)) ? 1 : 0;
-            }
-            gmap[p] = (uint16_t)((rank < M && cp > 0) ? rank * 64 : hb + p * R);
-            if (rank == 0) ghot[0] = cp > 0 ? p : -1;
+            const unsigned long long v = ((unsigned long long)s1[p] << 32) | (0xFFFFFFFFull - (uint32_t)p);
+            best = v > best ? v : best;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(best, off);
+            best = o > best ? o : best;
+        }
+        if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long bb = 0;
+            for (int w = 0; w < HL_THREADS / 64; ++w) bb = s_best[w] > bb ? s_best[w] : bb;
+            ghot[0] = (bb >> 32) ? (int32_t)(0xFFFFFFFFull - (bb & 0xFFFFFFFFull)) : -1;
         }
     }
     if (FIN) {
@@ -672,11 +656,6 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
-__global__ void k_em_map_init(int n_pat, int hb, int R, uint16_t *__restrict__ gmap, int32_t *__restrict__ ghot) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < n_pat) gmap[p] = (uint16_t)(hb + p * R);  // every pattern in the cold tier until ranked
-    if (p == 0) ghot[0] = -1;
-}
 
 // Final E-step: mp[i] = mpat[code[i]] for pairs [start, start + n).  Each lane turns two codes into
 // one 16-byte store of two doubles, so a wave instruction writes 1 KiB contiguous (the 8 B/pair of
@@ -770,34 +749,23 @@ static int pat_args(spk_ctx *ctx, double lambda, double one_minus, const double 
 using namespace spk;
 
 
-// The LDS plan of k_em_iter: R lane-private copies per pattern (64 .. 4) and, with R < 64, hb counter words
-// of 64-copy slots for the most frequent patterns (hb = 64 x M, M <= EM_TIER) when they fit next to the map.
-// R = 0: no lane path (the pattern space exceeds the LDS, or 2^32 or more pairs: k_em_iter sums its rows in
-// uint32); those take k_hist (uint64 counters) + k_em_finalize.
+// The LDS plan of k_em_iter: R lane-private copies per pattern (64 .. 4).  R = 0: no lane path (the pattern
+// space exceeds the LDS, or 2^32 or more pairs: k_em_iter sums its rows in uint32); those take k_hist (uint64
+// counters) + k_em_finalize.
 struct LanePlan {
-    int R = 0, hb = 0;
+    int R = 0;
     size_t bytes = 0;  // dynamic LDS of the launch
 };
 
 static LanePlan lane_plan(spk_ctx *ctx) {
     LanePlan L;
     const int64_t n_pat = ctx->n_patterns;
-    const int64_t budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block) - HL_STATIC_LDS;
+    const int64_t budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block);
     int R = 64;
     while (R >= 4 && n_pat * R * 4 > budget) R >>= 1;
     if (R < 4 || !ctx->hist_lanes || ctx->n_pairs >= (int64_t)UINT32_MAX) return L;
     L.R = R;
-    int64_t bytes = n_pat * R * 4;
-    if (R < 64) {
-        const int64_t map = (n_pat * 2 + 15) / 16 * 16;
-        int64_t M = EM_TIER;
-        while (M >= 16 && bytes + map + M * 64 * 4 > budget) M >>= 1;
-        if (M >= 16 && (M * 64 + n_pat * R) < 65536) {  // map entries are uint16 word offsets
-            L.hb = (int)(M * 64);
-            bytes += map + M * 64 * 4;
-        }
-    }
-    L.bytes = (size_t)std::max<int64_t>(bytes, (int64_t)sizeof(PatArgs));
+    L.bytes = (size_t)std::max<int64_t>(n_pat * R * 4, (int64_t)sizeof(PatArgs));
     return L;
 }
 
@@ -808,17 +776,16 @@ static int64_t lane_grid(spk_ctx *ctx) {
 }
 
 // The reduction rows and the ticket of k_em_iter (zero between launches: the last workgroup resets them,
-// zeroed here only when allocated) and the two-tier map, ranked again (by the launch's last workgroup) when
-// the pair set, the pattern space or the plan changed; repeated comparison passes over the same pairs keep it.
+// zeroed here only when allocated) and its uncounted pattern, found again (by the launch's last workgroup)
+// when the pair set or the pattern space changed; repeated comparison passes over the same pairs keep it.
 struct EmState {
     unsigned int *ticket = nullptr;
     uint32_t *arow = nullptr;
-    uint16_t *gmap = nullptr;
     int32_t *ghot = nullptr;
     int refresh = 0;
 };
 
-static int em_state(spk_ctx *ctx, const LanePlan &L, EmState &S) {
+static int em_state(spk_ctx *ctx, EmState &S) {
     if (!ctx->em_ticket.p) {
         SPK_TRY(ctx->em_ticket.alloc(1));
         SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, 4, ctx->stream));
@@ -830,21 +797,14 @@ static int em_state(spk_ctx *ctx, const LanePlan &L, EmState &S) {
     }
     S.ticket = ctx->em_ticket.p;
     S.arow = ctx->em_row.p;
-    if (L.hb) {
-        const std::vector<int64_t> key = {(int64_t)ctx->pairs_epoch, ctx->n_pairs, ctx->n_patterns, ctx->code_bytes,
-                                          L.R, L.hb};
-        if (ctx->em_map_key != key || !ctx->em_map.p) {
-            SPK_TRY(ctx->em_map.alloc((size_t)ctx->n_patterns));
-            SPK_TRY(ctx->em_hot.alloc(1));
-            k_em_map_init<<<(unsigned)((ctx->n_patterns + 255) / 256), 256, 0, ctx->stream>>>(
-                (int)ctx->n_patterns, L.hb, L.R, ctx->em_map.p, ctx->em_hot.p);
-            SPK_HIP(hipGetLastError());
-            ctx->em_map_key = key;
-            S.refresh = 1;
-        }
-        S.gmap = ctx->em_map.p;
-        S.ghot = ctx->em_hot.p;
+    if (!ctx->em_hot.p) {
+        SPK_TRY(ctx->em_hot.alloc(1));
+        SPK_HIP(hipMemsetAsync(ctx->em_hot.p, 0xFF, sizeof(int32_t), ctx->stream));
     }
+    const std::vector<int64_t> key = {(int64_t)ctx->pairs_epoch, ctx->n_pairs, ctx->n_patterns, ctx->code_bytes};
+    S.refresh = ctx->em_hot_key != key ? 1 : 0;
+    ctx->em_hot_key = key;
+    S.ghot = ctx->em_hot.p;
     return SPK_OK;
 }
 
@@ -854,26 +814,21 @@ static void launch_em_iter(spk_ctx *ctx, const LanePlan &L, const EmState &S, in
     const int64_t P = ctx->n_pairs;
     const int fence = ctx->em_fence ? 1 : 0;
     const unsigned grid = (unsigned)g;
-    if (ctx->code_bytes == 2) {
-        const auto *c = reinterpret_cast<const uint16_t *>(ctx->codes.p);
-        if (L.hb) k_em_iter<uint16_t, R, FIN, true><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
-            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, S.gmap, S.ghot, L.hb, S.refresh, (int)L.bytes);
-        else k_em_iter<uint16_t, R, FIN, false><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
-            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, nullptr, nullptr, 0, 0, (int)L.bytes);
-    } else {
-        const auto *c = reinterpret_cast<const uint32_t *>(ctx->codes.p);
-        if (L.hb) k_em_iter<uint32_t, R, FIN, true><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
-            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, S.gmap, S.ghot, L.hb, S.refresh, (int)L.bytes);
-        else k_em_iter<uint32_t, R, FIN, false><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
-            c, P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow, nullptr, nullptr, 0, 0, (int)L.bytes);
-    }
+    if (ctx->code_bytes == 2)
+        k_em_iter<uint16_t, R, FIN><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow,
+            S.ghot, S.refresh, (int)L.bytes);
+    else
+        k_em_iter<uint32_t, R, FIN><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow,
+            S.ghot, S.refresh, (int)L.bytes);
 }
 
 template <bool FIN>
 static int launch_em_lanes(spk_ctx *ctx, const LanePlan &L, const PatArgs &A, double *mpat, double *llpat,
                            double *cpat, double *out, unsigned long long *h) {
     EmState S;
-    SPK_TRY(em_state(ctx, L, S));
+    SPK_TRY(em_state(ctx, S));
     const int64_t g = lane_grid(ctx);
     switch (L.R) {
         case 64: launch_em_iter<64, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
@@ -952,7 +907,7 @@ static int finalize_from(spk_ctx *ctx, const unsigned long long *h, const PatArg
 extern "C" int spk_em_set_lane_histogram(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx && on >= 0 && on <= 2, SPK_E_INVALID, "spk_em_set_lane_histogram: mode 0, 1 or 2");
     ctx->hist_lanes = on != 0;
-    ctx->em_fence = on == 2;
+    ctx->em_fence = on != 2;
     return SPK_OK;
 }
 

@@ -691,7 +691,8 @@ __device__ int jw_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1
 // both rows' bit-planes are loaded in the same round trip as the records and the distance comes
 // from them alone (lev_rows_planes).  Rows without planes (> 64 units or a unit >= 256) go to the
 // global-memory pass.  A kernel of its own, so its register budget is not the JW path's.
-__device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level) {
+__device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level,
+                        int lim = LEV_NO_CAP) {
     uint64_t pa[N_PLANES], pb[N_PLANES];
     {
         const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
@@ -729,7 +730,8 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
                 if (lev < 0) {
                     if (eq == 1) lev = 0;
                     else if (!planes) return ST_NEEDS_SLOW;
-                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
+                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np, lim);
+                    if (lev == LEV_CAPPED) return ST_CAPPED;
                 }
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
@@ -802,7 +804,10 @@ __device__ inline void lev_sort_items(int &key, bool &have, int32_t &p, int32_t 
     key = s_key[t];
 }
 
-constexpr int LEV_WAVES = 5;
+#ifndef SPK_LEV_WAVES
+#define SPK_LEV_WAVES 5
+#endif
+constexpr int LEV_WAVES = SPK_LEV_WAVES;
 // The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD): capped at
 // 4 waves (128 VGPRs, 40 B of spills) it measured the same on MI355X (52.1 vs 52.3 us per call).
 constexpr int JW_WAVES = 1;
@@ -813,6 +818,8 @@ constexpr int JWC_WAVES = 4;
 struct ExactCols {
     int n;
     int g;  // blocks per column
+    int lim;  // X_LEV: scan cap (LEV_NO_CAP: none); capped cells go to the column's capped list
+    int src;  // X_LEV: 0 = the exact list, 1 = the capped list (the uncapped second pass)
     int si[4];
     int k[4], col[4];  // the columns' code positions and table columns (= simple[si].k / .col): the
                        // list bounds and the column descriptors load in one round, not after simple[si]
@@ -854,8 +861,9 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         s_c0 = A.cols0[colx];
         s_c1 = A.cols1[colx];
     }
-    const int64_t n = exact_count(A, xinfo, k);
-    const int32_t *items = xlist + xinfo[k];
+    const bool second = MODE == X_LEV && C.src == 1;  // the uncapped pass over the capped list
+    const int64_t n = second ? (xinfo[2 * A.K] ? 0 : (int64_t)A.slow_count[3 * A.K + k]) : exact_count(A, xinfo, k);
+    const int32_t *items = (second ? A.capped : xlist) + xinfo[k];
     const int64_t stride = (int64_t)C.g * X_THREADS;
     // software pipeline: the next item's pair rows (and, for Levenshtein, the rows' lengths) are in
     // flight while this one is evaluated
@@ -888,7 +896,7 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
             if (regroup) key2 = lev_work_bin(s_c0.meta[x2].len16, s_c1.meta[y2].len16);
         }
         if (regroup) lev_sort_items(key, have, p, x, y);
-        bool to_slow = false;
+        bool to_slow = false, capped = false;
         if (have && regroup && key >= 128) {
             // a row past 64 units (work bins 128 +): no 64-bit planes, the 128-bit slow pass takes the cell --
             // straight to its list, without loading the rows' planes and records first
@@ -896,17 +904,19 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         } else if (have) {
             int level = 0;
             int st;
-            if constexpr (MODE == X_LEV) st = lev_cell(sc, s_c0, s_c1, x, y, level);
+            if constexpr (MODE == X_LEV) st = lev_cell(sc, s_c0, s_c1, x, y, level, C.lim);
             else if constexpr (MODE == X_JW) st = jw_cell(sc, s_c0, s_c1, x, y, level);
             else st = simple_exact(A, sc, s_c0, s_c1, x, y, level);
 #ifdef SPK_X_STAMPS
             if (x_t2 == 0) x_t2 = wall_clock64() + (unsigned long long)(level & 0);
 #endif
-            if (st != ST_DONE) to_slow = true;
+            if (st == ST_CAPPED) capped = true;
+            else if (st != ST_DONE) to_slow = true;
             else if (C.n > 1) code_add_atomic(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
             else code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
         }
         wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
+        if (MODE == X_LEV && C.lim < LEV_NO_CAP) wave_append(A.capped + xinfo[k], A.slow_count + 3 * A.K + k, capped, p);
 #ifdef SPK_X_STAMPS
         x_cells += have ? 1 : 0;
 #endif
@@ -933,6 +943,462 @@ extern "C" int spk_debug_x_stamps(uint64_t *out, int n) {
     return SPK_OK;
 }
 #endif
+
+// ---- Levenshtein exact pass with lane refill from a per-wave queue ----------------------------------------------
+// In k_gamma_exact_simple<X_LEV> one lane scans one cell and a wave runs as long as its slowest lane: nearly every
+// wave of 64 cells holds one that runs to the end (a pair within the cut) while most stop early, so a wave ran
+// ~2-3x the mean trip count (tools/lev_refill_sim.py over the synthetic data: cfg5 addresses 12.8 steps per cell
+// on average with the diagonal exit, 39 for the slowest of 64; cfg2 emails 7.5 vs 14.6).  Here a lane that
+// finishes takes another cell, so a wave's steps follow the mean:
+//   - batch: all 64 lanes set up the next 64 cells of the wave's range at once (full SIMD width, as the per-lane
+//     kernel does): NULL / equal / length-gap / empty-remainder cells finish there, cells with a row past 64
+//     units or a unit >= 256 go to the slow list, and the rest -- stripped planes, lengths, cut -- go into the
+//     wave's LDS queue.  The batch runs when the queue is empty; its rows' records and planes were loaded by the
+//     previous batch (three-stage prefetch: list entries, row ids, records + planes), and it is the only place
+//     the loop touches global memory, so no wait in the loop waits on a load issued less than a batch ago;
+//   - round (every LEVQ_STEPS scan steps): finished cells' levels (table lookups, no fp64) go to an LDS result
+//     buffer (written as code adds at the next batch), and idle lanes take queued cells (LDS reads) when
+//     LEVQ_ADOPT or more are idle or few lanes still scan;
+//   - step: 32-bit words when every scanning lane's pattern has <= 32 units, else 64-bit; the text bit of
+//     step j is read from the fixed text planes (bfe).  Early exit on the end cell's diagonal (D[j + m - n][j] >
+//     cut proves the distance > cut: values never decrease along a diagonal), tested every LEVQ_STEPS steps.
+// Levels are lev_cell's: the same tests in the same order on the same (cut + 1 clamped) distance.
+constexpr int LEVQ_WAVES = 4;       // waves per SIMD (VGPR budget 128; the NP = 8 form takes 3)
+#ifndef SPK_LEVQ_ADOPT
+#define SPK_LEVQ_ADOPT 16
+#endif
+#ifndef SPK_LEVQ_STEPS
+#define SPK_LEVQ_STEPS 2
+#endif
+constexpr int LEVQ_ADOPT = SPK_LEVQ_ADOPT;  // idle lanes that trigger a hand-out while many lanes still scan
+constexpr int LEVQ_STEPS = SPK_LEVQ_STEPS;  // scan steps between rounds
+static_assert(32 % LEVQ_STEPS == 0, "k_lev_refill moves a text's upper plane words down between blocks, at j = 32");
+constexpr int LEVQ_WG_PER_CU = 4;
+constexpr int LEVQ_S = 129;         // len_l + len_r of rows with planes (<= 64 units each)
+
+// lev_cell's level of a cell from eq (1 equal / 0 unequal) and the clamped distance; nsum = na + nb.
+__device__ inline int lev_level_of(const SimpleCol &sc, int eq, int lev, int nsum) {
+    const double den = (double)nsum / 2.0;
+    for (int i = 0; i < sc.n_tests; ++i) {
+        const int op = sc.op[i], cmp = sc.cmp[i];
+        int r;
+        if (op == SPK_OP_STR_CMP) r = ((eq == 1) == (cmp == SPK_CMP_EQ)) ? KT : KF;
+        else if (op == SPK_OP_LEVRATIO && den == 0.0) r = KN;
+        else r = op == SPK_OP_LEV ? cmpd((double)lev, sc.t[i], cmp) : cmpd((double)lev / den, sc.t[i], cmp);
+        if (r == KT) return sc.level[i];
+    }
+    return sc.else_level;
+}
+
+// Diagnostic build only (-DSPK_LEVQ_STATS): per-launch totals of k_lev_refill's schedule (tools/ab_lev_refill.py
+// prints them): waves, batches, rounds, hand-out rounds, wave-steps by word width, lane-steps, cells scanned,
+// cycles in batches / in steps / in the whole loop.
+#ifdef SPK_LEVQ_STATS
+__device__ unsigned long long g_levq[16];
+#define LEVQ_STAT(i, v) (st_[i] += (unsigned long long)(v))
+#else
+#define LEVQ_STAT(i, v) ((void)0)
+#endif
+template <int NP>
+__global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_refill(GammaArgs A, int si, const int32_t *xlist,
+                                                                      const int64_t *xinfo) {
+    constexpr int WPB = X_THREADS / 64;
+    constexpr int QW = 4 * NP + 2;  // queue entry words: P (lo, hi), T (lo, hi) per plane, p, m | n | cut | nsum
+    __shared__ SimpleCol s_sc;
+    __shared__ ColDesc s_c0, s_c1;
+    __shared__ uint32_t s_q[WPB][QW][64];
+    __shared__ int32_t s_slow[WPB][128];
+    __shared__ uint32_t s_res[WPB][2][128];  // finished cells: p, code delta
+    __shared__ int8_t s_bp[LEVQ_S][MAX_TESTS];  // largest clamped distance passing test i (eq = 0), -1 none
+    __shared__ uint8_t s_cut[LEVQ_S];
+    __shared__ int s_tab;
+    if (threadIdx.x == 0) {
+        s_sc = A.simple[si];
+        s_c0 = A.cols0[s_sc.col];
+        s_c1 = A.cols1[s_sc.col];
+    }
+    __syncthreads();
+    const SimpleCol &sc = s_sc;
+    // per len_l + len_r: the cut and each test's threshold (the filter's integer forms: lev_a, the ratio tables)
+    for (int S = threadIdx.x; S < LEVQ_S; S += X_THREADS) {
+        const int c = simple_lev_cut(sc, S, 0);
+        s_cut[S] = (uint8_t)(c < 127 ? c : 127);  // distances here are <= 64: any cut >= 64 is no cut
+        for (int i = 0; i < sc.n_tests; ++i) {
+            int bp = -1;
+            if (sc.op[i] == SPK_OP_STR_CMP) bp = sc.cmp[i] == SPK_CMP_EQ ? -1 : 127;
+            else if (sc.op[i] == SPK_OP_LEV) bp = sc.lev_a[i];
+            else if (sc.thr_off[i] >= 0) bp = A.thr[sc.thr_off[i] + S];
+            s_bp[S][i] = (int8_t)(bp < -1 ? -1 : (bp > 127 ? 127 : bp));
+        }
+    }
+    if (threadIdx.x == 0) {  // every test a `<=` / `<` on the distance or a string (in)equality: levels by table
+        int ok = 1;
+        for (int i = 0; i < sc.n_tests; ++i) {
+            const int op = sc.op[i];
+            if (op == SPK_OP_LEV) ok &= (sc.tflag[i] & (TF_GE | TF_EXACT)) ? 0 : 1;
+            else if (op == SPK_OP_LEVRATIO) ok &= sc.thr_off[i] >= 0 ? 1 : 0;
+            else ok &= op == SPK_OP_STR_CMP ? 1 : 0;
+        }
+        s_tab = ok;
+    }
+    __syncthreads();
+    const bool tab = s_tab != 0;
+    const int k = sc.k, n_tests = sc.n_tests;
+    const uint32_t stride = (uint32_t)sc.stride;
+    auto level_of = [&](int lev, int S) -> int {  // eq = 0
+        if (!tab) return lev_level_of(sc, 0, lev, S);
+        int level = sc.else_level;
+        for (int i = n_tests - 1; i >= 0; --i) level = lev <= s_bp[S][i] ? sc.level[i] : level;
+        return level;
+    };
+    const int64_t n_items = exact_count(A, xinfo, k);
+    const int32_t *items = xlist + xinfo[k];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    // the wave's contiguous range of batches (64 list entries each)
+    const int64_t n_batches = (n_items + 63) / 64;
+    const int64_t n_waves = (int64_t)gridDim.x * WPB;
+    const int64_t per = (n_batches + n_waves - 1) / n_waves;
+    const int64_t w = (int64_t)blockIdx.x * WPB + wv;
+    const int64_t b_end = (w + 1) * per < n_batches ? (w + 1) * per : n_batches;
+    int64_t bn = w * per < b_end ? w * per : b_end;  // wave-uniform: next batch to set up
+    if (bn >= b_end) return;  // whole waves only: no barrier follows
+    // global-address-space views of the rows' records and planes (global_load, not flat: a flat load also
+    // counts against lgkmcnt, so the LDS reads after it would wait for the gather)
+    typedef const __attribute__((address_space(1))) uint32_t GWord;
+    typedef const __attribute__((address_space(1))) uint64_t GPlane;
+    // (read through the kernel-argument pointers, so they stay in scalar registers)
+    const int colx = A.simple[si].col;
+    GWord *meta0 = (GWord *)A.cols0[colx].meta, *meta1 = (GWord *)A.cols1[colx].meta;
+    GPlane *plane0 = (GPlane *)A.cols0[colx].planes, *plane1 = (GPlane *)A.cols1[colx].planes;
+    int32_t *slow_list = A.slow + A.slow_off[k];
+    unsigned int *slow_count = A.slow_count + k;
+    // list entry of this lane in batch b, clamped into the range (unconditional loads: no divergent skips)
+    auto entry = [&](int64_t b) -> int32_t {
+        const int64_t bb = b < b_end ? b : b_end - 1;
+        int64_t i = bb * 64 + lane;
+        i = i < n_items ? i : n_items - 1;
+        return items[i];
+    };
+    // staged batch: records (key, len16, head, cpf) and planes 0 .. NP - 1 of both rows
+    uint32_t ska = 0, skb = 0, sfa = 0, sfb = 0;
+    int32_t sla = 0, slb = 0;
+    uint64_t sha = 0, shb = 0;
+    uint64_t sqa[NP], sqb[NP];
+    auto stage = [&](int32_t x, int32_t y) {
+        GWord *ma = meta0 + (int64_t)x * 8, *mb = meta1 + (int64_t)y * 8;
+        ska = ma[0];
+        sla = (int32_t)ma[1];
+        sha = ((uint64_t)ma[5] << 32) | ma[4];
+        sfa = ma[7];
+        skb = mb[0];
+        slb = (int32_t)mb[1];
+        shb = ((uint64_t)mb[5] << 32) | mb[4];
+        sfb = mb[7];
+        GPlane *qa = plane0 + (int64_t)x * N_PLANES, *qb = plane1 + (int64_t)y * N_PLANES;
+#pragma unroll
+        for (int b = 0; b < NP; ++b) {
+            sqa[b] = qa[b];
+            sqb[b] = qb[b];
+        }
+    };
+    // prefetch pipeline: p0 = entry(bn) with its rows staged, p1 = entry(bn + 1) with row ids x1 / y1, p2 =
+    // entry(bn + 2)
+    int32_t p0 = entry(bn), p1 = entry(bn + 1), p2 = entry(bn + 2);
+    int32_t x1 = A.pl[p1], y1 = A.pr[p1];
+    stage(A.pl[p0], A.pr[p0]);
+    int q_head = 0, q_count = 0, n_res = 0, n_slow = 0;  // wave-uniform
+#ifdef SPK_LEVQ_STATS
+    unsigned long long st_[16] = {};
+    const unsigned long long t_loop = clock64();
+#endif
+    // the lane's cell: `active` while it holds one, `run` while its scan has text units left
+    bool active = false, run = false;
+    int32_t p = 0;
+    uint32_t P[2 * NP], T[2 * NP];  // (lo, hi) words of the pattern / text planes
+#pragma unroll
+    for (int b = 0; b < 2 * NP; ++b) P[b] = T[b] = 0;
+    uint64_t VP = 0, VN = 0;
+    int m = 1, n = 0, j = 0, cut = 0, S = 0;
+    auto flush_res = [&]() {  // the buffered code adds (fire-and-forget atomics)
+        for (int i = lane; i < n_res; i += 64) code_add_atomic(A, (int32_t)s_res[wv][0][i], s_res[wv][1][i]);
+        n_res = 0;
+    };
+    auto flush_slow = [&](int cnt) {  // the first cnt (<= 64) buffered slow cells to the slow list
+        unsigned int base = 0;
+        if (lane == 0) base = atomicAdd(slow_count, (unsigned int)cnt);
+        base = __shfl(base, 0);
+        if (lane < cnt) slow_list[base + lane] = s_slow[wv][lane];
+        const int rest = n_slow - cnt;
+        const int32_t moved = lane < rest ? s_slow[wv][cnt + lane] : 0;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < rest) s_slow[wv][lane] = moved;
+        __builtin_amdgcn_wave_barrier();
+        n_slow = rest;
+    };
+    for (;;) {
+        // ---- round: cells whose scan reached the end of the text, or whose end-cell diagonal passed the cut
+        // (D[j + m - n][j] > cut proves the distance > cut: values never decrease along a diagonal), get their
+        // level into the result buffer
+        {
+            bool fin = false;
+            int lev = 0;
+            if (active) {
+                const int i_end = run ? j + (m - n) : m;  // the end cell's diagonal, or row m at j = n
+                const uint64_t M = low_mask<uint64_t>(i_end);
+                const int d = j + popc_w(VP & M) - popc_w(VN & M);
+                fin = !run || d > cut;
+                lev = d > cut ? cut + 1 : d;
+            }
+            const unsigned long long fm = __ballot(fin);
+            if (fm) {
+                if (fin) {
+                    const int r = n_res + __popcll(fm & below);
+                    s_res[wv][0][r] = (uint32_t)p;
+                    s_res[wv][1][r] = (uint32_t)(level_of(lev, S) + 1) * stride;
+                    active = run = false;
+                }
+                __builtin_amdgcn_wave_barrier();
+                n_res += __popcll(fm);
+                if (n_res > 64) flush_res();  // (a batch flushes it; this only when batches ran out)
+            }
+        }
+        // a text past 32 units: its upper plane words move down once the scan reaches unit 32 (blocks of
+        // LEVQ_STEPS steps start at multiples of LEVQ_STEPS, a divisor of 32)
+        if (__any(run && j == 32)) {
+            if (run && j == 32) {
+#pragma unroll
+                for (int b = 0; b < NP; ++b) T[2 * b] = T[2 * b + 1];
+            }
+        }
+        const int n_act = __popcll(__ballot(active));
+        // ---- batch: set up the next 64 cells when the queue is empty
+        LEVQ_STAT(2, 1);
+        if (q_count == 0 && bn < b_end && (64 - n_act >= LEVQ_ADOPT || n_act == 0)) {
+#ifdef SPK_LEVQ_STATS
+            const unsigned long long t_b = clock64();
+            LEVQ_STAT(1, 1);
+#endif
+            // Order: (0) a full slow buffer's device atomic (its return waits for everything in flight -- here
+            // only the previous batch's loads and code adds), (1) the setup from the staged registers, (2) the
+            // next prefetch loads, (3) LDS writes and fire-and-forget code adds: nothing after (2) waits on a load
+            if (n_slow >= 64) flush_slow(64);
+            const int32_t pc = p0;
+            const int64_t left = n_items - bn * 64;
+            const bool valid = lane < left;
+            bool to_slow = false, done = false, scan = false, a_pat = false;
+            int level = 0, pre = 0;
+            uint32_t pk = 0;
+            if (valid) {
+                const RecMeta ma = {ska, sla, 0, sha, 0, sfa}, mb = {skb, slb, 0, shb, 0, sfb};
+                const int la = sla, lb = slb;
+                const int na = meta_cplen(ma), nb = meta_cplen(mb), s2 = na + nb;
+                if (la < 0 || lb < 0) {
+                    level = sc.null_level;
+                    done = true;
+                } else {
+                    const bool planes = (sfa & sfb & CPF_PLANES) != 0;
+                    int eq = meta_equal(ma, mb);
+                    if (eq < 0 && planes) {  // hash match without dictionary ids: the planes are the units
+                        bool same = la == lb;
+#pragma unroll
+                        for (int b = 0; b < NP; ++b) same = same && sqa[b] == sqb[b];
+                        eq = same ? 1 : 0;
+                    }
+                    if (eq == 1) {
+                        level = lev_level_of(sc, 1, 0, s2);
+                        done = true;
+                    } else if (!planes) {
+                        to_slow = true;  // > 64 units or a unit >= 256: the slow list's 128-bit / DP passes
+                    } else {
+                        const int c = s_cut[s2];
+                        int lev = -1;
+                        if (la == 0 || lb == 0) {
+                            lev = la + lb;
+                        } else {
+                            const int mn = la < lb ? la : lb;
+                            uint64_t d = 0, e = 0;
+#pragma unroll
+                            for (int b = 0; b < NP; ++b) {
+                                d |= sqa[b] ^ sqb[b];
+                                e |= (sqa[b] << (64 - la)) ^ (sqb[b] << (64 - lb));
+                            }
+                            pre = d ? __ffsll((unsigned long long)d) - 1 : 64;
+                            if (pre > mn) pre = mn;
+                            int suf = e ? __clzll((long long)e) : 64;
+                            if (suf > mn - pre) suf = mn - pre;
+                            const int ra = la - pre - suf, rb = lb - pre - suf;
+                            if (ra == 0 || rb == 0) {
+                                lev = ra + rb;
+                            } else {
+                                a_pat = ra >= rb;
+                                const int mm = a_pat ? ra : rb, nn = a_pat ? rb : ra;
+                                if (mm - nn > c) {
+                                    lev = c + 1;  // the length gap alone exceeds the cut
+                                } else {
+                                    pk = (uint32_t)mm | ((uint32_t)nn << 8) | ((uint32_t)c << 16) | ((uint32_t)s2 << 24);
+                                    scan = true;
+                                }
+                            }
+                        }
+                        if (!scan) {
+                            level = level_of(lev > c ? c + 1 : lev, s2);
+                            done = true;
+                        }
+                    }
+                }
+            }
+            // scan cells into the (empty) queue: the stripped planes, the longer remainder as the pattern
+            const unsigned long long sm = __ballot(scan);
+            if (scan) {
+                const int r = __popcll(sm & below);
+#pragma unroll
+                for (int b = 0; b < NP; ++b) {
+                    const uint64_t pp = (a_pat ? sqa[b] : sqb[b]) >> pre;
+                    const uint64_t tt = (a_pat ? sqb[b] : sqa[b]) >> pre;
+                    s_q[wv][2 * b][r] = (uint32_t)pp;
+                    s_q[wv][2 * b + 1][r] = (uint32_t)(pp >> 32);
+                    s_q[wv][2 * NP + 2 * b][r] = (uint32_t)tt;
+                    s_q[wv][2 * NP + 2 * b + 1][r] = (uint32_t)(tt >> 32);
+                }
+                s_q[wv][4 * NP][r] = (uint32_t)pc;
+                s_q[wv][4 * NP + 1][r] = pk;
+            }
+            q_head = 0;
+            q_count = __popcll(sm);
+            LEVQ_STAT(8, q_count);
+            // slow cells into the slow buffer
+            const unsigned long long wm = __ballot(to_slow);
+            if (wm) {
+                if (to_slow) s_slow[wv][n_slow + __popcll(wm & below)] = pc;
+                n_slow += __popcll(wm);
+            }
+            __builtin_amdgcn_wave_barrier();
+            // the prefetch pipeline moves one batch on: rows of bn + 1, row ids of bn + 2, entries of bn + 3
+            ++bn;
+            stage(x1, y1);
+            x1 = A.pl[p2];
+            y1 = A.pr[p2];
+            p0 = p1;
+            p1 = p2;
+            p2 = entry(bn + 2);
+            // settled cells' and buffered code adds (fire-and-forget)
+            if (done) code_add_atomic(A, pc, (uint32_t)(level + 1) * stride);
+            if (n_res) flush_res();
+            __builtin_amdgcn_wave_barrier();
+#ifdef SPK_LEVQ_STATS
+            LEVQ_STAT(9, clock64() - t_b);
+#endif
+        }
+        // ---- round: idle lanes take queued cells
+        if (q_count > 0) {
+            const unsigned long long im = __ballot(!active);
+            const int n_idle = __popcll(im);
+            if (n_idle >= LEVQ_ADOPT || 64 - n_idle < LEVQ_ADOPT) {
+                LEVQ_STAT(3, 1);
+                const int r = __popcll(im & below);
+                if (!active && r < q_count) {
+                    const int e = q_head + r;
+#pragma unroll
+                    for (int b = 0; b < NP; ++b) {
+                        P[2 * b] = s_q[wv][2 * b][e];
+                        P[2 * b + 1] = s_q[wv][2 * b + 1][e];
+                        T[2 * b] = s_q[wv][2 * NP + 2 * b][e];
+                        T[2 * b + 1] = s_q[wv][2 * NP + 2 * b + 1][e];
+                    }
+                    p = (int32_t)s_q[wv][4 * NP][e];
+                    const uint32_t pk = s_q[wv][4 * NP + 1][e];
+                    m = (int)(pk & 0xFF);
+                    n = (int)((pk >> 8) & 0xFF);
+                    cut = (int)((pk >> 16) & 0xFF);
+                    S = (int)(pk >> 24);
+                    VP = ~0ull;
+                    VN = 0;
+                    j = 0;
+                    active = run = true;
+                }
+                const int taken = n_idle < q_count ? n_idle : q_count;
+                q_head += taken;
+                q_count -= taken;
+            }
+        }
+        if (!__any(active)) {
+            if (bn >= b_end && q_count == 0) break;
+            continue;
+        }
+        // ---- LEVQ_STEPS scan steps of the lanes whose text has units left (a lane stops at j = n: its exec
+        // bit drops, no branch).  The word width is a wave-uniform choice per block of steps: 64-bit words only
+        // when some scanning lane needs them in the block.  A pattern of > 32 units needs them from text unit
+        // J0 = 31 - cut on (Ukkonen, as myers_plane_text_lazy): D[i][j] >= i - j, so rows >= 33 cannot hold a
+        // value <= cut before it, and until then a 32-bit step leaves rows 33 .. m at D[32][j] + (i - 32)
+        // (VP bits set, VN bits clear above row 32) -- upper bounds that differ from the true values only where
+        // both are > cut, so the cut tests and the clamped distance read the same.  The text's plane words are
+        // read at bit j & 31 of T[2b]; a lane's upper words move down at j = 32 (in the round, above).
+        bool need64 = false;
+        if (run && m > 32) need64 = j + LEVQ_STEPS > (cut < 31 ? 31 - cut : 0);
+        const bool wide = __any(need64);
+#ifdef SPK_LEVQ_STATS
+        const unsigned long long t_s = clock64();
+        LEVQ_STAT(wide ? 5 : 4, LEVQ_STEPS);
+        LEVQ_STAT(7, __popcll(__ballot(run)));
+#endif
+        if (!wide) {
+            for (int s = 0; s < LEVQ_STEPS; ++s) {
+                if (run) {
+                    uint32_t eq = ~0u;
+#pragma unroll
+                    for (int b = 0; b < NP; ++b)
+                        eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)T[2 * b], j, 1), P[2 * b]);
+                    uint32_t vp = (uint32_t)VP, vn = (uint32_t)VN;
+                    const uint32_t x = eq | vn;
+                    const uint32_t d0 = (((x & vp) + vp) ^ vp) | x;
+                    const uint32_t hp = (vn | ~(d0 | vp)) << 1 | 1u;
+                    const uint32_t hn = (d0 & vp) << 1;
+                    vp = hn | ~(d0 | hp);
+                    vn = hp & d0;
+                    VP = 0xFFFFFFFF00000000ull | vp;  // rows 33 .. m: D[32][j] + (i - 32)
+                    VN = vn;
+                    ++j;
+                    run = j < n;
+                }
+            }
+        } else {
+            for (int s = 0; s < LEVQ_STEPS; ++s) {
+                if (run) {
+                    const uint32_t jj = (uint32_t)j & 31u;
+                    uint32_t e0 = ~0u, e1 = ~0u;
+#pragma unroll
+                    for (int b = 0; b < NP; ++b) {
+                        const uint32_t mb = (uint32_t)__builtin_amdgcn_sbfe((int)T[2 * b], jj, 1);
+                        e0 = eq_plane(e0, mb, P[2 * b]);
+                        e1 = eq_plane(e1, mb, P[2 * b + 1]);
+                    }
+                    const uint64_t eq = ((uint64_t)e1 << 32) | e0;
+                    const uint64_t x = eq | VN;
+                    const uint64_t d0 = (((x & VP) + VP) ^ VP) | x;
+                    const uint64_t hp = (VN | ~(d0 | VP)) << 1 | 1ull;
+                    const uint64_t hn = (d0 & VP) << 1;
+                    VP = hn | ~(d0 | hp);
+                    VN = hp & d0;
+                    ++j;
+                    run = j < n;
+                }
+            }
+        }
+#ifdef SPK_LEVQ_STATS
+        LEVQ_STAT(10, clock64() - t_s);
+#endif
+    }
+#ifdef SPK_LEVQ_STATS
+    LEVQ_STAT(11, clock64() - t_loop);
+    LEVQ_STAT(0, 1);
+    if (lane == 0)
+        for (int i = 0; i < 12; ++i) atomicAdd(&g_levq[i], st_[i]);
+#endif
+    if (n_res) flush_res();
+    if (n_slow >= 64) flush_slow(64);
+    if (n_slow) flush_slow(n_slow);
+}
 
 // Global-memory pass over column k's slow list (length on the device; usually empty).  Cells with a
 // string past SLOW_LIMIT units go on to the huge pass: their list (counter slow_count[2K + k]) takes
@@ -968,7 +1434,7 @@ __global__ __launch_bounds__(64) void k_gamma_huge(GammaArgs A, int k, const int
 // (lev_rows_planes128) -- free-text columns such as cfg5's addresses land here; any other cell
 // (non-Latin-1 or longer rows) runs the global-memory evaluation of k_gamma_slow.
 __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y,
-                           int &level) {
+                           int &level, int lim = LEV_NO_CAP) {
     const RecMeta ma = c0.meta[x], mb = c1.meta[y];
     if (ma.len16 < 0 || mb.len16 < 0) {
         level = sc.null_level;
@@ -1022,8 +1488,11 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
             if (op == SPK_OP_LEVRATIO && den == 0.0) {
                 r = KN;
             } else {
-                if (lev < 0)
-                    lev = eq == 1 ? 0 : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
+                if (lev < 0) {
+                    lev = eq == 1 ? 0
+                                  : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np, lim);
+                    if (lev == LEV_CAPPED) return ST_CAPPED;
+                }
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
         }
@@ -1039,8 +1508,13 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
 // Cells without planes on both rows are handed on (rest list: column k's exact-list region, free
 // once the exact pass ran, and counter slow_count[K + k]) to k_gamma_rest, so this kernel does not
 // carry the general interpreter's registers (the 128-bit scan alone holds ~100).
+// Two phases (lim < LEV_NO_CAP): the first (src 0) scans at most lim text units per cell and lists the cells that
+// neither ended nor exited by then (the capped list, counter slow_count[4K + k]); the second (src 1) scans those
+// uncapped.  A wave runs as long as its slowest cell, and cfg5's long addresses scan 9 units on average but 45
+// for the slowest of 64 (tools/lev_refill_sim.py): the first phase bounds every wave, the second runs only the
+// few long scans, together.
 __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int si, int32_t *xlist,
-                                                              const int64_t *xinfo) {
+                                                              const int64_t *xinfo, int lim, int src) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
     if (threadIdx.x == 0) {
@@ -1050,17 +1524,18 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int s
     }
     __syncthreads();
     const int k = s_sc.k;
-    const int64_t n = A.slow_count[k];
-    const int32_t *items = A.slow + A.slow_off[k];
+    const int64_t n = src ? A.slow_count[4 * A.K + k] : A.slow_count[k];
+    const int32_t *items = src ? A.capped + xinfo[k] : A.slow + A.slow_off[k];
     int32_t *rest = xlist + xinfo[k];
     // (regrouping these cells by work bin, as k_gamma_exact_simple does for free-text columns,
     // measured no faster here: 2.43-2.47 ms per cfg5 call either way)
     for (int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * X_THREADS) {
         const int32_t p = items[i];
         int level = 0;
-        const bool done = lev_cell128(s_sc, s_c0, s_c1, A.pl[p], A.pr[p], level) == ST_DONE;
-        if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
-        wave_append(rest, A.slow_count + A.K + k, !done, p);
+        const int st = lev_cell128(s_sc, s_c0, s_c1, A.pl[p], A.pr[p], level, lim);
+        if (st == ST_DONE) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        wave_append(rest, A.slow_count + A.K + k, st != ST_DONE && st != ST_CAPPED, p);
+        if (lim < LEV_NO_CAP) wave_append(A.capped + xinfo[k], A.slow_count + 4 * A.K + k, st == ST_CAPPED, p);
     }
 }
 
@@ -1481,7 +1956,7 @@ struct GammaPlan {
     GammaArgs A{};
     std::vector<SimpleCol> simple;
     std::vector<int> simple_of;
-    std::vector<char> may_exact, huge_in_slow;
+    std::vector<char> may_exact, huge_in_slow, free_text;
     std::vector<char> slow_skipped;  // columns whose slow-list kernels this call did not launch
     int K = 0, n_regions = 0, n_info = 0, n_cnt = 0, n_all = 0;
     int64_t g_exact = 1, max_units = 1;
@@ -1504,7 +1979,11 @@ static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
         if (lev) {
             constexpr int SLOWLEV_WG_PER_CU = 8;  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU at once
             const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SLOWLEV_WG_PER_CU * ctx->n_cu));
-            k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
+            const int cap = ctx->lev_cap_slow > 0 ? ctx->lev_cap_slow : LEV_NO_CAP;
+            k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p, cap, 0);
+            if (cap < LEV_NO_CAP)
+                k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p,
+                                                                               LEV_NO_CAP, 1);
             k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
         } else {
             k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
@@ -1523,8 +2002,9 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         return skip && (ctx->slow_force_skip ||
                         (ctx->slow_seen_valid && k < (int)ctx->slow_seen.size() && !ctx->slow_seen[k]));
     };
-    SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));
+    SPK_TRY(ctx->xlist.alloc((size_t)(3 * cap)));
     A.slow = ctx->xlist.p + cap;
+    A.capped = ctx->xlist.p + 2 * cap;
     A.slow_off = ctx->xinfo.p;
     ctx->xcap = cap;
     if (A.P <= 0) {
@@ -1582,7 +2062,21 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         if (fused) continue;
         const ColSet one_k{1, {k, 0, 0, 0}};
         k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
-        if (lev) {
+        if (lev && ctx->lev_refill) {
+            // one resident round (LEVQ_WAVES per SIMD, 3 for NP = 8): every wave owns a contiguous range of the list
+            const int64_t wg_cu = simple[si].np >= 8 ? 3 : LEVQ_WG_PER_CU;
+            const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, wg_cu * ctx->n_cu));
+            SPK_TRY(ctx->xbegin(k));
+            switch (simple[si].np) {
+                case 5: k_lev_refill<5><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                case 6: k_lev_refill<6><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                case 7: k_lev_refill<7><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                default: k_lev_refill<8><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+            }
+            SPK_TRY(ctx->xend(k));
+            if (quiet(k)) G.slow_skipped[k] = 1;
+            else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
+        } else if (lev) {
             ExactCols one{};
             one.n = 1;
             // one resident round: the grid-stride loop gives every block a fixed share of the list, so a
@@ -1593,9 +2087,20 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
             one.si[0] = si;
             one.k[0] = simple[si].k;
             one.col[0] = simple[si].col;
+            // two phases in free-text columns (rows past 64 units: their scans spread widely), see k_gamma_slow_lev
+            const bool free_text = G.free_text[k] != 0;
+            one.lim = (free_text && ctx->lev_cap_exact > 0) ? ctx->lev_cap_exact : LEV_NO_CAP;
+            one.src = 0;
             SPK_TRY(ctx->xbegin(k));
             k_gamma_exact_simple<X_LEV><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
                                                                                       ctx->xinfo.p);
+            if (one.lim < LEV_NO_CAP) {
+                ExactCols two = one;
+                two.lim = LEV_NO_CAP;
+                two.src = 1;
+                k_gamma_exact_simple<X_LEV><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, two, ctx->xlist.p,
+                                                                                          ctx->xinfo.p);
+            }
             SPK_TRY(ctx->xend(k));
             if (quiet(k)) G.slow_skipped[k] = 1;
             else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
@@ -1906,7 +2411,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     // One device info block, read back with one copy: xinfo (k_prefix: list bases and counts, overflow,
     // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed per window.
     const int n_info = 2 * K + 2;
-    const int n_cnt = (3 * K + 1) / 2;  // int64 slots of the 3K uint32 list lengths
+    const int n_cnt = (5 * K + 1) / 2;  // int64 slots of the 5K uint32 list lengths
     const int n_all = n_info + n_cnt + 2;  // + the error word and k_prefix's completion counter
     SPK_TRY(ctx->xinfo.alloc((size_t)n_all));
     SPK_TRY(ctx->pinned_info((size_t)n_all));
@@ -1958,6 +2463,11 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     G.may_exact.assign(K, 1);  // columns whose filter can leave cells undecided
     for (const SimpleCol &sc : simple)
         if (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids)) G.may_exact[sc.k] = 0;
+    G.free_text.assign(K, 0);  // simple columns with rows past 64 UTF-8 bytes on both sides (planes_hi)
+    for (const SimpleCol &sc : simple) {
+        const Column *a = t0.cols[sc.col], *b = t1.cols[sc.col];
+        G.free_text[sc.k] = (a && b && a->planes_hi.n && b->planes_hi.n) ? 1 : 0;
+    }
     G.huge_in_slow.assign(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
     for (int k = 0; k < K; ++k)
         G.huge_in_slow[k] = (G.may_exact[k] && G.simple_of[k] >= 0 && simple[G.simple_of[k]].cls == SC_LEV) ? 1 : 0;
@@ -2338,5 +2848,31 @@ extern "C" int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs) {
 extern "C" int spk_gammas_windows(spk_ctx *ctx, int64_t *out) {
     SPK_REQUIRE(ctx && out, SPK_E_INVALID, "spk_gammas_windows: bad args");
     *out = ctx->last_windows;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_set_lev_kernel(spk_ctx *ctx, int mode) {
+    SPK_REQUIRE(ctx && (mode == 0 || mode == 1), SPK_E_INVALID, "spk_gammas_set_lev_kernel: mode 0 or 1");
+    ctx->lev_refill = mode == 1;
+    return SPK_OK;
+}
+
+#ifdef SPK_LEVQ_STATS
+extern "C" int spk_debug_levq_stats(uint64_t *out, int reset) {
+    SPK_HIP(hipDeviceSynchronize());
+    SPK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_levq), sizeof(uint64_t) * 16));
+    if (reset) {
+        static const unsigned long long zero[16] = {};
+        SPK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_levq), zero, sizeof(zero)));
+    }
+    return SPK_OK;
+}
+#endif
+
+extern "C" int spk_gammas_set_lev_caps(spk_ctx *ctx, int exact_cap, int slow_cap) {
+    SPK_REQUIRE(ctx && exact_cap >= 0 && slow_cap >= 0 && exact_cap % 4 == 0 && slow_cap % 4 == 0, SPK_E_INVALID,
+                "spk_gammas_set_lev_caps: caps >= 0, multiples of 4 (0 = one uncapped pass)");
+    ctx->lev_cap_exact = exact_cap;
+    ctx->lev_cap_slow = slow_cap;
     return SPK_OK;
 }

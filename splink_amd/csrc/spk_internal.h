@@ -300,6 +300,9 @@ struct spk_ctx {
     // (settle_gammas runs them if the list is not empty after all)
     std::vector<uint8_t> slow_seen;
     bool slow_seen_valid = false;
+    bool lev_refill = false;       // Levenshtein exact pass: k_lev_refill (else k_gamma_exact_simple<X_LEV>)
+    int lev_cap_exact = 0;         // two-phase Levenshtein passes: scan cap of the first phase (0 = one pass) --
+    int lev_cap_slow = 0;          // exact pass in free-text columns, slow pass (rows of 65..128 units)
     bool slow_force_skip = false;  // tests: leave every slow-list launch to settle_gammas
     uint64_t slow_key_pairs = 0, slow_key_tables = 0;
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
@@ -309,9 +312,8 @@ struct spk_ctx {
     spk::DevBuf<double> mpat, llpat, cpat, stats, mu;  // per pattern: mp, ln(...), count; statistics; m / u
     spk::DevBuf<unsigned int> em_ticket;  // k_em_iter's last-workgroup ticket (kept zero between launches)
     spk::DevBuf<uint32_t> em_row;         // its reduction rows (kept zero between launches)
-    spk::DevBuf<uint16_t> em_map;         // its two-tier map: pattern -> first counter word (spk_em.hip)
-    spk::DevBuf<int32_t> em_hot;          // the pattern it does not count (rank 0 of the map; -1 none)
-    std::vector<int64_t> em_map_key;      // the pair set / pattern space / LDS plan the map was ranked for
+    spk::DevBuf<int32_t> em_hot;          // the pattern it does not count with R < 64 lane copies (-1: none yet)
+    std::vector<int64_t> em_hot_key;      // the pair set / pattern space it was found for
     double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;
     int n_cu = 256;                   // compute units of the device (grid sizing)
@@ -345,7 +347,7 @@ struct spk_ctx {
     spk::DevBuf<unsigned int> tf_runs, tf_nruns;
     std::vector<int64_t> tf_key;
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
-    bool em_fence = false;   // k_em_iter: release fence before each ticket (spk_em_set_lane_histogram mode 2)
+    bool em_fence = true;    // k_em_iter: release fence before each ticket (spk_em_set_lane_histogram 2: none)
 
     // asynchronous EM iteration (spk_em_iteration_start / _wait): the statistics land in h_stats behind
     // ev_stats; the arguments are kept so that the launch can be repeated when the codes it read are

@@ -496,19 +496,24 @@ __device__ inline int diag_score(W vp, W vn, int j, int m, int n) {
 // NP: the scans read planes 0..NP-1 only.  A caller passes NP < 8 when every unit of the column
 // (both sides) has the same bits NP..7 (e.g. 7 for ASCII text): those planes' terms then only touch
 // mask bits above the pattern, which never reach the rows below (carries and shifts move upward).
+// lim: scan at most lim text units (a multiple of 4); a cell that neither ended nor exited by then returns
+// LEV_CAPPED, and its caller hands it to a second, uncapped pass (the two-phase exact and slow passes).
+constexpr int LEV_CAPPED = -2;
+constexpr int LEV_NO_CAP = 1 << 30;
 template <typename W, int NP = N_PLANES>
 __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
-                                       int cut) {
+                                       int cut, int lim = LEV_NO_CAP) {
+    const int nl = n < lim ? n : lim;
     W pl[N_PLANES];
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
     W vp = ~(W)0, vn = 0;
     const W M = low_mask<W>(m);
-    for (int h = 0; h < 2 && 32 * h < n; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
+    for (int h = 0; h < 2 && 32 * h < nl; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
         uint32_t tw[N_PLANES];
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
-        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        const int jn = nl - 32 * h < 32 ? nl - 32 * h : 32;
         for (int jj = 0; jj < jn; ++jj) {
             W eq = ~(W)0;
 #pragma unroll
@@ -520,16 +525,12 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
             const W hn = (d0 & vp) << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
-            // The bound dist - (units left) never decreases and ends at dist, so testing it every
-            // fourth unit plus clamping at the end returns cut + 1 for exactly the cells a per-unit
-            // test cuts.
-            if ((jj & 3) == 3) {
-                const int j = 32 * h + jj;
-                const int dist = j + 1 + popc_w(vp & M) - popc_w(vn & M);
-                if (dist - (n - 1 - j) > cut) return cut + 1;
-            }
+            // every fourth unit: the end cell's diagonal (diag_score; it dominates the bound dist - (units
+            // left)).  Clamping at the end returns cut + 1 for every cell whose distance passes the cut.
+            if ((jj & 3) == 3 && diag_score<W>(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
+    if (nl < n) return LEV_CAPPED;
     const int dist = n + popc_w(vp & M) - popc_w(vn & M);
     return dist > cut ? cut + 1 : dist;
 }
@@ -545,7 +546,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
 // same loops with their one word.  cfg2 emails: most waves hold a cell of 33+ units, cut ~ 10.
 template <int NP = N_PLANES>
 __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
-                                            int cut) {
+                                            int cut, int lim = LEV_NO_CAP) {
     const bool wide = m > 32;
     const int mine = wide ? (cut < 31 ? 31 - cut : 0) : 32;
     int lo = 0, hi = 32;  // wave minimum of `mine` (active lanes) by bisection over ballots
@@ -563,7 +564,8 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
     }
     uint32_t vp = ~0u, vn = 0;
     const uint32_t M1 = low_mask<uint32_t>(wide ? 32 : m);  // the rows the first phase scores
-    const int j1 = n < J0 ? n : J0;
+    const int nl = n < lim ? n : lim;
+    const int j1 = nl < J0 ? nl : J0;
     for (int j = 0; j < j1; ++j) {
         uint32_t eq = ~0u;
 #pragma unroll
@@ -574,23 +576,23 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
         const uint32_t hn = (d0 & vp) << 1;
         vp = hn | ~(d0 | hp);
         vn = hp & d0;
-        if (!wide && (j & 3) == 3) {
-            const int dist = j + 1 + popc_w(vp & M1) - popc_w(vn & M1);
-            if (dist - (n - 1 - j) > cut) return cut + 1;
-        }
+        // the end cell's diagonal (diag_score) -- for a wide pattern too: its row i* = j + 1 + m - n <= 31
+        // here (m - n <= cut, j < J0 <= 31 - cut) is one of the rows this phase tracks exactly
+        if ((j & 3) == 3 && diag_score<uint32_t>(vp, vn, j, m, n) > cut) return cut + 1;
     }
-    if (n <= J0) {
+    if (n <= J0 && n <= lim) {
         const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 32 : 0);
         return dist > cut ? cut + 1 : dist;
     }
+    if (nl <= J0) return LEV_CAPPED;  // lim < n, reached in the first phase
     // rows 33..m enter with vertical deltas +1 (D[32][J0] + (i - 32))
     uint64_t VP = (uint64_t)vp | 0xFFFFFFFF00000000ull, VN = vn;
     const uint64_t M2 = low_mask<uint64_t>(m);
-    for (int h = J0 >> 5; h < 2 && 32 * h < n; ++h) {
+    for (int h = J0 >> 5; h < 2 && 32 * h < nl; ++h) {
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
         const int jb = 32 * h < J0 ? J0 - 32 * h : 0;
-        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        const int jn = nl - 32 * h < 32 ? nl - 32 * h : 32;
         for (int jj = jb; jj < jn; ++jj) {
             uint64_t eq = ~0ull;
 #pragma unroll
@@ -602,13 +604,10 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
             const uint64_t hn = (d0 & VP) << 1;
             VP = hn | ~(d0 | hp);
             VN = hp & d0;
-            if ((jj & 3) == 3) {
-                const int j = 32 * h + jj;
-                const int dist = j + 1 + popc_w(VP & M2) - popc_w(VN & M2);
-                if (dist - (n - 1 - j) > cut) return cut + 1;
-            }
+            if ((jj & 3) == 3 && diag_score<uint64_t>(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
+    if (nl < n) return LEV_CAPPED;
     const int dist = n + popc_w(VP & M2) - popc_w(VN & M2);
     return dist > cut ? cut + 1 : dist;
 }
@@ -620,7 +619,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
 // the scan runs over the shorter one.  `cut` as in lev_planes.
 template <int NP>
 __device__ inline int lev_rows_planes_np(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
-                                         int cut) {
+                                         int cut, int lim = LEV_NO_CAP) {
     if (la == 0) return lb;
     if (lb == 0) return la;
     const int mn = la < lb ? la : lb;
@@ -639,6 +638,7 @@ __device__ inline int lev_rows_planes_np(const uint64_t (&pa)[N_PLANES], int la,
     if (rb == 0) return ra;
     const bool a_pat = ra >= rb;
     const int m = a_pat ? ra : rb, n = a_pat ? rb : ra;
+    if (m - n > cut) return cut + 1;  // the length gap alone (the lazy scans' diagonal tests rely on m - n <= cut)
     uint64_t P[N_PLANES], T[N_PLANES];
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) {
@@ -646,18 +646,18 @@ __device__ inline int lev_rows_planes_np(const uint64_t (&pa)[N_PLANES], int la,
         T[b] = (a_pat ? pb[b] : pa[b]) >> pre;
     }
     // one word width for all active lanes: a wave that mixed both would run both loops
-    if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P, m, T, n, cut);
-    return myers_plane_text_lazy<NP>(P, m, T, n, cut);
+    if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P, m, T, n, cut, lim);
+    return myers_plane_text_lazy<NP>(P, m, T, n, cut, lim);
 }
 
 // np: planes the scans need (wave-uniform; see myers_plane_text), 8 when unknown.
 __device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
-                                      int cut, int np = N_PLANES) {
+                                      int cut, int np = N_PLANES, int lim = LEV_NO_CAP) {
     switch (np) {
-        case 5: return lev_rows_planes_np<5>(pa, la, pb, lb, cut);
-        case 6: return lev_rows_planes_np<6>(pa, la, pb, lb, cut);
-        case 7: return lev_rows_planes_np<7>(pa, la, pb, lb, cut);
-        default: return lev_rows_planes_np<N_PLANES>(pa, la, pb, lb, cut);
+        case 5: return lev_rows_planes_np<5>(pa, la, pb, lb, cut, lim);
+        case 6: return lev_rows_planes_np<6>(pa, la, pb, lb, cut, lim);
+        case 7: return lev_rows_planes_np<7>(pa, la, pb, lb, cut, lim);
+        default: return lev_rows_planes_np<N_PLANES>(pa, la, pb, lb, cut, lim);
     }
 }
 
@@ -726,7 +726,7 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
 // their text in the cheaper first phase.
 template <int NP = N_PLANES>
 __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
-                                               int cut) {
+                                               int cut, int lim = LEV_NO_CAP) {
     const bool wide = m > 64;
     const int mine = wide ? (cut < 63 ? 63 - cut : 0) : 128;
     int lo = 0, hi = 128;  // wave minimum of `mine` (active lanes) by bisection over ballots
@@ -741,7 +741,8 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (uint64_t)P[b];
     uint64_t vp = ~0ull, vn = 0;
     const uint64_t M1 = low_mask<uint64_t>(wide ? 64 : m);  // the rows the first phase scores
-    const int j1 = n < J0 ? n : J0;
+    const int nl = n < lim ? n : lim;
+    const int j1 = nl < J0 ? nl : J0;
     for (int h = 0; h < 4 && 32 * h < j1; ++h) {
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -757,22 +758,24 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
             const uint64_t hn = (d0 & vp) << 1;
             vp = hn | ~(d0 | hp);
             vn = hp & d0;
-            if (!wide && (jj & 3) == 3 && diag_score<uint64_t>(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;
+            // diagonal exit for a wide pattern too: row i* = j + 1 + m - n <= 63 here (m - n <= cut, j < J0 <= 63 - cut)
+            if ((jj & 3) == 3 && diag_score<uint64_t>(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
-    if (n <= J0) {
+    if (n <= J0 && n <= lim) {
         const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 64 : 0);
         return dist > cut ? cut + 1 : dist;
     }
+    if (nl <= J0) return LEV_CAPPED;  // lim < n, reached in the first phase
     // rows 65..m enter with vertical deltas +1 (D[64][J0] + (i - 64))
     u128 VP = (u128)vp | ((u128)~0ull << 64), VN = vn;
 
-    for (int h = J0 >> 5; h < 4 && 32 * h < n; ++h) {
+    for (int h = J0 >> 5; h < 4 && 32 * h < nl; ++h) {
         uint32_t tw[N_PLANES];
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
         const int jb = 32 * h < J0 ? J0 - 32 * h : 0;
-        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        const int jn = nl - 32 * h < 32 ? nl - 32 * h : 32;
         for (int jj = jb; jj < jn; ++jj) {
             uint64_t e0 = ~0ull, e1 = ~0ull;
 #pragma unroll
@@ -790,6 +793,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
             if ((jj & 3) == 3 && diag_score128(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
+    if (nl < n) return LEV_CAPPED;
     const int dist = diag_score128(VP, VN, n - 1, m, n);
     return dist > cut ? cut + 1 : dist;
 }
@@ -799,7 +803,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
 // one-word scan (the same word width for the whole wave), else the 128-bit one.
 template <int NP>
 __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
-                                            int cut) {
+                                            int cut, int lim = LEV_NO_CAP) {
     if (la == 0) return lb;
     if (lb == 0) return la;
     const int mn = la < lb ? la : lb;
@@ -818,6 +822,7 @@ __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, 
     if (rb == 0) return ra;
     const bool a_pat = ra >= rb;
     const int m = a_pat ? ra : rb, n = a_pat ? rb : ra;
+    if (m - n > cut) return cut + 1;  // the length gap alone (the lazy scans' diagonal tests rely on m - n <= cut)
     u128 P[N_PLANES], T[N_PLANES];
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) {
@@ -831,19 +836,19 @@ __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, 
             P64[b] = (uint64_t)P[b];
             T64[b] = (uint64_t)T[b];
         }
-        if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P64, m, T64, n, cut);
-        return myers_plane_text_lazy<NP>(P64, m, T64, n, cut);
+        if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P64, m, T64, n, cut, lim);
+        return myers_plane_text_lazy<NP>(P64, m, T64, n, cut, lim);
     }
-    return myers_plane_text128_lazy<NP>(P, m, T, n, cut);
+    return myers_plane_text128_lazy<NP>(P, m, T, n, cut, lim);
 }
 
 __device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
-                                         int cut, int np = N_PLANES) {
+                                         int cut, int np = N_PLANES, int lim = LEV_NO_CAP) {
     switch (np) {
-        case 5: return lev_rows_planes128_np<5>(pa, la, pb, lb, cut);
-        case 6: return lev_rows_planes128_np<6>(pa, la, pb, lb, cut);
-        case 7: return lev_rows_planes128_np<7>(pa, la, pb, lb, cut);
-        default: return lev_rows_planes128_np<N_PLANES>(pa, la, pb, lb, cut);
+        case 5: return lev_rows_planes128_np<5>(pa, la, pb, lb, cut, lim);
+        case 6: return lev_rows_planes128_np<6>(pa, la, pb, lb, cut, lim);
+        case 7: return lev_rows_planes128_np<7>(pa, la, pb, lb, cut, lim);
+        default: return lev_rows_planes128_np<N_PLANES>(pa, la, pb, lb, cut, lim);
     }
 }
 

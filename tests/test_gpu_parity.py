@@ -587,7 +587,7 @@ def test_em_histogram_kernels_agree(amd, n_levels):
     codes = ((g.astype(np.int64) + 1) * stride).sum(axis=1)
     want = np.bincount(codes, minlength=n_pat)
     got = []
-    for lanes in (1, 0, 2):  # 2: lane counters with a release fence before each last-arriver ticket
+    for lanes in (1, 0, 2):  # 2: lane counters without the release fence before each last-arriver ticket
         ctx.em_set_lane_histogram(lanes)
         hist = np.zeros(n_pat, dtype=np.uint64)
         import torch
@@ -641,6 +641,23 @@ def _mutate(rng, s, k, alpha):
     return "".join(s)
 
 
+# Levenshtein pass variants that must give the same codes: (exact kernel, exact-pass cap, slow-pass cap) --
+# one uncapped pass, tiny first-phase caps (most cells go through both phases), the lane-refill kernel
+LEV_VARIANTS = [(0, 0, 0), (0, 4, 4), (0, 12, 8), (1, 0, 4)]
+
+
+def _lev_variants_agree(job, settings, want):
+    try:
+        for kern, xcap, scap in LEV_VARIANTS:
+            job.ctx.gammas_set_lev_kernel(kern)
+            job.ctx.gammas_set_lev_caps(xcap, scap)
+            job.gammas(settings)
+            assert (job.gammas_host() == want).all(), (kern, xcap, scap)
+    finally:
+        job.ctx.gammas_set_lev_kernel(0)
+        job.ctx.gammas_set_lev_caps(0, 0)
+
+
 def test_levenshtein_levels_exact(amd):
     """Exact Levenshtein in the template exact pass (bit-plane path, unit path, the 128-bit plane path
     of the slow list and the global-memory pass): six `<=` levels reveal the distance up to 5, a
@@ -673,7 +690,8 @@ def test_levenshtein_levels_exact(amd):
         {"custom_name": "lv", "custom_columns_used": ["a"], "num_levels": 7, "case_expression": exact,
          "m_probabilities": [0.1, 0.1, 0.1, 0.1, 0.1, 0.2, 0.3], "u_probabilities": [0.4, 0.2, 0.1, 0.1, 0.1, 0.05, 0.05]},
         {"custom_name": "lr", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": ratio}]}
-    got = add_gammas(df, st, amd).gamma_matrix()
+    gf = add_gammas(df, st, amd)
+    got = gf.gamma_matrix()
     for i, (a, b) in enumerate(zip(left, right)):
         if a is None or b is None:
             assert got[i, 0] == -1 and got[i, 1] == -1
@@ -687,6 +705,7 @@ def test_levenshtein_levels_exact(amd):
             q = d / den if den else None
             want = 2 if q is not None and q <= 0.2 else (1 if q is not None and q <= 0.4 else 0)
         assert got[i, 1] == want, (a, b, d, got[i, 1])
+    _lev_variants_agree(gf.job, gf.settings, got)
 
 
 @pytest.mark.parametrize("alpha,planes", [
@@ -721,7 +740,8 @@ def test_levenshtein_reduced_planes(amd, alpha, planes):
          "m_probabilities": [0.1, 0.1, 0.1, 0.1, 0.1, 0.2, 0.3], "u_probabilities": [0.4, 0.2, 0.1, 0.1, 0.1, 0.05, 0.05]},
         {"custom_name": "lr", "custom_columns_used": ["a"], "num_levels": 4,
          "case_expression": cs.sql_gen_case_stmt_levenshtein_4("a")}]}
-    got = add_gammas(df, st, amd).gamma_matrix()
+    gf = add_gammas(df, st, amd)
+    got = gf.gamma_matrix()
     for i, (a, b) in enumerate(zip(left, right)):
         if a is None or b is None:
             assert got[i, 0] == -1 and got[i, 1] == -1
@@ -731,6 +751,7 @@ def test_levenshtein_reduced_planes(amd, alpha, planes):
         den = (len(a) + len(b)) / 2.0
         want = 3 if a == b else (2 if den and d / den <= 0.2 else (1 if den and d / den <= 0.4 else 0))
         assert got[i, 1] == want, (a, b, d, got[i, 1])
+    _lev_variants_agree(gf.job, gf.settings, got)
 
 
 def test_exact_work_lists_grow(amd):
@@ -796,6 +817,8 @@ def test_cfg5_address_column_at_scale(amd):
     job.ctx.gammas_set_simple(1)
     job.gammas(st)
     assert (job.gammas_host() == ref).all()
+    # every Levenshtein pass variant (one pass, two phases at tiny caps, lane refill): the same vectors
+    _lev_variants_agree(job, st, ref)
 
 
 def test_row_image_rebuilt_when_layout_changes(amd):

@@ -151,6 +151,12 @@ def main():
         lam, rows = m_step_rows(stats, names, nlev)
         params._update_params(lam, rows)
     wall["em_iterations"] = time.perf_counter() - t
+    # how concentrated the comparison patterns are (what bounds the lane-private E+M histogram)
+    hist_t = job._device_hist()
+    job.ctx.em_histogram(hist_t.data_ptr())
+    hist_h = np.sort(hist_t.cpu().numpy())[::-1]
+    patterns = {"n_patterns": int(len(hist_h)), "occupied": int((hist_h > 0).sum()),
+                "top_share": [round(float(x) / max(int(hist_h.sum()), 1), 5) for x in hist_h[:16]]}
     t = time.perf_counter()
     mp = job.score(params.params["λ"], params._level_probabilities(), want_host=False)
     torch.cuda.synchronize()
@@ -183,6 +189,7 @@ def main():
         "device_ms": {"block": block_dev, "gamma_pass_first": gamma_dev, "gamma_pass": gamma_warm,
                       "em_per_iter_mean": float(np.mean(em_dev)), "score": score_dev},
         "exact_cells_per_column": exact_cells,
+        "pattern_concentration": patterns,
         "pairs_per_s_job": P / total,
         "pairs_per_s_gamma_plus_em_iter": P / ((gamma_warm + float(np.mean(em_dev))) / 1e3),
         "generation_s_excluded": gen_s,

@@ -33,7 +33,7 @@ import re
 # Every kernel spk_gammas launches (spk_gamma.hip, spk_filter.hip); tests/test_traffic_record.py checks
 # the list against the sources' launch sites, so a renamed or new kernel cannot drop out of the group.
 GAMMA_KERNELS = ("k_build_image", "k_view_image", "k_filter", "k_gamma_filter", "k_gamma_exact",
-                 "k_gamma_exact_simple", "k_gamma_slow", "k_gamma_slow_lev", "k_gamma_rest", "k_gamma_huge",
+                 "k_gamma_exact_simple", "k_lev_refill", "k_gamma_slow", "k_gamma_slow_lev", "k_gamma_rest", "k_gamma_huge",
                  "k_compact", "k_prefix")
 # launched from the same sources by other entry points (spk_gammas_load / _copy, the bulk UDFs)
 NOT_GAMMA_KERNELS = ("k_codes_from_gammas", "k_gammas_from_codes", "k_udf", "k_udf_huge")
