@@ -262,14 +262,10 @@ int spk_gammas_simple_count(spk_ctx *ctx, int *out);
  * spk_gammas ran. */
 int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs);
 int spk_gammas_windows(spk_ctx *ctx, int64_t *out);
-/* Levenshtein exact pass kernel (same codes either way; for A/B tests): 1 = lane refill (default: a lane that
- * finishes its cell takes the next one of its wave's range), 0 = one cell per lane per wave round. */
+/* Levenshtein exact pass kernel (same codes in every mode; for A/B tests): 2 = lane refill (a lane that finishes
+ * its cell takes the next one from its wave's queue) in free-text columns -- rows past 64 units on both sides --
+ * and one cell per lane elsewhere (default), 1 = lane refill everywhere, 0 = one cell per lane everywhere. */
 int spk_gammas_set_lev_kernel(spk_ctx *ctx, int mode);
-/* Two-phase Levenshtein passes (same codes; tuning / A/B): the first phase scans at most `cap` text units per
- * cell, the cells it leaves go to a second, uncapped phase.  exact_cap applies to the exact pass of free-text
- * columns (rows past 64 units), slow_cap to the slow pass (rows of 65..128 units); 0 = one uncapped pass;
- * multiples of 4. */
-int spk_gammas_set_lev_caps(spk_ctx *ctx, int exact_cap, int slow_cap);
 /* Filter regions (workgroups) the last spk_gammas ran over the second rule's view-ordered image. */
 int spk_gammas_view_regions(spk_ctx *ctx, int64_t *out);
 

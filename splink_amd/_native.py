@@ -53,7 +53,7 @@ EXPORTS = [
     "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_raw_utf8_arrow_chunks", "spk_table_digest", "spk_raw_release",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
     "spk_em_finalize_start", "spk_gammas_exact_ms", "spk_gammas_set_window", "spk_gammas_windows",
-    "spk_gammas_set_lev_kernel", "spk_gammas_set_lev_caps",
+    "spk_gammas_set_lev_kernel",
 ]
 TF_LIMBS = 14  # SPK_TF_LIMBS
 
@@ -389,13 +389,9 @@ class Context:
         return n.value
 
     def gammas_set_lev_kernel(self, mode: int):
-        """Levenshtein exact pass: 1 lane refill (default), 0 one cell per lane (same codes; A/B tests)."""
+        """Levenshtein exact pass (same codes; A/B tests): 2 lane refill in free-text columns, one cell per lane
+        elsewhere (default); 1 lane refill everywhere; 0 one cell per lane everywhere."""
         check(self._lib.spk_gammas_set_lev_kernel(self._h, ctypes.c_int(int(mode))), "spk_gammas_set_lev_kernel")
-
-    def gammas_set_lev_caps(self, exact_cap: int, slow_cap: int):
-        """Two-phase Levenshtein passes: first-phase scan caps (0 = one uncapped pass; same codes, A/B)."""
-        check(self._lib.spk_gammas_set_lev_caps(self._h, ctypes.c_int(int(exact_cap)), ctypes.c_int(int(slow_cap))),
-              "spk_gammas_set_lev_caps")
 
     def lds_per_block(self) -> int:
         n = ctypes.c_int(0)

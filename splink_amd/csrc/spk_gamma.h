@@ -13,7 +13,7 @@ constexpr int X_THREADS = 256;  // exact pass
 constexpr int U_THREADS = 128;  // UDF kernel: 2 x 64 x 128 x 2 B = 32 KiB of LDS per block
 
 enum Mode { M_FILTER = 0, M_EXACT = 1, M_SLOW = 2, M_HUGE = 3 };
-enum Status { ST_DONE = 0, ST_UNDECIDED = 1, ST_NEEDS_SLOW = 2, ST_CAPPED = 3 };  // CAPPED: scan hit its step cap
+enum Status { ST_DONE = 0, ST_UNDECIDED = 1, ST_NEEDS_SLOW = 2 };
 
 // A "simple" comparison column: the shape every case_statements.py template has --
 //   WHEN x_l IS NULL OR x_r IS NULL THEN null_level
@@ -119,9 +119,7 @@ struct GammaArgs {
     int n_regions;
     int32_t *slow;             // slow-pass lists, column k at slow_off[k]
     const int64_t *slow_off;
-    unsigned int *slow_count;  // [5K]: slow lists, k_gamma_slow_lev's rest lists, huge lists, the exact and
-                               // slow passes' capped lists (two-phase Levenshtein)
-    int32_t *capped;           // capped lists of the Levenshtein passes, column k at capped + xinfo[k]
+    unsigned int *slow_count;  // [3K]: slow lists, k_gamma_slow_lev's rest lists, huge lists
     int *err;
     const SimpleCol *simple;   // filter pass: simple columns ...
     int n_simple;

@@ -691,8 +691,7 @@ __device__ int jw_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1
 // both rows' bit-planes are loaded in the same round trip as the records and the distance comes
 // from them alone (lev_rows_planes).  Rows without planes (> 64 units or a unit >= 256) go to the
 // global-memory pass.  A kernel of its own, so its register budget is not the JW path's.
-__device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level,
-                        int lim = LEV_NO_CAP) {
+__device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level) {
     uint64_t pa[N_PLANES], pb[N_PLANES];
     {
         const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
@@ -730,8 +729,7 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
                 if (lev < 0) {
                     if (eq == 1) lev = 0;
                     else if (!planes) return ST_NEEDS_SLOW;
-                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np, lim);
-                    if (lev == LEV_CAPPED) return ST_CAPPED;
+                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
                 }
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
@@ -805,7 +803,7 @@ __device__ inline void lev_sort_items(int &key, bool &have, int32_t &p, int32_t 
 }
 
 #ifndef SPK_LEV_WAVES
-#define SPK_LEV_WAVES 5
+#define SPK_LEV_WAVES 4
 #endif
 constexpr int LEV_WAVES = SPK_LEV_WAVES;
 // The Jaro-Winkler variant keeps its full register budget (138 VGPRs, 3 waves per SIMD): capped at
@@ -818,8 +816,6 @@ constexpr int JWC_WAVES = 4;
 struct ExactCols {
     int n;
     int g;  // blocks per column
-    int lim;  // X_LEV: scan cap (LEV_NO_CAP: none); capped cells go to the column's capped list
-    int src;  // X_LEV: 0 = the exact list, 1 = the capped list (the uncapped second pass)
     int si[4];
     int k[4], col[4];  // the columns' code positions and table columns (= simple[si].k / .col): the
                        // list bounds and the column descriptors load in one round, not after simple[si]
@@ -861,9 +857,8 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         s_c0 = A.cols0[colx];
         s_c1 = A.cols1[colx];
     }
-    const bool second = MODE == X_LEV && C.src == 1;  // the uncapped pass over the capped list
-    const int64_t n = second ? (xinfo[2 * A.K] ? 0 : (int64_t)A.slow_count[3 * A.K + k]) : exact_count(A, xinfo, k);
-    const int32_t *items = (second ? A.capped : xlist) + xinfo[k];
+    const int64_t n = exact_count(A, xinfo, k);
+    const int32_t *items = xlist + xinfo[k];
     const int64_t stride = (int64_t)C.g * X_THREADS;
     // software pipeline: the next item's pair rows (and, for Levenshtein, the rows' lengths) are in
     // flight while this one is evaluated
@@ -896,7 +891,7 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
             if (regroup) key2 = lev_work_bin(s_c0.meta[x2].len16, s_c1.meta[y2].len16);
         }
         if (regroup) lev_sort_items(key, have, p, x, y);
-        bool to_slow = false, capped = false;
+        bool to_slow = false;
         if (have && regroup && key >= 128) {
             // a row past 64 units (work bins 128 +): no 64-bit planes, the 128-bit slow pass takes the cell --
             // straight to its list, without loading the rows' planes and records first
@@ -904,19 +899,17 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         } else if (have) {
             int level = 0;
             int st;
-            if constexpr (MODE == X_LEV) st = lev_cell(sc, s_c0, s_c1, x, y, level, C.lim);
+            if constexpr (MODE == X_LEV) st = lev_cell(sc, s_c0, s_c1, x, y, level);
             else if constexpr (MODE == X_JW) st = jw_cell(sc, s_c0, s_c1, x, y, level);
             else st = simple_exact(A, sc, s_c0, s_c1, x, y, level);
 #ifdef SPK_X_STAMPS
             if (x_t2 == 0) x_t2 = wall_clock64() + (unsigned long long)(level & 0);
 #endif
-            if (st == ST_CAPPED) capped = true;
-            else if (st != ST_DONE) to_slow = true;
+            if (st != ST_DONE) to_slow = true;
             else if (C.n > 1) code_add_atomic(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
             else code_add(A, p, (uint32_t)(level + 1) * (uint32_t)sc.stride);
         }
         wave_append(A.slow + A.slow_off[k], A.slow_count + k, to_slow, p);
-        if (MODE == X_LEV && C.lim < LEV_NO_CAP) wave_append(A.capped + xinfo[k], A.slow_count + 3 * A.K + k, capped, p);
 #ifdef SPK_X_STAMPS
         x_cells += have ? 1 : 0;
 #endif
@@ -1434,7 +1427,7 @@ __global__ __launch_bounds__(64) void k_gamma_huge(GammaArgs A, int k, const int
 // (lev_rows_planes128) -- free-text columns such as cfg5's addresses land here; any other cell
 // (non-Latin-1 or longer rows) runs the global-memory evaluation of k_gamma_slow.
 __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y,
-                           int &level, int lim = LEV_NO_CAP) {
+                           int &level) {
     const RecMeta ma = c0.meta[x], mb = c1.meta[y];
     if (ma.len16 < 0 || mb.len16 < 0) {
         level = sc.null_level;
@@ -1488,11 +1481,8 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
             if (op == SPK_OP_LEVRATIO && den == 0.0) {
                 r = KN;
             } else {
-                if (lev < 0) {
-                    lev = eq == 1 ? 0
-                                  : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np, lim);
-                    if (lev == LEV_CAPPED) return ST_CAPPED;
-                }
+                if (lev < 0)
+                    lev = eq == 1 ? 0 : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
         }
@@ -1508,13 +1498,8 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
 // Cells without planes on both rows are handed on (rest list: column k's exact-list region, free
 // once the exact pass ran, and counter slow_count[K + k]) to k_gamma_rest, so this kernel does not
 // carry the general interpreter's registers (the 128-bit scan alone holds ~100).
-// Two phases (lim < LEV_NO_CAP): the first (src 0) scans at most lim text units per cell and lists the cells that
-// neither ended nor exited by then (the capped list, counter slow_count[4K + k]); the second (src 1) scans those
-// uncapped.  A wave runs as long as its slowest cell, and cfg5's long addresses scan 9 units on average but 45
-// for the slowest of 64 (tools/lev_refill_sim.py): the first phase bounds every wave, the second runs only the
-// few long scans, together.
 __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int si, int32_t *xlist,
-                                                              const int64_t *xinfo, int lim, int src) {
+                                                              const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
     if (threadIdx.x == 0) {
@@ -1524,18 +1509,17 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int s
     }
     __syncthreads();
     const int k = s_sc.k;
-    const int64_t n = src ? A.slow_count[4 * A.K + k] : A.slow_count[k];
-    const int32_t *items = src ? A.capped + xinfo[k] : A.slow + A.slow_off[k];
+    const int64_t n = A.slow_count[k];
+    const int32_t *items = A.slow + A.slow_off[k];
     int32_t *rest = xlist + xinfo[k];
     // (regrouping these cells by work bin, as k_gamma_exact_simple does for free-text columns,
     // measured no faster here: 2.43-2.47 ms per cfg5 call either way)
     for (int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * X_THREADS) {
         const int32_t p = items[i];
         int level = 0;
-        const int st = lev_cell128(s_sc, s_c0, s_c1, A.pl[p], A.pr[p], level, lim);
-        if (st == ST_DONE) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
-        wave_append(rest, A.slow_count + A.K + k, st != ST_DONE && st != ST_CAPPED, p);
-        if (lim < LEV_NO_CAP) wave_append(A.capped + xinfo[k], A.slow_count + 4 * A.K + k, st == ST_CAPPED, p);
+        const bool done = lev_cell128(s_sc, s_c0, s_c1, A.pl[p], A.pr[p], level) == ST_DONE;
+        if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        wave_append(rest, A.slow_count + A.K + k, !done, p);
     }
 }
 
@@ -1979,11 +1963,7 @@ static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
         if (lev) {
             constexpr int SLOWLEV_WG_PER_CU = 8;  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU at once
             const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SLOWLEV_WG_PER_CU * ctx->n_cu));
-            const int cap = ctx->lev_cap_slow > 0 ? ctx->lev_cap_slow : LEV_NO_CAP;
-            k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p, cap, 0);
-            if (cap < LEV_NO_CAP)
-                k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p,
-                                                                               LEV_NO_CAP, 1);
+            k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
             k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
         } else {
             k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);
@@ -2002,9 +1982,8 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         return skip && (ctx->slow_force_skip ||
                         (ctx->slow_seen_valid && k < (int)ctx->slow_seen.size() && !ctx->slow_seen[k]));
     };
-    SPK_TRY(ctx->xlist.alloc((size_t)(3 * cap)));
+    SPK_TRY(ctx->xlist.alloc((size_t)(2 * cap)));
     A.slow = ctx->xlist.p + cap;
-    A.capped = ctx->xlist.p + 2 * cap;
     A.slow_off = ctx->xinfo.p;
     ctx->xcap = cap;
     if (A.P <= 0) {
@@ -2062,7 +2041,7 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         if (fused) continue;
         const ColSet one_k{1, {k, 0, 0, 0}};
         k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
-        if (lev && ctx->lev_refill) {
+        if (lev && (ctx->lev_kernel == 1 || (ctx->lev_kernel == 2 && G.free_text[k]))) {
             // one resident round (LEVQ_WAVES per SIMD, 3 for NP = 8): every wave owns a contiguous range of the list
             const int64_t wg_cu = simple[si].np >= 8 ? 3 : LEVQ_WG_PER_CU;
             const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, wg_cu * ctx->n_cu));
@@ -2087,20 +2066,9 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
             one.si[0] = si;
             one.k[0] = simple[si].k;
             one.col[0] = simple[si].col;
-            // two phases in free-text columns (rows past 64 units: their scans spread widely), see k_gamma_slow_lev
-            const bool free_text = G.free_text[k] != 0;
-            one.lim = (free_text && ctx->lev_cap_exact > 0) ? ctx->lev_cap_exact : LEV_NO_CAP;
-            one.src = 0;
             SPK_TRY(ctx->xbegin(k));
             k_gamma_exact_simple<X_LEV><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, one, ctx->xlist.p,
                                                                                       ctx->xinfo.p);
-            if (one.lim < LEV_NO_CAP) {
-                ExactCols two = one;
-                two.lim = LEV_NO_CAP;
-                two.src = 1;
-                k_gamma_exact_simple<X_LEV><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, two, ctx->xlist.p,
-                                                                                          ctx->xinfo.p);
-            }
             SPK_TRY(ctx->xend(k));
             if (quiet(k)) G.slow_skipped[k] = 1;
             else SPK_TRY(enqueue_slow(ctx, G, k, nullptr));
@@ -2411,7 +2379,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     // One device info block, read back with one copy: xinfo (k_prefix: list bases and counts, overflow,
     // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed per window.
     const int n_info = 2 * K + 2;
-    const int n_cnt = (5 * K + 1) / 2;  // int64 slots of the 5K uint32 list lengths
+    const int n_cnt = (3 * K + 1) / 2;  // int64 slots of the 3K uint32 list lengths
     const int n_all = n_info + n_cnt + 2;  // + the error word and k_prefix's completion counter
     SPK_TRY(ctx->xinfo.alloc((size_t)n_all));
     SPK_TRY(ctx->pinned_info((size_t)n_all));
@@ -2852,8 +2820,8 @@ extern "C" int spk_gammas_windows(spk_ctx *ctx, int64_t *out) {
 }
 
 extern "C" int spk_gammas_set_lev_kernel(spk_ctx *ctx, int mode) {
-    SPK_REQUIRE(ctx && (mode == 0 || mode == 1), SPK_E_INVALID, "spk_gammas_set_lev_kernel: mode 0 or 1");
-    ctx->lev_refill = mode == 1;
+    SPK_REQUIRE(ctx && mode >= 0 && mode <= 2, SPK_E_INVALID, "spk_gammas_set_lev_kernel: mode 0, 1 or 2");
+    ctx->lev_kernel = mode;
     return SPK_OK;
 }
 
@@ -2868,11 +2836,3 @@ extern "C" int spk_debug_levq_stats(uint64_t *out, int reset) {
     return SPK_OK;
 }
 #endif
-
-extern "C" int spk_gammas_set_lev_caps(spk_ctx *ctx, int exact_cap, int slow_cap) {
-    SPK_REQUIRE(ctx && exact_cap >= 0 && slow_cap >= 0 && exact_cap % 4 == 0 && slow_cap % 4 == 0, SPK_E_INVALID,
-                "spk_gammas_set_lev_caps: caps >= 0, multiples of 4 (0 = one uncapped pass)");
-    ctx->lev_cap_exact = exact_cap;
-    ctx->lev_cap_slow = slow_cap;
-    return SPK_OK;
-}

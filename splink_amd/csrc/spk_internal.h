@@ -300,9 +300,8 @@ struct spk_ctx {
     // (settle_gammas runs them if the list is not empty after all)
     std::vector<uint8_t> slow_seen;
     bool slow_seen_valid = false;
-    bool lev_refill = false;       // Levenshtein exact pass: k_lev_refill (else k_gamma_exact_simple<X_LEV>)
-    int lev_cap_exact = 0;         // two-phase Levenshtein passes: scan cap of the first phase (0 = one pass) --
-    int lev_cap_slow = 0;          // exact pass in free-text columns, slow pass (rows of 65..128 units)
+    int lev_kernel = 2;            // Levenshtein exact pass: 0 k_gamma_exact_simple<X_LEV>, 1 k_lev_refill, 2 refill in
+                                   // free-text columns (rows past 64 units), one cell per lane elsewhere
     bool slow_force_skip = false;  // tests: leave every slow-list launch to settle_gammas
     uint64_t slow_key_pairs = 0, slow_key_tables = 0;
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths

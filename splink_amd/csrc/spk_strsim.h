@@ -496,24 +496,19 @@ __device__ inline int diag_score(W vp, W vn, int j, int m, int n) {
 // NP: the scans read planes 0..NP-1 only.  A caller passes NP < 8 when every unit of the column
 // (both sides) has the same bits NP..7 (e.g. 7 for ASCII text): those planes' terms then only touch
 // mask bits above the pattern, which never reach the rows below (carries and shifts move upward).
-// lim: scan at most lim text units (a multiple of 4); a cell that neither ended nor exited by then returns
-// LEV_CAPPED, and its caller hands it to a second, uncapped pass (the two-phase exact and slow passes).
-constexpr int LEV_CAPPED = -2;
-constexpr int LEV_NO_CAP = 1 << 30;
 template <typename W, int NP = N_PLANES>
 __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
-                                       int cut, int lim = LEV_NO_CAP) {
-    const int nl = n < lim ? n : lim;
+                                       int cut) {
     W pl[N_PLANES];
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
     W vp = ~(W)0, vn = 0;
     const W M = low_mask<W>(m);
-    for (int h = 0; h < 2 && 32 * h < nl; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
+    for (int h = 0; h < 2 && 32 * h < n; ++h) {  // text units [32h, 32h + 32) from 32-bit plane words
         uint32_t tw[N_PLANES];
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
-        const int jn = nl - 32 * h < 32 ? nl - 32 * h : 32;
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
         for (int jj = 0; jj < jn; ++jj) {
             W eq = ~(W)0;
 #pragma unroll
@@ -530,7 +525,6 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
             if ((jj & 3) == 3 && diag_score<W>(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
-    if (nl < n) return LEV_CAPPED;
     const int dist = n + popc_w(vp & M) - popc_w(vn & M);
     return dist > cut ? cut + 1 : dist;
 }
@@ -546,7 +540,7 @@ __device__ inline int myers_plane_text(const uint64_t (&P)[N_PLANES], int m, con
 // same loops with their one word.  cfg2 emails: most waves hold a cell of 33+ units, cut ~ 10.
 template <int NP = N_PLANES>
 __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m, const uint64_t (&T)[N_PLANES], int n,
-                                            int cut, int lim = LEV_NO_CAP) {
+                                            int cut) {
     const bool wide = m > 32;
     const int mine = wide ? (cut < 31 ? 31 - cut : 0) : 32;
     int lo = 0, hi = 32;  // wave minimum of `mine` (active lanes) by bisection over ballots
@@ -564,8 +558,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
     }
     uint32_t vp = ~0u, vn = 0;
     const uint32_t M1 = low_mask<uint32_t>(wide ? 32 : m);  // the rows the first phase scores
-    const int nl = n < lim ? n : lim;
-    const int j1 = nl < J0 ? nl : J0;
+    const int j1 = n < J0 ? n : J0;
     for (int j = 0; j < j1; ++j) {
         uint32_t eq = ~0u;
 #pragma unroll
@@ -580,19 +573,18 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
         // here (m - n <= cut, j < J0 <= 31 - cut) is one of the rows this phase tracks exactly
         if ((j & 3) == 3 && diag_score<uint32_t>(vp, vn, j, m, n) > cut) return cut + 1;
     }
-    if (n <= J0 && n <= lim) {
+    if (n <= J0) {
         const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 32 : 0);
         return dist > cut ? cut + 1 : dist;
     }
-    if (nl <= J0) return LEV_CAPPED;  // lim < n, reached in the first phase
     // rows 33..m enter with vertical deltas +1 (D[32][J0] + (i - 32))
     uint64_t VP = (uint64_t)vp | 0xFFFFFFFF00000000ull, VN = vn;
     const uint64_t M2 = low_mask<uint64_t>(m);
-    for (int h = J0 >> 5; h < 2 && 32 * h < nl; ++h) {
+    for (int h = J0 >> 5; h < 2 && 32 * h < n; ++h) {
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
         const int jb = 32 * h < J0 ? J0 - 32 * h : 0;
-        const int jn = nl - 32 * h < 32 ? nl - 32 * h : 32;
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
         for (int jj = jb; jj < jn; ++jj) {
             uint64_t eq = ~0ull;
 #pragma unroll
@@ -607,7 +599,6 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
             if ((jj & 3) == 3 && diag_score<uint64_t>(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
-    if (nl < n) return LEV_CAPPED;
     const int dist = n + popc_w(VP & M2) - popc_w(VN & M2);
     return dist > cut ? cut + 1 : dist;
 }
@@ -619,7 +610,7 @@ __device__ inline int myers_plane_text_lazy(const uint64_t (&P)[N_PLANES], int m
 // the scan runs over the shorter one.  `cut` as in lev_planes.
 template <int NP>
 __device__ inline int lev_rows_planes_np(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
-                                         int cut, int lim = LEV_NO_CAP) {
+                                         int cut) {
     if (la == 0) return lb;
     if (lb == 0) return la;
     const int mn = la < lb ? la : lb;
@@ -646,18 +637,18 @@ __device__ inline int lev_rows_planes_np(const uint64_t (&pa)[N_PLANES], int la,
         T[b] = (a_pat ? pb[b] : pa[b]) >> pre;
     }
     // one word width for all active lanes: a wave that mixed both would run both loops
-    if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P, m, T, n, cut, lim);
-    return myers_plane_text_lazy<NP>(P, m, T, n, cut, lim);
+    if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P, m, T, n, cut);
+    return myers_plane_text_lazy<NP>(P, m, T, n, cut);
 }
 
 // np: planes the scans need (wave-uniform; see myers_plane_text), 8 when unknown.
 __device__ inline int lev_rows_planes(const uint64_t (&pa)[N_PLANES], int la, const uint64_t (&pb)[N_PLANES], int lb,
-                                      int cut, int np = N_PLANES, int lim = LEV_NO_CAP) {
+                                      int cut, int np = N_PLANES) {
     switch (np) {
-        case 5: return lev_rows_planes_np<5>(pa, la, pb, lb, cut, lim);
-        case 6: return lev_rows_planes_np<6>(pa, la, pb, lb, cut, lim);
-        case 7: return lev_rows_planes_np<7>(pa, la, pb, lb, cut, lim);
-        default: return lev_rows_planes_np<N_PLANES>(pa, la, pb, lb, cut, lim);
+        case 5: return lev_rows_planes_np<5>(pa, la, pb, lb, cut);
+        case 6: return lev_rows_planes_np<6>(pa, la, pb, lb, cut);
+        case 7: return lev_rows_planes_np<7>(pa, la, pb, lb, cut);
+        default: return lev_rows_planes_np<N_PLANES>(pa, la, pb, lb, cut);
     }
 }
 
@@ -726,7 +717,7 @@ __device__ inline int myers_plane_text128(const u128 (&P)[N_PLANES], int m, cons
 // their text in the cheaper first phase.
 template <int NP = N_PLANES>
 __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
-                                               int cut, int lim = LEV_NO_CAP) {
+                                               int cut) {
     const bool wide = m > 64;
     const int mine = wide ? (cut < 63 ? 63 - cut : 0) : 128;
     int lo = 0, hi = 128;  // wave minimum of `mine` (active lanes) by bisection over ballots
@@ -741,8 +732,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
     for (int b = 0; b < N_PLANES; ++b) pl[b] = (uint64_t)P[b];
     uint64_t vp = ~0ull, vn = 0;
     const uint64_t M1 = low_mask<uint64_t>(wide ? 64 : m);  // the rows the first phase scores
-    const int nl = n < lim ? n : lim;
-    const int j1 = nl < J0 ? nl : J0;
+    const int j1 = n < J0 ? n : J0;
     for (int h = 0; h < 4 && 32 * h < j1; ++h) {
         uint32_t tw[N_PLANES];
 #pragma unroll
@@ -762,20 +752,19 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
             if ((jj & 3) == 3 && diag_score<uint64_t>(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
-    if (n <= J0 && n <= lim) {
+    if (n <= J0) {
         const int dist = n + popc_w(vp & M1) - popc_w(vn & M1) + (wide ? m - 64 : 0);
         return dist > cut ? cut + 1 : dist;
     }
-    if (nl <= J0) return LEV_CAPPED;  // lim < n, reached in the first phase
     // rows 65..m enter with vertical deltas +1 (D[64][J0] + (i - 64))
     u128 VP = (u128)vp | ((u128)~0ull << 64), VN = vn;
 
-    for (int h = J0 >> 5; h < 4 && 32 * h < nl; ++h) {
+    for (int h = J0 >> 5; h < 4 && 32 * h < n; ++h) {
         uint32_t tw[N_PLANES];
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
         const int jb = 32 * h < J0 ? J0 - 32 * h : 0;
-        const int jn = nl - 32 * h < 32 ? nl - 32 * h : 32;
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
         for (int jj = jb; jj < jn; ++jj) {
             uint64_t e0 = ~0ull, e1 = ~0ull;
 #pragma unroll
@@ -793,7 +782,6 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
             if ((jj & 3) == 3 && diag_score128(VP, VN, 32 * h + jj, m, n) > cut) return cut + 1;
         }
     }
-    if (nl < n) return LEV_CAPPED;
     const int dist = diag_score128(VP, VN, n - 1, m, n);
     return dist > cut ? cut + 1 : dist;
 }
@@ -803,7 +791,7 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
 // one-word scan (the same word width for the whole wave), else the 128-bit one.
 template <int NP>
 __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
-                                            int cut, int lim = LEV_NO_CAP) {
+                                            int cut) {
     if (la == 0) return lb;
     if (lb == 0) return la;
     const int mn = la < lb ? la : lb;
@@ -836,19 +824,19 @@ __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, 
             P64[b] = (uint64_t)P[b];
             T64[b] = (uint64_t)T[b];
         }
-        if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P64, m, T64, n, cut, lim);
-        return myers_plane_text_lazy<NP>(P64, m, T64, n, cut, lim);
+        if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P64, m, T64, n, cut);
+        return myers_plane_text_lazy<NP>(P64, m, T64, n, cut);
     }
-    return myers_plane_text128_lazy<NP>(P, m, T, n, cut, lim);
+    return myers_plane_text128_lazy<NP>(P, m, T, n, cut);
 }
 
 __device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
-                                         int cut, int np = N_PLANES, int lim = LEV_NO_CAP) {
+                                         int cut, int np = N_PLANES) {
     switch (np) {
-        case 5: return lev_rows_planes128_np<5>(pa, la, pb, lb, cut, lim);
-        case 6: return lev_rows_planes128_np<6>(pa, la, pb, lb, cut, lim);
-        case 7: return lev_rows_planes128_np<7>(pa, la, pb, lb, cut, lim);
-        default: return lev_rows_planes128_np<N_PLANES>(pa, la, pb, lb, cut, lim);
+        case 5: return lev_rows_planes128_np<5>(pa, la, pb, lb, cut);
+        case 6: return lev_rows_planes128_np<6>(pa, la, pb, lb, cut);
+        case 7: return lev_rows_planes128_np<7>(pa, la, pb, lb, cut);
+        default: return lev_rows_planes128_np<N_PLANES>(pa, la, pb, lb, cut);
     }
 }
 

@@ -641,21 +641,16 @@ def _mutate(rng, s, k, alpha):
     return "".join(s)
 
 
-# Levenshtein pass variants that must give the same codes: (exact kernel, exact-pass cap, slow-pass cap) --
-# one uncapped pass, tiny first-phase caps (most cells go through both phases), the lane-refill kernel
-LEV_VARIANTS = [(0, 0, 0), (0, 4, 4), (0, 12, 8), (1, 0, 4)]
-
-
 def _lev_variants_agree(job, settings, want):
+    """Every Levenshtein exact-pass kernel choice (spk_gammas_set_lev_kernel: one cell per lane, lane refill,
+    refill in free-text columns only) gives the same codes."""
     try:
-        for kern, xcap, scap in LEV_VARIANTS:
+        for kern in (0, 1, 2):
             job.ctx.gammas_set_lev_kernel(kern)
-            job.ctx.gammas_set_lev_caps(xcap, scap)
             job.gammas(settings)
-            assert (job.gammas_host() == want).all(), (kern, xcap, scap)
+            assert (job.gammas_host() == want).all(), kern
     finally:
-        job.ctx.gammas_set_lev_kernel(0)
-        job.ctx.gammas_set_lev_caps(0, 0)
+        job.ctx.gammas_set_lev_kernel(2)
 
 
 def test_levenshtein_levels_exact(amd):
@@ -817,7 +812,7 @@ def test_cfg5_address_column_at_scale(amd):
     job.ctx.gammas_set_simple(1)
     job.gammas(st)
     assert (job.gammas_host() == ref).all()
-    # every Levenshtein pass variant (one pass, two phases at tiny caps, lane refill): the same vectors
+    # every Levenshtein exact-pass kernel (one cell per lane, lane refill, auto): the same vectors
     _lev_variants_agree(job, st, ref)
 
 

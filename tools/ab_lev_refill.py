@@ -1,10 +1,9 @@
-"""Comparison pass time under Levenshtein pass variants on a bench workload (cfg2 / cfg5 columns, 1M records),
-with identical codes required across all of them.  A variant is KERNEL:EXACT_CAP:SLOW_CAP -- KERNEL 0 = one cell
-per lane (k_gamma_exact_simple), 1 = lane refill (k_lev_refill); the caps are the two-phase passes' first-phase
-scan caps (spk_gammas_set_lev_caps, 0 = one uncapped pass).  Reports the γ pass (device ms) and each column's
+"""Comparison pass time under the Levenshtein exact-pass kernels (spk_gammas_set_lev_kernel: 0 = one cell per
+lane, 1 = lane refill everywhere, 2 = refill in free-text columns only) on a bench workload (cfg2 / cfg5 columns,
+1M records), with identical codes required across all of them.  Reports the γ pass (device ms) and each column's
 exact-pass launch time, medians of `reps`.
 
-    python tools/ab_lev_refill.py [config] [reps] [variant ...]
+    python tools/ab_lev_refill.py [config] [reps] [mode ...]
 """
 import ctypes
 import os
@@ -23,7 +22,7 @@ from splink_amd.synthetic import cfg_settings, make_records  # noqa: E402
 
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-variants = sys.argv[3:] or ["0:0:0", "0:24:8", "1:0:8"]
+variants = sys.argv[3:] or ["0", "1", "2"]
 cols = ["first_name", "surname", "dob", "city", "email"] + (["address"] if cfg == 5 else [])
 df = make_records(1_000_000, surname_vocab=15000, with_address=cfg == 5, arrow=True)[["unique_id"] + cols]
 params = Params(cfg_settings(cfg), AmdSession(0))
@@ -49,9 +48,8 @@ def read_stats(reset=True):
 codes = {}
 for rnd in range(2):
     for v in variants:
-        kern, xcap, scap = (int(x) for x in v.split(":"))
+        kern = int(v)
         job.ctx.gammas_set_lev_kernel(kern)
-        job.ctx.gammas_set_lev_caps(xcap, scap)
         if stats is not None:
             read_stats()
         g, x = [], []
@@ -60,16 +58,15 @@ for rnd in range(2):
             g.append(job.ctx.kernel_ms()["gamma"])
             x.append(job.ctx.gammas_exact_ms(K))
         codes[v] = job.gammas_host()
-        if stats is not None and kern == 1:
+        if stats is not None and kern > 0:
             d = dict(zip(STAT_NAMES, read_stats()[:12].tolist()))
             w = max(d["waves"], 1)
             print(f"  {v} schedule per wave ({d['waves']} waves): "
                   f"{ {k: round(val / w, 1) for k, val in d.items() if k != 'waves'} }", flush=True)
         if rnd:
             xm = np.median(np.array(x), axis=0)
-            print(f"cfg{cfg} {v}: pairs {job.n_pairs}, γ pass median {np.median(g):.3f} ms (min {min(g):.3f}); exact "
+            print(f"cfg{cfg} lev kernel {v}: pairs {job.n_pairs}, γ pass median {np.median(g):.3f} ms (min {min(g):.3f}); exact "
                   "launches ms " + ", ".join(f"{n} {val:.3f}" for n, val in zip(names, xm) if val >= 0), flush=True)
-job.ctx.gammas_set_lev_kernel(0)
-job.ctx.gammas_set_lev_caps(0, 0)
+job.ctx.gammas_set_lev_kernel(2)
 ref = codes[variants[0]]
 print("identical codes:", all(bool(np.array_equal(ref, c)) for c in codes.values()))
