@@ -256,8 +256,9 @@ def main():
             pmc = json.load(f)
         issue = {"source": os.path.relpath(PMC_FILE, ROOT) + ": rocprofv3 --pmc SQ_* passes of this command",
                  "peak_note": "valu_util = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles at 2.4 GHz)"}
-        for name, key in (("filter", "k_filter"), ("levenshtein_exact", "k_gamma_exact_simple<true"),
-                          ("jw_exact", "k_gamma_exact_simple<false")):
+        for name, key in (("filter", "k_filter"), ("levenshtein_exact", "k_gamma_exact_simple<1,"),
+                          ("levenshtein_refill", "k_lev_refill"), ("levenshtein_slow", "k_gamma_slow_lev"),
+                          ("jw_exact", "k_gamma_exact_simple<2,")):
             for k, v in pmc.items():
                 if key in k:
                     issue[name] = {x: round(float(v[x]), 4) for x in ("valu_util", "salu_util", "wait_frac", "l2_hit")

@@ -262,9 +262,10 @@ int spk_gammas_simple_count(spk_ctx *ctx, int *out);
  * spk_gammas ran. */
 int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs);
 int spk_gammas_windows(spk_ctx *ctx, int64_t *out);
-/* Levenshtein exact pass kernel (same codes in every mode; for A/B tests): 2 = lane refill (a lane that finishes
- * its cell takes the next one from its wave's queue) in free-text columns -- rows past 64 units on both sides --
- * and one cell per lane elsewhere (default), 1 = lane refill everywhere, 0 = one cell per lane everywhere. */
+/* Levenshtein pass kernels (same codes in every mode; for A/B tests): 2 = lane refill (a lane that finishes its
+ * cell takes the next one from its wave's queue) in the exact pass of free-text columns -- rows past 64 units on
+ * both sides -- and one cell per lane elsewhere (default), 1 = lane refill in every exact pass and in the 128-bit
+ * slow pass, 0 = one cell per lane everywhere. */
 int spk_gammas_set_lev_kernel(spk_ctx *ctx, int mode);
 /* Filter regions (workgroups) the last spk_gammas ran over the second rule's view-ordered image. */
 int spk_gammas_view_regions(spk_ctx *ctx, int64_t *out);

@@ -42,9 +42,16 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
 }
 
 // One thread per row: decode the row's UTF-8 into UTF-16 units at its aligned start, count code
-// points, hash the units and build the bucket sketch used by the comparison filters.
+// points, hash the units and build the bucket sketch used by the comparison filters, the head units and
+// the bit-planes -- all in the one pass over the bytes.
 // Surrogate-encoded (CESU / "surrogatepass") 3-byte sequences decode to lone surrogate units,
 // exactly as a Java String would hold them.
+//
+// Four bytes at a time: a dword-aligned window of the source (two aligned dword loads and a byte shift) whose
+// four bytes are all ASCII becomes four units at once -- plane bits by a multiply that gathers bit b of the
+// four bytes into a nibble, the units as one 8-byte store when aligned.  Other bytes take the code-point
+// path.  (The one-byte-per-iteration loop was a chain of dependent byte loads and re-read the units it had
+// written to build the planes: 0.55 ms per million rows at cfg5.)
 
 // perm (optional): row `row` of the table is row perm[row] of the source buffers (src_off / bytes /
 // valid / ids); off8 is then the layout of the permuted rows (exclusive scan of their byte lengths).
@@ -72,57 +79,108 @@ __global__ void k_utf8_decode(int64_t n, const int64_t *__restrict__ off8, const
         return;
     }
     const int64_t *so = src_off ? src_off : off8;
-    int64_t b = so[src], e = so[src + 1];
+    const int64_t b0 = so[src], e = so[src + 1];
     uint16_t *dst = units + start;
+    const int cap = planes_hi ? PLANES2_MAX : 64;  // units the planes can hold
     int32_t nu = 0, nc = 0;
-    uint64_t h = 1469598103934665603ull, sk = 0;
-    while (b < e) {
-        uint32_t c0 = bytes[b];
+    uint64_t h = 1469598103934665603ull, sk = 0, head = 0;
+    uint64_t pl[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0}, ph[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool latin = true;  // every unit so far < 256
+    auto put = [&](uint32_t u) {  // one unit, the code-point path
+        if (nu < 4) head |= (uint64_t)u << (16 * nu);
+        latin = latin && u < 256u;
+        if (latin && nu < cap) {
+#pragma unroll
+            for (int b = 0; b < N_PLANES; ++b) {
+                const uint64_t bit = (uint64_t)((u >> b) & 1u);
+                if (nu < 64) pl[b] |= bit << nu;
+                else ph[b] |= bit << (nu - 64);
+            }
+        }
+        dst[nu++] = (uint16_t)u;
+        h = (h ^ u) * 1099511628211ull;
+        sketch_add(sk, u);
+    };
+    // dword view of the source bytes from the dword boundary at or below `bytes` (an Arrow buffer may start
+    // anywhere); a dword holding a byte of the column lies inside its allocation
+    const uint32_t mis = (uint32_t)((uintptr_t)bytes & 3u);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(bytes - mis);
+    int64_t pos = b0;
+    while (pos < e) {
+        if (pos + 4 <= e) {
+            const int64_t ap = pos + mis;
+            const uint32_t sh = (uint32_t)(ap & 3);
+            const uint32_t lo = w[ap >> 2], hi = sh ? w[(ap >> 2) + 1] : 0u;  // (ap + 3 >> 2: a byte of the row)
+            const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+            if ((v & 0x80808080u) == 0) {  // four ASCII bytes: four units
+                const uint32_t u0 = v & 0xFFu, u1 = (v >> 8) & 0xFFu, u2 = (v >> 16) & 0xFFu, u3 = v >> 24;
+                if (nu < 4) {
+                    const uint64_t q = (uint64_t)u0 | ((uint64_t)u1 << 16) | ((uint64_t)u2 << 32) | ((uint64_t)u3 << 48);
+                    head |= q << (16 * nu);
+                }
+                if (latin && nu < cap) {
+#pragma unroll
+                    for (int b = 0; b < N_PLANES; ++b) {
+                        // bit b of the four bytes (bits 0, 8, 16, 24 after the shift) into bits 28 .. 31
+                        const uint64_t nib = (uint64_t)((((v >> b) & 0x01010101u) * 0x10204080u) >> 28);
+                        if (nu < 64) {
+                            pl[b] |= nib << nu;
+                            if (nu > 60) ph[b] |= nib >> (64 - nu);
+                        } else {
+                            ph[b] |= nib << (nu - 64);
+                        }
+                    }
+                }
+                if ((nu & 3) == 0) {
+                    *reinterpret_cast<uint2 *>(dst + nu) = make_uint2(u0 | (u1 << 16), u2 | (u3 << 16));
+                } else {
+                    dst[nu] = (uint16_t)u0;
+                    dst[nu + 1] = (uint16_t)u1;
+                    dst[nu + 2] = (uint16_t)u2;
+                    dst[nu + 3] = (uint16_t)u3;
+                }
+                h = (h ^ u0) * 1099511628211ull;
+                h = (h ^ u1) * 1099511628211ull;
+                h = (h ^ u2) * 1099511628211ull;
+                h = (h ^ u3) * 1099511628211ull;
+                sketch_add(sk, u0);
+                sketch_add(sk, u1);
+                sketch_add(sk, u2);
+                sketch_add(sk, u3);
+                nu += 4;
+                nc += 4;
+                pos += 4;
+                continue;
+            }
+        }
+        uint32_t c0 = bytes[pos];
         uint32_t cp;
         int len;
         if (c0 < 0x80) { cp = c0; len = 1; }
         else if (c0 < 0xE0) { cp = c0 & 0x1F; len = 2; }
         else if (c0 < 0xF0) { cp = c0 & 0x0F; len = 3; }
         else { cp = c0 & 0x07; len = 4; }
-        for (int i = 1; i < len && b + i < e; ++i) cp = (cp << 6) | (bytes[b + i] & 0x3F);
-        b += len;
+        for (int i = 1; i < len && pos + i < e; ++i) cp = (cp << 6) | (bytes[pos + i] & 0x3F);
+        pos += len;
         if (cp >= 0x10000) {
-            uint32_t v = cp - 0x10000;
-            uint16_t hi = (uint16_t)(0xD800 + (v >> 10)), lo = (uint16_t)(0xDC00 + (v & 0x3FF));
-            dst[nu++] = hi;
-            dst[nu++] = lo;
-            h = (h ^ hi) * 1099511628211ull;
-            h = (h ^ lo) * 1099511628211ull;
-            sketch_add(sk, hi);
-            sketch_add(sk, lo);
+            const uint32_t v = cp - 0x10000;
+            put(0xD800u + (v >> 10));
+            put(0xDC00u + (v & 0x3FFu));
         } else {
-            dst[nu++] = (uint16_t)cp;
-            h = (h ^ cp) * 1099511628211ull;
-            sketch_add(sk, cp);
+            put(cp);
         }
         ++nc;
     }
     // bit-planes for Latin-1 rows of <= 64 units (one word) or, when the column has planes_hi,
     // <= PLANES2_MAX units (two words)
-    uint64_t pl[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0}, ph[N_PLANES] = {0, 0, 0, 0, 0, 0, 0, 0};
-    bool latin = nu <= (planes_hi ? PLANES2_MAX : 64);
-    for (int i = 0; latin && i < nu; ++i) {
-        const uint32_t c = dst[i];
-        if (c >= 256) { latin = false; break; }
-#pragma unroll
-        for (int b = 0; b < N_PLANES; ++b) {
-            const uint64_t bit = (uint64_t)((c >> b) & 1u) << (i & 63);
-            if (i < 64) pl[b] |= bit;
-            else ph[b] |= bit;
-        }
-    }
+    latin = latin && nu <= cap;
     const bool ok = latin && nu <= 64, ok2 = latin && nu > 64;
 #pragma unroll
     for (int b = 0; b < N_PLANES; ++b) planes[row * N_PLANES + b] = (ok || ok2) ? pl[b] : 0;
     if (planes_hi)
 #pragma unroll
         for (int b = 0; b < N_PLANES; ++b) planes_hi[row * N_PLANES + b] = ok2 ? ph[b] : 0;
-    for (int i = 0; i < 4 && i < nu; ++i) m.head |= (uint64_t)dst[i] << (16 * i);
+    m.head = head;
     m.len16 = nu;
     m.cpf = (uint32_t)nc | (ok ? CPF_PLANES : 0u) | (ok2 ? CPF_PLANES2 : 0u) | (ids ? CPF_ID : 0u);
     h ^= (uint64_t)nu;

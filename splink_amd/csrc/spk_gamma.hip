@@ -967,7 +967,6 @@ constexpr int LEVQ_ADOPT = SPK_LEVQ_ADOPT;  // idle lanes that trigger a hand-ou
 constexpr int LEVQ_STEPS = SPK_LEVQ_STEPS;  // scan steps between rounds
 static_assert(32 % LEVQ_STEPS == 0, "k_lev_refill moves a text's upper plane words down between blocks, at j = 32");
 constexpr int LEVQ_WG_PER_CU = 4;
-constexpr int LEVQ_S = 129;         // len_l + len_r of rows with planes (<= 64 units each)
 
 // lev_cell's level of a cell from eq (1 equal / 0 unequal) and the clamped distance; nsum = na + nb.
 __device__ inline int lev_level_of(const SimpleCol &sc, int eq, int lev, int nsum) {
@@ -992,18 +991,45 @@ __device__ unsigned long long g_levq[16];
 #else
 #define LEVQ_STAT(i, v) ((void)0)
 #endif
-template <int NP>
-__global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_refill(GammaArgs A, int si, const int32_t *xlist,
-                                                                      const int64_t *xinfo) {
+// WW = 64-bit words per plane row: 1 = the exact pass over rows of <= 64 units (cells the filter listed; cells
+// with a longer or non-Latin-1 row go on to the slow list), 2 = the slow pass over rows of <= 128 units (cells the
+// exact pass listed there; cells with a row past 128 units or a unit >= 256 go on to the rest list).
+template <int WW>
+struct RefillWord {
+    typedef uint64_t type;
+};
+template <>
+struct RefillWord<2> {
+    typedef u128 type;
+};
+template <int WW>
+__device__ inline int refill_popc(typename RefillWord<WW>::type x) {
+    if constexpr (WW == 1) return __builtin_popcountll((unsigned long long)x);
+    else return popc128(x);
+}
+template <int WW>
+__device__ inline typename RefillWord<WW>::type refill_mask(int i) {  // bits [0, i), 1 <= i <= 64 WW
+    typedef typename RefillWord<WW>::type W;
+    return i >= 64 * WW ? ~(W)0 : (((W)1 << i) - 1);
+}
+
+template <int NP, int WW>
+__global__ __launch_bounds__(X_THREADS, WW == 2 ? 2 : (NP == 8 ? 3 : LEVQ_WAVES)) void k_lev_refill(
+    GammaArgs A, int si, int32_t *xlist, const int64_t *xinfo) {
+    typedef typename RefillWord<WW>::type Word;
     constexpr int WPB = X_THREADS / 64;
-    constexpr int QW = 4 * NP + 2;  // queue entry words: P (lo, hi), T (lo, hi) per plane, p, m | n | cut | nsum
+    constexpr int PW = 2 * WW;                  // 32-bit words per plane row
+    constexpr int QP = 2 * PW * NP;             // queue words of the pattern and text planes
+    constexpr int QW = QP + (WW == 1 ? 2 : 3);  // + p, m | n | cut (| nsum when WW = 1), nsum (WW = 2)
+    constexpr int S_MAX = 128 * WW + 1;         // len_l + len_r of rows this pass scans, plus one
+    constexpr int CUT_MAX = 128 * WW - 1;       // distances here are <= 64 WW: a larger cut is no cut
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
     __shared__ uint32_t s_q[WPB][QW][64];
     __shared__ int32_t s_slow[WPB][128];
-    __shared__ uint32_t s_res[WPB][2][128];  // finished cells: p, code delta
-    __shared__ int8_t s_bp[LEVQ_S][MAX_TESTS];  // largest clamped distance passing test i (eq = 0), -1 none
-    __shared__ uint8_t s_cut[LEVQ_S];
+    __shared__ uint32_t s_res[WPB][2][128];      // finished cells: p, code delta
+    __shared__ int16_t s_bp[S_MAX][MAX_TESTS];  // largest clamped distance passing test i (eq = 0), -1 none
+    __shared__ uint8_t s_cut[S_MAX];
     __shared__ int s_tab;
     if (threadIdx.x == 0) {
         s_sc = A.simple[si];
@@ -1013,15 +1039,19 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
     __syncthreads();
     const SimpleCol &sc = s_sc;
     // per len_l + len_r: the cut and each test's threshold (the filter's integer forms: lev_a, the ratio tables)
-    for (int S = threadIdx.x; S < LEVQ_S; S += X_THREADS) {
+    for (int S = threadIdx.x; S < S_MAX; S += X_THREADS) {
         const int c = simple_lev_cut(sc, S, 0);
-        s_cut[S] = (uint8_t)(c < 127 ? c : 127);  // distances here are <= 64: any cut >= 64 is no cut
+        s_cut[S] = (uint8_t)(c < CUT_MAX ? c : CUT_MAX);
         for (int i = 0; i < sc.n_tests; ++i) {
             int bp = -1;
-            if (sc.op[i] == SPK_OP_STR_CMP) bp = sc.cmp[i] == SPK_CMP_EQ ? -1 : 127;
+            if (sc.op[i] == SPK_OP_STR_CMP) bp = sc.cmp[i] == SPK_CMP_EQ ? -1 : CUT_MAX + 1;
             else if (sc.op[i] == SPK_OP_LEV) bp = sc.lev_a[i];
-            else if (sc.thr_off[i] >= 0) bp = A.thr[sc.thr_off[i] + S];
-            s_bp[S][i] = (int8_t)(bp < -1 ? -1 : (bp > 127 ? 127 : bp));
+            else if (sc.thr_off[i] >= 0 && S < THR_S) bp = A.thr[sc.thr_off[i] + S];
+            else if (sc.thr_off[i] >= 0) {  // len_l + len_r past the host tables (WW = 2: S = 256): the same scan
+                const double den = (double)S / 2.0;
+                for (int v = 0; v <= CUT_MAX + 1 && cmpd((double)v / den, sc.t[i], sc.cmp[i]) == KT; ++v) bp = v;
+            }
+            s_bp[S][i] = (int16_t)(bp < -1 ? -1 : (bp > CUT_MAX + 1 ? CUT_MAX + 1 : bp));
         }
     }
     if (threadIdx.x == 0) {  // every test a `<=` / `<` on the distance or a string (in)equality: levels by table
@@ -1044,8 +1074,11 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
         for (int i = n_tests - 1; i >= 0; --i) level = lev <= s_bp[S][i] ? sc.level[i] : level;
         return level;
     };
-    const int64_t n_items = exact_count(A, xinfo, k);
-    const int32_t *items = xlist + xinfo[k];
+    // the input list and where the cells this pass cannot scan go
+    const int64_t n_items = WW == 1 ? exact_count(A, xinfo, k) : (int64_t)A.slow_count[k];
+    const int32_t *items = WW == 1 ? xlist + xinfo[k] : A.slow + A.slow_off[k];
+    int32_t *out_list = WW == 1 ? A.slow + A.slow_off[k] : xlist + xinfo[k];
+    unsigned int *out_count = A.slow_count + (WW == 1 ? k : A.K + k);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const unsigned long long below = (1ull << lane) - 1ull;
     // the wave's contiguous range of batches (64 list entries each)
@@ -1064,8 +1097,7 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
     const int colx = A.simple[si].col;
     GWord *meta0 = (GWord *)A.cols0[colx].meta, *meta1 = (GWord *)A.cols1[colx].meta;
     GPlane *plane0 = (GPlane *)A.cols0[colx].planes, *plane1 = (GPlane *)A.cols1[colx].planes;
-    int32_t *slow_list = A.slow + A.slow_off[k];
-    unsigned int *slow_count = A.slow_count + k;
+    GPlane *hi0 = (GPlane *)A.cols0[colx].planes_hi, *hi1 = (GPlane *)A.cols1[colx].planes_hi;
     // list entry of this lane in batch b, clamped into the range (unconditional loads: no divergent skips)
     auto entry = [&](int64_t b) -> int32_t {
         const int64_t bb = b < b_end ? b : b_end - 1;
@@ -1073,11 +1105,15 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
         i = i < n_items ? i : n_items - 1;
         return items[i];
     };
-    // staged batch: records (key, len16, head, cpf) and planes 0 .. NP - 1 of both rows
+    // staged batch: records (key, len16, head, cpf) and planes 0 .. NP - 1 of both rows (WW = 2: both words)
     uint32_t ska = 0, skb = 0, sfa = 0, sfb = 0;
     int32_t sla = 0, slb = 0;
     uint64_t sha = 0, shb = 0;
-    uint64_t sqa[NP], sqb[NP];
+    uint64_t sqa[WW][NP], sqb[WW][NP];
+#pragma unroll
+    for (int h = 0; h < WW; ++h)
+#pragma unroll
+        for (int b = 0; b < NP; ++b) sqa[h][b] = sqb[h][b] = 0;
     auto stage = [&](int32_t x, int32_t y) {
         GWord *ma = meta0 + (int64_t)x * 8, *mb = meta1 + (int64_t)y * 8;
         ska = ma[0];
@@ -1091,8 +1127,16 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
         GPlane *qa = plane0 + (int64_t)x * N_PLANES, *qb = plane1 + (int64_t)y * N_PLANES;
 #pragma unroll
         for (int b = 0; b < NP; ++b) {
-            sqa[b] = qa[b];
-            sqb[b] = qb[b];
+            sqa[0][b] = qa[b];
+            sqb[0][b] = qb[b];
+        }
+        if constexpr (WW == 2) {  // units 64 .. 127 (zero in rows of <= 64 units); a side without them: zero
+            GPlane *ra = hi0 ? hi0 + (int64_t)x * N_PLANES : nullptr, *rb = hi1 ? hi1 + (int64_t)y * N_PLANES : nullptr;
+#pragma unroll
+            for (int b = 0; b < NP; ++b) {
+                sqa[1][b] = ra ? ra[b] : 0ull;
+                sqb[1][b] = rb ? rb[b] : 0ull;
+            }
         }
     };
     // prefetch pipeline: p0 = entry(bn) with its rows staged, p1 = entry(bn + 1) with row ids x1 / y1, p2 =
@@ -1108,20 +1152,20 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
     // the lane's cell: `active` while it holds one, `run` while its scan has text units left
     bool active = false, run = false;
     int32_t p = 0;
-    uint32_t P[2 * NP], T[2 * NP];  // (lo, hi) words of the pattern / text planes
+    uint32_t P[PW * NP], T[PW * NP];  // plane b: words [PW b, PW b + PW) of the pattern / text planes
 #pragma unroll
-    for (int b = 0; b < 2 * NP; ++b) P[b] = T[b] = 0;
-    uint64_t VP = 0, VN = 0;
+    for (int b = 0; b < PW * NP; ++b) P[b] = T[b] = 0;
+    Word VP = 0, VN = 0;
     int m = 1, n = 0, j = 0, cut = 0, S = 0;
     auto flush_res = [&]() {  // the buffered code adds (fire-and-forget atomics)
         for (int i = lane; i < n_res; i += 64) code_add_atomic(A, (int32_t)s_res[wv][0][i], s_res[wv][1][i]);
         n_res = 0;
     };
-    auto flush_slow = [&](int cnt) {  // the first cnt (<= 64) buffered slow cells to the slow list
+    auto flush_slow = [&](int cnt) {  // the first cnt (<= 64) buffered cells to the output list
         unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(slow_count, (unsigned int)cnt);
+        if (lane == 0) base = atomicAdd(out_count, (unsigned int)cnt);
         base = __shfl(base, 0);
-        if (lane < cnt) slow_list[base + lane] = s_slow[wv][lane];
+        if (lane < cnt) out_list[base + lane] = s_slow[wv][lane];
         const int rest = n_slow - cnt;
         const int32_t moved = lane < rest ? s_slow[wv][cnt + lane] : 0;
         __builtin_amdgcn_wave_barrier();
@@ -1138,8 +1182,8 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
             int lev = 0;
             if (active) {
                 const int i_end = run ? j + (m - n) : m;  // the end cell's diagonal, or row m at j = n
-                const uint64_t M = low_mask<uint64_t>(i_end);
-                const int d = j + popc_w(VP & M) - popc_w(VN & M);
+                const Word M = refill_mask<WW>(i_end);
+                const int d = j + refill_popc<WW>(VP & M) - refill_popc<WW>(VN & M);
                 fin = !run || d > cut;
                 lev = d > cut ? cut + 1 : d;
             }
@@ -1156,12 +1200,14 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
                 if (n_res > 64) flush_res();  // (a batch flushes it; this only when batches ran out)
             }
         }
-        // a text past 32 units: its upper plane words move down once the scan reaches unit 32 (blocks of
-        // LEVQ_STEPS steps start at multiples of LEVQ_STEPS, a divisor of 32)
-        if (__any(run && j == 32)) {
-            if (run && j == 32) {
+        // a text past 32 units: its next plane words move down whenever the scan reaches a multiple of 32 units
+        // (blocks of LEVQ_STEPS steps start at multiples of LEVQ_STEPS, a divisor of 32)
+        if (__any(run && j > 0 && (j & 31) == 0)) {
+            if (run && j > 0 && (j & 31) == 0) {
 #pragma unroll
-                for (int b = 0; b < NP; ++b) T[2 * b] = T[2 * b + 1];
+                for (int b = 0; b < NP; ++b)
+#pragma unroll
+                    for (int h = 0; h + 1 < PW; ++h) T[PW * b + h] = T[PW * b + h + 1];
             }
         }
         const int n_act = __popcll(__ballot(active));
@@ -1172,7 +1218,7 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
             const unsigned long long t_b = clock64();
             LEVQ_STAT(1, 1);
 #endif
-            // Order: (0) a full slow buffer's device atomic (its return waits for everything in flight -- here
+            // Order: (0) a full output buffer's device atomic (its return waits for everything in flight -- here
             // only the previous batch's loads and code adds), (1) the setup from the staged registers, (2) the
             // next prefetch loads, (3) LDS writes and fire-and-forget code adds: nothing after (2) waits on a load
             if (n_slow >= 64) flush_slow(64);
@@ -1180,58 +1226,72 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
             const int64_t left = n_items - bn * 64;
             const bool valid = lane < left;
             bool to_slow = false, done = false, scan = false, a_pat = false;
-            int level = 0, pre = 0;
-            uint32_t pk = 0;
+            int level = 0, pre = 0, mm = 0, nn = 0, c = 0, s2 = 0;
             if (valid) {
                 const RecMeta ma = {ska, sla, 0, sha, 0, sfa}, mb = {skb, slb, 0, shb, 0, sfb};
                 const int la = sla, lb = slb;
-                const int na = meta_cplen(ma), nb = meta_cplen(mb), s2 = na + nb;
+                const int na = meta_cplen(ma), nb = meta_cplen(mb);
+                s2 = na + nb;
+                // WW = 1: 64-bit planes on both sides; WW = 2: 64- or 128-bit planes (a row of 65 .. 128
+                // units has its units 64 .. 127 in planes_hi)
+                constexpr uint32_t ANY = WW == 1 ? CPF_PLANES : (CPF_PLANES | CPF_PLANES2);
+                const bool planes = (sfa & ANY) && (sfb & ANY) && (WW == 1 || ((!(sfa & CPF_PLANES2) || hi0) &&
+                                                                                (!(sfb & CPF_PLANES2) || hi1)));
                 if (la < 0 || lb < 0) {
                     level = sc.null_level;
                     done = true;
                 } else {
-                    const bool planes = (sfa & sfb & CPF_PLANES) != 0;
                     int eq = meta_equal(ma, mb);
                     if (eq < 0 && planes) {  // hash match without dictionary ids: the planes are the units
                         bool same = la == lb;
 #pragma unroll
-                        for (int b = 0; b < NP; ++b) same = same && sqa[b] == sqb[b];
+                        for (int h = 0; h < WW; ++h)
+#pragma unroll
+                            for (int b = 0; b < NP; ++b) same = same && sqa[h][b] == sqb[h][b];
                         eq = same ? 1 : 0;
                     }
                     if (eq == 1) {
                         level = lev_level_of(sc, 1, 0, s2);
                         done = true;
                     } else if (!planes) {
-                        to_slow = true;  // > 64 units or a unit >= 256: the slow list's 128-bit / DP passes
+                        to_slow = true;  // WW = 1: the slow list; WW = 2: the rest list (the interpreter)
                     } else {
-                        const int c = s_cut[s2];
+                        c = s_cut[s2];
                         int lev = -1;
                         if (la == 0 || lb == 0) {
                             lev = la + lb;
                         } else {
                             const int mn = la < lb ? la : lb;
-                            uint64_t d = 0, e = 0;
+                            Word d = 0, e = 0;
 #pragma unroll
                             for (int b = 0; b < NP; ++b) {
-                                d |= sqa[b] ^ sqb[b];
-                                e |= (sqa[b] << (64 - la)) ^ (sqb[b] << (64 - lb));
+                                Word wa = sqa[0][b], wb = sqb[0][b];
+                                if constexpr (WW == 2) {
+                                    wa |= (Word)sqa[1][b] << 64;
+                                    wb |= (Word)sqb[1][b] << 64;
+                                }
+                                d |= wa ^ wb;
+                                e |= (wa << (64 * WW - la)) ^ (wb << (64 * WW - lb));
                             }
-                            pre = d ? __ffsll((unsigned long long)d) - 1 : 64;
+                            if constexpr (WW == 1) {
+                                pre = d ? __ffsll((unsigned long long)d) - 1 : 64;
+                            } else {
+                                pre = ctz128(d);
+                            }
                             if (pre > mn) pre = mn;
-                            int suf = e ? __clzll((long long)e) : 64;
+                            int suf;
+                            if constexpr (WW == 1) suf = e ? __clzll((long long)e) : 64;
+                            else suf = clz128(e);
                             if (suf > mn - pre) suf = mn - pre;
                             const int ra = la - pre - suf, rb = lb - pre - suf;
                             if (ra == 0 || rb == 0) {
                                 lev = ra + rb;
                             } else {
                                 a_pat = ra >= rb;
-                                const int mm = a_pat ? ra : rb, nn = a_pat ? rb : ra;
-                                if (mm - nn > c) {
-                                    lev = c + 1;  // the length gap alone exceeds the cut
-                                } else {
-                                    pk = (uint32_t)mm | ((uint32_t)nn << 8) | ((uint32_t)c << 16) | ((uint32_t)s2 << 24);
-                                    scan = true;
-                                }
+                                mm = a_pat ? ra : rb;
+                                nn = a_pat ? rb : ra;
+                                if (mm - nn > c) lev = c + 1;  // the length gap alone exceeds the cut
+                                else scan = true;
                             }
                         }
                         if (!scan) {
@@ -1247,20 +1307,31 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
                 const int r = __popcll(sm & below);
 #pragma unroll
                 for (int b = 0; b < NP; ++b) {
-                    const uint64_t pp = (a_pat ? sqa[b] : sqb[b]) >> pre;
-                    const uint64_t tt = (a_pat ? sqb[b] : sqa[b]) >> pre;
-                    s_q[wv][2 * b][r] = (uint32_t)pp;
-                    s_q[wv][2 * b + 1][r] = (uint32_t)(pp >> 32);
-                    s_q[wv][2 * NP + 2 * b][r] = (uint32_t)tt;
-                    s_q[wv][2 * NP + 2 * b + 1][r] = (uint32_t)(tt >> 32);
+                    Word wa = sqa[0][b], wb = sqb[0][b];
+                    if constexpr (WW == 2) {
+                        wa |= (Word)sqa[1][b] << 64;
+                        wb |= (Word)sqb[1][b] << 64;
+                    }
+                    const Word pp = (a_pat ? wa : wb) >> pre;
+                    const Word tt = (a_pat ? wb : wa) >> pre;
+#pragma unroll
+                    for (int h = 0; h < PW; ++h) {
+                        s_q[wv][PW * b + h][r] = (uint32_t)(pp >> (32 * h));
+                        s_q[wv][PW * NP + PW * b + h][r] = (uint32_t)(tt >> (32 * h));
+                    }
                 }
-                s_q[wv][4 * NP][r] = (uint32_t)pc;
-                s_q[wv][4 * NP + 1][r] = pk;
+                s_q[wv][QP][r] = (uint32_t)pc;
+                if constexpr (WW == 1) {
+                    s_q[wv][QP + 1][r] = (uint32_t)mm | ((uint32_t)nn << 8) | ((uint32_t)c << 16) | ((uint32_t)s2 << 24);
+                } else {
+                    s_q[wv][QP + 1][r] = (uint32_t)mm | ((uint32_t)nn << 8) | ((uint32_t)c << 16);
+                    s_q[wv][QP + 2][r] = (uint32_t)s2;
+                }
             }
             q_head = 0;
             q_count = __popcll(sm);
             LEVQ_STAT(8, q_count);
-            // slow cells into the slow buffer
+            // cells this pass cannot scan into the output buffer
             const unsigned long long wm = __ballot(to_slow);
             if (wm) {
                 if (to_slow) s_slow[wv][n_slow + __popcll(wm & below)] = pc;
@@ -1293,19 +1364,17 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
                 if (!active && r < q_count) {
                     const int e = q_head + r;
 #pragma unroll
-                    for (int b = 0; b < NP; ++b) {
-                        P[2 * b] = s_q[wv][2 * b][e];
-                        P[2 * b + 1] = s_q[wv][2 * b + 1][e];
-                        T[2 * b] = s_q[wv][2 * NP + 2 * b][e];
-                        T[2 * b + 1] = s_q[wv][2 * NP + 2 * b + 1][e];
+                    for (int b = 0; b < PW * NP; ++b) {
+                        P[b] = s_q[wv][b][e];
+                        T[b] = s_q[wv][PW * NP + b][e];
                     }
-                    p = (int32_t)s_q[wv][4 * NP][e];
-                    const uint32_t pk = s_q[wv][4 * NP + 1][e];
+                    p = (int32_t)s_q[wv][QP][e];
+                    const uint32_t pk = s_q[wv][QP + 1][e];
                     m = (int)(pk & 0xFF);
                     n = (int)((pk >> 8) & 0xFF);
                     cut = (int)((pk >> 16) & 0xFF);
-                    S = (int)(pk >> 24);
-                    VP = ~0ull;
+                    S = WW == 1 ? (int)(pk >> 24) : (int)s_q[wv][QP + 2][e];
+                    VP = ~(Word)0;
                     VN = 0;
                     j = 0;
                     active = run = true;
@@ -1320,37 +1389,47 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
             continue;
         }
         // ---- LEVQ_STEPS scan steps of the lanes whose text has units left (a lane stops at j = n: its exec
-        // bit drops, no branch).  The word width is a wave-uniform choice per block of steps: 64-bit words only
-        // when some scanning lane needs them in the block.  A pattern of > 32 units needs them from text unit
-        // J0 = 31 - cut on (Ukkonen, as myers_plane_text_lazy): D[i][j] >= i - j, so rows >= 33 cannot hold a
-        // value <= cut before it, and until then a 32-bit step leaves rows 33 .. m at D[32][j] + (i - 32)
-        // (VP bits set, VN bits clear above row 32) -- upper bounds that differ from the true values only where
-        // both are > cut, so the cut tests and the clamped distance read the same.  The text's plane words are
-        // read at bit j & 31 of T[2b]; a lane's upper words move down at j = 32 (in the round, above).
-        bool need64 = false;
-        if (run && m > 32) need64 = j + LEVQ_STEPS > (cut < 31 ? 31 - cut : 0);
-        const bool wide = __any(need64);
+        // bit drops, no branch).  The word width is a wave-uniform choice per block of steps: the full width only
+        // when some scanning lane needs it in the block.  A pattern of more than H = 32 WW units needs it from
+        // text unit J0 = (H - 1) - cut on (Ukkonen, as myers_plane_text_lazy): D[i][j] >= i - j, so rows > H
+        // cannot hold a value <= cut before it, and until then a half-width step leaves rows H + 1 .. m at
+        // D[H][j] + (i - H) (VP bits set, VN bits clear above row H) -- upper bounds that differ from the true
+        // values only where both are > cut, so the cut tests and the clamped distance read the same.  The text's
+        // plane words are read at bit j & 31 of T[PW b]; a lane's next words move down at multiples of 32 (in
+        // the round, above).
+        constexpr int H = 32 * WW;
+        bool need_full = false;
+        if (run && m > H) need_full = j + LEVQ_STEPS > (cut < H - 1 ? H - 1 - cut : 0);
+        const bool wide = __any(need_full);
 #ifdef SPK_LEVQ_STATS
         const unsigned long long t_s = clock64();
         LEVQ_STAT(wide ? 5 : 4, LEVQ_STEPS);
         LEVQ_STAT(7, __popcll(__ballot(run)));
 #endif
         if (!wide) {
+            typedef typename std::conditional<WW == 1, uint32_t, uint64_t>::type Half;
             for (int s = 0; s < LEVQ_STEPS; ++s) {
                 if (run) {
-                    uint32_t eq = ~0u;
+                    const uint32_t jj = (uint32_t)j & 31u;
+                    Half eq = ~(Half)0;
 #pragma unroll
-                    for (int b = 0; b < NP; ++b)
-                        eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)T[2 * b], j, 1), P[2 * b]);
-                    uint32_t vp = (uint32_t)VP, vn = (uint32_t)VN;
-                    const uint32_t x = eq | vn;
-                    const uint32_t d0 = (((x & vp) + vp) ^ vp) | x;
-                    const uint32_t hp = (vn | ~(d0 | vp)) << 1 | 1u;
-                    const uint32_t hn = (d0 & vp) << 1;
+                    for (int b = 0; b < NP; ++b) {
+                        const uint32_t mb = (uint32_t)__builtin_amdgcn_sbfe((int)T[PW * b], jj, 1);
+                        if constexpr (WW == 1) {
+                            eq = eq_plane(eq, mb, P[PW * b]);
+                        } else {
+                            eq = eq_plane(eq, mb, ((uint64_t)P[PW * b + 1] << 32) | P[PW * b]);
+                        }
+                    }
+                    Half vp = (Half)VP, vn = (Half)VN;
+                    const Half x = eq | vn;
+                    const Half d0 = (((x & vp) + vp) ^ vp) | x;
+                    const Half hp = (vn | ~(d0 | vp)) << 1 | (Half)1;
+                    const Half hn = (d0 & vp) << 1;
                     vp = hn | ~(d0 | hp);
                     vn = hp & d0;
-                    VP = 0xFFFFFFFF00000000ull | vp;  // rows 33 .. m: D[32][j] + (i - 32)
-                    VN = vn;
+                    VP = (~(Word)0 << H) | (Word)vp;  // rows H + 1 .. m: D[H][j] + (i - H)
+                    VN = (Word)vn;
                     ++j;
                     run = j < n;
                 }
@@ -1359,18 +1438,22 @@ __global__ __launch_bounds__(X_THREADS, NP == 8 ? 3 : LEVQ_WAVES) void k_lev_ref
             for (int s = 0; s < LEVQ_STEPS; ++s) {
                 if (run) {
                     const uint32_t jj = (uint32_t)j & 31u;
-                    uint32_t e0 = ~0u, e1 = ~0u;
+                    uint32_t e[PW];
+#pragma unroll
+                    for (int h = 0; h < PW; ++h) e[h] = ~0u;
 #pragma unroll
                     for (int b = 0; b < NP; ++b) {
-                        const uint32_t mb = (uint32_t)__builtin_amdgcn_sbfe((int)T[2 * b], jj, 1);
-                        e0 = eq_plane(e0, mb, P[2 * b]);
-                        e1 = eq_plane(e1, mb, P[2 * b + 1]);
+                        const uint32_t mb = (uint32_t)__builtin_amdgcn_sbfe((int)T[PW * b], jj, 1);
+#pragma unroll
+                        for (int h = 0; h < PW; ++h) e[h] = eq_plane(e[h], mb, P[PW * b + h]);
                     }
-                    const uint64_t eq = ((uint64_t)e1 << 32) | e0;
-                    const uint64_t x = eq | VN;
-                    const uint64_t d0 = (((x & VP) + VP) ^ VP) | x;
-                    const uint64_t hp = (VN | ~(d0 | VP)) << 1 | 1ull;
-                    const uint64_t hn = (d0 & VP) << 1;
+                    Word eq = 0;
+#pragma unroll
+                    for (int h = 0; h < PW; ++h) eq |= (Word)e[h] << (32 * h);
+                    const Word x = eq | VN;
+                    const Word d0 = (((x & VP) + VP) ^ VP) | x;
+                    const Word hp = (VN | ~(d0 | VP)) << 1 | (Word)1;
+                    const Word hn = (d0 & VP) << 1;
                     VP = hn | ~(d0 | hp);
                     VN = hp & d0;
                     ++j;
@@ -1960,7 +2043,18 @@ static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
         const int si = G.simple_of[k];
         const bool lev = si >= 0 && G.simple[si].cls == SC_LEV;
         const ColSet one_k{1, {k, 0, 0, 0}};
-        if (lev) {
+        if (lev && ctx->lev_kernel == 1) {
+            // lane refill over 128-bit planes (A/B only: 5.13 -> 5.47 ms per cfg5 γ pass against k_gamma_slow_lev,
+            // DESIGN.md §4): 2 waves per SIMD (its LDS queue), one resident round
+            const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)2 * ctx->n_cu));
+            switch (G.simple[si].np) {
+                case 5: k_lev_refill<5, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                case 6: k_lev_refill<6, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                case 7: k_lev_refill<7, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                default: k_lev_refill<8, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+            }
+            k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
+        } else if (lev) {
             constexpr int SLOWLEV_WG_PER_CU = 8;  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU at once
             const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SLOWLEV_WG_PER_CU * ctx->n_cu));
             k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
@@ -2047,10 +2141,10 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
             const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, wg_cu * ctx->n_cu));
             SPK_TRY(ctx->xbegin(k));
             switch (simple[si].np) {
-                case 5: k_lev_refill<5><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
-                case 6: k_lev_refill<6><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
-                case 7: k_lev_refill<7><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
-                default: k_lev_refill<8><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                case 5: k_lev_refill<5, 1><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                case 6: k_lev_refill<6, 1><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                case 7: k_lev_refill<7, 1><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
+                default: k_lev_refill<8, 1><<<(unsigned)g_lev, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
             }
             SPK_TRY(ctx->xend(k));
             if (quiet(k)) G.slow_skipped[k] = 1;
