@@ -352,20 +352,32 @@ __global__ void k_arrow_rebase(int64_t n, int64_t *__restrict__ off, int64_t bas
 }
 __global__ void k_arrow_lengths(int64_t n, const int64_t *__restrict__ off, const uint8_t *__restrict__ valid,
                                 unsigned long long *__restrict__ stats) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // grid-stride over the rows, then wave and workgroup reductions: one atomic per workgroup (an atomic per
+    // wave on the same two words serialised at L2: 180 us per million rows)
+    __shared__ unsigned long long s_len[4], s_empty[4];
     unsigned long long len = 0, empty = 0;
-    if (i < n) {
-        len = (unsigned long long)(off[i + 1] - off[i]);
-        empty = (valid[i] && len == 0) ? 1ull : 0ull;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long l = (unsigned long long)(off[i + 1] - off[i]);
+        len = l > len ? l : len;
+        empty |= (valid[i] && l == 0) ? 1ull : 0ull;
     }
-    // wave maximum / or, one atomic per wave
     for (int o = 32; o >= 1; o >>= 1) {
         const unsigned long long a = __shfl_xor(len, o), e = __shfl_xor(empty, o);
         len = a > len ? a : len;
         empty |= e;
     }
-    if ((threadIdx.x & 63) == 0 && (len || empty)) {
-        atomicMax(&stats[0], len);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_len[wv] = len;
+        s_empty[wv] = empty;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < (int)(blockDim.x >> 6); ++q) {
+            len = s_len[q] > len ? s_len[q] : len;
+            empty |= s_empty[q];
+        }
+        if (len) atomicMax(&stats[0], len);
         if (empty) atomicOr(&stats[1], 1ull);
     }
 }
@@ -476,7 +488,9 @@ int spk_raw_utf8_arrow(spk_ctx *ctx, int raw, int64_t n, const int64_t *offsets,
     SPK_TRY(st.alloc(2));
     SPK_HIP(hipMemsetAsync(st.p, 0, 16, ctx->stream));
     k_arrow_rebase<<<grid(n + 1), 256, 0, ctx->stream>>>(n, r->off.p, ends[0], d_bm, validity_bit_offset, r->valid.p);
-    if (n) k_arrow_lengths<<<grid(n), 256, 0, ctx->stream>>>(n, r->off.p, r->valid.p, st.p);
+    if (n)
+        k_arrow_lengths<<<(unsigned)std::min<int64_t>(grid(n), 4 * (int64_t)ctx->n_cu), 256, 0, ctx->stream>>>(
+            n, r->off.p, r->valid.p, st.p);
     SPK_HIP(hipGetLastError());
     unsigned long long h[2] = {0, 0};
     SPK_HIP(hipMemcpyAsync(h, st.p, 16, hipMemcpyDeviceToHost, ctx->stream));
@@ -533,7 +547,9 @@ int spk_raw_utf8_arrow_chunks(spk_ctx *ctx, int raw, int n_chunks, const int64_t
     DevBuf<unsigned long long> st;
     SPK_TRY(st.alloc(2));
     SPK_HIP(hipMemsetAsync(st.p, 0, 16, ctx->stream));
-    if (n) k_arrow_lengths<<<grid(n), 256, 0, ctx->stream>>>(n, r->off.p, r->valid.p, st.p);
+    if (n)
+        k_arrow_lengths<<<(unsigned)std::min<int64_t>(grid(n), 4 * (int64_t)ctx->n_cu), 256, 0, ctx->stream>>>(
+            n, r->off.p, r->valid.p, st.p);
     SPK_HIP(hipGetLastError());
     unsigned long long h[2] = {0, 0};
     SPK_HIP(hipMemcpyAsync(h, st.p, 16, hipMemcpyDeviceToHost, ctx->stream));

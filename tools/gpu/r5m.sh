@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   > gpurun_out/r5m_suite.log 2>&1 || { tail -30 gpurun_out/r5m_suite.log; exit 1; }
 tail -1 gpurun_out/r5m_suite.log
-timeout -k 10 300 python -u tools/ab_lev_refill.py 5 6 0 2 2>&1 | grep -v amdgpu.ids > gpurun_out/r5m_ab.log || { cat gpurun_out/r5m_ab.log; exit 1; }
+timeout -k 10 300 python -u tools/ab_lev_refill.py 5 4 0 2 1 2>&1 | grep -v amdgpu.ids > gpurun_out/r5m_ab.log || { cat gpurun_out/r5m_ab.log; exit 1; }
 cat gpurun_out/r5m_ab.log
 bash tools/gpu/r5d.sh r5m || exit 1
 RULES="l.surname = r.surname|l.dob = r.dob and l.city = r.city"
