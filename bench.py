@@ -332,26 +332,14 @@ def em_streaming(job, names, nlev, params, reps, iters=10):
     del big
     cb = 2 if job.ctx.n_patterns() <= 65536 else 4
     lam, lp = params.params["λ"], params._level_probabilities()
-
-    def em_ms():
-        job.em_stats(lam, lp)
-        ms = job.ctx.kernel_ms()
-        return ms["em_hist"], max(ms["em_final"], 0.0)
-
-    # pattern codes (occupied-pattern ids off), then the same iterations as a job runs them: the launch after
-    # one that counted these codes re-encodes them as dense ids, the later ones stream those
-    job.ctx.em_set_dense(False)
     for _ in range(2):
-        em_ms()
-    codes_ms = float(np.median([sum(em_ms()) for _ in range(iters)]))
-    job.ctx.em_set_dense(True)
-    encode_ms = sum(em_ms())
-    dense = job.ctx.em_dense_info()
+        job.em_stats(lam, lp)
     hist, fin = [], []
     for _ in range(iters):
-        h_ms, f_ms = em_ms()
-        hist.append(h_ms)
-        fin.append(f_ms)
+        job.em_stats(lam, lp)
+        ms = job.ctx.kernel_ms()
+        hist.append(ms["em_hist"])
+        fin.append(max(ms["em_final"], 0.0))
     sc = []
     for _ in range(3):
         job.score(lam, lp, want_host=False)
@@ -366,9 +354,7 @@ def em_streaming(job, names, nlev, params, reps, iters=10):
             "k_score": {"bound": "hbm", "avg_launch_ms": s, "algorithmic_bytes_per_launch": sb,
                         "achieved": sb / (s / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": sb / (s / 1e3) / 1e9 / HBM_PEAK_GBS},
-            "em_restream_pairs_per_s": P / (h / 1e3),
-            "em_occupied_patterns": {"occupied": dense[0], "n_patterns": int(job.ctx.n_patterns()), "lane_copies": dense[1],
-                                     "pattern_code_launch_ms": codes_ms, "encoding_launch_ms": encode_ms}}
+            "em_restream_pairs_per_s": P / (h / 1e3)}
 
 
 def lev_scan_cells(a: str, b: str, cut: int) -> int:

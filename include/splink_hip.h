@@ -308,13 +308,6 @@ int spk_em_histogram(spk_ctx *ctx, uint64_t *d_hist);
  * into one LDS histogram, 2 = as 1 without the fence (relies on gfx950 draining the row atomics before the
  * ticket).  For testing and measurement. */
 int spk_em_set_lane_histogram(spk_ctx *ctx, int on);
-/* Occupied-pattern ids (default on, same result): when the lane counters hold fewer than 64 copies of the
- * pattern space, the lane launch after one that counted the current codes re-encodes them as dense ids of
- * the patterns that occur (written once, 2 B per pair) and the launches after it stream those with more
- * copies.  spk_em_dense_info: out[0] = occupied patterns of the last encoding, out[1] = lane copies of the
- * dense launches (0: not in use for the current codes). */
-int spk_em_set_dense(spk_ctx *ctx, int on);
-int spk_em_dense_info(spk_ctx *ctx, int32_t *out);
 /* E-step per pattern with the reference's literal arithmetic, then the M-step sums:
  * out_stats (host) = [Σmp, rows, non-null rows, Σ ln(λΠm + (1-λ)Πu), non-null ln rows] + per column k,
  * per level v in -1..L_k-1:

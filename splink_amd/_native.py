@@ -46,8 +46,7 @@ EXPORTS = [
     "spk_pairs_count", "spk_pairs_copy", "spk_pairs_load", "spk_gammas", "spk_gammas_copy", "spk_gammas_load",
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_em_iteration", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
-    "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram",
-    "spk_em_set_dense", "spk_em_dense_info", "spk_table_set_rank_null",
+    "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
@@ -418,16 +417,6 @@ class Context:
         """True / 1: lane-private counters, release fence before each last-arriver ticket (default); False / 0:
         wave-ballot histogram; 2: lane counters without the fence (A/B)."""
         check(self._lib.spk_em_set_lane_histogram(self._h, ctypes.c_int(int(on))), "spk_em_set_lane_histogram")
-
-    def em_set_dense(self, on: bool):
-        """Occupied-pattern ids for the E+M launches after the first on the same codes (default on)."""
-        check(self._lib.spk_em_set_dense(self._h, ctypes.c_int(1 if on else 0)), "spk_em_set_dense")
-
-    def em_dense_info(self):
-        """(occupied patterns, lane copies of the dense launches; 0 = not in use for the current codes)."""
-        out = (ctypes.c_int32 * 2)()
-        check(self._lib.spk_em_dense_info(self._h, out), "spk_em_dense_info")
-        return int(out[0]), int(out[1])
 
     def em_histogram(self, d_hist_ptr: int = 0):
         check(self._lib.spk_em_histogram(self._h, ctypes.c_void_p(d_hist_ptr)), "spk_em_histogram")

@@ -445,34 +445,19 @@ __global__ __launch_bounds__(EF_THREADS) void k_em_finalize(PatArgs A0, const un
 // the parameters while the others stream (published with its ticket), so the finishing workgroup only runs
 // the M-step sums.  R < 64: ghot[0] is the pattern not counted (-1: none yet); `refresh` makes the last
 // workgroup write the most frequent pattern there for the next launches.
-//
-// Occupied-pattern ids (MODE): a comparison pass fills only part of its pattern space (cfg5's 100M-record
-// share: 605 of 2880 patterns), but the lane copies R are sized for all of it.  Once a launch has counted
-// the current codes (cpat), the next one (MODE 1) reads them through an LDS map pattern -> dense id, counts
-// the dense ids with the R the occupied patterns allow and writes them (u16) to dense_out; the launches
-// after it (MODE 2) stream the dense ids.  Bins are dense ids in both; the last workgroup scatters them back
-// to the pattern space (orig) before the E-step, so the statistics are those of MODE 0 bit for bit.
 __host__ __device__ inline int64_t part_stride(int64_t n_pat) { return (n_pat + 31) / 32 * 32; }  // whole 128-B lines
-struct DenseArgs {
-    int n_bins = 0;                     // dense ids (MODE 1 / 2)
-    const uint16_t *map = nullptr;      // MODE 1: pattern -> dense id (staged in LDS past the counters)
-    uint16_t *out = nullptr;            // MODE 1: the dense ids written
-    const int32_t *orig = nullptr;      // dense id -> pattern
-};
-template <typename CodeT, int R, bool FIN, int MODE>
+template <typename CodeT, int R, bool FIN>
 __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict__ codes, int64_t P, PatArgs A0,
                                                         unsigned int *__restrict__ ticket, double *__restrict__ mpat,
                                                         double *__restrict__ llpat, double *__restrict__ cpat,
                                                         double *__restrict__ out, unsigned long long *__restrict__ out_hist,
                                                         int fence, uint32_t *__restrict__ arow,
-                                                        int32_t *__restrict__ ghot, int refresh, int lds_bytes,
-                                                        DenseArgs D) {
+                                                        int32_t *__restrict__ ghot, int refresh, int lds_bytes) {
     extern __shared__ uint32_t sh[];
     __shared__ bool s_last;
     const int n_pat = A0.n_pat;
-    const int n_bins = MODE ? D.n_bins : n_pat;
-    const int n_cnt = n_bins * R;  // counter words
-    constexpr bool HOT = R < 64 && MODE == 0;
+    const int n_cnt = n_pat * R;  // counter words
+    constexpr bool HOT = R < 64;
 #ifdef SPK_EM_STAMPS
     const unsigned long long t_start = wall_clock64();
     if (blockIdx.x == 0) EM_STAMP(0);
@@ -492,9 +477,6 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         __syncthreads();
     }
     for (int b = threadIdx.x; b < n_cnt; b += HL_THREADS) sh[b] = 0;
-    uint16_t *smap = reinterpret_cast<uint16_t *>(sh + n_cnt);
-    if (MODE == 1)
-        for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) smap[b] = D.map[b];
     // HOT: the most frequent pattern (-1: none yet) is not counted at all and the last workgroup sets its bin
     // to P minus every other bin (exact: every one of the P codes is streamed once and is < n_pat; P < 2^32 on
     // this path).  With R = 64 the compare would only cost issue slots in an issue-bound loop (cfg2 0.121 ->
@@ -516,38 +498,6 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
 #pragma unroll
         for (int j = 0; j < 32 / BITS; ++j) count_code(BITS == 32 ? w : ((w >> (BITS * j)) & ((1u << BITS) - 1u)));
     };
-    // one 16-byte vector of codes (index vi): counted, and in MODE 1 mapped to dense ids and stored
-    // MODE 1 in two halves: every map read of the vectors at hand first, then the counter adds (the compiler
-    // cannot tell the map from the counters, so a read after an add waits for it)
-    auto map_vec = [&](const u32x4 &x, uint32_t *d) {
-        const uint32_t in[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            d[2 * j] = smap[in[j] & 0xFFFFu];
-            d[2 * j + 1] = smap[in[j] >> 16];
-        }
-    };
-    auto put_ids = [&](const uint32_t *d, int64_t vi) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) count_code(d[j]);
-        // a global (not flat) store: a flat one may alias the LDS and would be ordered against the ds ops
-        const u32x4 ov = {d[0] | (d[1] << 16), d[2] | (d[3] << 16), d[4] | (d[5] << 16), d[6] | (d[7] << 16)};
-        typedef __attribute__((address_space(1))) u32x4 GVec;
-        ((GVec *)D.out)[vi] = ov;
-    };
-    auto count_vec = [&](const u32x4 &x, int64_t vi) {
-        if constexpr (MODE == 1) {
-            static_assert(VEC == 8, "dense ids re-encode uint16 codes");
-            uint32_t d[8];
-            map_vec(x, d);
-            put_ids(d, vi);
-        } else {
-            count_word(x.x);
-            count_word(x.y);
-            count_word(x.z);
-            count_word(x.w);
-        }
-    };
     // software-pipelined 16-byte nontemporal loads, 2 x HL_UNROLL in flight per lane
     const int64_t step = HL_UNROLL * stride;
     bool have = v + (HL_UNROLL - 1) * stride < n_vec;
@@ -560,36 +510,32 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         const int64_t vn = v + step;
         const bool hn = vn + (HL_UNROLL - 1) * stride < n_vec;
         // unconditional loads (the last round re-reads its own vectors): under a branch the wait before the
-        // counting had to cover the path without them, vmcnt(0), and the next loads were not in flight
+        // counting has to cover the path without them
         const int64_t vl = hn ? vn : v;
         u32x4 x[HL_UNROLL];
 #pragma unroll
         for (int u = 0; u < HL_UNROLL; ++u) x[u] = __builtin_nontemporal_load(cv + vl + u * stride);
-        if constexpr (MODE == 1) {
-            uint32_t d[HL_UNROLL][8];
 #pragma unroll
-            for (int u = 0; u < HL_UNROLL; ++u) map_vec(w[u], d[u]);
-#pragma unroll
-            for (int u = 0; u < HL_UNROLL; ++u) put_ids(d[u], v + u * stride);
-        } else {
-#pragma unroll
-            for (int u = 0; u < HL_UNROLL; ++u) count_vec(w[u], v + u * stride);
+        for (int u = 0; u < HL_UNROLL; ++u) {
+            count_word(w[u].x);
+            count_word(w[u].y);
+            count_word(w[u].z);
+            count_word(w[u].w);
         }
 #pragma unroll
         for (int u = 0; u < HL_UNROLL; ++u) w[u] = x[u];
         v = vn;
         have = hn;
     }
-    for (; v < n_vec; v += stride) count_vec(cv[v], v);
+    for (; v < n_vec; v += stride) {
+        const u32x4 x = cv[v];
+        count_word(x.x);
+        count_word(x.y);
+        count_word(x.z);
+        count_word(x.w);
+    }
     if (blockIdx.x == (pre ? 1u : 0u))  // tail (P not a multiple of VEC)
-        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) {
-            uint32_t c = (uint32_t)codes[p];
-            if (MODE == 1) {
-                c = smap[c];
-                D.out[p] = (uint16_t)c;
-            }
-            count_code(c);
-        }
+        for (int64_t p = n_vec * VEC + threadIdx.x; p < P; p += HL_THREADS) count_code((uint32_t)codes[p]);
     __syncthreads();
 #ifdef SPK_EM_STAMPS
     const unsigned long long t_streamed = wall_clock64();
@@ -616,7 +562,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     const int G = (int)gridDim.x;
     const int64_t ps = part_stride(n_pat);
     uint32_t *my_row = arow + (int64_t)(blockIdx.x % EM_AROWS) * ps;
-    for (int b = threadIdx.x; b < n_bins; b += HL_THREADS) {
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
         uint32_t c = 0;
 #pragma unroll
         for (int k = 0; k < R; ++k) c += sh[b * R + ((k + b) & (R - 1))];  // rotate: spread banks
@@ -641,7 +587,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     const int nr = G < EM_AROWS ? G : EM_AROWS;
     // every row's bin first (independent loads in flight together), then the zeroing stores: a store
     // behind each load to the same address serialised the round trips
-    for (int b = threadIdx.x; b < n_bins; b += HL_THREADS) {
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS) {
         uint32_t vr[EM_AROWS];
 #pragma unroll
         for (int r = 0; r < EM_AROWS; ++r)
@@ -652,7 +598,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         s1[b] = c;
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < n_bins; b += HL_THREADS)
+    for (int b = threadIdx.x; b < n_pat; b += HL_THREADS)
         for (int r = 0; r < nr; ++r) arow[r * ps + b] = 0u;
     if (HOT && hot0 < (uint32_t)n_pat) {  // the uncounted pattern's bin: P minus every other bin
         __shared__ uint32_t s_rest[HL_THREADS / 64];
@@ -670,24 +616,12 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
         __syncthreads();
     }
     EM_STAMP(6);
-    uint32_t *cnt = s1;
-    if (MODE) {  // dense bins back to the pattern space (n_bins + n_pat words of LDS: lane_plan)
-        cnt = sh + n_bins;
-        for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) cnt[p] = 0u;
-        __syncthreads();
-        for (int d = threadIdx.x; d < n_bins; d += HL_THREADS) cnt[D.orig[d]] = s1[d];
-        __syncthreads();
-    }
     // thread t owns bins p = t, t + HL_THREADS, ... (the same mapping as em_finalize_block's loop, so
     // the count it parks in cpat is read back by the thread that wrote it)
     for (int p = threadIdx.x; p < n_pat; p += HL_THREADS) {
-        const unsigned long long c = cnt[p];
-        if (FIN) {
-            cpat[p] = (double)c;
-        } else {
-            out_hist[p] = c;
-            if (cpat) cpat[p] = (double)c;  // the occupancy the next launch may re-encode by
-        }
+        const unsigned long long c = s1[p];
+        if (FIN) cpat[p] = (double)c;
+        else out_hist[p] = c;
     }
     if (HOT && refresh) {  // the most frequent pattern (ties: the lower one) for the next launches
         __shared__ unsigned long long s_best[HL_THREADS / 64];
@@ -723,6 +657,60 @@ __global__ __launch_bounds__(HL_THREADS) void k_em_iter(const CodeT *__restrict_
     if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
+// The uncounted pattern of k_em_iter's first launch on a pair set, guessed from a sample: ghot[0] = the most
+// frequent code (ties: the lower one) among HS_SAMPLES 16-byte vectors spread evenly over the codes.  Without
+// it that launch counted every pair of the dominant pattern into its R lane copies, a same-address LDS atomic
+// chain (cfg5's 100M-record share: 2.5 ms against 0.42 for the launches after it).  Any frequent pattern is a
+// good guess: the counts are exact whichever it is (P minus every other bin).  One workgroup; each equal-code
+// group of a wave adds once per lane group led by the wave's first active code (the dominant one, mostly).
+constexpr int HS_THREADS = 1024;
+constexpr int64_t HS_SAMPLES = 8192;
+template <typename CodeT>
+__global__ __launch_bounds__(HS_THREADS) void k_em_hot_sample(const CodeT *__restrict__ codes, int64_t P, int n_pat,
+                                                              int32_t *__restrict__ ghot) {
+    extern __shared__ uint32_t bins[];  // n_pat
+    __shared__ unsigned long long s_best[HS_THREADS / 64];
+    for (int b = threadIdx.x; b < n_pat; b += HS_THREADS) bins[b] = 0;
+    __syncthreads();
+    auto count = [&](uint32_t c) {
+        const uint32_t lead = __builtin_amdgcn_readfirstlane(c);
+        const unsigned long long m = __ballot(c == lead);
+        if (c != lead) atomicAdd(&bins[c], 1u);
+        else if ((int)__lane_id() == __ffsll((long long)m) - 1) atomicAdd(&bins[lead], (uint32_t)__popcll(m));
+    };
+    constexpr int VEC = 16 / sizeof(CodeT);
+    constexpr int BITS = 8 * sizeof(CodeT);
+    const int64_t n_vec = P / VEC;
+    const int64_t S = n_vec < HS_SAMPLES ? n_vec : HS_SAMPLES;
+    const u32x4 *cv = reinterpret_cast<const u32x4 *>(codes);
+    for (int64_t i = threadIdx.x; i < S; i += HS_THREADS) {
+        const u32x4 x = cv[i * n_vec / S];
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 32 / BITS; ++k) count(BITS == 32 ? w[j] : (w[j] >> (BITS * k)) & ((1u << (BITS & 31)) - 1u));
+    }
+    for (int64_t p = n_vec * VEC + threadIdx.x; S == 0 && p < P; p += HS_THREADS) atomicAdd(&bins[codes[p]], 1u);
+    __syncthreads();
+    unsigned long long best = 0;
+    for (int p = threadIdx.x; p < n_pat; p += HS_THREADS) {
+        const unsigned long long v = ((unsigned long long)bins[p] << 32) | (0xFFFFFFFFull - (uint32_t)p);
+        best = v > best ? v : best;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bb = 0;
+        for (int w = 0; w < HS_THREADS / 64; ++w) bb = s_best[w] > bb ? s_best[w] : bb;
+        ghot[0] = (bb >> 32) ? (int32_t)(0xFFFFFFFFull - (bb & 0xFFFFFFFFull)) : -1;
+    }
+}
 
 // Final E-step: mp[i] = mpat[code[i]] for pairs [start, start + n).  Each lane turns two codes into
 // one 16-byte store of two doubles, so a wave instruction writes 1 KiB contiguous (the 8 B/pair of
@@ -822,89 +810,18 @@ using namespace spk;
 struct LanePlan {
     int R = 0;
     size_t bytes = 0;  // dynamic LDS of the launch
-    int mode = 0;      // k_em_iter MODE: 0 pattern codes, 1 re-encode to dense ids, 2 dense ids
-    DenseArgs D;
 };
-
-// k_em_iter's own __shared__ words (1.3 KiB) come out of the same LDS as the dynamic counters
-constexpr int64_t HL_STATIC_LDS = 2048;
-static int64_t lds_budget(spk_ctx *ctx) { return std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block) - HL_STATIC_LDS; }
-
-// The most lane copies (64 .. 4, 0: none) for n_bins bins with `extra` bytes of LDS beside the counters.
-static int lane_copies(spk_ctx *ctx, int64_t n_bins, int64_t extra) {
-    int R = 64;
-    while (R >= 4 && n_bins * R * 4 + extra > lds_budget(ctx)) R >>= 1;
-    return R < 4 ? 0 : R;
-}
 
 static LanePlan lane_plan(spk_ctx *ctx) {
     LanePlan L;
     const int64_t n_pat = ctx->n_patterns;
-    const int R = lane_copies(ctx, n_pat, 0);
-    if (!R || !ctx->hist_lanes || ctx->n_pairs >= (int64_t)UINT32_MAX) return L;
+    const int64_t budget = std::min<int64_t>(HL_LDS_BYTES, ctx->lds_per_block);
+    int R = 64;
+    while (R >= 4 && n_pat * R * 4 > budget) R >>= 1;
+    if (R < 4 || !ctx->hist_lanes || ctx->n_pairs >= (int64_t)UINT32_MAX) return L;
     L.R = R;
     L.bytes = (size_t)std::max<int64_t>(n_pat * R * 4, (int64_t)sizeof(PatArgs));
     return L;
-}
-
-// The codes' identity for the occupied-pattern ids: pair set, pattern space, generation, corrections.
-static std::vector<int64_t> codes_key(spk_ctx *ctx) {
-    return {(int64_t)ctx->pairs_epoch, ctx->n_pairs,     ctx->n_patterns,
-            ctx->code_bytes,           (int64_t)ctx->gamma_seq, (int64_t)ctx->codes_fix_seq};
-}
-
-// Switches a lane plan to the occupied-pattern ids when they allow more lane copies: MODE 2 when em_dense
-// already holds the current codes, MODE 1 when the last lane launch counted them (em_cnt_key; its counts in
-// cpat after a FIN launch, in em_occ after a histogram launch), else unchanged.  Building the map reads the
-// counts back once per generation of codes (a few KiB, synchronous).
-static int dense_plan(spk_ctx *ctx, LanePlan &L) {
-    // (uint32 codes -- more than 65535 patterns -- never take the lane path: see lane_plan)
-    if (!L.R || L.R == 64 || !ctx->em_dense_on || ctx->n_pairs == 0 || ctx->code_bytes != 2) return SPK_OK;
-    const std::vector<int64_t> key = codes_key(ctx);
-    const int64_t n_pat = ctx->n_patterns;
-    if (ctx->em_dense_key != key) {
-        const spk::DevBuf<double> &src = ctx->em_cnt_fin ? ctx->cpat : ctx->em_occ;
-        if (ctx->em_cnt_key != key || !src.p || src.n < (size_t)n_pat) return SPK_OK;
-        std::vector<double> cnt((size_t)n_pat);
-        SPK_HIP(hipMemcpyAsync(cnt.data(), src.p, (size_t)n_pat * 8, hipMemcpyDeviceToHost, ctx->stream));
-        SPK_HIP(hipStreamSynchronize(ctx->stream));
-        std::vector<uint16_t> map((size_t)n_pat, 0);
-        std::vector<int32_t> orig;
-        for (int64_t p = 0; p < n_pat; ++p)
-            if (cnt[p] > 0.0) {
-                map[p] = (uint16_t)orig.size();
-                orig.push_back((int32_t)p);
-                if (orig.size() > 0xFFFF) return SPK_OK;
-            }
-        const int64_t nd = (int64_t)orig.size();
-        const int64_t map_bytes = (n_pat * 2 + 3) / 4 * 4;
-        ctx->em_dense_key = key;
-        ctx->em_dense_R = 0;
-        ctx->em_dense_n = (int)nd;
-        const int R1 = lane_copies(ctx, nd, map_bytes), R2 = lane_copies(ctx, nd, 0);
-        if (nd == 0 || R1 <= L.R || R2 <= L.R || (nd + n_pat) * 4 > lds_budget(ctx)) return SPK_OK;
-        SPK_TRY(ctx->em_dense.alloc((size_t)ctx->n_pairs + 8));
-        SPK_TRY(ctx->em_dense_map.alloc((size_t)n_pat));
-        SPK_TRY(ctx->em_dense_orig.alloc((size_t)nd));
-        SPK_HIP(hipMemcpyAsync(ctx->em_dense_map.p, map.data(), (size_t)n_pat * 2, hipMemcpyHostToDevice, ctx->stream));
-        SPK_HIP(hipMemcpyAsync(ctx->em_dense_orig.p, orig.data(), (size_t)nd * 4, hipMemcpyHostToDevice, ctx->stream));
-        SPK_HIP(hipStreamSynchronize(ctx->stream));  // pageable sources
-        L.mode = 1;
-        L.R = R1;
-        L.bytes = (size_t)std::max<int64_t>({nd * R1 * 4 + map_bytes, (nd + n_pat) * 4, (int64_t)sizeof(PatArgs)});
-        L.D.map = ctx->em_dense_map.p;
-        L.D.out = ctx->em_dense.p;
-        ctx->em_dense_R = R2;  // the launches after this one
-    } else {
-        if (!ctx->em_dense_R) return SPK_OK;
-        const int64_t nd = ctx->em_dense_n;
-        L.mode = 2;
-        L.R = ctx->em_dense_R;
-        L.bytes = (size_t)std::max<int64_t>({nd * L.R * 4, (nd + n_pat) * 4, (int64_t)sizeof(PatArgs)});
-    }
-    L.D.n_bins = ctx->em_dense_n;
-    L.D.orig = ctx->em_dense_orig.p;
-    return SPK_OK;
 }
 
 // Grid of the lane-histogram launches: one 1024-thread workgroup per CU.
@@ -923,7 +840,8 @@ struct EmState {
     int refresh = 0;
 };
 
-static int em_state(spk_ctx *ctx, EmState &S) {
+// (allocations and their clears: before the launch's timing events, by the callers)
+static int em_state_alloc(spk_ctx *ctx) {
     if (!ctx->em_ticket.p) {
         SPK_TRY(ctx->em_ticket.alloc(1));
         SPK_HIP(hipMemsetAsync(ctx->em_ticket.p, 0, 4, ctx->stream));
@@ -933,12 +851,19 @@ static int em_state(spk_ctx *ctx, EmState &S) {
         SPK_TRY(ctx->em_row.alloc(ps));
         SPK_HIP(hipMemsetAsync(ctx->em_row.p, 0, ps * 4, ctx->stream));
     }
-    S.ticket = ctx->em_ticket.p;
-    S.arow = ctx->em_row.p;
     if (!ctx->em_hot.p) {
         SPK_TRY(ctx->em_hot.alloc(1));
         SPK_HIP(hipMemsetAsync(ctx->em_hot.p, 0xFF, sizeof(int32_t), ctx->stream));
     }
+    return SPK_OK;
+}
+
+static int em_state(spk_ctx *ctx, EmState &S) {
+    SPK_REQUIRE(ctx->em_ticket.p && ctx->em_hot.p && ctx->em_row.p &&
+                    ctx->em_row.n >= (size_t)part_stride(ctx->n_patterns) * EM_AROWS,
+                SPK_E_STATE, "k_em_iter state not allocated");
+    S.ticket = ctx->em_ticket.p;
+    S.arow = ctx->em_row.p;
     const std::vector<int64_t> key = {(int64_t)ctx->pairs_epoch, ctx->n_pairs, ctx->n_patterns, ctx->code_bytes};
     S.refresh = ctx->em_hot_key != key ? 1 : 0;
     ctx->em_hot_key = key;
@@ -946,48 +871,62 @@ static int em_state(spk_ctx *ctx, EmState &S) {
     return SPK_OK;
 }
 
-template <typename CodeT, int R, bool FIN, int MODE>
+template <int R, bool FIN>
 static void launch_em_iter(spk_ctx *ctx, const LanePlan &L, const EmState &S, int64_t g, const PatArgs &A,
                            double *mpat, double *llpat, double *cpat, double *out, unsigned long long *h) {
-    const CodeT *codes = MODE == 2 ? reinterpret_cast<const CodeT *>(ctx->em_dense.p)
-                                   : reinterpret_cast<const CodeT *>(ctx->codes.p);
-    k_em_iter<CodeT, R, FIN, MODE><<<(unsigned)g, HL_THREADS, L.bytes, ctx->stream>>>(
-        codes, ctx->n_pairs, A, S.ticket, mpat, llpat, cpat, out, h, ctx->em_fence ? 1 : 0, S.arow, S.ghot, S.refresh,
-        (int)L.bytes, L.D);
+    const int64_t P = ctx->n_pairs;
+    const int fence = ctx->em_fence ? 1 : 0;
+    const unsigned grid = (unsigned)g;
+    if (ctx->code_bytes == 2)
+        k_em_iter<uint16_t, R, FIN><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            reinterpret_cast<const uint16_t *>(ctx->codes.p), P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow,
+            S.ghot, S.refresh, (int)L.bytes);
+    else
+        k_em_iter<uint32_t, R, FIN><<<grid, HL_THREADS, L.bytes, ctx->stream>>>(
+            reinterpret_cast<const uint32_t *>(ctx->codes.p), P, A, S.ticket, mpat, llpat, cpat, out, h, fence, S.arow,
+            S.ghot, S.refresh, (int)L.bytes);
 }
 
-template <int R, bool FIN>
-static void launch_em_modes(spk_ctx *ctx, const LanePlan &L, const EmState &S, int64_t g, const PatArgs &A,
-                            double *mpat, double *llpat, double *cpat, double *out, unsigned long long *h) {
-    if (L.mode == 2) launch_em_iter<uint16_t, R, FIN, 2>(ctx, L, S, g, A, mpat, llpat, cpat, out, h);
-    else if (L.mode == 1) launch_em_iter<uint16_t, R, FIN, 1>(ctx, L, S, g, A, mpat, llpat, cpat, out, h);
-    else if (ctx->code_bytes == 2) launch_em_iter<uint16_t, R, FIN, 0>(ctx, L, S, g, A, mpat, llpat, cpat, out, h);
-    else launch_em_iter<uint32_t, R, FIN, 0>(ctx, L, S, g, A, mpat, llpat, cpat, out, h);
-}
-
-// cpat receives the launch's counts (FIN: ctx->cpat; else em_occ) and em_cnt_key says whose.
 template <bool FIN>
 static int launch_em_lanes(spk_ctx *ctx, const LanePlan &L, const PatArgs &A, double *mpat, double *llpat,
                            double *cpat, double *out, unsigned long long *h) {
     EmState S;
     SPK_TRY(em_state(ctx, S));
     const int64_t g = lane_grid(ctx);
+    if (S.refresh && L.R < 64) {  // a new pair set: guess the uncounted pattern before the first launch
+        const size_t shm = (size_t)ctx->n_patterns * 4;
+        if (ctx->code_bytes == 2)
+            k_em_hot_sample<uint16_t><<<1, HS_THREADS, shm, ctx->stream>>>(
+                reinterpret_cast<const uint16_t *>(ctx->codes.p), ctx->n_pairs, (int)ctx->n_patterns, S.ghot);
+        else
+            k_em_hot_sample<uint32_t><<<1, HS_THREADS, shm, ctx->stream>>>(
+                reinterpret_cast<const uint32_t *>(ctx->codes.p), ctx->n_pairs, (int)ctx->n_patterns, S.ghot);
+    }
     switch (L.R) {
-        case 64: launch_em_modes<64, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
-        case 32: launch_em_modes<32, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
-        case 16: launch_em_modes<16, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
-        case 8: launch_em_modes<8, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
-        default: launch_em_modes<4, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        case 64: launch_em_iter<64, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        case 32: launch_em_iter<32, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        case 16: launch_em_iter<16, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        case 8: launch_em_iter<8, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
+        default: launch_em_iter<4, FIN>(ctx, L, S, g, A, mpat, llpat, cpat, out, h); break;
     }
     SPK_HIP(hipGetLastError());
-    ctx->em_cnt_key = cpat ? codes_key(ctx) : std::vector<int64_t>{};
-    ctx->em_cnt_fin = FIN;
     return SPK_OK;
 }
 
-// k_em_finalize rewrites cpat from a histogram the caller chose: it no longer holds a lane launch's counts.
-static void cpat_rewritten(spk_ctx *ctx) {
-    if (ctx->em_cnt_fin) ctx->em_cnt_key.clear();
+// Each translation unit's kernels are one code object, loaded by HIP at the first launch of any of them:
+// about 1.2 ms of host time that landed between the first E+M launch's timing events on MI355X (a 0.42 ms
+// kernel timed at 1.67 ms; rocprofv3 kernel trace, profiles/r5_fulljob_em_trace.txt).  The first E+M call
+// of a process launches an empty k_pattern_mp before its events instead.  (Loading it in spk_ctx_create
+// with hipFuncGetAttributes cost 0.55 s of job setup: it loaded far more than this code object.)
+static int em_load_code_object(spk_ctx *ctx) {
+    static bool loaded[64] = {};  // per device (the code object is loaded per device)
+    const int d = ctx->device;
+    if (d < 64 && loaded[d]) return SPK_OK;
+    PatArgs A{};
+    k_pattern_mp<<<1, 64, 0, ctx->stream>>>(A, nullptr, nullptr);  // n_pat = 0: no thread does anything
+    SPK_HIP(hipGetLastError());
+    if (d < 64) loaded[d] = true;
+    return SPK_OK;
 }
 
 // The pattern histogram into d_hist (NULL = the context's).
@@ -1000,14 +939,14 @@ static int enqueue_histogram(spk_ctx *ctx, uint64_t *d_hist) {
     }
     const int64_t P = ctx->n_pairs;
     const int vec = 16 / ctx->code_bytes;
-    LanePlan L = lane_plan(ctx);
-    if (L.R) SPK_TRY(ctx->em_occ.alloc((size_t)n_pat));
-    SPK_TRY(dense_plan(ctx, L));  // (its host work and allocations outside the timed launch)
+    const LanePlan L = lane_plan(ctx);
+    if (L.R) SPK_TRY(em_state_alloc(ctx));
+    SPK_TRY(em_load_code_object(ctx));
     SPK_TRY(ctx->begin(K_EMHIST));
     if (L.R) {
         PatArgs A{};
         A.n_pat = (int)n_pat;
-        SPK_TRY(launch_em_lanes<false>(ctx, L, A, nullptr, nullptr, ctx->em_occ.p, nullptr, h));
+        SPK_TRY(launch_em_lanes<false>(ctx, L, A, nullptr, nullptr, nullptr, nullptr, h));
     } else {
         SPK_HIP(hipMemsetAsync(h, 0, (size_t)n_pat * 8, ctx->stream));
         int64_t blocks = (P / vec + H_THREADS - 1) / H_THREADS;
@@ -1046,7 +985,6 @@ static int finalize_from(spk_ctx *ctx, const unsigned long long *h, const PatArg
     SPK_REQUIRE(!ctx->em_pending, SPK_E_STATE, "spk_em_finalize: an asynchronous iteration is pending (spk_em_iteration_wait)");
     SPK_TRY(em_buffers(ctx, n_stats));
     SPK_TRY(ctx->begin(K_EMFIN));
-    cpat_rewritten(ctx);
     k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, h, ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p);
     SPK_HIP(hipGetLastError());
     SPK_TRY(ctx->end(K_EMFIN));
@@ -1060,20 +998,6 @@ extern "C" int spk_em_set_lane_histogram(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx && on >= 0 && on <= 2, SPK_E_INVALID, "spk_em_set_lane_histogram: mode 0, 1 or 2");
     ctx->hist_lanes = on != 0;
     ctx->em_fence = on != 2;
-    return SPK_OK;
-}
-
-extern "C" int spk_em_set_dense(spk_ctx *ctx, int on) {
-    SPK_REQUIRE(ctx && (on == 0 || on == 1), SPK_E_INVALID, "spk_em_set_dense: 0 or 1");
-    ctx->em_dense_on = on != 0;
-    return SPK_OK;
-}
-
-extern "C" int spk_em_dense_info(spk_ctx *ctx, int32_t *out) {
-    SPK_REQUIRE(ctx && out, SPK_E_INVALID, "spk_em_dense_info: null arg");
-    const bool cur = ctx->em_dense_on && ctx->em_dense_key == codes_key(ctx);
-    out[0] = cur ? ctx->em_dense_n : 0;
-    out[1] = cur ? ctx->em_dense_R : 0;
     return SPK_OK;
 }
 
@@ -1125,17 +1049,17 @@ static int enqueue_em(spk_ctx *ctx) {
     const int n_stats = ctx->em_n_stats;
     SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_iteration: n_stats mismatch");
     SPK_TRY(em_buffers(ctx, n_stats));
-    LanePlan L = lane_plan(ctx);
-    SPK_TRY(dense_plan(ctx, L));
+    SPK_TRY(em_load_code_object(ctx));
+    const LanePlan L = lane_plan(ctx);
     if (!L.R) {
         SPK_TRY(enqueue_histogram(ctx, nullptr));
         SPK_TRY(ctx->begin(K_EMFIN));
-        cpat_rewritten(ctx);
         k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, reinterpret_cast<const unsigned long long *>(ctx->hist.p),
                                                          ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p);
         SPK_HIP(hipGetLastError());
         SPK_TRY(ctx->end(K_EMFIN));
     } else {
+        SPK_TRY(em_state_alloc(ctx));
         SPK_TRY(ctx->begin(K_EMHIST));
         SPK_TRY(launch_em_lanes<true>(ctx, L, A, ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p, nullptr));
         SPK_TRY(ctx->end(K_EMHIST));
@@ -1148,7 +1072,10 @@ static int enqueue_em(spk_ctx *ctx) {
 
 namespace spk {
 int em_requeue(spk_ctx *ctx) { return enqueue_em(ctx); }
+
 }  // namespace spk
+
+
 
 #ifdef SPK_EM_STAMPS
 extern "C" int spk_debug_em_stamps(uint64_t *out) {
@@ -1199,7 +1126,6 @@ extern "C" int spk_em_finalize_start(spk_ctx *ctx, const uint64_t *d_hist, doubl
     SPK_REQUIRE(n_stats == N_HEAD + 4 * A.n_slots, SPK_E_INVALID, "spk_em_finalize_start: n_stats mismatch");
     SPK_TRY(em_buffers(ctx, n_stats));
     SPK_TRY(ctx->begin(K_EMFIN));
-    cpat_rewritten(ctx);
     k_em_finalize<<<1, EF_THREADS, 0, ctx->stream>>>(A, reinterpret_cast<const unsigned long long *>(d_hist),
                                                      ctx->mpat.p, ctx->llpat.p, ctx->cpat.p, ctx->stats.p);
     SPK_HIP(hipGetLastError());

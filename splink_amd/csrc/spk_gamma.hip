@@ -2196,7 +2196,6 @@ static int settle_info(spk_ctx *ctx, bool *fixed);
 int settle_gammas(spk_ctx *ctx, bool *fixed) {
     bool f = false;
     SPK_TRY(settle_info(ctx, &f));
-    if (f) ++ctx->codes_fix_seq;
     if (fixed) *fixed = f;
     // an asynchronous EM iteration enqueued on these codes read them before the correction: repeat it
     if (f && ctx->em_pending && ctx->em_seq == ctx->gamma_seq) {

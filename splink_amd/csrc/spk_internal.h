@@ -313,20 +313,7 @@ struct spk_ctx {
     spk::DevBuf<uint32_t> em_row;         // its reduction rows (kept zero between launches)
     spk::DevBuf<int32_t> em_hot;          // the pattern it does not count with R < 64 lane copies (-1: none yet)
     std::vector<int64_t> em_hot_key;      // the pair set / pattern space it was found for
-    // Occupied-pattern ids (k_em_iter modes 1 / 2): the codes of the current generation re-encoded as dense
-    // ids of the patterns that occur, so that later launches count them with more lane copies.
-    spk::DevBuf<uint16_t> em_dense;       // the dense ids, one per pair
-    spk::DevBuf<uint16_t> em_dense_map;   // pattern -> dense id
-    spk::DevBuf<int32_t> em_dense_orig;   // dense id -> pattern
-    int em_dense_n = 0;                   // occupied patterns
-    int em_dense_R = 0;                   // lane copies of the dense launches (0: not worth it for this key)
-    bool em_dense_on = true;              // spk_em_set_dense
-    std::vector<int64_t> em_dense_key;    // the codes em_dense encodes (codes_key())
-    spk::DevBuf<double> em_occ;           // a histogram lane launch's counts per pattern
-    std::vector<int64_t> em_cnt_key;      // the codes the last lane launch counted (into cpat / em_occ)
-    bool em_cnt_fin = false;              // ... into cpat (a FIN launch)
-    uint64_t codes_fix_seq = 0;           // settle_gammas corrections of the codes so far
-    double *h_stats = nullptr;       // pinned host copy of the statistics vector
+    double *h_stats = nullptr;        // pinned host copy of the statistics vector
     size_t h_stats_n = 0;
     int n_cu = 256;                   // compute units of the device (grid sizing)
     int lds_per_block = 64 * 1024;    // LDS a workgroup may allocate (device attribute)

@@ -932,53 +932,3 @@ def test_tf_bit_identical_across_runs_and_ranks(amd, tmp_path):
     a = both["tf_adjusted_match_prob"].to_numpy(dtype=np.float64)
     b = single["tf_adjusted_match_prob"].to_numpy(dtype=np.float64)
     assert np.array_equal(a, b, equal_nan=True)
-
-
-@pytest.mark.parametrize("occupied,want_r", [(40, 64), (600, 64), (700, 32), (1500, 16), (3125, 0)])
-def test_em_dense_ids(amd, occupied, want_r):
-    """Occupied-pattern ids: in a 3125-pattern space (8 lane copies) of which `occupied` patterns occur, the
-    E+M launch after the first on the same codes re-encodes them as dense ids and the later ones stream
-    those with want_r copies (0: all patterns occur, no gain); every iteration's statistics and the
-    histogram equal the pattern-code launches' bit for bit, and a new generation of codes starts over."""
-    import torch
-    from splink_amd import _native as N
-    n_levels = [4] * 5
-    n_pat = 5 ** 5
-    rng = np.random.Generator(np.random.PCG64(occupied))
-    pats = rng.permutation(n_pat)[:occupied]
-    P = 2_000_003
-    w = 1.0 / np.arange(1, occupied + 1) ** 1.1  # skewed: a few patterns hold most pairs
-    codes = np.concatenate([pats, rng.choice(pats, P - occupied, p=w / w.sum())])
-    g = np.stack([(codes // 5 ** k) % 5 - 1 for k in range(5)], axis=1).astype(np.int8)
-    lam, m, u = 0.3, [], []
-    for L in n_levels:
-        pm = np.linspace(1.0, 2.0, L)
-        m += list(pm / pm.sum())
-        u += list(pm[::-1] / pm.sum())
-    n_stats = 5 + 4 * sum(L + 1 for L in n_levels)
-    ctx = N.Context(0)
-
-    def run(dense):
-        ctx.em_set_dense(dense)
-        ctx.gammas_load(n_levels, g)  # a new generation of codes
-        assert ctx.em_dense_info() == (0, 0)
-        out, info = [], []
-        for it in range(4):
-            out.append(ctx.em_iteration(lam + 0.05 * it, 1.0 - (lam + 0.05 * it), m, u, n_stats))
-            info.append(ctx.em_dense_info())
-        d = torch.full((n_pat,), -1, dtype=torch.int64, device="cuda:0")
-        torch.cuda.synchronize()
-        ctx.em_histogram(d.data_ptr())
-        return out, info, d.cpu().numpy()
-
-    off, info_off, h_off = run(False)
-    on, info_on, h_on = run(True)
-    assert ctx.n_patterns() == n_pat
-    assert all(i == (0, 0) for i in info_off)
-    assert info_on[0] == (0, 0)  # the first launch counts the pattern codes
-    assert all(i == ((occupied, want_r) if want_r else (occupied, 0)) for i in info_on[1:]), info_on
-    for a, b in zip(off, on):
-        assert np.array_equal(a, b)
-    want = np.bincount(codes, minlength=n_pat)
-    assert np.array_equal(h_off, want) and np.array_equal(h_on, want)
-    assert off[0][1] == P

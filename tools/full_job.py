@@ -67,8 +67,6 @@ def main():
                     help="generate the records as this many independent chunks over one vocabulary, in parallel "
                          "(synthetic.make_records_parallel; 0 = the serial make_records)")
     ap.add_argument("--workers", type=int, default=16)
-    ap.add_argument("--no-em-dense", dest="em_dense", action="store_false",
-                    help="E+M launches on the pattern codes only (no occupied-pattern ids; A/B)")
     ap.add_argument("--no-prefetch", dest="prefetch", action="store_false",
                     help="upload the comparison-only columns in the first comparison call (no background prefetch)")
     a = ap.parse_args()
@@ -126,7 +124,6 @@ def main():
     pre = _comparison_only_columns(st, st["blocking_rules"], inputs[0].columns) if a.prefetch else None
     job = Job(st["link_type"], inputs, "unique_id", 0, shard=(shard, n_shards), prefetch=pre)
     job.ctx.enable_timing(True)
-    job.ctx.em_set_dense(a.em_dense)
     wall["job_setup_incl_uid_rank"] = time.perf_counter() - t
     t = time.perf_counter()
     job.block(st["blocking_rules"])
@@ -154,7 +151,6 @@ def main():
         lam, rows = m_step_rows(stats, names, nlev)
         params._update_params(lam, rows)
     wall["em_iterations"] = time.perf_counter() - t
-    dense_info = job.ctx.em_dense_info()
     # how concentrated the comparison patterns are (what bounds the lane-private E+M histogram)
     hist_t = job._device_hist()
     job.ctx.em_histogram(hist_t.data_ptr())
@@ -193,7 +189,6 @@ def main():
         "device_ms": {"block": block_dev, "gamma_pass_first": gamma_dev, "gamma_pass": gamma_warm,
                       "em_per_iter_mean": float(np.mean(em_dev)), "score": score_dev,
                       "em_per_iter": [round(x, 4) for x in em_dev]},
-        "em_dense_ids": dict(zip(("occupied", "lane_copies"), dense_info)),
         "exact_cells_per_column": exact_cells,
         "pattern_concentration": patterns,
         "pairs_per_s_job": P / total,
