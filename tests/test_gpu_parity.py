@@ -932,3 +932,29 @@ def test_tf_bit_identical_across_runs_and_ranks(amd, tmp_path):
     a = both["tf_adjusted_match_prob"].to_numpy(dtype=np.float64)
     b = single["tf_adjusted_match_prob"].to_numpy(dtype=np.float64)
     assert np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("P", [1, 7, 8, 9, 4097, 131075])
+def test_em_first_launch_small_pair_sets(amd, P):
+    """The first E+M launch on a pair set guesses its uncounted pattern from a sample (k_em_hot_sample; below
+    one 16-byte vector of codes it counts them all): exact counts for pair sets around the vector width, in a
+    3125-pattern space (8 lane copies), on fresh contexts so every launch here is a first one."""
+    import torch
+    from splink_amd import _native as N
+    n_levels = [4] * 5
+    rng = np.random.Generator(np.random.PCG64(P))
+    g = rng.integers(-1, 4, (P, 5)).astype(np.int8)
+    g[: P // 2] = 2  # one pattern holds half of the pairs
+    stride = np.cumprod([1] + [L + 1 for L in n_levels[:-1]])
+    want = np.bincount(((g.astype(np.int64) + 1) * stride).sum(axis=1), minlength=5 ** 5)
+    for first in ("histogram", "iteration"):
+        ctx = N.Context(0)
+        ctx.gammas_load(n_levels, g)
+        if first == "iteration":
+            m = [0.25] * 20
+            stats = ctx.em_iteration(0.3, 0.7, m, m, 5 + 4 * 25)
+            assert stats[1] == P
+        d = torch.full((5 ** 5,), -1, dtype=torch.int64, device="cuda:0")
+        torch.cuda.synchronize()
+        ctx.em_histogram(d.data_ptr())
+        assert np.array_equal(d.cpu().numpy(), want)
