@@ -390,7 +390,8 @@ class Context:
 
     def gammas_set_lev_kernel(self, mode: int):
         """Levenshtein exact pass (same codes; A/B tests): 2 lane refill in free-text columns, one cell per lane
-        elsewhere (default); 1 lane refill everywhere; 0 one cell per lane everywhere."""
+        elsewhere (default); 1 lane refill everywhere; 0 one cell per lane everywhere; 3 as 2 without the
+        character-bag decisions before the refill pass."""
         check(self._lib.spk_gammas_set_lev_kernel(self._h, ctypes.c_int(int(mode))), "spk_gammas_set_lev_kernel")
 
     def lds_per_block(self) -> int:

@@ -563,6 +563,73 @@ __device__ inline int64_t exact_count(const GammaArgs &A, const int64_t *xinfo, 
     return xinfo[2 * A.K] ? 0 : xinfo[A.K + k];
 }
 
+__device__ inline int simple_lev_cut(const SimpleCol &sc, int ncp_a, int ncp_b);
+__device__ inline int lev_level_of(const SimpleCol &sc, int eq, int lev, int nsum);
+
+// Upper bound on the multiset intersection of two rows from their character-bag rows (k_bag_rows), or -1 when
+// a bucket is saturated on both sides.  Σ min(a, b) = (Σ a + Σ b - Σ |a - b|) / 2 over the nibbles, spread to
+// bytes (v_sad_u8 sums four absolute byte differences).
+__device__ inline int bag_inter_ub(const uint4 &a0, const uint4 &a1, const uint4 &b0, const uint4 &b1) {
+    const uint32_t wa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w & 0xFFFFu};
+    const uint32_t wb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w & 0xFFFFu};
+    uint32_t sad = 0, sa = 0, sb = 0, sat = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t la = wa[q] & 0x0F0F0F0Fu, ha = (wa[q] >> 4) & 0x0F0F0F0Fu;
+        const uint32_t lb = wb[q] & 0x0F0F0F0Fu, hb = (wb[q] >> 4) & 0x0F0F0F0Fu;
+        sad = __builtin_amdgcn_sad_u8(la, lb, sad);
+        sad = __builtin_amdgcn_sad_u8(ha, hb, sad);
+        sa = __builtin_amdgcn_sad_u8(la, 0u, sa);
+        sa = __builtin_amdgcn_sad_u8(ha, 0u, sa);
+        sb = __builtin_amdgcn_sad_u8(lb, 0u, sb);
+        sb = __builtin_amdgcn_sad_u8(hb, 0u, sb);
+        const uint32_t t = wa[q] & wb[q];
+        sat |= t & (t >> 1) & (t >> 2) & (t >> 3) & 0x11111111u;
+    }
+    if (sat) return -1;
+    const int oa = (int)((a1.w >> 16) & 0xFFu), ob = (int)((b1.w >> 16) & 0xFFu);
+    return (int)((sa + sb - sad) / 2u) + (oa < ob ? oa : ob);
+}
+
+// k_compact for a free-text Levenshtein column read by k_lev_refill: a listed cell whose rows' bag distance
+// already exceeds the cut is decided here (its level is lev_cell's for any distance past the cut) and its list
+// slot becomes -1, which the exact pass skips; the others are copied as k_compact copies them.
+__global__ void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restrict__ xpref,
+                              int32_t *__restrict__ xlist, const int64_t *__restrict__ xinfo) {
+    if (xinfo[2 * A.K]) return;  // overflow: the host re-runs the phase
+    __shared__ SimpleCol s_sc;
+    if (threadIdx.x == 0) s_sc = A.simple[si];
+    __syncthreads();
+    const SimpleCol &sc = s_sc;
+    const int64_t *pref = xpref + (int64_t)k * (A.n_regions + 1);
+    const Region R = my_region(A);
+    const int32_t *src = region_list(A, k, R);
+    const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
+    int32_t *dst = xlist + xinfo[k] + pref[blockIdx.x];
+    const uint4 *bag0 = A.cols0[sc.col].bag, *bag1 = A.cols1[sc.col].bag;
+    const uint32_t stride = (uint32_t)sc.stride;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const int32_t p = src[i];
+        const int64_t x = A.pl[p], y = A.pr[p];
+        const uint4 a0 = bag0[2 * x], a1 = bag0[2 * x + 1], b0 = bag1[2 * y], b1 = bag1[2 * y + 1];
+        const int la = (int)(a1.w >> 24), lb = (int)(b1.w >> 24);
+        int32_t out = p;
+        if (la != 255 && lb != 255) {
+            int inter = bag_inter_ub(a0, a1, b0, b1);
+            if (inter >= 0) {
+                const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
+                inter = inter < mn ? inter : mn;
+                const int cut = simple_lev_cut(sc, la, lb);
+                if (mx - inter > cut) {  // unequal rows (a positive bag distance), distance past the cut
+                    code_add_atomic(A, p, (uint32_t)(lev_level_of(sc, 0, cut + 1, la + lb) + 1) * stride);
+                    out = -1;
+                }
+            }
+        }
+        dst[i] = out;
+    }
+}
+
 // Exact pass over column k through the interpreter.
 __global__ __launch_bounds__(X_THREADS) void k_gamma_exact(GammaArgs A, int k, const int32_t *xlist,
                                                             const int64_t *xinfo) {
@@ -1141,9 +1208,11 @@ __global__ __launch_bounds__(X_THREADS, WW == 2 ? 2 : (NP == 8 ? 3 : LEVQ_WAVES)
     };
     // prefetch pipeline: p0 = entry(bn) with its rows staged, p1 = entry(bn + 1) with row ids x1 / y1, p2 =
     // entry(bn + 2)
+    // (-1: a cell k_compact_lev decided; its loads read pair 0 harmlessly)
+    auto pair_of = [](int32_t q) { return q < 0 ? 0 : q; };
     int32_t p0 = entry(bn), p1 = entry(bn + 1), p2 = entry(bn + 2);
-    int32_t x1 = A.pl[p1], y1 = A.pr[p1];
-    stage(A.pl[p0], A.pr[p0]);
+    int32_t x1 = A.pl[pair_of(p1)], y1 = A.pr[pair_of(p1)];
+    stage(A.pl[pair_of(p0)], A.pr[pair_of(p0)]);
     int q_head = 0, q_count = 0, n_res = 0, n_slow = 0;  // wave-uniform
 #ifdef SPK_LEVQ_STATS
     unsigned long long st_[16] = {};
@@ -1224,7 +1293,7 @@ __global__ __launch_bounds__(X_THREADS, WW == 2 ? 2 : (NP == 8 ? 3 : LEVQ_WAVES)
             if (n_slow >= 64) flush_slow(64);
             const int32_t pc = p0;
             const int64_t left = n_items - bn * 64;
-            const bool valid = lane < left;
+            const bool valid = lane < left && pc >= 0;
             bool to_slow = false, done = false, scan = false, a_pat = false;
             int level = 0, pre = 0, mm = 0, nn = 0, c = 0, s2 = 0;
             if (valid) {
@@ -1341,8 +1410,8 @@ __global__ __launch_bounds__(X_THREADS, WW == 2 ? 2 : (NP == 8 ? 3 : LEVQ_WAVES)
             // the prefetch pipeline moves one batch on: rows of bn + 1, row ids of bn + 2, entries of bn + 3
             ++bn;
             stage(x1, y1);
-            x1 = A.pl[p2];
-            y1 = A.pr[p2];
+            x1 = A.pl[pair_of(p2)];
+            y1 = A.pr[pair_of(p2)];
             p0 = p1;
             p1 = p2;
             p2 = entry(bn + 2);
@@ -2023,7 +2092,7 @@ struct GammaPlan {
     GammaArgs A{};
     std::vector<SimpleCol> simple;
     std::vector<int> simple_of;
-    std::vector<char> may_exact, huge_in_slow, free_text;
+    std::vector<char> may_exact, huge_in_slow, free_text, bag;
     std::vector<char> slow_skipped;  // columns whose slow-list kernels this call did not launch
     int K = 0, n_regions = 0, n_info = 0, n_cnt = 0, n_all = 0;
     int64_t g_exact = 1, max_units = 1;
@@ -2134,8 +2203,12 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         for (int c = 0; c < jw.n; ++c) fused = fused || jw.si[c] == si;
         if (fused) continue;
         const ColSet one_k{1, {k, 0, 0, 0}};
-        k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
-        if (lev && (ctx->lev_kernel == 1 || (ctx->lev_kernel == 2 && G.free_text[k]))) {
+        const bool refill = lev && (ctx->lev_kernel == 1 || (ctx->lev_kernel == 2 && G.free_text[k]));
+        if (refill && G.bag[k])
+            k_compact_lev<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, k, si, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
+        else
+            k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
+        if (refill) {
             // one resident round (LEVQ_WAVES per SIMD, 3 for NP = 8): every wave owns a contiguous range of the list
             const int64_t wg_cu = simple[si].np >= 8 ? 3 : LEVQ_WG_PER_CU;
             const int64_t g_lev = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, wg_cu * ctx->n_cu));
@@ -2526,9 +2599,11 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     for (const SimpleCol &sc : simple)
         if (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids)) G.may_exact[sc.k] = 0;
     G.free_text.assign(K, 0);  // simple columns with rows past 64 UTF-8 bytes on both sides (planes_hi)
+    G.bag.assign(K, 0);        // ... and character-bag rows on both sides (k_compact_lev)
     for (const SimpleCol &sc : simple) {
         const Column *a = t0.cols[sc.col], *b = t1.cols[sc.col];
         G.free_text[sc.k] = (a && b && a->planes_hi.n && b->planes_hi.n) ? 1 : 0;
+        G.bag[sc.k] = (G.free_text[sc.k] && a->bag.n && b->bag.n && ctx->lev_bag) ? 1 : 0;
     }
     G.huge_in_slow.assign(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
     for (int k = 0; k < K; ++k)
@@ -2914,8 +2989,9 @@ extern "C" int spk_gammas_windows(spk_ctx *ctx, int64_t *out) {
 }
 
 extern "C" int spk_gammas_set_lev_kernel(spk_ctx *ctx, int mode) {
-    SPK_REQUIRE(ctx && mode >= 0 && mode <= 2, SPK_E_INVALID, "spk_gammas_set_lev_kernel: mode 0, 1 or 2");
-    ctx->lev_kernel = mode;
+    SPK_REQUIRE(ctx && mode >= 0 && mode <= 3, SPK_E_INVALID, "spk_gammas_set_lev_kernel: mode 0 .. 3");
+    ctx->lev_kernel = mode == 3 ? 2 : mode;
+    ctx->lev_bag = mode != 3;
     return SPK_OK;
 }
 

@@ -100,6 +100,7 @@ struct ColDesc {
     const RecMeta *meta;     // COL_STR
     const uint64_t *planes;  // COL_STR, [n][N_PLANES]
     const uint64_t *planes_hi;  // COL_STR, [n][N_PLANES] units 64..127 (CPF_PLANES2 rows), or null
+    const uint4 *bag;        // COL_STR with planes_hi: [n][2] character-bag rows (k_bag_rows), or null
     const double *val;       // COL_NUM
     const uint8_t *valid;   // COL_NUM
 };
@@ -139,6 +140,7 @@ struct Column {
     DevBuf<RecMeta> meta;
     DevBuf<uint64_t> planes;
     DevBuf<uint64_t> planes_hi;  // allocated only when some row has more than 64 UTF-8 bytes
+    DevBuf<uint4> bag;           // with planes_hi: 32-byte character-bag row per row (k_bag_rows)
     DevBuf<double> val;
     DevBuf<uint8_t> valid;
     bool has_ids = false;  // COL_STR: RecMeta.key is a dictionary id
@@ -300,6 +302,7 @@ struct spk_ctx {
     // (settle_gammas runs them if the list is not empty after all)
     std::vector<uint8_t> slow_seen;
     bool slow_seen_valid = false;
+    bool lev_bag = true;           // k_compact_lev's bag-distance decisions before a refill pass (mode 3: off)
     int lev_kernel = 2;            // Levenshtein exact pass: 0 k_gamma_exact_simple<X_LEV>, 1 k_lev_refill, 2 refill in
                                    // free-text columns (rows past 64 units), one cell per lane elsewhere
     bool slow_force_skip = false;  // tests: leave every slow-list launch to settle_gammas

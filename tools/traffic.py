@@ -34,7 +34,7 @@ import re
 # the list against the sources' launch sites, so a renamed or new kernel cannot drop out of the group.
 GAMMA_KERNELS = ("k_build_image", "k_view_image", "k_filter", "k_gamma_filter", "k_gamma_exact",
                  "k_gamma_exact_simple", "k_lev_refill", "k_gamma_slow", "k_gamma_slow_lev", "k_gamma_rest", "k_gamma_huge",
-                 "k_compact", "k_prefix")
+                 "k_compact", "k_compact_lev", "k_prefix")
 # launched from the same sources by other entry points (spk_gammas_load / _copy, the bulk UDFs)
 NOT_GAMMA_KERNELS = ("k_codes_from_gammas", "k_gammas_from_codes", "k_udf", "k_udf_huge")
 GAMMA = re.compile(r"\b(?:spk::)?(" + "|".join(GAMMA_KERNELS) + r")\b")
