@@ -27,7 +27,7 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
             d.meta = c->meta.p;
             d.planes = c->planes.p;
             d.planes_hi = c->planes_hi.n ? c->planes_hi.p : nullptr;
-            d.bag = c->planes_hi.n && c->bag.n ? c->bag.p : nullptr;
+            d.bag = c->bag.n ? c->bag.p : nullptr;
         } else if (c && c->kind == COL_NUM) {
             d.val = c->val.p;
             d.valid = c->valid.p;
@@ -224,14 +224,15 @@ __global__ void k_unit_bits(int64_t n, const RecMeta *__restrict__ meta, const u
     }
 }
 
-// Character-bag rows of a free-text column (rows past 64 UTF-8 bytes exist): per row 32 bytes, the counts of
+// Character-bag rows of a free-text string column that a Levenshtein comparison reads: per row 32 bytes, the counts of
 // 60 buckets in 4-bit saturating nibbles ('a'-'z', 'A'-'Z', digits mod 8: words 0-6 and the low half of word
 // 7), then the count of the row's other units (byte 30) and its length (byte 31; 255: no bag -- NULL, past 128
 // units, or a surrogate pair, whose units are not its code points).  The Levenshtein distance of two rows is
 // at least their bag distance max(la, lb) - |A ∩ B| (one edit changes one unit of either multiset), and the
 // intersection is at most Σ min over the buckets plus min(other_a, other_b): k_compact_lev decides the listed
-// cells whose bound already exceeds the cut (cfg5 addresses: 47 % of the listed cells, host emulation).
-// One thread per row, its nibbles in LDS (dynamic bucket index).
+// cells whose bound already exceeds the cut (cfg5 addresses: 5.69 of 15.90 M listed cells).  Built on first
+// use (spk_gammas), dropped when the column is decoded again.  One thread per row, its nibbles in LDS
+// (dynamic bucket index).
 constexpr int BAG_THREADS = 256;
 __global__ __launch_bounds__(BAG_THREADS) void k_bag_rows(int64_t n, const RecMeta *__restrict__ meta,
                                                           const uint16_t *__restrict__ units, uint4 *__restrict__ bag) {
@@ -267,16 +268,19 @@ __global__ __launch_bounds__(BAG_THREADS) void k_bag_rows(int64_t n, const RecMe
     bag[2 * row + 1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
-int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c) {
-    c->unit_bits = false;
-    if (c->planes_hi.n && n > 0) {
-        SPK_TRY(c->bag.alloc((size_t)(2 * n + 2)));
+int build_bag_rows(spk_ctx *ctx, int64_t n, Column *c) {
+    SPK_TRY(c->bag.alloc((size_t)(2 * n + 2)));
+    if (n > 0) {
         k_bag_rows<<<(unsigned)((n + BAG_THREADS - 1) / BAG_THREADS), BAG_THREADS, 0, ctx->stream>>>(n, c->meta.p,
                                                                                                   c->units.p, c->bag.p);
         SPK_HIP(hipGetLastError());
-    } else {
-        c->bag.release();
     }
+    return SPK_OK;
+}
+
+int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c) {
+    c->unit_bits = false;
+    c->bag.release();  // the rows changed: built again on first use
     if (n <= 0) return SPK_OK;
     DevBuf<unsigned int> d;
     SPK_TRY(d.alloc(2));

@@ -591,13 +591,16 @@ __device__ inline int bag_inter_ub(const uint4 &a0, const uint4 &a1, const uint4
     return (int)((sa + sb - sad) / 2u) + (oa < ob ? oa : ob);
 }
 
-// k_compact for a free-text Levenshtein column read by k_lev_refill: a listed cell whose rows' bag distance
-// already exceeds the cut is decided here (its level is lev_cell's for any distance past the cut) and its list
-// slot becomes -1, which the exact pass skips; the others are copied as k_compact copies them.
-__global__ void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restrict__ xpref,
-                              int32_t *__restrict__ xlist, const int64_t *__restrict__ xinfo) {
+// k_compact for a Levenshtein column: a listed cell whose rows' bag distance already exceeds the cut is decided
+// here (its level is lev_cell's for any distance past the cut); the others are packed to the front of the
+// region's slice of the list in order, and the slice's tail is -1, which the exact passes skip (whole waves of
+// it, mostly).
+constexpr int CL_THREADS = 256;
+__global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restrict__ xpref,
+                                                            int32_t *__restrict__ xlist, const int64_t *__restrict__ xinfo) {
     if (xinfo[2 * A.K]) return;  // overflow: the host re-runs the phase
     __shared__ SimpleCol s_sc;
+    __shared__ int s_kept[CL_THREADS / 64];
     if (threadIdx.x == 0) s_sc = A.simple[si];
     __syncthreads();
     const SimpleCol &sc = s_sc;
@@ -608,26 +611,45 @@ __global__ void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restr
     int32_t *dst = xlist + xinfo[k] + pref[blockIdx.x];
     const uint4 *bag0 = A.cols0[sc.col].bag, *bag1 = A.cols1[sc.col].bag;
     const uint32_t stride = (uint32_t)sc.stride;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const int32_t p = src[i];
-        const int64_t x = A.pl[p], y = A.pr[p];
-        const uint4 a0 = bag0[2 * x], a1 = bag0[2 * x + 1], b0 = bag1[2 * y], b1 = bag1[2 * y + 1];
-        const int la = (int)(a1.w >> 24), lb = (int)(b1.w >> 24);
-        int32_t out = p;
-        if (la != 255 && lb != 255) {
-            int inter = bag_inter_ub(a0, a1, b0, b1);
-            if (inter >= 0) {
-                const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
-                inter = inter < mn ? inter : mn;
-                const int cut = simple_lev_cut(sc, la, lb);
-                if (mx - inter > cut) {  // unequal rows (a positive bag distance), distance past the cut
-                    code_add_atomic(A, p, (uint32_t)(lev_level_of(sc, 0, cut + 1, la + lb) + 1) * stride);
-                    out = -1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int64_t kept = 0;  // block-uniform
+    for (int64_t i0 = 0; i0 < n; i0 += CL_THREADS) {
+        const int64_t i = i0 + threadIdx.x;
+        bool keep = false;
+        int32_t p = 0;
+        if (i < n) {
+            p = src[i];
+            keep = true;
+            const int64_t x = A.pl[p], y = A.pr[p];
+            const uint4 a0 = bag0[2 * x], a1 = bag0[2 * x + 1], b0 = bag1[2 * y], b1 = bag1[2 * y + 1];
+            const int la = (int)(a1.w >> 24), lb = (int)(b1.w >> 24);
+            if (la != 255 && lb != 255) {
+                int inter = bag_inter_ub(a0, a1, b0, b1);
+                if (inter >= 0) {
+                    const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
+                    inter = inter < mn ? inter : mn;
+                    const int cut = simple_lev_cut(sc, la, lb);
+                    if (mx - inter > cut) {  // unequal rows (a positive bag distance), distance past the cut
+                        code_add_atomic(A, p, (uint32_t)(lev_level_of(sc, 0, cut + 1, la + lb) + 1) * stride);
+                        keep = false;
+                    }
                 }
             }
         }
-        dst[i] = out;
+        const unsigned long long m = __ballot(keep);
+        if (lane == 0) s_kept[wv] = __popcll(m);
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < CL_THREADS / 64; ++q) {
+            off += q < wv ? s_kept[q] : 0;
+            tot += s_kept[q];
+        }
+        if (keep) dst[kept + off + __popcll(m & ((1ull << lane) - 1ull))] = p;
+        kept += tot;
+        __syncthreads();
     }
+    for (int64_t i = kept + threadIdx.x; i < n; i += CL_THREADS) dst[i] = -1;
 }
 
 // Exact pass over column k through the interpreter.
@@ -930,11 +952,11 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
     // software pipeline: the next item's pair rows (and, for Levenshtein, the rows' lengths) are in
     // flight while this one is evaluated
     int64_t i = bid * X_THREADS + threadIdx.x;
-    int32_t p = 0, x = 0, y = 0, key = LEV_BINS - 1;
+    int32_t p = -1, x = 0, y = 0, key = LEV_BINS - 1;  // p = -1: no cell (past the list, or a k_compact_lev slot)
     if (i < n) {
         p = items[i];
-        x = A.pl[p];
-        y = A.pr[p];
+        x = A.pl[p < 0 ? 0 : p];
+        y = A.pr[p < 0 ? 0 : p];
     }
     __syncthreads();
 #ifdef SPK_X_STAMPS
@@ -946,16 +968,16 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
     // the sort's barriers cost more than it saves (cfg2 email: 475 -> 505 us), so they keep the old order.
     constexpr bool LEV = MODE == X_LEV;
     const bool regroup = LEV && s_c0.planes_hi != nullptr && s_c1.planes_hi != nullptr;  // block-uniform
-    if (regroup && i < n) key = lev_work_bin(s_c0.meta[x].len16, s_c1.meta[y].len16);
+    if (regroup && p >= 0) key = lev_work_bin(s_c0.meta[x].len16, s_c1.meta[y].len16);
     for (int64_t base = bid * X_THREADS; base < n; base += stride) {  // block-uniform
-        bool have = i < n;
+        bool have = p >= 0;
         const int64_t i2 = i + stride;
-        int32_t p2 = 0, x2 = 0, y2 = 0, key2 = LEV_BINS - 1;
+        int32_t p2 = -1, x2 = 0, y2 = 0, key2 = LEV_BINS - 1;
         if (i2 < n) {
             p2 = items[i2];
-            x2 = A.pl[p2];
-            y2 = A.pr[p2];
-            if (regroup) key2 = lev_work_bin(s_c0.meta[x2].len16, s_c1.meta[y2].len16);
+            x2 = A.pl[p2 < 0 ? 0 : p2];
+            y2 = A.pr[p2 < 0 ? 0 : p2];
+            if (regroup && p2 >= 0) key2 = lev_work_bin(s_c0.meta[x2].len16, s_c1.meta[y2].len16);
         }
         if (regroup) lev_sort_items(key, have, p, x, y);
         bool to_slow = false;
@@ -2204,8 +2226,9 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         if (fused) continue;
         const ColSet one_k{1, {k, 0, 0, 0}};
         const bool refill = lev && (ctx->lev_kernel == 1 || (ctx->lev_kernel == 2 && G.free_text[k]));
-        if (refill && G.bag[k])
-            k_compact_lev<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, k, si, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
+        if (lev && G.bag[k])
+            k_compact_lev<<<(unsigned)G.n_regions, CL_THREADS, 0, ctx->stream>>>(A, k, si, ctx->xpref.p, ctx->xlist.p,
+                                                                                ctx->xinfo.p);
         else
             k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
         if (refill) {
@@ -2452,6 +2475,27 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         sc.has_ids = (t0.cols[sc.col]->has_ids && t1.cols[sc.col]->has_ids) ? 1 : 0;
         implied_equal(ctx, t0, t1, sc);
     }
+    // character-bag rows of the free-text Levenshtein columns' strings (k_compact_lev), built on first use.
+    // Free-text only: in cfg2's emails the bound decided 15 % of the listed cells (1.23 of 8.10 M), and the
+    // compaction's gathers cost more than the scans it saved (γ pass 1.070 -> 1.168 ms; cfg5's addresses
+    // 4.88 -> 3.85 ms; profiles/r5_ab_lev_bag.log).
+    if (ctx->lev_bag) {
+        bool built[2] = {false, false};
+        for (const SimpleCol &sc : simple) {
+            if (sc.cls != SC_LEV || sc.kind != SK_STR || !t0.cols[sc.col]->planes_hi.n || !t1.cols[sc.col]->planes_hi.n)
+                continue;
+            for (int s = 0; s < 2; ++s) {
+                Table &t = s ? t1 : t0;
+                Column *c = t.cols[sc.col];
+                if (c->kind != COL_STR || c->bag.n || t.n <= 0) continue;
+                SPK_TRY(build_bag_rows(ctx, t.n, c));
+                t.desc_dirty = true;
+                built[s] = true;
+            }
+        }
+        if (built[0]) SPK_TRY(ensure_desc(ctx, t0));
+        if (built[1]) SPK_TRY(ensure_desc(ctx, t1));
+    }
     // threshold tables of the Levenshtein-ratio tests (SimpleCol.thr_off)
     std::vector<int16_t> thr_tab;
     for (SimpleCol &sc : simple) {
@@ -2599,11 +2643,11 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     for (const SimpleCol &sc : simple)
         if (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids)) G.may_exact[sc.k] = 0;
     G.free_text.assign(K, 0);  // simple columns with rows past 64 UTF-8 bytes on both sides (planes_hi)
-    G.bag.assign(K, 0);        // ... and character-bag rows on both sides (k_compact_lev)
+    G.bag.assign(K, 0);        // free-text Levenshtein columns with character-bag rows (k_compact_lev)
     for (const SimpleCol &sc : simple) {
         const Column *a = t0.cols[sc.col], *b = t1.cols[sc.col];
         G.free_text[sc.k] = (a && b && a->planes_hi.n && b->planes_hi.n) ? 1 : 0;
-        G.bag[sc.k] = (G.free_text[sc.k] && a->bag.n && b->bag.n && ctx->lev_bag) ? 1 : 0;
+        G.bag[sc.k] = (G.free_text[sc.k] && sc.cls == SC_LEV && a->bag.n && b->bag.n && ctx->lev_bag) ? 1 : 0;
     }
     G.huge_in_slow.assign(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
     for (int k = 0; k < K; ++k)
