@@ -594,7 +594,8 @@ __device__ inline int bag_inter_ub(const uint4 &a0, const uint4 &a1, const uint4
 // k_compact for a Levenshtein column: a listed cell whose rows' bag distance already exceeds the cut is decided
 // here (its level is lev_cell's for any distance past the cut); the others are packed to the front of the
 // region's slice of the list in order, and the slice's tail is -1, which the exact passes skip (whole waves of
-// it, mostly).
+// it, mostly).  0.206 ms per cfg5 call; four cells per thread per round (their loads in flight together) took
+// 0.260, and unordered packing through one LDS counter per workgroup (no barriers) 0.210.
 constexpr int CL_THREADS = 256;
 __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restrict__ xpref,
                                                             int32_t *__restrict__ xlist, const int64_t *__restrict__ xinfo) {
