@@ -592,17 +592,25 @@ __device__ inline int bag_inter_ub(const uint4 &a0, const uint4 &a1, const uint4
 }
 
 // k_compact for a Levenshtein column: a listed cell whose rows' bag distance already exceeds the cut is decided
-// here (its level is lev_cell's for any distance past the cut); the others are packed to the front of the
+// here (its level is lev_cell's for any distance past the cut), one with a row past 64 units goes straight to
+// the slow list; the others are packed to the front of the
 // region's slice of the list in order, and the slice's tail is -1, which the exact passes skip (whole waves of
 // it, mostly).  0.206 ms per cfg5 call; four cells per thread per round (their loads in flight together) took
 // 0.260, and unordered packing through one LDS counter per workgroup (no barriers) 0.210.
 constexpr int CL_THREADS = 256;
+constexpr int CL_SLOW = 1024;  // LDS buffer of slow-list cells per workgroup
 __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restrict__ xpref,
                                                             int32_t *__restrict__ xlist, const int64_t *__restrict__ xinfo) {
     if (xinfo[2 * A.K]) return;  // overflow: the host re-runs the phase
     __shared__ SimpleCol s_sc;
     __shared__ int s_kept[CL_THREADS / 64];
-    if (threadIdx.x == 0) s_sc = A.simple[si];
+    __shared__ int32_t s_slow[CL_SLOW];
+    __shared__ int s_ns;
+    __shared__ unsigned int s_sbase;
+    if (threadIdx.x == 0) {
+        s_sc = A.simple[si];
+        s_ns = 0;
+    }
     __syncthreads();
     const SimpleCol &sc = s_sc;
     const int64_t *pref = xpref + (int64_t)k * (A.n_regions + 1);
@@ -613,10 +621,19 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
     const uint4 *bag0 = A.cols0[sc.col].bag, *bag1 = A.cols1[sc.col].bag;
     const uint32_t stride = (uint32_t)sc.stride;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t *slow_list = A.slow + A.slow_off[k];
+    auto flush_slow = [&]() {  // the buffered slow cells to the slow list: one device atomic
+        const int c = s_ns;
+        if (threadIdx.x == 0) s_sbase = atomicAdd(A.slow_count + k, (unsigned int)c);
+        __syncthreads();
+        for (int j = threadIdx.x; j < c; j += CL_THREADS) slow_list[s_sbase + j] = s_slow[j];
+        __syncthreads();
+        if (threadIdx.x == 0) s_ns = 0;
+    };
     int64_t kept = 0;  // block-uniform
     for (int64_t i0 = 0; i0 < n; i0 += CL_THREADS) {
         const int64_t i = i0 + threadIdx.x;
-        bool keep = false;
+        bool keep = false, slow = false;
         int32_t p = 0;
         if (i < n) {
             p = src[i];
@@ -625,6 +642,9 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
             const uint4 a0 = bag0[2 * x], a1 = bag0[2 * x + 1], b0 = bag1[2 * y], b1 = bag1[2 * y + 1];
             const int la = (int)(a1.w >> 24), lb = (int)(b1.w >> 24);
             if (la != 255 && lb != 255) {
+                // a row past 64 units has no 64-bit planes: the exact pass would only pass the cell on to the
+                // 128-bit slow pass, after loading its rows -- it goes to the slow list from here
+                slow = la > 64 || lb > 64;
                 int inter = bag_inter_ub(a0, a1, b0, b1);
                 if (inter >= 0) {
                     const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
@@ -632,10 +652,19 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
                     const int cut = simple_lev_cut(sc, la, lb);
                     if (mx - inter > cut) {  // unequal rows (a positive bag distance), distance past the cut
                         code_add_atomic(A, p, (uint32_t)(lev_level_of(sc, 0, cut + 1, la + lb) + 1) * stride);
-                        keep = false;
+                        keep = slow = false;
                     }
                 }
             }
+        }
+        const unsigned long long ms = __ballot(keep && slow);
+        if (ms) {  // into the workgroup's LDS buffer (the device counter once per CL_SLOW cells: a shared
+                   // counter per wave serialised, 2.9 ms per cfg5 call)
+            int sb = 0;
+            if (lane == 0) sb = atomicAdd(&s_ns, __popcll(ms));
+            sb = __shfl(sb, 0);
+            if (keep && slow) s_slow[sb + __popcll(ms & ((1ull << lane) - 1ull))] = p;
+            keep = keep && !slow;
         }
         const unsigned long long m = __ballot(keep);
         if (lane == 0) s_kept[wv] = __popcll(m);
@@ -648,6 +677,7 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
         }
         if (keep) dst[kept + off + __popcll(m & ((1ull << lane) - 1ull))] = p;
         kept += tot;
+        if (s_ns > CL_SLOW - CL_THREADS || i0 + CL_THREADS >= n) flush_slow();  // block-uniform (after the barrier)
         __syncthreads();
     }
     for (int64_t i = kept + threadIdx.x; i < n; i += CL_THREADS) dst[i] = -1;
