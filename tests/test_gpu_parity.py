@@ -958,3 +958,57 @@ def test_em_first_launch_small_pair_sets(amd, P):
         torch.cuda.synchronize()
         ctx.em_histogram(d.data_ptr())
         assert np.array_equal(d.cpu().numpy(), want)
+
+
+def test_levenshtein_bag_decisions(amd):
+    """Character-bag decisions before the free-text exact pass (k_bag_rows / k_compact_lev): address-like
+    strings of 20-140 units (mixed case, digits, spaces, punctuation, Latin-1 and supplementary-plane
+    characters, NULLs), unrelated pairs (mostly decided by their bags) and near copies (scanned); levels equal
+    the oracle's, some list slots were decided (-1), and every kernel mode, with and without the decisions,
+    gives the same codes.  Buckets saturate on long runs of one letter, which the bound then leaves alone."""
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(77))
+    alpha = list("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789 ,.-()") + ["é", "ß", "\U0001F600"]
+    def rnd(n):
+        return "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), n))
+    left, right = [], []
+    for n in [20, 40, 63, 64, 65, 66, 90, 127, 128, 140]:
+        for rep in range(40):
+            a = rnd(n)
+            if rep < 25:
+                b = rnd(int(rng.integers(max(1, n - 10), n + 10)))  # unrelated
+            elif rep < 35:
+                b = _mutate(rng, a, int(rng.integers(0, max(2, n // 4))), alpha[:62])  # near copy
+            elif rep < 38:
+                a = "a" * n
+                b = "a" * (n - 3) + "bcd"  # a bucket saturated on both sides
+            else:
+                b = a
+            left.append(a)
+            right.append(b)
+    left += [None, "x" * 70, None]
+    right += ["y" * 70, None, None]
+    df = pd.DataFrame({"a_l": left, "a_r": right})
+    ratio = ("case when a_l is null or a_r is null then -1 when a_l = a_r then 3 "
+             "when levenshtein(a_l, a_r)/((length(a_l) + length(a_r))/2) <= 0.2 then 2 "
+             "when levenshtein(a_l, a_r)/((length(a_l) + length(a_r))/2) <= 0.4 then 1 else 0 end")
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "lr", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": ratio}]}
+    gf = add_gammas(df, st, amd)
+    got = gf.gamma_matrix()
+    for i, (a, b) in enumerate(zip(left, right)):
+        if a is None or b is None:
+            assert got[i, 0] == -1
+            continue
+        if a == b:
+            assert got[i, 0] == 3
+            continue
+        d = orc.levenshtein(a, b)
+        ca, cb = len(a.encode("utf-16-le")) // 2, len(b.encode("utf-16-le")) // 2
+        q = d / ((len(a) + len(b)) / 2.0)
+        want = 2 if q <= 0.2 else (1 if q <= 0.4 else 0)
+        assert got[i, 0] == want, (a, b, d, ca, cb, got[i, 0])
+    n_exact = gf.job.ctx.gammas_exact_counts(1)[0]
+    items = gf.job.ctx.gammas_exact_list(0, int(n_exact))
+    assert (items < 0).sum() > 0, "no cell was decided from its character bag"
+    _lev_variants_agree(gf.job, gf.settings, got)
