@@ -416,7 +416,8 @@ def string_rates(job, st, pairs, g_ms):
             vals = t[c["col_name"]]
             ln = vals.str.len().fillna(0).to_numpy(np.int64)
             items = job.ctx.gammas_exact_list(k, int(exact[k]))
-            n_bag = int((items < 0).sum())  # decided by their character-bag distance (k_compact_lev): no scan
+            # -1 slots (k_compact_lev): decided by their character-bag distance, or sent straight to the slow pass
+            n_bag = int((items < 0).sum())
             items = items[items >= 0]
             nominal = int(np.dot(ln[l[items]], ln[r[items]]))
             # cells the scans actually update, from a host restatement of the scan over a random sample of
@@ -435,7 +436,7 @@ def string_rates(job, st, pairs, g_ms):
                 cnt += 1
             scanned = tot / cnt * len(items) if cnt else None
             sec_x = xms[k] / 1e3 if xms[k] > 0 else None
-            lev[c["col_name"]] = {"exact_cells": int(exact[k]), "bag_decided_cells": n_bag, "exact_pass_ms": xms[k],
+            lev[c["col_name"]] = {"exact_cells": int(exact[k]), "cells_compacted_out": n_bag, "exact_pass_ms": xms[k],
                                   "dp_cells_nominal": nominal,
                                   "gcups_nominal": nominal / sec_x / 1e9 if sec_x else None,
                                   "dp_cells_scanned_est": scanned,
