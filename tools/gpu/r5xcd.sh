@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5: XCD-grouped region mapping in k_filter (tools/abx/filter_xcd.so, -DSPK_FILTER_XCD=1) against the
 # in-tree build, alternating, cfg2 and cfg5 γ pass; codes must match.
+# (the SPK_FILTER_XCD variant was removed after this A/B: profiles/r5_ab_filter_xcd.log)
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 : > gpurun_out/r5xcd.log
 for lib in A B A B; do
