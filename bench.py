@@ -37,6 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r5_traffic.json")
 # per-kernel issue counters of the same command (rocprofv3 --pmc passes, tools/pmc_summary.py)
 PMC_FILE = os.path.join(ROOT, "profiles", "r5_pmc_kernels.json")
+PMC_FILE_CFG5 = os.path.join(ROOT, "profiles", "r5_cfg5_lev_pmc.json")  # tools/gpu/pmc_cfg5_lev.sh
 COLS = ["first_name", "surname", "dob", "city", "email"]
 WORKLOADS = {2: "cfg2: synthetic person-record dedupe, 1M x sqrt(N) records, blocking surname|dob, "
                 "5 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3)",
@@ -251,16 +252,18 @@ def main():
     # The γ kernels are issue-bound, not HBM-bound: their VALU / SALU issue against the SIMD peaks and
     # the share of wave time stalled, from the committed counter passes of this command
     issue = None
-    if os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
+    pmc_file = PMC_FILE_CFG5 if args.config == 5 else PMC_FILE
+    if os.path.exists(pmc_file):
+        with open(pmc_file) as f:
             pmc = json.load(f)
-        issue = {"source": os.path.relpath(PMC_FILE, ROOT) + ": rocprofv3 --pmc SQ_* passes of this command",
-                 "peak_note": "valu_util = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles at 2.4 GHz)"}
+        issue = {"source": os.path.relpath(pmc_file, ROOT) + ": rocprofv3 --pmc SQ_* passes of this config's "
+                 "comparison pass", "peak_note": "valu_util = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles "
+                 "at 2.4 GHz); kernels that ran under 10 us per launch (near-empty lists) are left out"}
         for name, key in (("filter", "k_filter"), ("levenshtein_exact", "k_gamma_exact_simple<1,"),
                           ("levenshtein_refill", "k_lev_refill"), ("levenshtein_slow", "k_gamma_slow_lev"),
-                          ("jw_exact", "k_gamma_exact_simple<2,")):
+                          ("bag_compaction", "k_compact_lev"), ("jw_exact", "k_gamma_exact_simple<2,")):
             for k, v in pmc.items():
-                if key in k:
+                if key in k and float(v.get("_dur_ns", 0.0)) >= 10000.0:
                     issue[name] = {x: round(float(v[x]), 4) for x in ("valu_util", "salu_util", "wait_frac", "l2_hit")
                                    if x in v}
                     break
