@@ -53,9 +53,64 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher's WORLD_SIZE: start N fresh rank processes of this script, one
+    per GPU (RANK = LOCAL_RANK = g, WORLD_SIZE = N, rendezvous on 127.0.0.1), and return the first non-zero
+    exit code, else 0.  This process never imports torch or touches a GPU (the ranks are children, not an
+    exec of it); rank 0 writes the JSON line to the inherited stdout.  A rank that fails ends the others
+    (they would wait in a collective for it)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for g in range(n):
+        env = dict(os.environ, RANK=str(g), LOCAL_RANK=str(g), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      start_new_session=True))
+    code = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if rc != 0 and code == 0:
+                    code = rc if rc > 0 else 128 - rc
+                    log(f"bench.py: rank {procs.index(p)} exited with {rc}; ending the other ranks")
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+    return code
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment this script starts them itself")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend: nccl (= RCCL) for the benchmark; gloo rehearses N ranks on the CPU "
+                         "(--dry-run) or on fewer GPUs (ranks share devices round-robin, exchange host-staged)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and rendezvous only: every rank joins the group and the all-reduce that counts "
+                         "them, rank 0 prints the line without running the workload (no GPU needed with gloo)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--records", type=int, default=1_000_000, help="records at N=1 (scaled by sqrt(N))")
@@ -70,16 +125,55 @@ def main():
                     help="separate E/M streaming row: the run's comparison vectors tiled this many times (0 = off)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ:
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            log(f"bench.py: --gpus {n}: need at least one rank")
+            sys.exit(2)
+        if n > 1:
+            sys.exit(launch_ranks(n, sys.argv[1:]))  # this process only waits for its ranks
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            log(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+            sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    n_dev = torch.cuda.device_count()
+    if args.backend == "nccl" and n_dev < world:
+        # RCCL runs one rank per GPU; refuse instead of benching fewer GPUs under a larger label
+        log(f"bench.py: --gpus {world} needs {world} visible GPUs, {n_dev} visible")
+        sys.exit(3)
+    if n_dev == 0 and not args.dry_run:
+        log("bench.py: no GPU visible (the workload runs on the GPU; --dry-run --backend gloo rehearses the launch)")
+        sys.exit(3)
+    dev = local % n_dev if n_dev else -1  # gloo rehearsal: ranks share the visible devices round-robin
+    if dev >= 0:
+        torch.cuda.set_device(dev)
+    ranks_seen = 1
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(0)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+            one = torch.ones(1, dtype=torch.int64, device=f"cuda:{dev}")
+        else:
+            dist.init_process_group("gloo")
+            one = torch.ones(1, dtype=torch.int64)
+        dist.all_reduce(one)
+        ranks_seen = int(one.item())
+        assert ranks_seen == dist.get_world_size() == world, (ranks_seen, world)
+    if args.dry_run:
+        if rank == 0:
+            print(json.dumps({"metric": "candidate pairs scored/sec (gammas+E+M per iter)", "value": None,
+                              "unit": "pairs/s", "n_gpus": world, "ranks_seen": ranks_seen, "backend": args.backend,
+                              "devices_visible": n_dev, "dry_run": True}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    local = dev
 
     from splink_amd import _native as N
     from splink_amd import distributed as D
@@ -284,6 +378,9 @@ def main():
         "value": total_pairs / (ms_per_step / 1e3),
         "unit": "pairs/s",
         "n_gpus": world,
+        "ranks_seen": ranks_seen,
+        "backend": args.backend if world > 1 else None,
+        "devices_used": min(world, n_dev),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -296,7 +393,9 @@ def main():
                    "records": n_records, "candidate_pairs": total_pairs, "comparison_columns": len(cols),
                    "candidate_ordinals_total": job.n_candidates, "shard": list(shard),
                    "comparison_windows": job.ctx.gammas_windows(),
-                   "parallelism": f"pair-ordinal shards x{world}, RCCL all-reduce of pattern histogram"},
+                   "parallelism": f"pair-ordinal shards x{world}, " + (
+                       "RCCL all-reduce of pattern histogram" if args.backend == "nccl" or world == 1 else
+                       "gloo all-reduce of pattern histogram (host-staged rehearsal, ranks sharing GPUs)")},
         "roofline": roofline,
         "roofline_em": em_roofline,
         "issue_gamma_kernels": issue,

@@ -264,8 +264,8 @@ int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs);
 int spk_gammas_windows(spk_ctx *ctx, int64_t *out);
 /* Levenshtein pass kernels (same codes in every mode; for A/B tests): 2 = lane refill (a lane that finishes its
  * cell takes the next one from its wave's queue) in the exact pass of free-text columns -- rows past 64 units on
- * both sides -- and one cell per lane elsewhere (default), 1 = lane refill in every exact pass and in the 128-bit
- * slow pass, 0 = one cell per lane everywhere, 3 = as 2 without the character-bag decisions that precede a
+ * both sides -- and one cell per lane elsewhere (default), 1 = lane refill in every exact pass (the 128-bit slow
+ * pass stays one cell per lane), 0 = one cell per lane everywhere, 3 = as 2 without the character-bag decisions that precede a
  * refill pass over a free-text column (k_compact_lev: cells whose bag distance exceeds the cut take their level
  * there).  Modes 1 and 2 make those decisions too. */
 int spk_gammas_set_lev_kernel(spk_ctx *ctx, int mode);

@@ -366,16 +366,22 @@ def _spark_concat_ws(sep, *args):
 
 
 def _spark_to_integral(v, bits):
-    """cast(x as int / bigint / smallint / tinyint) (UTF8String.toInt / toLong, Spark 2.4)."""
+    """cast(x as int / bigint / smallint / tinyint) (UTF8String.toInt / toLong, Spark 2.4).  A number:
+    Cast.castToInt / castToShort / castToByte take `numeric.toInt(b)` (a double saturates at the int range,
+    NaN -> 0; bigint: Double.toLong at the long range) and narrow with the JVM's wrapping .toShort / .toByte;
+    an integral value narrows by wrapping.  (Restated from Spark 2.4's Cast.scala, which is not in
+    /root/reference: parity unpinned for out-of-range numbers.)"""
     if v is None:
         return None
+    lim = 2 ** (bits - 1)
     if isinstance(v, float):
         if v != v:
             return 0
-        lim = 2 ** (bits - 1)
-        return lim - 1 if v >= lim else (-lim if v < -lim else int(v))
+        sat = 2 ** 63 if bits == 64 else 2 ** 31
+        x = sat - 1 if v >= sat else (-sat if v < -sat else int(v))
+        return ((x + lim) % (2 * lim)) - lim
     if isinstance(v, int):
-        return v
+        return ((v + lim) % (2 * lim)) - lim
     m = re.fullmatch(r"([+-]?)([0-9]*)(\.[0-9]*)?", v)
     if not m or v in ("", "+", "-"):
         return None

@@ -8,7 +8,7 @@ are no rules.  The pairs are generated on the GPU (spk_block) and stay there.
 import pandas as pd
 
 from .check_types import check_types
-from .engine import Job, columns_to_retain_blocking, distributed_shard, session_device
+from .engine import Job, columns_to_retain_blocking, distributed_shard, session_device, string_columns_read
 from .frames import ComparisonFrame
 
 
@@ -45,24 +45,23 @@ def _block(settings, spark, df_l, df_r, df, rules):
     # comparison-only string columns start their upload at once, behind the unique-id ranks and the blocking
     # work (Job.prefetch_strings)
     job = Job(settings["link_type"], tables, settings["unique_id_column_name"], session_device(spark),
-              shard=distributed_shard(), prefetch=_comparison_only_columns(settings, rules, tables[0].columns))
+              shard=distributed_shard(), prefetch=_comparison_only_columns(settings, rules, tables))
     job.block(list(rules))
     return ComparisonFrame(job, settings)
 
 
-def _comparison_only_columns(settings, rules, columns):
-    """Input columns the comparison columns read that no blocking rule mentions (those are uploaded by the
-    blocking pass itself, which must not wait behind a prefetch)."""
+def _comparison_only_columns(settings, rules, tables):
+    """Input string columns the comparison program reads as bare operands that no blocking rule mentions
+    (those are uploaded by the blocking pass itself, which must not wait behind a prefetch).  A column read
+    only through a derived expression (`lower(first_name_l)`) is not one: the derived column is what goes to
+    the device."""
     import re
     used = set(re.findall(r"[a-z_][a-z_0-9]*", " ".join(rules).lower()))
-    by_lower = {str(c).lower(): c for c in columns}
-    out = []
-    for c in settings["comparison_columns"]:
-        for name in ([c["col_name"]] if "col_name" in c else []) + list(c.get("custom_columns_used", [])):
-            canon = by_lower.get(str(name).lower())
-            if canon is not None and canon.lower() not in used and canon not in out:
-                out.append(canon)
-    return out
+    try:
+        names = string_columns_read(settings, tables)
+    except Exception:  # noqa: BLE001 -- only a prefetch: the program's own error surfaces in add_gammas
+        return []
+    return [c for c in names if c.lower() not in used]
 
 
 @check_types

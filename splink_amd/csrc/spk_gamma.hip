@@ -876,8 +876,7 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
 // past the end of the list.
 constexpr int LEV_BINS = 192;
 __device__ inline int lev_work_bin(int la, int lb) {
-    la = la < 0 ? 0 : la;
-    lb = lb < 0 ? 0 : lb;
+    if (la < 0 || lb < 0) return 0;  // a NULL row: lev_cell settles it at once (not the slow list)
     const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
     return (mx > 64 ? 128 : (mx > 32 ? 64 : 0)) + (mn < 63 ? mn : 63);
 }
@@ -2165,18 +2164,9 @@ static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
         const int si = G.simple_of[k];
         const bool lev = si >= 0 && G.simple[si].cls == SC_LEV;
         const ColSet one_k{1, {k, 0, 0, 0}};
-        if (lev && ctx->lev_kernel == 1) {
-            // lane refill over 128-bit planes (A/B only: 5.13 -> 5.47 ms per cfg5 γ pass against k_gamma_slow_lev,
-            // DESIGN.md §4): 2 waves per SIMD (its LDS queue), one resident round
-            const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)2 * ctx->n_cu));
-            switch (G.simple[si].np) {
-                case 5: k_lev_refill<5, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
-                case 6: k_lev_refill<6, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
-                case 7: k_lev_refill<7, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
-                default: k_lev_refill<8, 2><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p); break;
-            }
-            k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
-        } else if (lev) {
+        if (lev) {
+            // (a lane-refill form of this pass over 128-bit planes lost 0.5 ms per cfg5 γ pass and was removed in
+            // round 6)
             constexpr int SLOWLEV_WG_PER_CU = 8;  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU at once
             const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SLOWLEV_WG_PER_CU * ctx->n_cu));
             k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
@@ -2593,8 +2583,11 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     // slow lists, huge cells) before the next one reuses the lists; the last is left pending as usual.
     const int64_t WMAX = ((int64_t)1 << 31) - ((int64_t)1 << 22);
     const int64_t wcap = ctx->gamma_window > 0 ? std::min<int64_t>(ctx->gamma_window, WMAX) : WMAX;
-    const int64_t n_win = std::max<int64_t>(1, (P + wcap - 1) / wcap);
-    const int64_t W = n_win == 1 ? P : ((P + n_win - 1) / n_win + 63) / 64 * 64;  // pairs per window (the last: rest)
+    const int64_t n_win0 = std::max<int64_t>(1, (P + wcap - 1) / wcap);
+    const int64_t W = n_win0 == 1 ? P : ((P + n_win0 - 1) / n_win0 + 63) / 64 * 64;  // pairs per window (the last: rest)
+    // rounding W up to a multiple of 64 can leave trailing windows empty (small test windows): count the
+    // windows from W itself
+    const int64_t n_win = n_win0 == 1 ? 1 : (P + W - 1) / W;
     // work lists only for the columns whose filter can leave cells undecided (a dictionary-id equality
     // or numeric column never does): one slot of W pair indices each
     std::vector<int32_t> wslot(K, 0);

@@ -137,6 +137,8 @@ def render_any(node) -> str:
 
 
 # ---- Spark semantics, per value --------------------------------------------------------------------
+# the optional float / double suffix only follows a decimal literal (the third alternative):
+# Double.parseDouble("Infinityd") / ("NaNf") throw, so Spark's cast gives NULL
 _JAVA_DOUBLE = re.compile(r"[+-]?(NaN|Infinity|((\d+\.?\d*|\.\d+)([eE][+-]?\d+)?)[fFdD]?)\Z")
 _JAVA_HEX = re.compile(r"([+-]?)(0[xX](?:[0-9a-fA-F]+\.?[0-9a-fA-F]*|\.[0-9a-fA-F]+)[pP][+-]?\d+)[fFdD]?\Z")
 
@@ -185,7 +187,10 @@ def spark_string_to_integral(s: str, bound: int) -> Optional[int]:
 
 
 def number_to_integral(x, bound: int) -> int:
-    """Scala Double.toInt / toLong (truncation; NaN -> 0; saturating)."""
+    """Spark 2.4 non-ANSI Cast of a number to an integral type: Scala Double.toLong for bigint (truncation,
+    NaN -> 0, saturating at the long range); for int / smallint / tinyint Double.toInt (saturating at the
+    int range) followed by the JVM's wrapping narrowing .toShort / .toByte (Cast.castToShort / castToByte:
+    `numeric.toInt(b).toShort`), so cast(40000.0 as smallint) is -25536."""
     if isinstance(x, (int, np.integer)) and not isinstance(x, bool):
         v = int(x)
         # integral narrowing wraps in the JVM (int -> smallint keeps the low bits)
@@ -193,11 +198,9 @@ def number_to_integral(x, bound: int) -> int:
     x = float(x)
     if math.isnan(x):
         return 0
-    if x >= bound:
-        return bound - 1
-    if x < -bound:
-        return -bound
-    return int(x)
+    sat = 2 ** 63 if bound >= 2 ** 63 else 2 ** 31
+    v = sat - 1 if x >= sat else (-sat if x < -sat else int(x))
+    return ((v + bound) % (2 * bound)) - bound
 
 
 def _is_null(v) -> bool:

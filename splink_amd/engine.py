@@ -81,6 +81,27 @@ def columns_to_retain_blocking(settings) -> List[str]:
     return list(cols)
 
 
+def schema_of(tables) -> Schema:
+    """Each column's form (str / num) over the input tables (the first table's wins)."""
+    forms = {}
+    for t in reversed(tables):
+        for c in t.columns:
+            forms[c] = T.natural_form(t[c])
+    return Schema(forms)
+
+
+def string_columns_read(settings, tables) -> List[str]:
+    """Input string columns the settings' comparison program reads as bare operands, in program order: its
+    derived columns (`lower(first_name)`, evaluated at ingest and uploaded under that name) and numeric
+    columns left out.  Compiles on the host only."""
+    prog = compile_comparisons(settings, schema_of(tables))
+    out = []
+    for name, form in prog.columns:
+        if form == "str" and name not in prog.derived and name in tables[0].columns and name not in out:
+            out.append(name)
+    return out
+
+
 class Job:
     """Record tables + pairs + codes living on one GPU.
 
@@ -103,11 +124,7 @@ class Job:
         self.shard, self.n_shards = shard
         self.ctx = N.Context(device)
         self.ctx.set_link_type(N.LINK_TYPES[link_type])
-        forms = {}
-        for t in reversed(self.inputs):
-            for c in t.columns:
-                forms[c] = T.natural_form(t[c])
-        self.schema = Schema(forms)
+        self.schema = schema_of(self.inputs)
         self._col_index = {}
         self._raw = {}
         self._next_raw = 0  # raw-column ids only go up: a released id is never handed out again
@@ -204,6 +221,19 @@ class Job:
         for key, chunks in todo:
             self._prefetch[key] = self._prefetch_pool.submit(_upload_utf8_chunks, chunks, self.device)
         return len(todo)
+
+    def drop_prefetch(self, keep=()):
+        """Drop the background uploads of columns not in `keep` (no comparison program adopted them: e.g. a
+        program that changed after blocking); their staging tensors go back to the device."""
+        drop = [k for k in self._prefetch if k[1] not in keep]
+        for key in drop:
+            fut = self._prefetch.pop(key)
+            if not fut.cancel():
+                fut.result()  # running or done: wait, then let its tensors go
+        if drop and not self._prefetch:
+            import torch
+            torch.cuda.empty_cache()
+        return len(drop)
 
     def raw_utf8(self, side: int, name: str) -> int:
         """Raw string column (input row order) on the device, uploaded once.  Arrow columns hand over their
@@ -450,6 +480,8 @@ class Job:
             for name, node in prog.derived.items():
                 self.add_derived(name, node)
             index = {k: self.column_index(*k) for k in prog.columns}
+            if self._prefetch:
+                self.drop_prefetch(keep={name for name, _ in prog.columns})
             lit_off, lit_bytes = prog.literal_buffers()
             args = N.Context.gammas_args(prog.programs, prog.when_first, prog.when_n, prog.when_level, prog.instrs,
                                          prog.native_operands(index), lit_off, lit_bytes)

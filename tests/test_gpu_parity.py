@@ -282,13 +282,17 @@ def test_levenshtein_cut_around_thresholds(amd):
     st = {"link_type": "dedupe_only", "comparison_columns": [
         {"custom_name": "lr", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": lr, **mu},
         {"custom_name": "la", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": la, **mu}]}
-    got = add_gammas(df, st, amd).gamma_matrix()
+    gf = add_gammas(df, st, amd)
+    got = gf.gamma_matrix()
     for i, (a, b) in enumerate(zip(left, right)):
         d = orc.levenshtein(a, b)
         r = d / ((len(a) + len(b)) / 2)
         want_r = 3 if a == b else 2 if r <= 0.2 else 1 if r <= 0.3 else 0
         want_a = 3 if d <= 3 else 2 if d <= 9 else 1 if d <= 20 else 0
         assert list(got[i]) == [want_r, want_a], (len(a), len(b), d, r, list(got[i]))
+    # every Levenshtein kernel mode (per lane, lane refill, refill in free-text columns, no bag decisions) is
+    # held to the same cut-edge cells
+    _lev_variants_agree(gf.job, gf.settings, got)
 
 
 def test_jw_filter_field_edges(amd):

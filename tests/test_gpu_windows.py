@@ -173,3 +173,34 @@ def test_prefetched_columns_match_direct_upload(amd, chunked):
     assert out[1][2] is not None  # the prefetched columns were adopted
     assert out[0][0] == out[1][0]
     assert (out[0][1] == out[1][1]).all()
+
+
+def test_prefetch_of_a_derived_only_column_is_dropped(amd):
+    """A column the comparison program reads only through a derived expression (jaro_winkler_sim over
+    lower(first_name)) is not prefetched by block_using_rules' choice, and a prefetch the program does not
+    adopt is dropped once the program is compiled (nothing left pending, its staging tensors released)."""
+    from splink_amd.blocking import _comparison_only_columns
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    from splink_amd.synthetic import cfg_settings
+    import pyarrow as pa
+    import pandas as pd
+    df = _records(5000, 54)
+    for c in COLS:
+        df[c] = pd.Series(pd.arrays.ArrowExtensionArray(pa.chunked_array([pa.array(df[c].tolist(),
+                                                                                   type=pa.large_string())])))
+    st = cfg_settings(2)
+    cc = [dict(c) for c in st["comparison_columns"]]
+    cc[0] = {"custom_name": "fn", "custom_columns_used": ["first_name"], "num_levels": 2,
+             "case_expression": "case when first_name_l is null or first_name_r is null then -1 "
+                                "when jaro_winkler_sim(lower(first_name_l), lower(first_name_r)) > 0.9 then 1 else 0 end"}
+    st = complete_settings_dict(dict(st, comparison_columns=cc), amd)
+    assert "first_name" not in _comparison_only_columns(st, st["blocking_rules"], [df])
+    job = Job("dedupe_only", [df], "unique_id", 0, prefetch=["first_name", "email"])
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    assert not job._prefetch
+    ref = Job("dedupe_only", [df], "unique_id", 0)
+    ref.block(st["blocking_rules"])
+    ref.gammas(st)
+    assert (job.gammas_host() == ref.gammas_host()).all()

@@ -200,7 +200,10 @@ def test_derived_values_match_oracle_functions():
     rng = np.random.Generator(np.random.PCG64(9))
     words = np.array(["Anna", " anna ", "ANNA", "", "  ", "O'Neil", "Straße", "İlker", "Zoë", "x y"], dtype=object)
     nums = np.array(["12", " 12", "12.9", "-0", "+13", "1e1", "abc", "", "99999999999", "7.", ".5", "-12.5",
-                     "1.8d", " 1.8 ", "Infinity", "-Infinity", "0x1p3", "0X1.Cp0", "+.5", "-", "."], dtype=object)
+                     "1.8d", " 1.8 ", "Infinity", "-Infinity", "0x1p3", "0X1.Cp0", "+.5", "-", ".",
+                     # double -> smallint / tinyint saturates at the int range, then wraps (Cast.castToShort);
+                     # a suffix after Infinity / NaN does not parse (NULL)
+                     "40000.5", "-40000", "1e10", "300.7", "-1e300", "Infinityd", "NaNf"], dtype=object)
     n = 400
     df = pd.DataFrame({"a": rng.choice(words, n), "b": rng.choice(words[:6], n), "n": rng.choice(nums, n)})
     for c in df.columns:
@@ -208,7 +211,8 @@ def test_derived_values_match_oracle_functions():
     df_arrow = df.astype({"b": pd.ArrowDtype(__import__("pyarrow").large_string())})
     exprs = ["lower(a)", "upper(trim(a))", "ltrim(a)", "rtrim(b)", "concat(a, ' ', b)", "concat_ws('|', a, b, n)",
              "cast(n as int)", "cast(n as bigint)", "cast(n as smallint)", "cast(n as double)",
-             "cast(cast(n as double) as int)", "substr(lower(a), 2, 3)", "lower(ifnull(a, b))", "upper(b)",
+             "cast(cast(n as double) as int)", "cast(cast(n as double) as smallint)",
+             "cast(cast(n as double) as tinyint)", "cast(cast(n as double) as bigint)", "substr(lower(a), 2, 3)", "lower(ifnull(a, b))", "upper(b)",
              "concat(b, '-', b)", "trim(b)"]
     con = orc.connect()
     df.to_sql("t", con, index=False)

@@ -121,7 +121,7 @@ def main():
     t = time.perf_counter()
     from splink_amd.blocking import _comparison_only_columns
     # the comparison-only columns upload in the background while the uid ranks and blocking run
-    pre = _comparison_only_columns(st, st["blocking_rules"], inputs[0].columns) if a.prefetch else None
+    pre = _comparison_only_columns(st, st["blocking_rules"], inputs) if a.prefetch else None
     job = Job(st["link_type"], inputs, "unique_id", 0, shard=(shard, n_shards), prefetch=pre)
     job.ctx.enable_timing(True)
     wall["job_setup_incl_uid_rank"] = time.perf_counter() - t
