@@ -53,6 +53,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+_LINE_FD = 1
+
+
+def emit(line: dict):
+    """The one JSON line of the run, on the process's original stdout."""
+    sys.stdout.flush()
+    os.write(_LINE_FD, (json.dumps(line) + "\n").encode())
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -140,6 +149,11 @@ def main():
             sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries only rank 0's JSON line: whatever the libraries print there (gloo's connection notes,
+    # RCCL / HIP diagnostics) goes to stderr
+    global _LINE_FD
+    _LINE_FD = os.dup(1)
+    os.dup2(2, 1)
     import torch
     n_dev = torch.cuda.device_count()
     if args.backend == "nccl" and n_dev < world:
@@ -166,9 +180,9 @@ def main():
         assert ranks_seen == dist.get_world_size() == world, (ranks_seen, world)
     if args.dry_run:
         if rank == 0:
-            print(json.dumps({"metric": "candidate pairs scored/sec (gammas+E+M per iter)", "value": None,
-                              "unit": "pairs/s", "n_gpus": world, "ranks_seen": ranks_seen, "backend": args.backend,
-                              "devices_visible": n_dev, "dry_run": True}), flush=True)
+            emit({"metric": "candidate pairs scored/sec (gammas+E+M per iter)", "value": None,
+                  "unit": "pairs/s", "n_gpus": world, "ranks_seen": ranks_seen, "backend": args.backend,
+                  "devices_visible": n_dev, "dry_run": True})
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
@@ -413,7 +427,7 @@ def main():
         "string_rates": rates,
         "em_at_scale": em_scale,
     }
-    print(json.dumps(out), flush=True)
+    emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()

@@ -20,8 +20,8 @@ def _run(args, env_extra=None, timeout=120):
 
 
 def _line(out):
-    lines = [x for x in out.splitlines() if x.startswith("{")]
-    assert len(lines) == 1, out
+    lines = [x for x in out.splitlines() if x.strip()]
+    assert len(lines) == 1, out  # stdout is the JSON line alone (gloo's own notes go to stderr)
     return json.loads(lines[0])
 
 
