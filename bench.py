@@ -110,6 +110,116 @@ def launch_ranks(n: int, argv) -> int:
     return code
 
 
+def timed_run(config, records, shard, world, rank, local, steps, warmup):
+    """Build one workload's job (records, blocking, first comparison pass) and time `steps` steps after
+    `warmup` untimed ones, bracketed by a barrier + device synchronisation; the wall time is the maximum
+    over ranks.  Returns the job and what the line reports about it."""
+    import torch
+    from splink_amd import distributed as D
+    from splink_amd.engine import Job, m_step_rows
+    from splink_amd.params import Params
+    from splink_amd.session import AmdSession
+    from splink_amd.synthetic import cfg_settings, make_records
+    t0 = time.time()
+    cols = COLS + (["address"] if config == 5 else [])
+    if config == 4:
+        # the job's size does not grow with N: its ordinal space is split over the ranks (strong scaling)
+        from splink_amd.synthetic import make_records_parallel
+        n_records = 20_000_000
+        df = make_records_parallel(n_records, 16, 16, surname_vocab=300_000)[["unique_id"] + cols]
+    else:
+        n_records = int(round(records * math.sqrt(world)))
+        # Arrow-backed string columns: the columnar form a Spark / Arrow source hands over (values identical
+        # to the object-column records; spk_raw_utf8 takes their buffers without a per-row pass)
+        df = make_records(n_records, surname_vocab=15000, with_address=config == 5, arrow=True)[["unique_id"] + cols]
+    log(f"[rank {rank}] generated {n_records} records in {time.time() - t0:.1f}s")
+
+    settings = cfg_settings(config, max_iterations=10)
+    params = Params(settings, AmdSession(local))
+    st = params.settings
+
+    job = Job("dedupe_only", [df], "unique_id", local, shard=shard)
+    job.ctx.enable_timing(True)
+    t0 = time.time()
+    job.block(st["blocking_rules"])
+    block_s = time.time() - t0
+    block_kernel_ms = job.ctx.kernel_ms()["block"]
+    log(f"[rank {rank}] blocking: {job.n_pairs} local pairs of {job.n_candidates} candidates "
+        f"({block_s:.2f}s wall incl. host key prep, {block_kernel_ms:.1f} ms device)")
+    t0 = time.time()
+    job.gammas(st)  # uploads columns (device decode through the clustering permutation), first launch
+    first_gammas_s = time.time() - t0
+    names, nlev = job.code_meta
+
+    host = {"gammas_call": [], "em_wait": [], "m_step_host": [], "em_start": []}
+    dev = {"gamma": [], "em_hist": [], "em_final": []}
+    pending = [False]
+
+    def finish_m_step():
+        """Statistics of the enqueued E+M iteration, then the host M-step (Params update)."""
+        t0 = time.perf_counter()
+        stats = job.em_wait()
+        t1 = time.perf_counter()
+        lam, rows = m_step_rows(stats, names, nlev)
+        params._update_params(lam, rows)
+        t2 = time.perf_counter()
+        host["em_wait"].append((t1 - t0) * 1e3)
+        host["m_step_host"].append((t2 - t1) * 1e3)
+        pending[0] = False
+        ms = job.ctx.kernel_ms_done()  # the newest completed launches (the next comparison pass may be running)
+        for k in dev:
+            dev[k].append(ms[k])
+
+    def step():
+        """Comparison pass i, then E+M iteration i.  Software-pipelined: pass i is queued before the host
+        finishes the M-step of iteration i - 1 (pass i does not depend on it; E+M i does), so the device
+        never waits for the host.  The order of device work and its results are those of the plain loop."""
+        t0 = time.perf_counter()
+        job.gammas(st)
+        t1 = time.perf_counter()
+        if pending[0]:
+            finish_m_step()
+        t2 = time.perf_counter()
+        job.em_start(params.params["λ"], params._level_probabilities())
+        pending[0] = True
+        t3 = time.perf_counter()
+        host["gammas_call"].append((t1 - t0) * 1e3)
+        host["em_start"].append((t3 - t2) * 1e3)
+
+    def barrier():
+        torch.cuda.synchronize()
+        D.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(warmup):
+        step()
+    if pending[0]:
+        finish_m_step()
+    for v in list(host.values()) + list(dev.values()):
+        v.clear()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    finish_m_step()  # the last iteration's M-step is part of the timed work
+    barrier()
+    elapsed = time.perf_counter() - t0
+    # per-launch device times of the timed steps (HIP events on the context stream, read as each
+    # launch completed)
+    gamma_ms = dev["gamma"]
+    hist_ms = dev["em_hist"]
+    fin_ms = [max(x, 0.0) for x in dev["em_final"]]  # one GPU: the E-step runs inside the histogram launch
+    local_pairs = job.n_pairs
+    elapsed = D.max_over_ranks(elapsed)
+    total_pairs = D.sum_over_ranks(local_pairs)
+    ms_per_step = elapsed * 1000.0 / steps
+
+    return argparse.Namespace(job=job, df=df, params=params, st=st, cols=cols, names=names, nlev=nlev,
+                              n_records=n_records, gamma_ms=gamma_ms, hist_ms=hist_ms, fin_ms=fin_ms, host=host,
+                              local_pairs=local_pairs, total_pairs=total_pairs, ms_per_step=ms_per_step,
+                              block_s=block_s, block_kernel_ms=block_kernel_ms, first_gammas_s=first_gammas_s)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -129,6 +239,8 @@ def main():
     ap.add_argument("--share", type=str, default=None,
                     help="k/n: run rank k's share of an n-rank job on this one GPU (e.g. --config 4 --share 0/8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cfg5-steps", type=int, default=10,
+                    help="the cfg5_columns sub-record of a one-GPU cfg2 run: steps timed (0 = off)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--em-scale", type=int, default=8,
                     help="separate E/M streaming row: the run's comparison vectors tiled this many times (0 = off)")
@@ -189,111 +301,16 @@ def main():
         return
     local = dev
 
-    from splink_amd import _native as N
-    from splink_amd import distributed as D
-    from splink_amd.engine import Job, m_step_rows
-    from splink_amd.params import Params
-    from splink_amd.session import AmdSession
-    from splink_amd.synthetic import cfg_settings, make_records
-
     shard = (rank, world)
     if args.share:
         k, n = (int(x) for x in args.share.split("/"))
         assert world == 1 and 0 <= k < n, "--share runs one rank's share on one GPU"
         shard = (k, n)
-    t0 = time.time()
-    cols = COLS + (["address"] if args.config == 5 else [])
-    if args.config == 4:
-        # the job's size does not grow with N: its ordinal space is split over the ranks (strong scaling)
-        from splink_amd.synthetic import make_records_parallel
-        n_records = 20_000_000
-        df = make_records_parallel(n_records, 16, 16, surname_vocab=300_000)[["unique_id"] + cols]
-    else:
-        n_records = int(round(args.records * math.sqrt(world)))
-        # Arrow-backed string columns: the columnar form a Spark / Arrow source hands over (values identical
-        # to the object-column records; spk_raw_utf8 takes their buffers without a per-row pass)
-        df = make_records(n_records, surname_vocab=15000, with_address=args.config == 5, arrow=True)[["unique_id"] + cols]
-    log(f"[rank {rank}] generated {n_records} records in {time.time() - t0:.1f}s")
-
-    settings = cfg_settings(args.config, max_iterations=10)
-    params = Params(settings, AmdSession(local))
-    st = params.settings
-
-    job = Job("dedupe_only", [df], "unique_id", local, shard=shard)
-    job.ctx.enable_timing(True)
-    t0 = time.time()
-    job.block(st["blocking_rules"])
-    block_s = time.time() - t0
-    block_kernel_ms = job.ctx.kernel_ms()["block"]
-    log(f"[rank {rank}] blocking: {job.n_pairs} local pairs of {job.n_candidates} candidates "
-        f"({block_s:.2f}s wall incl. host key prep, {block_kernel_ms:.1f} ms device)")
-    t0 = time.time()
-    job.gammas(st)  # uploads columns (device decode through the clustering permutation), first launch
-    first_gammas_s = time.time() - t0
-    names, nlev = job.code_meta
-
-    host = {"gammas_call": [], "em_wait": [], "m_step_host": [], "em_start": []}
-    dev = {"gamma": [], "em_hist": [], "em_final": []}
-    pending = [False]
-
-    def finish_m_step():
-        """Statistics of the enqueued E+M iteration, then the host M-step (Params update)."""
-        t0 = time.perf_counter()
-        stats = job.em_wait()
-        t1 = time.perf_counter()
-        lam, rows = m_step_rows(stats, names, nlev)
-        params._update_params(lam, rows)
-        t2 = time.perf_counter()
-        host["em_wait"].append((t1 - t0) * 1e3)
-        host["m_step_host"].append((t2 - t1) * 1e3)
-        pending[0] = False
-        ms = job.ctx.kernel_ms_done()  # the newest completed launches (the next comparison pass may be running)
-        for k in dev:
-            dev[k].append(ms[k])
-
-    def step():
-        """Comparison pass i, then E+M iteration i.  Software-pipelined: pass i is queued before the host
-        finishes the M-step of iteration i - 1 (pass i does not depend on it; E+M i does), so the device
-        never waits for the host.  The order of device work and its results are those of the plain loop."""
-        t0 = time.perf_counter()
-        job.gammas(st)
-        t1 = time.perf_counter()
-        if pending[0]:
-            finish_m_step()
-        t2 = time.perf_counter()
-        job.em_start(params.params["λ"], params._level_probabilities())
-        pending[0] = True
-        t3 = time.perf_counter()
-        host["gammas_call"].append((t1 - t0) * 1e3)
-        host["em_start"].append((t3 - t2) * 1e3)
-
-    def barrier():
-        torch.cuda.synchronize()
-        D.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    if pending[0]:
-        finish_m_step()
-    for v in list(host.values()) + list(dev.values()):
-        v.clear()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    finish_m_step()  # the last iteration's M-step is part of the timed work
-    barrier()
-    elapsed = time.perf_counter() - t0
-    # per-launch device times of the timed steps (HIP events on the context stream, read as each
-    # launch completed)
-    gamma_ms = dev["gamma"]
-    hist_ms = dev["em_hist"]
-    fin_ms = [max(x, 0.0) for x in dev["em_final"]]  # one GPU: the E-step runs inside the histogram launch
-    local_pairs = job.n_pairs
-    elapsed = D.max_over_ranks(elapsed)
-    total_pairs = D.sum_over_ranks(local_pairs)
-    ms_per_step = elapsed * 1000.0 / args.steps
+    R = timed_run(args.config, args.records, shard, world, rank, local, args.steps, args.warmup)
+    job, df, params, st, cols, names, nlev = R.job, R.df, R.params, R.st, R.cols, R.names, R.nlev
+    n_records, gamma_ms, hist_ms, fin_ms, host = R.n_records, R.gamma_ms, R.hist_ms, R.fin_ms, R.host
+    local_pairs, total_pairs, ms_per_step = R.local_pairs, R.total_pairs, R.ms_per_step
+    block_s, block_kernel_ms, first_gammas_s = R.block_s, R.block_kernel_ms, R.first_gammas_s
 
     # ---- full job (blocking excluded from the metric): score pass for the record
     t0 = time.perf_counter()
@@ -357,24 +374,7 @@ def main():
         roofline["traffic_source"] = em_roofline["traffic_source"] = (
             os.path.relpath(TRAFFIC_FILE, ROOT) + ": rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command")
 
-    # The γ kernels are issue-bound, not HBM-bound: their VALU / SALU issue against the SIMD peaks and
-    # the share of wave time stalled, from the committed counter passes of this command
-    issue = None
-    pmc_file = PMC_FILE_CFG5 if args.config == 5 else PMC_FILE
-    if os.path.exists(pmc_file):
-        with open(pmc_file) as f:
-            pmc = json.load(f)
-        issue = {"source": os.path.relpath(pmc_file, ROOT) + ": rocprofv3 --pmc SQ_* passes of this config's "
-                 "comparison pass", "peak_note": "valu_util = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles "
-                 "at 2.4 GHz); kernels that ran under 10 us per launch (near-empty lists) are left out"}
-        for name, key in (("filter", "k_filter"), ("levenshtein_exact", "k_gamma_exact_simple<1,"),
-                          ("levenshtein_refill", "k_lev_refill"), ("levenshtein_slow", "k_gamma_slow_lev"),
-                          ("bag_compaction", "k_compact_lev"), ("jw_exact", "k_gamma_exact_simple<2,")):
-            for k, v in pmc.items():
-                if key in k and float(v.get("_dur_ns", 0.0)) >= 10000.0:
-                    issue[name] = {x: round(float(v[x]), 4) for x in ("valu_util", "salu_util", "wait_frac", "l2_hit")
-                                   if x in v}
-                    break
+    issue = issue_counters(args.config)
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -427,11 +427,55 @@ def main():
         "string_rates": rates,
         "em_at_scale": em_scale,
     }
+    if world == 1 and args.config == 2 and args.cfg5_steps > 0 and not args.share:
+        # cfg5's columns in the same run, after the headline (never the headline): the free-text address
+        # column's Levenshtein passes are the other workload the comparison kernels are tuned on
+        del job, R
+        out["cfg5_columns"] = cfg5_record(args, local)
     emit(out)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
+
+
+def issue_counters(config):
+    """The γ kernels are issue-bound, not HBM-bound: their VALU / SALU issue against the SIMD peaks and the
+    share of wave time stalled, from the committed counter passes of this config's bench command."""
+    pmc_file = PMC_FILE_CFG5 if config == 5 else PMC_FILE
+    if not os.path.exists(pmc_file):
+        return None
+    with open(pmc_file) as f:
+        pmc = json.load(f)
+    issue = {"source": os.path.relpath(pmc_file, ROOT) + ": rocprofv3 --pmc SQ_* passes of this config's "
+             "comparison pass", "peak_note": "valu_util = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles "
+             "at 2.4 GHz); kernels that ran under 10 us per launch (near-empty lists) are left out"}
+    for name, key in (("filter", "k_filter"), ("levenshtein_exact", "k_gamma_exact_simple<1,"),
+                      ("levenshtein_refill", "k_lev_refill"), ("levenshtein_slow", "k_gamma_slow_lev"),
+                      ("bag_compaction", "k_compact_lev"), ("jw_exact", "k_gamma_exact_simple<2,")):
+        for k, v in pmc.items():
+            if key in k and float(v.get("_dur_ns", 0.0)) >= 10000.0:
+                issue[name] = {x: round(float(v[x]), 4) for x in ("valu_util", "salu_util", "wait_frac", "l2_hit",
+                                                                   "_dur_ns") if x in v}
+                break
+    return issue
+
+
+def cfg5_record(args, local):
+    """`bench.py --config 5` at one GPU, timed in the default run after the cfg2 headline: step time, the γ
+    pass and its per-column exact passes, E+M, and the committed counters of its Levenshtein kernels."""
+    R = timed_run(5, args.records, (0, 1), 1, 0, local, args.cfg5_steps, min(args.warmup, 3))
+    job, names = R.job, R.names
+    g_ms = float(np.mean(R.gamma_ms))
+    em_ms = float(np.mean(R.hist_ms)) + float(np.mean(R.fin_ms))
+    xms = job.ctx.gammas_exact_ms(len(names))
+    return {"workload": WORKLOADS[5], "records": R.n_records, "candidate_pairs": R.total_pairs,
+            "steps": args.cfg5_steps, "warmup": min(args.warmup, 3), "ms_per_step": R.ms_per_step,
+            "value": R.total_pairs / (R.ms_per_step / 1e3), "unit": "pairs/s",
+            "breakdown_ms": {"gamma": g_ms, "em": em_ms,
+                             "exact_pass_per_column": {n: float(x) for n, x in zip(names, xms) if x > 0}},
+            "exact_cells_per_column": dict(zip(names, [int(x) for x in job.ctx.gammas_exact_counts(len(names))])),
+            "issue_gamma_kernels": issue_counters(5)}
 
 
 def em_streaming(job, names, nlev, params, reps, iters=10):

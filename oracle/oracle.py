@@ -582,13 +582,37 @@ def tf_adjust_codes(codes_l, codes_r, mp, lam):
     bayes(mp, adj).  Σmp per value is np.bincount's running sum in pair order, as the scalar loop."""
     codes_l = np.asarray(codes_l, dtype=np.int64)
     codes_r = np.asarray(codes_r, dtype=np.int64)
+    n_v = int(max(codes_l.max(initial=-1), codes_r.max(initial=-1))) + 1
+    s, c = tf_value_sums(codes_l, codes_r, mp, n_v)
+    return tf_adjust_with_sums(codes_l, codes_r, mp, lam, s, c)
+
+
+def tf_value_sums(codes_l, codes_r, mp, n_values, sums=None, counts=None):
+    """Per value v: Σ mp and the count over pairs with code_l = code_r = v and a non-NULL mp
+    (term_frequencies.py:49-65).  Added to `sums` / `counts` when given, so the pairs of a large job can be
+    taken chunk by chunk."""
+    codes_l = np.asarray(codes_l, dtype=np.int64)
+    codes_r = np.asarray(codes_r, dtype=np.int64)
+    mp = np.asarray(mp, dtype=np.float64)
+    good = (codes_l >= 0) & (codes_l == codes_r) & ~np.isnan(mp)
+    s = np.bincount(codes_l[good], weights=mp[good], minlength=n_values)
+    c = np.bincount(codes_l[good], minlength=n_values)
+    if sums is None:
+        return s, c
+    sums += s
+    counts += c
+    return sums, counts
+
+
+def tf_adjust_with_sums(codes_l, codes_r, mp, lam, s, c):
+    """tf_adjust_codes' adjustment of the pairs given, from per-value sums and counts over all the job's
+    pairs (tf_value_sums; term_frequencies.py:68-117)."""
+    codes_l = np.asarray(codes_l, dtype=np.int64)
+    codes_r = np.asarray(codes_r, dtype=np.int64)
     mp = np.asarray(mp, dtype=np.float64)
     one_minus = float(repr(1 - lam))
     ok = (codes_l >= 0) & (codes_l == codes_r)
-    good = ok & ~np.isnan(mp)
-    n_v = int(max(codes_l.max(initial=-1), codes_r.max(initial=-1))) + 1
-    s = np.bincount(codes_l[good], weights=mp[good], minlength=n_v)
-    c = np.bincount(codes_l[good], minlength=n_v)
+    n_v = len(s)
     with np.errstate(invalid="ignore", divide="ignore"):
         adj_lambda = np.where(c > 0, s / np.maximum(c, 1), np.nan)
         tnum = adj_lambda * one_minus

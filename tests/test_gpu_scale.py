@@ -122,6 +122,21 @@ def column_in_row_order(job, side, col):
     return v if perm is None else v.take(np.asarray(perm)).reset_index(drop=True)
 
 
+def oracle_sample(job, specs, cols, sl, sr):
+    """oracle.template_gammas of the pairs (sl[i], sr[i]) (device row order), from only the rows they use."""
+    if job.link_type == "link_only":  # rows index the two tables
+        ul, il = np.unique(sl, return_inverse=True)
+        ur, ir = np.unique(sr, return_inverse=True)
+        tl, tr = rows_of(job, 0, ul), rows_of(job, job.r_side(), ur)
+        ocl = [orc.StrCol(tl[c].tolist()) for c in cols]
+        ocr = [orc.StrCol(tr[c].tolist()) for c in cols]
+        return orc.template_gammas(specs, ocl, ocr, il.astype(np.int32), ir.astype(np.int32))
+    rows, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
+    sub = rows_of(job, 0, rows)
+    ocols = [orc.StrCol(sub[c].tolist()) for c in cols]
+    return orc.template_gammas(specs, ocols, ocols, inv[:len(sl)].astype(np.int32), inv[len(sl):].astype(np.int32))
+
+
 def check_shard(job, params, cols, iters, sample=2_000_000):
     """Parity of one GPU's share of a big job: every comparison vector of a strided sample of `sample`
     pairs bit-exact against oracle.template_gammas, `iters` EM iterations of λ / m / u and every pair's
@@ -131,21 +146,7 @@ def check_shard(job, params, cols, iters, sample=2_000_000):
     l, r = job.pair_rows()
     step = max(1, job.n_pairs // sample)
     idx = np.arange(0, job.n_pairs, step)
-    sl, sr = l[idx], r[idx]
-    if job.link_type == "link_only":  # rows index the two tables
-        ul, il = np.unique(sl, return_inverse=True)
-        ur, ir = np.unique(sr, return_inverse=True)
-        tl, tr = rows_of(job, 0, ul), rows_of(job, job.r_side(), ur)
-        ocl = [orc.StrCol(tl[c].tolist()) for c in cols]
-        ocr = [orc.StrCol(tr[c].tolist()) for c in cols]
-        ref = orc.template_gammas(specs, ocl, ocr, il.astype(np.int32), ir.astype(np.int32))
-        del ocl, ocr, tl, tr
-    else:
-        rows, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
-        sub = rows_of(job, 0, rows)
-        ocols = [orc.StrCol(sub[c].tolist()) for c in cols]
-        ref = orc.template_gammas(specs, ocols, ocols, inv[:len(sl)].astype(np.int32), inv[len(sl):].astype(np.int32))
-        del ocols, sub
+    ref = oracle_sample(job, specs, cols, l[idx], r[idx])
     gam = job.gammas_host()
     bad = np.nonzero((gam[idx] != ref).any(axis=1))[0]
     assert len(bad) == 0, (len(bad), idx[bad[:5]])
@@ -195,11 +196,7 @@ def check_shard_streamed(job, params, cols, iters, sample=2_000_000, chunk=1 << 
     assert int(hist.sum()) == P
     sl, sr, sg = np.concatenate(sl), np.concatenate(sr), np.concatenate(sg)
     assert len(sl) == (P + step - 1) // step
-    rows, inv = np.unique(np.concatenate([sl, sr]), return_inverse=True)
-    sub = rows_of(job, 0, rows)
-    ocols = [orc.StrCol(sub[c].tolist()) for c in cols]
-    ref = orc.template_gammas(specs, ocols, ocols, inv[:len(sl)].astype(np.int32), inv[len(sl):].astype(np.int32))
-    del ocols, sub
+    ref = oracle_sample(job, specs, cols, sl, sr)
     bad = np.nonzero((sg != ref).any(axis=1))[0]
     assert len(bad) == 0, (len(bad), bad[:5] * step)
     lam0, lp0 = params.params["λ"], params._level_probabilities()
@@ -283,19 +280,20 @@ def test_cfg5_shard_full_size(amd, heartbeat):
     check_shard(job, params, cols, 10)
 
 
-def test_cfg3_shard_full_size(amd, heartbeat):
-    """BASELINE configs[2] at one GPU's share: link_only between two 10M-record tables (halves of one 20M
-    population, so duplicates straddle them), rules surname | dob | email (~3.1e9 candidates, past 2^31),
-    shard 0 of 8 (~386M pairs), tf on surname.  Comparison-vector sample, EM and match_probability as
-    check_shard; then every pair's tf_adjusted_match_prob against oracle.tf_adjust_codes over
-    host-factorised surnames at 1e-9 (blocking.py:95-160, term_frequencies.py:49-168)."""
+@pytest.fixture(scope="module")
+def cfg3_inputs():
+    from splink_amd.synthetic import make_records_parallel
+    df = make_records_parallel(20_000_000, 16, 16, surname_vocab=300_000)[["unique_id"] + COLS]
+    return [df.iloc[:10_000_000].reset_index(drop=True), df.iloc[10_000_000:].reset_index(drop=True)]
+
+
+def cfg3_job(amd, inputs, shard):
+    """BASELINE configs[2]: link_only between two 10M-record tables (halves of one 20M population, so
+    duplicates straddle them), rules surname | dob | email (~3.1e9 candidates, past 2^31), tf on surname;
+    `shard` of its pair ordinals."""
     from splink_amd.engine import Job
     from splink_amd.params import Params
-    from splink_amd.synthetic import cfg_settings, make_records_parallel
-    from splink_amd.term_frequencies import _bayes_pair
-    df = make_records_parallel(20_000_000, 16, 16, surname_vocab=300_000)[["unique_id"] + COLS]
-    inputs = [df.iloc[:10_000_000].reset_index(drop=True), df.iloc[10_000_000:].reset_index(drop=True)]
-    del df
+    from splink_amd.synthetic import cfg_settings
     settings = cfg_settings(4, max_iterations=10)
     settings["link_type"] = "link_only"
     settings["blocking_rules"] = ["l.surname = r.surname", "l.dob = r.dob", "l.email = r.email"]
@@ -304,21 +302,77 @@ def test_cfg3_shard_full_size(amd, heartbeat):
             c["term_frequency_adjustments"] = True
     params = Params(settings, amd)
     st = params.settings
-    job = Job("link_only", inputs, "unique_id", 0, shard=(0, 8))
-    del inputs
+    job = Job("link_only", inputs, "unique_id", 0, shard=shard)
     job.block(st["blocking_rules"])
-    assert job.n_candidates > 2 ** 31 and job.n_pairs > 300_000_000
+    assert job.n_candidates > 2 ** 31
     job.gammas(st)
-    mp, l, r = check_shard(job, params, COLS, 10)
-    # tf on surname with the device dictionary ids (the product path: term_frequencies.py's GPU stage)
-    col = job._col_index[("surname", "str")]
-    n_values = job.ctx.tf_column_values(col)
-    sums, counts = job.ctx.tf_accumulate_column(col, n_values)
-    with np.errstate(invalid="ignore", divide="ignore"):
-        adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
-    table = _bayes_pair(adj_lambda, float(1 - params.params["λ"]))
-    tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
+    return job, params
+
+
+def surname_codes(job):
+    """Host value codes of surname on both sides (device row order, -1 = NULL), one code space."""
     vl, vr = column_in_row_order(job, 0, "surname"), column_in_row_order(job, job.r_side(), "surname")
     codes, _ = pd.factorize(pd.concat([vl, vr], ignore_index=True), use_na_sentinel=True)
-    want, _ = orc.tf_adjust_codes(codes[:len(vl)][l], codes[len(vl):][r], mp, params.params["λ"])
+    return codes[:len(vl)], codes[len(vl):], int(codes.max()) + 1
+
+
+def device_tf_table(job, params):
+    """The product path's tf table on surname (term_frequencies.py's GPU stage): per-value Σmp and counts
+    over the device dictionary ids, then bayes(adj_lambda, 1 - λ)."""
+    from splink_amd.term_frequencies import _bayes_pair
+    col = job._col_index[("surname", "str")]
+    sums, counts = job.ctx.tf_accumulate_column(col, job.ctx.tf_column_values(col))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
+    return col, _bayes_pair(adj_lambda, float(1 - params.params["λ"]))
+
+
+def test_cfg3_shard_full_size(amd, heartbeat, cfg3_inputs):
+    """BASELINE configs[2] at one GPU's share of 8 (~386M pairs).  Comparison-vector sample, EM and
+    match_probability as check_shard; then every pair's tf_adjusted_match_prob against oracle.tf_adjust_codes
+    over host-factorised surnames at 1e-9 (blocking.py:95-160, term_frequencies.py:49-168)."""
+    job, params = cfg3_job(amd, cfg3_inputs, (0, 8))
+    assert job.n_pairs > 300_000_000
+    mp, l, r = check_shard(job, params, COLS, 10)
+    col, table = device_tf_table(job, params)
+    tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
+    cl, cr, _ = surname_codes(job)
+    want, _ = orc.tf_adjust_codes(cl[l], cr[r], mp, params.params["λ"])
     assert np.allclose(tf_mp, want, rtol=1e-9, atol=0, equal_nan=True)
+
+
+@pytest.mark.timeout(900)
+def test_cfg3_one_gpu_full_size(amd, heartbeat, cfg3_inputs):
+    """BASELINE configs[2] whole on ONE GPU: ~3.09e9 link_only pairs in one context (past 2^31, so the
+    comparison pass runs as ordinal windows), tf on surname.  check_shard_streamed (a 2M-pair strided sample
+    of comparison vectors bit-exact, 10 EM iterations on the host-counted pattern histogram of every pair,
+    every match_probability at 1e-9); then the per-value (Σmp, count) of equal-surname pairs accumulated on
+    the host chunk by chunk over all pairs, and tf_adjusted_match_prob over 16 ranges spread across the
+    ordinals (window edges included) at 1e-9 against oracle.tf_adjust_with_sums (term_frequencies.py:49-65,
+    :122-168 have no size limit)."""
+    job, params = cfg3_job(amd, cfg3_inputs, (0, 1))
+    P = job.n_pairs
+    assert P > 2 ** 31 and job.ctx.gammas_windows() >= 2
+    check_shard_streamed(job, params, COLS, 10)
+    cl, cr, n_v = surname_codes(job)
+    lam = params.params["λ"]
+    m_t, u_t = job.flat_tables(params._level_probabilities())
+    sums, counts = np.zeros(n_v), np.zeros(n_v, dtype=np.int64)
+    chunk = 1 << 27
+    for c0 in range(0, P, chunk):  # the device's mp buffer is filled range by range, as on the host
+        n = min(chunk, P - c0)
+        mp = job.ctx.score(float(lam), float(1 - lam), m_t, u_t, c0, n)
+        l, r = job.ctx.pairs_copy(c0, n)
+        orc.tf_value_sums(cl[l], cr[r], mp, n_v, sums, counts)
+        del mp, l, r
+    col, table = device_tf_table(job, params)
+    W = -(-P // job.ctx.gammas_windows())
+    starts = sorted(set([int(x) for x in np.linspace(0, P - (1 << 20), 14)] + [max(0, W - (1 << 19))] +
+                        [max(0, min(P - (1 << 20), 2 * W - (1 << 19)))]))
+    for s0 in starts:
+        n = min(1 << 20, P - s0)
+        tf_mp, _ = job.ctx.tf_apply_columns([col], [table], s0, n, want_adj=False)
+        mp = job.ctx.score(float(lam), float(1 - lam), m_t, u_t, s0, n)
+        l, r = job.ctx.pairs_copy(s0, n)
+        want, _ = orc.tf_adjust_with_sums(cl[l], cr[r], mp, lam, sums, counts)
+        assert np.allclose(tf_mp, want, rtol=1e-9, atol=0, equal_nan=True), s0
