@@ -28,7 +28,6 @@ int ensure_desc(spk_ctx *ctx, Table &t) {
             d.planes = c->planes.p;
             d.planes_hi = c->planes_hi.n ? c->planes_hi.p : nullptr;
             d.bag = c->bag.n ? c->bag.p : nullptr;
-            d.bigram = c->bigram.n ? c->bigram.p : nullptr;
         } else if (c && c->kind == COL_NUM) {
             d.val = c->val.p;
             d.valid = c->valid.p;
@@ -279,65 +278,9 @@ int build_bag_rows(spk_ctx *ctx, int64_t n, Column *c) {
     return SPK_OK;
 }
 
-// Bigram-count rows of a short-string column that a Levenshtein comparison reads (rows of at most 64 units: the
-// exact pass's own; free-text columns take character-bag rows).  Per row 32 bytes: 120 buckets of 2-bit
-// saturating counts of the row's bigrams (consecutive code-point pairs, hashed), buckets 16 w .. 16 w + 15 in word
-// w (words 0-6, and the low half of word 7 for buckets 112-119), then the row's length in byte 31 (255: no row --
-// NULL, past 254 units, or a surrogate pair, whose units are not its code points).  The q-gram lemma (Ukkonen
-// 1992, q = 2): every edit destroys at most two of a string's bigram occurrences, so two strings within edit
-// distance k share at least max(la, lb) - 1 - 2k bigrams (multiset intersection), and Σ min over the buckets
-// bounds that intersection from above (hashing only merges bigrams).  k_compact_lev<true> decides the listed cells
-// whose bound falls short for k = cut - 1, i.e. whose distance is at least the cut: in cfg2's emails most listed
-// cells are unrelated addresses of one surname or date of birth (distance ~0.8 x length against a cut of ~0.3 x
-// length; host simulation: 90 % of them decided, the character bag decided 15 %).  Built on first use, dropped when
-// the column is decoded again.  One thread per row, its counts in LDS (dynamic bucket index).
-constexpr int BIGRAM_BUCKETS = 120;
-__device__ __host__ inline uint32_t bigram_bucket(uint32_t c1, uint32_t c2) {
-    uint32_t x = (c1 * 0x9E3779B1u) ^ (c2 * 0x85EBCA77u);
-    x = (x ^ (x >> 15)) * 0x2C1B3C6Du;
-    return (x >> 16) % (uint32_t)BIGRAM_BUCKETS;
-}
-__global__ __launch_bounds__(BAG_THREADS) void k_bigram_rows(int64_t n, const RecMeta *__restrict__ meta,
-                                                             const uint16_t *__restrict__ units, uint4 *__restrict__ out) {
-    __shared__ uint32_t s_w[BAG_THREADS][9];  // (stride 9: rows of consecutive threads in different banks)
-    const int64_t row = (int64_t)blockIdx.x * BAG_THREADS + threadIdx.x;
-    if (row >= n) return;
-    uint32_t *w = s_w[threadIdx.x];
-    for (int q = 0; q < 8; ++q) w[q] = 0;
-    const RecMeta m = meta[row];
-    const int len = m.len16;
-    if (len >= 0 && len <= 254 && meta_cplen(m) == len) {
-        const uint16_t *u = units + meta_off(m);
-        uint32_t prev = len ? u[0] : 0u;
-        for (int i = 1; i < len; ++i) {
-            const uint32_t c = u[i];
-            const uint32_t b = bigram_bucket(prev, c), sh = (b & 15u) * 2u;
-            const uint32_t x = w[b >> 4];
-            if (((x >> sh) & 3u) < 3u) w[b >> 4] = x + (1u << sh);
-            prev = c;
-        }
-        w[7] |= (uint32_t)len << 24;
-    } else {
-        w[7] = 0xFF000000u;
-    }
-    out[2 * row] = make_uint4(w[0], w[1], w[2], w[3]);
-    out[2 * row + 1] = make_uint4(w[4], w[5], w[6], w[7]);
-}
-
-int build_bigram_rows(spk_ctx *ctx, int64_t n, Column *c) {
-    SPK_TRY(c->bigram.alloc((size_t)(2 * n + 2)));
-    if (n > 0) {
-        k_bigram_rows<<<(unsigned)((n + BAG_THREADS - 1) / BAG_THREADS), BAG_THREADS, 0, ctx->stream>>>(
-            n, c->meta.p, c->units.p, c->bigram.p);
-        SPK_HIP(hipGetLastError());
-    }
-    return SPK_OK;
-}
-
 int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c) {
     c->unit_bits = false;
     c->bag.release();  // the rows changed: built again on first use
-    c->bigram.release();
     if (n <= 0) return SPK_OK;
     DevBuf<unsigned int> d;
     SPK_TRY(d.alloc(2));

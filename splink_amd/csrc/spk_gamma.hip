@@ -591,37 +591,14 @@ __device__ inline int bag_inter_ub(const uint4 &a0, const uint4 &a1, const uint4
     return (int)((sa + sb - sad) / 2u) + (oa < ob ? oa : ob);
 }
 
-// Upper bound on the bigram multiset intersection of two rows from their bigram-count rows (k_bigram_rows), or -1
-// when a bucket is saturated on both sides.  Per 2-bit field, min(a, b) = 2 m1 + m0 with m1 = a1 b1 and m0 = a0 b0 |
-// a1 ~b1 b0 | ~a1 b1 a0 (the high / low bits of the fields), summed by popcounts.
-__device__ inline int bigram_inter_ub(const uint4 &a0, const uint4 &a1, const uint4 &b0, const uint4 &b1) {
-    const uint32_t wa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w & 0xFFFFu};
-    const uint32_t wb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w & 0xFFFFu};
-    constexpr uint32_t L = 0x55555555u;
-    int sum = 0;
-    uint32_t sat = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const uint32_t ah = (wa[q] >> 1) & L, al = wa[q] & L, bh = (wb[q] >> 1) & L, bl = wb[q] & L;
-        const uint32_t m1 = ah & bh;
-        const uint32_t m0 = (al & bl) | (ah & ~bh & bl) | (~ah & bh & al);
-        sum += 2 * __popc(m1) + __popc(m0);
-        sat |= m1 & al & bl;
-    }
-    return sat ? -1 : sum;
-}
-
 // k_compact for a Levenshtein column: a listed cell whose rows' bag distance already exceeds the cut is decided
 // here (its level is lev_cell's for any distance past the cut), one with a row past 64 units goes straight to
 // the slow list; the others are packed to the front of the
 // region's slice of the list in order, and the slice's tail is -1, which the exact passes skip (whole waves of
 // it, mostly).  0.206 ms per cfg5 call; four cells per thread per round (their loads in flight together) took
 // 0.260, and unordered packing through one LDS counter per workgroup (no barriers) 0.210.
-// BIGRAM: a short-string column (rows of at most 64 units) with bigram-count rows instead: a cell whose bigram
-// bound shows a distance of at least the cut is decided here (k_bigram_rows: the q-gram lemma), no slow routing.
 constexpr int CL_THREADS = 256;
 constexpr int CL_SLOW = 1024;  // LDS buffer of slow-list cells per workgroup
-template <bool BIGRAM>
 __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restrict__ xpref,
                                                             int32_t *__restrict__ xlist, const int64_t *__restrict__ xinfo) {
     if (xinfo[2 * A.K]) return;  // overflow: the host re-runs the phase
@@ -641,8 +618,7 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
     const int32_t *src = region_list(A, k, R);
     const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
     int32_t *dst = xlist + xinfo[k] + pref[blockIdx.x];
-    const uint4 *bag0 = BIGRAM ? A.cols0[sc.col].bigram : A.cols0[sc.col].bag;
-    const uint4 *bag1 = BIGRAM ? A.cols1[sc.col].bigram : A.cols1[sc.col].bag;
+    const uint4 *bag0 = A.cols0[sc.col].bag, *bag1 = A.cols1[sc.col].bag;
     const uint32_t stride = (uint32_t)sc.stride;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int32_t *slow_list = A.slow + A.slow_off[k];
@@ -665,15 +641,7 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
             const int64_t x = A.pl[p], y = A.pr[p];
             const uint4 a0 = bag0[2 * x], a1 = bag0[2 * x + 1], b0 = bag1[2 * y], b1 = bag1[2 * y + 1];
             const int la = (int)(a1.w >> 24), lb = (int)(b1.w >> 24);
-            if (BIGRAM && la != 255 && lb != 255) {
-                const int cut = simple_lev_cut(sc, la, lb);
-                const int inter = bigram_inter_ub(a0, a1, b0, b1);
-                // distance <= cut - 1 would leave max(la, lb) - 1 - 2 (cut - 1) bigrams in common
-                if (cut >= 1 && cut < (1 << 29) && inter >= 0 && inter < (la > lb ? la : lb) - 1 - 2 * (cut - 1)) {
-                    code_add_atomic(A, p, (uint32_t)(lev_level_of(sc, 0, cut, la + lb) + 1) * stride);
-                    keep = false;
-                }
-            } else if (la != 255 && lb != 255) {
+            if (la != 255 && lb != 255) {
                 // a row past 64 units has no 64-bit planes: the exact pass would only pass the cell on to the
                 // 128-bit slow pass, after loading its rows -- it goes to the slow list from here
                 slow = la > 64 || lb > 64;
@@ -2176,7 +2144,7 @@ struct GammaPlan {
     GammaArgs A{};
     std::vector<SimpleCol> simple;
     std::vector<int> simple_of;
-    std::vector<char> may_exact, huge_in_slow, free_text, bag, bigram;
+    std::vector<char> may_exact, huge_in_slow, free_text, bag;
     std::vector<char> slow_skipped;  // columns whose slow-list kernels this call did not launch
     int K = 0, n_regions = 0, n_info = 0, n_cnt = 0, n_all = 0;
     int64_t g_exact = 1, max_units = 1;
@@ -2280,11 +2248,8 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         const ColSet one_k{1, {k, 0, 0, 0}};
         const bool refill = lev && (ctx->lev_kernel == 1 || (ctx->lev_kernel == 2 && G.free_text[k]));
         if (lev && G.bag[k])
-            k_compact_lev<false><<<(unsigned)G.n_regions, CL_THREADS, 0, ctx->stream>>>(A, k, si, ctx->xpref.p,
-                                                                                       ctx->xlist.p, ctx->xinfo.p);
-        else if (lev && G.bigram[k])
-            k_compact_lev<true><<<(unsigned)G.n_regions, CL_THREADS, 0, ctx->stream>>>(A, k, si, ctx->xpref.p,
-                                                                                      ctx->xlist.p, ctx->xinfo.p);
+            k_compact_lev<<<(unsigned)G.n_regions, CL_THREADS, 0, ctx->stream>>>(A, k, si, ctx->xpref.p, ctx->xlist.p,
+                                                                                ctx->xinfo.p);
         else
             k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
         if (refill) {
@@ -2535,18 +2500,16 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     // Free-text only: in cfg2's emails the bound decided 15 % of the listed cells (1.23 of 8.10 M), and the
     // compaction's gathers cost more than the scans it saved (γ pass 1.070 -> 1.168 ms; cfg5's addresses
     // 4.88 -> 3.85 ms; profiles/r5_ab_lev_bag.log).
-    // Bigram-count rows of the other Levenshtein string columns (short strings, k_bigram_rows).
     if (ctx->lev_bag) {
         bool built[2] = {false, false};
         for (const SimpleCol &sc : simple) {
-            if (sc.cls != SC_LEV || sc.kind != SK_STR) continue;
-            const bool free_text = t0.cols[sc.col]->planes_hi.n && t1.cols[sc.col]->planes_hi.n;
+            if (sc.cls != SC_LEV || sc.kind != SK_STR || !t0.cols[sc.col]->planes_hi.n || !t1.cols[sc.col]->planes_hi.n)
+                continue;
             for (int s = 0; s < 2; ++s) {
                 Table &t = s ? t1 : t0;
                 Column *c = t.cols[sc.col];
-                if (c->kind != COL_STR || t.n <= 0 || (free_text ? c->bag.n : c->bigram.n)) continue;
-                if (free_text) SPK_TRY(build_bag_rows(ctx, t.n, c));
-                else SPK_TRY(build_bigram_rows(ctx, t.n, c));
+                if (c->kind != COL_STR || c->bag.n || t.n <= 0) continue;
+                SPK_TRY(build_bag_rows(ctx, t.n, c));
                 t.desc_dirty = true;
                 built[s] = true;
             }
@@ -2705,13 +2668,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         if (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids)) G.may_exact[sc.k] = 0;
     G.free_text.assign(K, 0);  // simple columns with rows past 64 UTF-8 bytes on both sides (planes_hi)
     G.bag.assign(K, 0);        // free-text Levenshtein columns with character-bag rows (k_compact_lev)
-    G.bigram.assign(K, 0);     // short-string Levenshtein columns with bigram-count rows (k_compact_lev<true>)
     for (const SimpleCol &sc : simple) {
         const Column *a = t0.cols[sc.col], *b = t1.cols[sc.col];
         G.free_text[sc.k] = (a && b && a->planes_hi.n && b->planes_hi.n) ? 1 : 0;
         G.bag[sc.k] = (G.free_text[sc.k] && sc.cls == SC_LEV && a->bag.n && b->bag.n && ctx->lev_bag) ? 1 : 0;
-        G.bigram[sc.k] = (!G.free_text[sc.k] && sc.cls == SC_LEV && sc.kind == SK_STR && a->bigram.n && b->bigram.n &&
-                          ctx->lev_bag) ? 1 : 0;
     }
     G.huge_in_slow.assign(K, 0);  // column k's huge list: slow-list region (Levenshtein) or exact-list region
     for (int k = 0; k < K; ++k)

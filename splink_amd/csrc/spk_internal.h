@@ -101,7 +101,6 @@ struct ColDesc {
     const uint64_t *planes;  // COL_STR, [n][N_PLANES]
     const uint64_t *planes_hi;  // COL_STR, [n][N_PLANES] units 64..127 (CPF_PLANES2 rows), or null
     const uint4 *bag;        // COL_STR: [n][2] character-bag rows (k_bag_rows), or null (not built)
-    const uint4 *bigram;     // COL_STR: [n][2] bigram-count rows (k_bigram_rows), or null (not built)
     const double *val;       // COL_NUM
     const uint8_t *valid;   // COL_NUM
 };
@@ -143,8 +142,6 @@ struct Column {
     DevBuf<uint64_t> planes_hi;  // allocated only when some row has more than 64 UTF-8 bytes
     DevBuf<uint4> bag;           // 32-byte character-bag row per row (k_bag_rows; built when a Levenshtein
                                  // comparison reads the column)
-    DevBuf<uint4> bigram;        // 32-byte bigram-count row per row (k_bigram_rows; built when a Levenshtein
-                                 // comparison of short strings reads the column)
     DevBuf<double> val;
     DevBuf<uint8_t> valid;
     bool has_ids = false;  // COL_STR: RecMeta.key is a dictionary id
@@ -398,7 +395,6 @@ int em_requeue(spk_ctx *ctx);
 int new_column(spk_ctx *ctx, int side, int col, Column **out);
 int launch_unit_bits(spk_ctx *ctx, int64_t n, Column *c);
 int build_bag_rows(spk_ctx *ctx, int64_t n, Column *c);
-int build_bigram_rows(spk_ctx *ctx, int64_t n, Column *c);
 int launch_utf8_decode(spk_ctx *ctx, int64_t n, const int64_t *off8, const int64_t *src_off, const int32_t *perm,
                        const uint8_t *bytes, const uint8_t *valid, Column *c, bool long_rows, const int64_t *ids);
 }
