@@ -605,6 +605,9 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
     __shared__ SimpleCol s_sc;
     __shared__ int s_kept[CL_THREADS / 64];
     __shared__ int32_t s_slow[CL_SLOW];
+    __shared__ uint8_t s_skey[CL_SLOW];     // the buffered slow cells' shorter row length (sort key)
+    __shared__ uint16_t s_srank[CL_SLOW];   // rank of each among the cells of its key
+    __shared__ unsigned int s_sbin[3 * 64];  // counting-sort bins (keys 0 .. 128)
     __shared__ int s_ns;
     __shared__ unsigned int s_sbase;
     if (threadIdx.x == 0) {
@@ -622,11 +625,33 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
     const uint32_t stride = (uint32_t)sc.stride;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int32_t *slow_list = A.slow + A.slow_off[k];
-    auto flush_slow = [&]() {  // the buffered slow cells to the slow list: one device atomic
+    // The buffered slow cells to the slow list (one device atomic), in order of their shorter row's length: the
+    // 128-bit pass runs a wave as long as its slowest lane, and cells of similar lengths scan similarly long
+    // (host simulation over cfg5's bag-filtered slow cells: lane utilisation 0.53 -> 0.60 sorted per 1,024 cells).
+    // A counting sort through LDS: one LDS atomic per cell, a 192-bin scan in wave 0, one scatter.
+    auto flush_slow = [&]() {
         const int c = s_ns;
         if (threadIdx.x == 0) s_sbase = atomicAdd(A.slow_count + k, (unsigned int)c);
+        if (threadIdx.x < 3 * 64) s_sbin[threadIdx.x] = 0;
         __syncthreads();
-        for (int j = threadIdx.x; j < c; j += CL_THREADS) slow_list[s_sbase + j] = s_slow[j];
+        for (int j = threadIdx.x; j < c; j += CL_THREADS) s_srank[j] = (uint16_t)atomicAdd(&s_sbin[s_skey[j]], 1u);
+        __syncthreads();
+        if (threadIdx.x < 64) {  // wave 0: exclusive scan, three bins per lane
+            const int t = threadIdx.x;
+            const unsigned int a = s_sbin[3 * t], b = s_sbin[3 * t + 1], d = s_sbin[3 * t + 2];
+            unsigned int v = a + b + d;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned int u = __shfl_up(v, off, 64);
+                if (t >= off) v += u;
+            }
+            const unsigned int ex = v - a - b - d;
+            s_sbin[3 * t] = ex;
+            s_sbin[3 * t + 1] = ex + a;
+            s_sbin[3 * t + 2] = ex + a + b;
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < c; j += CL_THREADS) slow_list[s_sbase + s_sbin[s_skey[j]] + s_srank[j]] = s_slow[j];
         __syncthreads();
         if (threadIdx.x == 0) s_ns = 0;
     };
@@ -635,6 +660,7 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
         const int64_t i = i0 + threadIdx.x;
         bool keep = false, slow = false;
         int32_t p = 0;
+        int skey = 0;
         if (i < n) {
             p = src[i];
             keep = true;
@@ -645,6 +671,7 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
                 // a row past 64 units has no 64-bit planes: the exact pass would only pass the cell on to the
                 // 128-bit slow pass, after loading its rows -- it goes to the slow list from here
                 slow = la > 64 || lb > 64;
+                skey = la < lb ? la : lb;  // <= 128: rows with bag rows have at most 128 units
                 int inter = bag_inter_ub(a0, a1, b0, b1);
                 if (inter >= 0) {
                     const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
@@ -663,7 +690,11 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
             int sb = 0;
             if (lane == 0) sb = atomicAdd(&s_ns, __popcll(ms));
             sb = __shfl(sb, 0);
-            if (keep && slow) s_slow[sb + __popcll(ms & ((1ull << lane) - 1ull))] = p;
+            if (keep && slow) {
+                const int q = sb + __popcll(ms & ((1ull << lane) - 1ull));
+                s_slow[q] = p;
+                s_skey[q] = (uint8_t)skey;
+            }
             keep = keep && !slow;
         }
         const unsigned long long m = __ballot(keep);
