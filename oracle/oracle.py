@@ -20,6 +20,7 @@ tests/test_oracle_golden.py).
 from __future__ import annotations
 
 import ctypes
+import datetime as _dt
 import os
 import re
 import sqlite3
@@ -417,6 +418,37 @@ _CASTS = {"int": lambda v: _spark_to_integral(v, 32), "integer": lambda v: _spar
           "double": _spark_to_double, "string": _s}
 
 
+def spark_literals(expr):
+    """Single-quoted string literals re-quoted for sqlite with the value Spark's parser reads (backslash escapes:
+    ParserUtils.unescapeSQLString -- \\0 \\b \\n \\r \\t \\Z \\\\ \\' \\", \\% / \\_ keep the backslash, any other escaped
+    character is itself, \\uXXXX, octal \\[01][0-7][0-7]); '' stays one quote."""
+    esc = {"0": "\0", "b": "\b", "n": "\n", "r": "\r", "t": "\t", "Z": "\x1a", "%": "\\%", "_": "\\_"}
+
+    def value(body):
+        out, i = "", 0
+        while i < len(body):
+            c = body[i]
+            if c == "'":  # '' (the tokenizer only lets doubled quotes through)
+                out += "'"
+                i += 2
+            elif c == "\\" and i + 1 < len(body):
+                if body[i + 1] == "u" and re.fullmatch(r"[0-9a-fA-F]{4}", body[i + 2:i + 6] or "") and i + 5 < len(body):
+                    out += chr(int(body[i + 2:i + 6], 16))
+                    i += 6
+                elif re.fullmatch(r"[01][0-7][0-7]", body[i + 1:i + 4]) and i + 3 < len(body):
+                    out += chr(int(body[i + 1:i + 4], 8))
+                    i += 4
+                else:
+                    out += esc.get(body[i + 1], body[i + 1])
+                    i += 2
+            else:
+                out += c
+                i += 1
+        return out
+
+    return re.sub(r"'((?:[^'\\]|\\.|'')*)'", lambda m: "'" + value(m.group(1)).replace("'", "''") + "'", expr)
+
+
 def rewrite_casts(expr):
     """CAST(x AS t) -> spark_cast_t(x) (sqlite's CAST has other semantics)."""
     out, i = [], 0
@@ -450,8 +482,106 @@ def rewrite_casts(expr):
         i = k + 1
 
 
+# ---- soundex, regular expressions, dates (Spark 2.4 built-ins; not in /root/reference: parity unpinned) -----------
+_SOUNDEX_CODES = dict(zip("ABCDEFGHIJKLMNOPQRSTUVWXYZ", "01230127022455012623017202"))
+
+
+def _spark_soundex(v):
+    """UTF8String.soundex: first byte an ASCII letter (else the input), then up to three codes of the later letters;
+    vowels and Y (0) and non-letters separate repeated codes, H and W (7) do not."""
+    if v is None:
+        return None
+    v = _s(v)
+    if not v:
+        return v
+    raw = v.encode("utf-8")
+    head = chr(raw[0]).upper() if raw[0] < 128 else ""
+    if head not in _SOUNDEX_CODES:
+        return v
+    out, prev = head, _SOUNDEX_CODES[head]
+    for byte in raw[1:]:
+        ch = chr(byte).upper() if byte < 128 else ""
+        code = _SOUNDEX_CODES.get(ch)
+        if code is None:
+            prev = "0"
+        elif code != "7":
+            if code not in ("0", prev):
+                out += code
+            prev = code
+        if len(out) == 4:
+            break
+    return (out + "000")[:4]
+
+
+def _java_rep(rep, m):
+    """Matcher.appendReplacement: \\c -> c, $g -> group g (digits taken while the group exists)."""
+    res, i = [], 0
+    while i < len(rep):
+        if rep[i] == "\\":
+            res.append(rep[i + 1])
+            i += 2
+        elif rep[i] == "$":
+            j = i + 2
+            while j < len(rep) and rep[j].isdigit() and int(rep[i + 1:j + 1]) <= m.re.groups:
+                j += 1
+            res.append(m.group(int(rep[i + 1:j])) or "")
+            i = j
+        else:
+            res.append(rep[i])
+            i += 1
+    return "".join(res)
+
+
+def _spark_regexp_replace(v, pat, rep):
+    if v is None or pat is None or rep is None:
+        return None
+    return re.compile(pat, re.ASCII).sub(lambda m: _java_rep(rep, m), _s(v))
+
+
+def _spark_regexp_extract(v, pat, idx=1):
+    if v is None or pat is None:
+        return None
+    m = re.compile(pat, re.ASCII).search(_s(v))
+    return (m.group(int(idx)) or "") if m else ""
+
+
+_DATE = re.compile(r"(\d{4})(?:-(\d*)(?:-(\d*))?)?(?:[ T].*)?", re.DOTALL)
+
+
+def _days(v):
+    """DateTimeUtils.stringToDate of a string as days since 1970-01-01 (None: not a date); dates from 1583 on
+    (the proleptic Gregorian calendar, where java's hybrid calendar agrees)."""
+    if v is None:
+        return None
+    m = _DATE.fullmatch(_s(v).strip(" "))
+    if not m:
+        return None
+    y = int(m.group(1))
+    mo = int(m.group(2)) if m.group(2) is not None and m.group(2) != "" else (0 if m.group(2) == "" else 1)
+    d = int(m.group(3)) if m.group(3) is not None and m.group(3) != "" else (0 if m.group(3) == "" else 1)
+    try:
+        return (_dt.date(y, mo, d) - _dt.date(1970, 1, 1)).days
+    except ValueError:
+        return None
+
+
+def _date_str(days):
+    return None if days is None else (_dt.date(1970, 1, 1) + _dt.timedelta(days=days)).isoformat()
+
+
 def connect():
     con = sqlite3.connect(":memory:")
+    con.create_function("soundex", 1, _spark_soundex, deterministic=True)
+    con.create_function("regexp_replace", 3, _spark_regexp_replace, deterministic=True)
+    con.create_function("regexp_extract", 2, _spark_regexp_extract, deterministic=True)
+    con.create_function("regexp_extract", 3, _spark_regexp_extract, deterministic=True)
+    con.create_function("to_date", 1, lambda v: _date_str(_days(v)), deterministic=True)
+    con.create_function("date_add", 2, lambda v, k: None if _days(v) is None else _date_str(_days(v) + int(k)),
+                        deterministic=True)
+    con.create_function("date_sub", 2, lambda v, k: None if _days(v) is None else _date_str(_days(v) - int(k)),
+                        deterministic=True)
+    con.create_function("datediff", 2, lambda a, b: None if _days(a) is None or _days(b) is None else _days(a) - _days(b),
+                        deterministic=True)
     con.create_function("jaro_winkler_sim", 2, jaro_winkler, deterministic=True)
     con.create_function("levenshtein", 2, _lev, deterministic=True)
     con.create_function("length", 1, _length, deterministic=True)
@@ -520,7 +650,7 @@ def sql_gammas(cmp_df, case_expressions):
     cmp_df.to_sql("cmp", con, index=False)
     out = np.empty((len(cmp_df), len(case_expressions)), dtype=np.int8)
     for k, expr in enumerate(case_expressions):
-        e = rewrite_casts(_strip_alias(expr))
+        e = rewrite_casts(spark_literals(_strip_alias(expr)))
         vals = [r[0] for r in con.execute(f"select {e} from cmp").fetchall()]
         out[:, k] = np.array([-99 if v is None else v for v in vals], dtype=np.int64)
     return out

@@ -198,6 +198,16 @@ class _ProgramBuilder:
         self.columns[(o.name, o.form)] = None
         return o
 
+    def _day_operand(self, node, shift: int) -> OperandSpec:
+        """The day number (days since 1970-01-01, + shift) of a date operand of datediff: a string literal is
+        parsed here (DateTimeUtils.stringToDate; NULL if it is not a date); a column or an expression of one record
+        becomes the derived numeric column datediff(date_add(x, shift), '1970-01-01') (derived.py)."""
+        if isinstance(node, Lit):
+            day = D.spark_string_to_date(node.value) if isinstance(node.value, str) else None
+            return OperandSpec(kind="num", num=float("nan") if day is None else float(day + shift), form="num")
+        inner = node if shift == 0 else Func("date_add", (node, Lit(shift)))
+        return self._derived_operand(Func("datediff", (inner, Lit("1970-01-01"))), "num", None, None)
+
     def _lit(self, s: str):
         if s not in self.literals:
             self.literals.append(s)
@@ -256,6 +266,20 @@ class _ProgramBuilder:
         elif kind in ("absdiff", "percdiff"):
             a, b = self.operand(v[1], "num"), self.operand(v[2], "num")
             self.emit("ABSDIFF" if kind == "absdiff" else "PERCDIFF", self._op(a), self._op(b), op, t=t)
+        elif kind == "absdatediff":
+            # abs(datediff(a, b)) cmp t = abs(day(a) - day(b)) cmp t over the operands' day numbers
+            a, b = self._day_operand(v[1], 0), self._day_operand(v[2], 0)
+            self.emit("ABSDIFF", self._op(a), self._op(b), op, t=t)
+        elif kind == "datediff":
+            # datediff(a, b) cmp t  <=>  day(a) cmp day(b) + t  (day numbers are integers: exact in fp64).  The shift
+            # is folded into b's derived column (date_add); a non-integral t first becomes the integral threshold
+            # with the same truth value for every integer
+            if t != int(t):
+                if op in ("=", "!="):
+                    raise ValueError(f"datediff(...) {op} {t}: a non-integral day count")
+                t = float(np.floor(t) if op in ("<=", ">") else np.ceil(t))
+            a, b = self._day_operand(v[1], 0), self._day_operand(v[2], int(t))
+            self.emit("NUM_CMP", self._op(a), self._op(b), op)
         else:
             raise ValueError(f"unsupported value expression {kind}")
 
@@ -304,6 +328,11 @@ def _classify(node):
         ad = _strip_abs_diff(node)
         if ad:
             return ("absdiff", ad[0], ad[1])
+        if node.name == "datediff" and len(node.args) == 2:
+            return ("datediff", node.args[0], node.args[1])
+        if (node.name == "abs" and len(node.args) == 1 and isinstance(node.args[0], Func)
+                and node.args[0].name == "datediff" and len(node.args[0].args) == 2):
+            return ("absdatediff", node.args[0].args[0], node.args[0].args[1])
         if node.name in ("substr", "substring", "ifnull", "coalesce", "nvl") or D.is_derived(node):
             return ("operand",)
         raise ValueError(f"unsupported function {node.name}() in case_expression")

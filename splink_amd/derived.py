@@ -48,7 +48,10 @@ try:
 except ImportError:  # pragma: no cover
     pa = pc = None
 
-STR_FUNCS = ("lower", "lcase", "upper", "ucase", "trim", "ltrim", "rtrim", "concat", "concat_ws")
+STR_FUNCS = ("lower", "lcase", "upper", "ucase", "trim", "ltrim", "rtrim", "concat", "concat_ws", "soundex",
+             "regexp_replace", "regexp_extract")
+# date functions of one record: their values are dates, kept on the device as numbers (days since 1970-01-01)
+DATE_FUNCS = ("to_date", "date_add", "date_sub", "datediff")
 CAST_TYPES = {"string": "str", "varchar": "str", "int": "int", "integer": "int", "bigint": "long",
               "long": "long", "smallint": "short", "short": "short", "tinyint": "byte", "byte": "byte",
               "double": "double"}
@@ -58,7 +61,7 @@ OPERAND_FUNCS = ("substr", "substring", "ifnull", "coalesce", "nvl")
 
 def is_derived(node) -> bool:
     """A node that makes its operand a derived column (a Spark built-in over one record)."""
-    return isinstance(node, Func) and (node.name in STR_FUNCS or node.name == "cast")
+    return isinstance(node, Func) and (node.name in STR_FUNCS or node.name in DATE_FUNCS or node.name == "cast")
 
 
 def cast_type(node: Func) -> str:
@@ -76,6 +79,8 @@ def form_of(node, col_form) -> str:
     if isinstance(node, Func):
         if node.name in STR_FUNCS or node.name in ("substr", "substring"):
             return "str"
+        if node.name in DATE_FUNCS:
+            return "num"
         if node.name == "cast":
             return "str" if cast_type(node) == "str" else "num"
         if node.name in ("ifnull", "coalesce", "nvl"):
@@ -118,7 +123,8 @@ def neutralise(node, column_ref) -> Tuple[object, Optional[int]]:
             if n.name == "cast":
                 cast_type(n)
                 return Func("cast", (walk(n.args[0]), n.args[1]))
-            if n.name in STR_FUNCS or n.name in OPERAND_FUNCS:
+            if n.name in STR_FUNCS or n.name in OPERAND_FUNCS or n.name in DATE_FUNCS:
+                check_args(n)
                 return Func(n.name, tuple(walk(a) for a in n.args))
             raise ValueError(f"unsupported function {n.name}() inside {render_any(node)}")
         raise ValueError(f"unsupported expression inside a derived column: {n}")
@@ -134,6 +140,225 @@ def render_any(node) -> str:
         return render(node)
     except ValueError:
         return str(node)
+
+
+def check_args(n: Func):
+    """Argument shapes of the functions whose later arguments must be literals (checked at compile time, so a
+    bad pattern fails as the reference's query would, before any row is evaluated)."""
+    if n.name in ("regexp_replace", "regexp_extract"):
+        want = (3,) if n.name == "regexp_replace" else (2, 3)
+        if len(n.args) not in want or not all(isinstance(a, Lit) and isinstance(a.value, str) for a in n.args[1:2]):
+            raise ValueError(f"{n.name}() needs a string-literal pattern")
+        pat = java_regex(n.args[1].value)
+        if n.name == "regexp_replace":
+            if not (isinstance(n.args[2], Lit) and isinstance(n.args[2].value, str)):
+                raise ValueError("regexp_replace() needs a string-literal replacement")
+            java_replacement(n.args[2].value, pat.groups)
+        else:
+            idx = n.args[2] if len(n.args) == 3 else Lit(1)  # Spark's default group: 1
+            if not (isinstance(idx, Lit) and isinstance(idx.value, int) and not isinstance(idx.value, bool)):
+                raise ValueError("regexp_extract() needs a literal group index")
+            if not 0 <= idx.value <= pat.groups:  # Matcher.group throws: the reference's query fails
+                raise ValueError(f"regexp_extract(): group {idx.value} of a pattern with {pat.groups} groups")
+    elif n.name in ("date_add", "date_sub"):
+        if len(n.args) != 2 or not (isinstance(n.args[1], Lit) and isinstance(n.args[1].value, int)
+                                    and not isinstance(n.args[1].value, bool)):
+            raise ValueError(f"{n.name}() needs a literal integer number of days")
+    elif n.name == "datediff" and len(n.args) != 2:
+        raise ValueError("datediff() takes two dates")
+    elif n.name in ("to_date", "soundex") and len(n.args) != 1:
+        raise ValueError(f"{n.name}() takes one argument (to_date with a format is not supported)")
+
+
+# ---- Spark semantics: soundex, regular expressions, dates ---------------------------------------------
+_US_ENGLISH = "01230127022455012623017202"  # UTF8String.soundex's code per letter A..Z (H, W: 7 = no separator)
+
+
+def spark_soundex(s: str) -> str:
+    """UTF8String.soundex (Spark 2.4): over the UTF-8 bytes; a first byte that is not an ASCII letter returns the
+    string unchanged; letters upper-cased; codes 0 (vowels, Y) separate equal codes, 7 (H, W) are skipped without
+    separating; non-letters separate; the first letter then up to three codes, padded with '0'."""
+    if s == "":
+        return s
+    b = s.encode("utf-8")
+    first = b[0] - 32 if 97 <= b[0] <= 122 else b[0]
+    if not 65 <= first <= 90:
+        return s
+    sx = [chr(first)]
+    last = _US_ENGLISH[first - 65]
+    for x in b[1:]:
+        x = x - 32 if 97 <= x <= 122 else x
+        if not 65 <= x <= 90:
+            last = "0"
+            continue
+        code = _US_ENGLISH[x - 65]
+        if code == "7":
+            continue
+        if code != "0" and code != last:
+            sx.append(code)
+            if len(sx) > 3:
+                break
+        last = code
+    return "".join(sx).ljust(4, "0")
+
+
+_REGEX_CACHE: Dict[str, "re.Pattern"] = {}
+
+
+def java_regex(pattern: str) -> "re.Pattern":
+    """A java.util.regex pattern (Spark's regexp_replace / regexp_extract) as a Python pattern.  The common
+    subset -- literals, classes, \\d \\w \\s \\b (ASCII in Java: re.ASCII), quantifiers (greedy / lazy), groups,
+    alternation, anchors -- means the same in both; constructs Python's re lacks (possessive quantifiers, atomic
+    groups, \\p{..} classes, \\Q..\\E) fail to compile here and raise ValueError."""
+    p = _REGEX_CACHE.get(pattern)
+    if p is None:
+        if re.search(r"\\[pPQEGZz]|\(\?>|[*+?}]\+", pattern):
+            raise ValueError(f"regular expression {pattern!r} uses a Java construct that is not supported")
+        try:
+            p = re.compile(pattern, re.ASCII)
+        except re.error as e:
+            raise ValueError(f"regular expression {pattern!r} does not compile: {e}") from None
+        _REGEX_CACHE[pattern] = p
+    return p
+
+
+def java_replacement(rep: str, groups: int):
+    """Matcher.appendReplacement's replacement string as a list of literal strings and group numbers: \\x is the
+    character x, $n a group (the longest group number that exists, as Java reads it), a '$' or '\\' at the end
+    is an error."""
+    parts: List[object] = []
+    lit = []
+    i = 0
+    while i < len(rep):
+        c = rep[i]
+        if c == "\\":
+            if i + 1 >= len(rep):
+                raise ValueError("regexp_replace(): character to be escaped is missing")
+            lit.append(rep[i + 1])
+            i += 2
+        elif c == "$":
+            if i + 1 >= len(rep) or not rep[i + 1].isdigit():
+                raise ValueError("regexp_replace(): illegal group reference")
+            g = int(rep[i + 1])
+            if g > groups:
+                raise ValueError(f"regexp_replace(): no group {g}")
+            i += 2
+            while i < len(rep) and rep[i].isdigit() and g * 10 + int(rep[i]) <= groups:
+                g = g * 10 + int(rep[i])
+                i += 1
+            if lit:
+                parts.append("".join(lit))
+                lit = []
+            parts.append(g)
+        else:
+            lit.append(c)
+            i += 1
+    if lit:
+        parts.append("".join(lit))
+    return parts
+
+
+def spark_regexp_replace(s: str, pattern: str, rep: str) -> str:
+    p = java_regex(pattern)
+    parts = java_replacement(rep, p.groups)
+    return p.sub(lambda m: "".join(x if isinstance(x, str) else (m.group(x) or "") for x in parts), s)
+
+
+def spark_regexp_extract(s: str, pattern: str, idx: int = 1) -> str:
+    """RegExpExtract: the group of the first match; '' without a match or for a group that did not take part."""
+    m = java_regex(pattern).search(s)
+    return "" if m is None else (m.group(idx) or "")
+
+
+class Day(int):
+    """A date value inside a derived expression: days since 1970-01-01 (rendered 'yyyy-MM-dd' as a string)."""
+
+
+_MONTH31 = (1, 3, 5, 7, 8, 10, 12)
+
+
+def _leap(y: int) -> bool:
+    return y % 4 == 0 and (y % 100 != 0 or y % 400 == 0)
+
+
+def epoch_day(y: int, m: int, d: int) -> int:
+    """Days since 1970-01-01 of a date as java.util.GregorianCalendar (GMT) reads it: Gregorian from 1582-10-15,
+    Julian before (the reference's Spark 2.4 uses the hybrid calendar; parity unpinned before 1582)."""
+    if (y, m, d) >= (1582, 10, 15):
+        a = (14 - m) // 12
+        yy, mm = y + 4800 - a, m + 12 * a - 3
+        jdn = d + (153 * mm + 2) // 5 + 365 * yy + yy // 4 - yy // 100 + yy // 400 - 32045
+    else:
+        a = (14 - m) // 12
+        yy, mm = y + 4800 - a, m + 12 * a - 3
+        jdn = d + (153 * mm + 2) // 5 + 365 * yy + yy // 4 - 32083
+    return jdn - 2440588
+
+
+def day_to_string(day: int) -> str:
+    """'yyyy-MM-dd' of a day number (Gregorian from 1582-10-15, Julian before, as epoch_day)."""
+    jdn = int(day) + 2440588
+    if jdn >= 2299161:  # 1582-10-15
+        a = jdn + 32044
+        b = (4 * a + 3) // 146097
+        c = a - 146097 * b // 4
+    else:
+        b = 0
+        c = jdn + 32082
+    d_ = (4 * c + 3) // 1461
+    e = c - 1461 * d_ // 4
+    m_ = (5 * e + 2) // 153
+    day_ = e - (153 * m_ + 2) // 5 + 1
+    month = m_ + 3 - 12 * (m_ // 10)
+    year = 100 * b + d_ - 4800 + m_ // 10
+    return f"{year:04d}-{month:02d}-{day_:02d}"
+
+
+def spark_string_to_date(s: str) -> Optional[int]:
+    """DateTimeUtils.stringToDate (Spark 2.4) as days since 1970-01-01; None = NULL.  Spaces trimmed; 'yyyy',
+    'yyyy-[m]m', 'yyyy-[m]m-[d]d', optionally followed by ' ' or 'T' and anything; the year exactly four digits;
+    missing month / day are 1; an impossible date is NULL."""
+    b = s.strip(" ").encode("utf-8")
+    seg = [1, 1, 1]
+    i = cur = j = 0
+    while j < len(b) and b[j] not in (0x20, 0x54):  # ' ', 'T'
+        c = b[j]
+        if i < 2 and c == 0x2D:  # '-'
+            if i == 0 and j != 4:
+                return None
+            seg[i] = cur
+            cur = 0
+            i += 1
+        elif 0x30 <= c <= 0x39:
+            cur = cur * 10 + (c - 0x30)
+        else:
+            return None
+        j += 1
+    if i == 0 and j != 4:
+        return None
+    seg[i] = cur
+    y, m, d = seg
+    if y < 0 or y > 9999 or m < 1 or m > 12 or d < 1 or d > 31:
+        return None
+    if m == 2 and d > (29 if _leap(y) else 28):
+        return None
+    if m not in _MONTH31 and d > 30:
+        return None
+    return epoch_day(y, m, d)
+
+
+def to_day(v) -> Optional[int]:
+    """A value as a date (days since 1970-01-01): a date value, a string (stringToDate), a datetime / date
+    object; numbers are not dates (NULL)."""
+    if v is None:
+        return None
+    if isinstance(v, Day):
+        return int(v)
+    if isinstance(v, str):
+        return spark_string_to_date(v)
+    if hasattr(v, "year") and hasattr(v, "month") and hasattr(v, "day"):
+        return epoch_day(int(v.year), int(v.month), int(v.day))
+    return None
 
 
 # ---- Spark semantics, per value --------------------------------------------------------------------
@@ -208,6 +433,8 @@ def _is_null(v) -> bool:
 
 
 def _to_str(v):
+    if isinstance(v, Day):
+        return day_to_string(v)
     return None if _is_null(v) else T.spark_str(v)
 
 
@@ -225,7 +452,7 @@ def eval_row(node, row) -> object:
             return None
         t = cast_type(node)
         if t == "str":
-            return T.spark_str(v)
+            return _to_str(v)
         if t == "double":
             return java_parse_double(v) if isinstance(v, str) else float(v)
         bound = INT_RANGE[t]
@@ -246,6 +473,24 @@ def eval_row(node, row) -> object:
     if name == "concat":
         parts = [_to_str(eval_row(a, row)) for a in node.args]
         return None if any(p is None for p in parts) else "".join(parts)
+    if name in DATE_FUNCS:
+        days = to_day(eval_row(node.args[0], row))
+        if days is None:
+            return None
+        if name == "to_date":
+            return Day(days)
+        if name in ("date_add", "date_sub"):
+            k = node.args[1].value
+            return Day(days + (k if name == "date_add" else -k))
+        other = to_day(eval_row(node.args[1], row))
+        return None if other is None else days - other  # datediff(end, start): an integer
+    if name in ("regexp_replace", "regexp_extract"):
+        s = _to_str(eval_row(node.args[0], row))
+        if s is None:
+            return None
+        if name == "regexp_replace":
+            return spark_regexp_replace(s, node.args[1].value, node.args[2].value)
+        return spark_regexp_extract(s, node.args[1].value, node.args[2].value if len(node.args) > 2 else 1)
     if name == "concat_ws":
         sep = _to_str(eval_row(node.args[0], row))
         if sep is None:
@@ -265,6 +510,8 @@ def eval_row(node, row) -> object:
         return s.lstrip(" ")
     if name == "rtrim":
         return s.rstrip(" ")
+    if name == "soundex":
+        return spark_soundex(s)
     raise ValueError(f"unsupported function {name}()")
 
 
@@ -347,7 +594,7 @@ def evaluate(node, df: pd.DataFrame, form: str) -> pd.Series:
         if arr is not None:
             return pd.Series(pd.arrays.ArrowExtensionArray(arr), index=df.index)
         return pd.Series(out, dtype=object, index=df.index)
-    num = np.array([np.nan if x is None else float(x) for x in out], dtype=np.float64)
+    num = np.array([np.nan if x is None else float(x) for x in out], dtype=np.float64)  # a date: its day number
     return pd.Series(num, index=df.index)
 
 

@@ -71,13 +71,49 @@ Node = Union[Lit, Col, Func, Bin, Un, IsNull, Case]
 _TOKEN = re.compile(r"""
     (?P<ws>\s+|--[^\n]*|/\*.*?\*/)
   | (?P<num>(?:\d+\.\d*|\.\d+|\d+)(?:[eE][+-]?\d+)?)
-  | (?P<str>'(?:[^']|'')*')
+  | (?P<str>'(?:[^'\\]|\\.|'')*')
   | (?P<qid>`[^`]*`|"[^"]*")
   | (?P<id>[A-Za-z_][A-Za-z_0-9$]*)
   | (?P<op><=|>=|<>|!=|==|[=<>+\-*/%(),.])
 """, re.VERBOSE | re.DOTALL)
 
 KEYWORDS = {"case", "when", "then", "else", "end", "and", "or", "not", "is", "null", "true", "false", "as"}
+
+
+_ESCAPES = {"0": "\u0000", "'": "'", '"': '"', "b": "\b", "n": "\n", "r": "\r", "t": "\t", "Z": "\u001A",
+            "\\": "\\", "%": "\\%", "_": "\\_"}
+
+
+def unescape_literal(quoted: str) -> str:
+    """The value of a single-quoted SQL string literal (quotes included), as Spark's parser reads it
+    (ParserUtils.unescapeSQLString, Spark 2.4): backslash escapes \\0 \\' \\" \\b \\n \\r \\t \\Z \\\\ (\\% and \\_
+    keep their backslash, any other escaped character stands for itself), \\uXXXX and three-digit octal \\[01][0-7][0-7].
+    A doubled quote '' stands for one quote (SQL-standard quoting, which the sqlite oracle and the reference's
+    generated SQL use; Spark itself would read 'a''b' as two adjacent literals)."""
+    b = quoted[1:-1]
+    out = []
+    i, n = 0, len(b)
+    while i < n:
+        c = b[i]
+        if c == "'" and i + 1 < n and b[i + 1] == "'":
+            out.append("'")
+            i += 2
+            continue
+        if c != "\\" or i + 1 >= n:
+            out.append(c)
+            i += 1
+            continue
+        nxt = b[i + 1]
+        if nxt == "u" and i + 5 < n and all(ch in "0123456789abcdefABCDEF" for ch in b[i + 2:i + 6]):
+            out.append(chr(int(b[i + 2:i + 6], 16)))
+            i += 6
+        elif i + 3 < n and b[i + 1] in "01" and b[i + 2] in "01234567" and b[i + 3] in "01234567":
+            out.append(chr(int(b[i + 1:i + 4], 8)))
+            i += 4
+        else:
+            out.append(_ESCAPES.get(nxt, nxt))
+            i += 2
+    return "".join(out)
 
 
 def tokenize(text: str):
@@ -93,7 +129,7 @@ def tokenize(text: str):
         if kind == "ws":
             continue
         if kind == "str":
-            toks.append(("str", val[1:-1].replace("''", "'")))
+            toks.append(("str", unescape_literal(val)))
         elif kind == "num":
             toks.append(("num", val))
         elif kind == "qid":

@@ -45,10 +45,24 @@ def _frame(n, seed):
         "age": rng.choice(ages, n),
         "height": rng.choice(heights, n),
         "city": rng.choice(np.array(["a", "b", "c", "d", "e"], dtype=object), n),
+        "visit": _visits(rng, n),
     })
-    for c in ["first_name", "surname", "age", "height"]:
+    for c in ["first_name", "surname", "age", "height", "visit"]:
         df.loc[rng.random(n) < 0.07, c] = None
     return df
+
+
+def _visits(rng, n):
+    """Date strings as a source hands them over: ISO dates, unpadded months / days, a year alone, times after
+    the date, surrounding spaces, and strings that are not dates (NULL for to_date / datediff)."""
+    base = np.datetime64("2019-06-01") + rng.integers(0, 900, n).astype("timedelta64[D]")
+    out = np.array([str(d) for d in base], dtype=object)
+    odd = rng.random(n)
+    for i in np.nonzero(odd < 0.25)[0]:
+        y, m, d = str(base[i]).split("-")
+        out[i] = rng.choice([f"{y}-{int(m)}-{int(d)}", f"{y}-{m}-{d} 10:30:00", f"{y}-{m}-{d}T08:00", f" {y}-{m}-{d} ",
+                             f"{y}-{m}", y, "2020-02-30", "20200101", "soon", ""])
+    return out
 
 
 EXPRS = [
@@ -91,6 +105,22 @@ EXPRS = [
     ("prefix", ["surname"], 2,
      "case when surname_l is null or surname_r is null then -1 "
      "when substr(lower(surname_l), 1, 3) = substr(lower(surname_r), 1, 3) then 1 else 0 end"),
+    # Spark built-ins added in round 6: soundex, regular expressions (one with a backslash escape in its literal:
+    # the SQL text '\\d' is the regex \d), dates kept as day numbers, datediff as a value test
+    ("sx", ["surname"], 2,
+     "case when surname_l is null or surname_r is null then -1 when soundex(surname_l) = soundex(surname_r) then 1 "
+     "else 0 end"),
+    ("rx", ["first_name", "age"], 4,
+     "case when first_name_l is null or first_name_r is null then -1 "
+     "when regexp_replace(lower(first_name_l), '[^a-z]', '') = regexp_replace(lower(first_name_r), '[^a-z]', '') "
+     "then 3 when regexp_extract(first_name_l, '^ *([A-Za-z])(.)', 2) = regexp_extract(first_name_r, '^ *([A-Za-z])(.)', 2) "
+     "then 2 when regexp_replace(age_l, '\\\\d', '#') = regexp_replace(age_r, '\\\\d', '#') then 1 else 0 end"),
+    ("dd", ["visit"], 5,
+     "case when to_date(visit_l) is null or to_date(visit_r) is null then -1 "
+     "when to_date(visit_l) = to_date(visit_r) then 4 "
+     "when abs(datediff(visit_l, visit_r)) <= 30 then 3 "
+     "when datediff(visit_l, visit_r) > 365 then 2 "
+     "when datediff(date_add(visit_l, 7), visit_r) < -100.5 then 1 else 0 end"),
     ("nulls", ["first_name", "age"], 3,
      "case when ifnull(lower(first_name_l), 'zz') = ifnull(lower(first_name_r), 'zz') then 2 "
      "when lower(ifnull(first_name_l, age_l)) = lower(ifnull(first_name_r, age_r)) then 1 else 0 end"),

@@ -120,7 +120,7 @@ def test_parser_basics():
 def test_compiler_rejects_unsupported_sql():
     schema = Schema({"a": "str", "b": "num"})
     bad = [
-        "case when a_l is null then -1 when soundex(a_l) = soundex(a_r) then 1 else 0 end",
+        "case when a_l is null then -1 when initcap(a_l) = initcap(a_r) then 1 else 0 end",
         "case when a_l = a_r then 1 end",  # no ELSE
         "case when a_l = a_r then 5 else 0 end",  # level out of range for 2 levels
         "case when a_l like 'x%' then 1 else 0 end",
@@ -240,3 +240,80 @@ def test_float64_encoding_keeps_infinities():
     vals, valid = encode_float64(pd.Series([1.5, float("inf"), -float("inf"), float("nan"), None]))
     assert valid.tolist() == [1, 1, 1, 0, 0]
     assert vals[1] == float("inf") and vals[2] == -float("inf") and vals[3] == 0.0
+
+
+def test_spark_builtins_match_oracle_functions():
+    """soundex / regexp_replace / regexp_extract / to_date / date_add / date_sub / datediff as derived columns
+    (derived.py, evaluated per row at ingest) equal the oracle's independent restatements in sqlite, on names,
+    punctuation, non-ASCII text and date strings in every shape stringToDate accepts or rejects (dates from 1583
+    on: before that the reference's hybrid calendar is Julian, parity unpinned)."""
+    import pandas as pd
+    from splink_amd import derived as D
+    words = ["Robert", "Rupert", "Rubin", "Ashcraft", "Tymczak", "Pfister", "Honeyman", "", "  x", "élan", "O'Hara",
+             "1abc", "Lee", "Gutierrez", "a-b-c", "Wh", None]
+    dates = ["2020-01-15", "2020-1-5", "2020", "2020-02-30", "1999-12-31 10:00", "2000-02-29T01:02", "20200101",
+             " 2021-03-04 ", "x", "", "1600-03-01", "2020-13-01", "2020-", "2020-05", "1970-01-01", None, "2021-02-29"]
+    df = pd.DataFrame({"a": words, "d": dates})
+    con = orc.connect()
+    df.to_sql("t", con, index=False)
+    exprs = ["soundex(a)", "soundex(lower(a))", "regexp_replace(a, '[aeiou]', '')", "regexp_replace(a, '(r)(u)', '$2$1')",
+             "regexp_extract(a, '([A-Z])([a-z]+)', 2)", "regexp_extract(a, 'x(y)?', 1)", "regexp_extract(a, '([a-z]+)')",
+             "regexp_replace(a, '\\\\d', '#')", "regexp_replace(a, 'a*', '-')", "regexp_replace(a, '(.)', '\\\\$$1')",
+             "cast(to_date(d) as string)", "datediff(d, '2020-01-01')", "cast(date_add(d, 40) as string)",
+             "datediff(date_sub(d, 3), '1970-01-01')", "datediff(to_date(d), to_date(d))"]
+    schema = Schema({"a": "str", "d": "str"})
+    for e in exprs:
+        node, _ = D.neutralise(parse(e), lambda c: (c.name, 0))
+        form = D.form_of(node, schema.form)
+        want = [r[0] for r in con.execute(f"select {orc.rewrite_casts(orc.spark_literals(e))} from t").fetchall()]
+        got = D.evaluate(node, df, form)
+        got = [None if (x is None or x is pd.NA or (isinstance(x, float) and math.isnan(x))) else x for x in got.tolist()]
+        if form == "num":
+            want = [None if w is None else float(w) for w in want]
+        assert got == want, (e, [(r, g, w) for r, g, w in zip(df.to_dict("records"), got, want) if g != w][:4])
+    # American Soundex reference values (H / W do not separate equal codes, vowels do)
+    assert [D.spark_soundex(x) for x in ["Robert", "Rupert", "Rubin", "Ashcraft", "Tymczak", "Pfister", "Honeyman"]] == \
+        ["R163", "R163", "R150", "A261", "T522", "P236", "H555"]
+    assert D.spark_string_to_date("1970-01-01") == 0 and D.day_to_string(D.epoch_day(1582, 10, 15) - 1) == "1582-10-04"
+
+
+def test_datediff_compiles_to_day_columns():
+    """abs(datediff(a_l, a_r)) <= t is ABSDIFF over the derived day-number column datediff(a, '1970-01-01'); a
+    signed datediff(a_l, a_r) cmp t is NUM_CMP against b's column shifted by t days (date_add), a non-integral t
+    first rounded to the integral threshold with the same truth value."""
+    from splink_amd import _native as N
+    schema = Schema({"a": "str", "b": "str"})
+    case = ("case when a_l is null or a_r is null then -1 when abs(datediff(a_l, a_r)) <= 30 then 3 "
+            "when datediff(a_l, b_r) > 365 then 2 when 10.5 >= datediff(b_l, a_r) then 1 else 0 end")
+    prog = compile_comparisons({"comparison_columns": [{"col_name": "a", "num_levels": 4, "case_expression": case}]},
+                               schema)
+    assert set(prog.derived) == {"datediff(a, '1970-01-01')", "datediff(date_add(b, 365), '1970-01-01')",
+                                 "datediff(b, '1970-01-01')", "datediff(date_add(a, 10), '1970-01-01')"}
+    ops = [i[0] for i in prog.instrs]
+    assert N.OP["ABSDIFF"] in ops and ops.count(N.OP["NUM_CMP"]) == 2
+    for bad in ["case when datediff(a_l, a_r) = 1.5 then 1 else 0 end",
+                "case when regexp_replace(a_l, b_l, '') = a_r then 1 else 0 end",
+                "case when regexp_replace(a_l, '(x', '') = a_r then 1 else 0 end",
+                "case when regexp_replace(a_l, 'x++', '') = a_r then 1 else 0 end",
+                "case when regexp_extract(a_l, '(x)', 2) = a_r then 1 else 0 end",
+                "case when regexp_extract(a_l, 'x') = a_r then 1 else 0 end",
+                "case when regexp_replace(a_l, '(x)', '$2') = a_r then 1 else 0 end",
+                "case when date_add(a_l, b_l) = a_r then 1 else 0 end",
+                "case when to_date(a_l, 'yyyy') = a_r then 1 else 0 end"]:
+        with pytest.raises(ValueError):
+            compile_comparisons({"comparison_columns": [{"col_name": "a", "num_levels": 2, "case_expression": bad}]},
+                                schema)
+
+
+def test_string_literals_unescape_as_spark():
+    """Backslash escapes in string literals as Spark's parser reads them (ParserUtils.unescapeSQLString); a doubled
+    quote is one quote."""
+    from splink_amd.sqlexpr import unescape_literal
+    cases = {"'abc'": "abc", "'it''s'": "it's", "'\\d+'": "d+", "'\\\\d+'": "\\d+", "'a\\nb'": "a\nb",
+             "'\\u0041x'": "Ax", "'\\101'": "A", "'\\%'": "\\%", "'\\''": "'", "'\\q'": "q", "'\\Z'": "\x1a"}
+    for q, want in cases.items():
+        assert unescape_literal(q) == want, q
+        assert parse(f"a_l = {q}").b.value == want
+    for q in cases:
+        sql = orc.spark_literals(f"select {q}")
+        assert orc.connect().execute(sql).fetchone()[0] == cases[q], q
