@@ -115,12 +115,11 @@ EXPRS = [
      "when regexp_replace(lower(first_name_l), '[^a-z]', '') = regexp_replace(lower(first_name_r), '[^a-z]', '') "
      "then 3 when regexp_extract(first_name_l, '^ *([A-Za-z])(.)', 2) = regexp_extract(first_name_r, '^ *([A-Za-z])(.)', 2) "
      "then 2 when regexp_replace(age_l, '\\\\d', '#') = regexp_replace(age_r, '\\\\d', '#') then 1 else 0 end"),
-    ("dd", ["visit"], 5,
+    ("dd", ["visit"], 4,
      "case when to_date(visit_l) is null or to_date(visit_r) is null then -1 "
-     "when to_date(visit_l) = to_date(visit_r) then 4 "
-     "when abs(datediff(visit_l, visit_r)) <= 30 then 3 "
-     "when datediff(visit_l, visit_r) > 365 then 2 "
-     "when datediff(date_add(visit_l, 7), visit_r) < -100.5 then 1 else 0 end"),
+     "when to_date(visit_l) = to_date(visit_r) then 3 "
+     "when abs(datediff(visit_l, visit_r)) <= 30 then 2 "
+     "when datediff(visit_l, visit_r) > 365 or datediff(date_add(visit_l, 7), visit_r) < -100.5 then 1 else 0 end"),
     ("nulls", ["first_name", "age"], 3,
      "case when ifnull(lower(first_name_l), 'zz') = ifnull(lower(first_name_r), 'zz') then 2 "
      "when lower(ifnull(first_name_l, age_l)) = lower(ifnull(first_name_r, age_r)) then 1 else 0 end"),
