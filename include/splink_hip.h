@@ -61,6 +61,13 @@ int spk_ctx_kernel_ms_done(spk_ctx *ctx, double *out5);
 int spk_ctx_enable_timing(spk_ctx *ctx, int on);
 /* LDS bytes one workgroup may allocate on the context's device (sizes the E/M histogram copies). */
 int spk_ctx_lds_per_block(spk_ctx *ctx, int *out);
+/* Device memory the context holds, by what it stores (bytes allocated): [0] raw input columns (Arrow
+ * buffers as handed over), [1] record encodings (decoded columns: units, metadata, bit-planes, bag rows,
+ * numeric values; row permutations, ranks, blocking keys), [2] filter row images, [3] candidate pairs (row
+ * indices, rule-view positions and rows), [4] comparison codes, [5] comparison work lists (filter lists,
+ * exact / slow lists, region counts), [6] EM, scoring and tf state, [7] the sum.  For sizing a share of a
+ * job against a device's memory (there is no reference counterpart: Spark spills). */
+int spk_ctx_memory(spk_ctx *ctx, int64_t *out8);
 
 /* ---- record tables (replaces createOrReplaceTempView of df / df_l / df_r,
  *      blocking.py:209-222, and the vertical concatenation of :70-93) ------------ */

@@ -47,7 +47,7 @@ EXPORTS = [
     "spk_n_patterns", "spk_gammas_deferred", "spk_em_histogram", "spk_em_finalize", "spk_em_iteration", "spk_score",
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
     "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
-    "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
+    "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_ctx_memory", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
     "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
     "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_raw_utf8_arrow_chunks", "spk_table_digest", "spk_raw_release",
@@ -398,6 +398,15 @@ class Context:
         n = ctypes.c_int(0)
         check(self._lib.spk_ctx_lds_per_block(self._h, ctypes.byref(n)), "spk_ctx_lds_per_block")
         return n.value
+
+    MEMORY_PARTS = ("raw_columns", "record_encodings", "row_images", "pairs", "codes", "work_lists", "em_score_tf",
+                    "total")
+
+    def memory(self) -> dict:
+        """Device bytes the context holds, by what they store (spk_ctx_memory)."""
+        out = np.zeros(8, dtype=np.int64)
+        check(self._lib.spk_ctx_memory(self._h, _ptr(out)), "spk_ctx_memory")
+        return dict(zip(self.MEMORY_PARTS, [int(x) for x in out]))
 
     def gammas_view_regions(self) -> int:
         n = ctypes.c_int64(0)

@@ -3057,6 +3057,36 @@ extern "C" int spk_gammas_set_simple(spk_ctx *ctx, int on) {
     return SPK_OK;
 }
 
+extern "C" int spk_ctx_memory(spk_ctx *ctx, int64_t *out8) {
+    SPK_REQUIRE(ctx && out8, SPK_E_INVALID, "spk_ctx_memory: null arg");
+    auto b = [](const auto &buf) { return (int64_t)(buf.n * sizeof(*buf.p)); };
+    int64_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (const RawCol *r : ctx->raw)
+        if (r) m[0] += b(r->off) + b(r->bytes) + b(r->i64) + b(r->valid);
+    for (const Table &t : ctx->table) {
+        m[1] += b(t.perm) + b(t.rank) + b(t.d_desc);
+        for (int w = 0; w < 2; ++w)
+            for (const DevBuf<int64_t> *k : t.key[w])
+                if (k) m[1] += b(*k);
+        for (const Column *c : t.cols)
+            if (c) m[1] += b(c->units) + b(c->meta) + b(c->planes) + b(c->planes_hi) + b(c->bag) + b(c->val) + b(c->valid);
+    }
+    for (int s = 0; s < 2; ++s) {
+        m[2] += b(ctx->img[s]);
+        for (int v = 0; v < MAX_VIEWS; ++v) m[2] += b(ctx->vimg[v][s]);
+    }
+    m[3] = b(ctx->pl) + b(ctx->pr) + b(ctx->pvl) + b(ctx->pvr);
+    for (int v = 0; v < MAX_VIEWS; ++v) m[3] += b(ctx->views[v].rowsL) + b(ctx->views[v].rowsR);
+    m[4] = b(ctx->codes);
+    m[5] = b(ctx->work) + b(ctx->xlist) + b(ctx->xpref) + b(ctx->xinfo) + b(ctx->region_count) + b(ctx->prog_blob);
+    m[6] = b(ctx->hist) + b(ctx->mpat) + b(ctx->llpat) + b(ctx->cpat) + b(ctx->stats) + b(ctx->mu) + b(ctx->em_ticket) +
+           b(ctx->em_row) + b(ctx->em_hot) + b(ctx->mp) + b(ctx->mpat_score) + b(ctx->tf_uniq) + b(ctx->tf_runs) +
+           b(ctx->tf_nruns);
+    for (int i = 0; i < 7; ++i) m[7] += m[i];
+    for (int i = 0; i < 8; ++i) out8[i] = m[i];
+    return SPK_OK;
+}
+
 extern "C" int spk_ctx_lds_per_block(spk_ctx *ctx, int *out) {
     SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
     *out = ctx->lds_per_block;

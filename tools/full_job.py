@@ -115,6 +115,11 @@ def main():
     def mem_mark(stage):
         free, _ = torch.cuda.mem_get_info(0)
         mem[f"after_{stage}_bytes"] = int(total_mem - free)
+        if "job" in locals_ref:  # what the library itself holds, by part (spk_ctx_memory)
+            mem[f"after_{stage}_library_by_part"] = locals_ref["job"].ctx.memory()
+            mem["peak_reserved_by_torch_bytes"] = int(torch.cuda.max_memory_reserved(0))
+
+    locals_ref = {}
 
     wall = {}
     t_job = time.perf_counter()
@@ -123,6 +128,7 @@ def main():
     # the comparison-only columns upload in the background while the uid ranks and blocking run
     pre = _comparison_only_columns(st, st["blocking_rules"], inputs) if a.prefetch else None
     job = Job(st["link_type"], inputs, "unique_id", 0, shard=(shard, n_shards), prefetch=pre)
+    locals_ref["job"] = job
     job.ctx.enable_timing(True)
     wall["job_setup_incl_uid_rank"] = time.perf_counter() - t
     t = time.perf_counter()
@@ -198,7 +204,8 @@ def main():
                        if a.chunks else "make_records (serial)"),
         "surname_vocab": a.surname_vocab,
         "blocking_rules": st["blocking_rules"],
-        "device_memory": {**mem, "peak_in_use_bytes": max(v for k, v in mem.items() if k.startswith("after_"))},
+        "device_memory": {**mem, "peak_in_use_bytes": max(v for k, v in mem.items()
+                                                             if k.startswith("after_") and k.endswith("_bytes"))},
         "lambda_final": params.params["λ"],
     }
     if not a.no_parity:
