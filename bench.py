@@ -423,6 +423,8 @@ def main():
         "input": "Arrow-backed string columns (pd.ArrowDtype(large_string)); keys, ids, ranks, clustering on the device",
         "deferred_pairs": job.ctx.gammas_deferred(),
         "exact_cells_per_column": dict(zip(names, job.ctx.gammas_exact_counts(len(names)))),
+        # pairs whose level the blocking key implies (the filter reads nothing for that column there)
+        "implied_pairs_per_column": dict(zip(names, job.ctx.gammas_implied_pairs(len(names)))),
         "cpu_baseline": cpu,
         "string_rates": rates,
         "em_at_scale": em_scale,
