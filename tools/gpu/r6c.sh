@@ -11,5 +11,7 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench
 python -c "
 import json; d=json.load(open('gpurun_out/${TAG}_bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['breakdown_ms']['gamma']); c=d['cfg5_columns']; print('cfg5', c['ms_per_step'], c['breakdown_ms'])
 print(d['string_rates']['levenshtein_exact_pass'])"
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --em-scale 0 > gpurun_out/${TAG}_benchprof.json 2> gpurun_out/${TAG}_benchprof.err
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --em-scale 0 --cfg5-steps 0 > gpurun_out/${TAG}_benchprof.json 2> gpurun_out/${TAG}_benchprof.err
+echo "prof exit $?"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_cfg5 -o run -- python -u bench.py --config 5 --steps 5 --warmup 2 --no-cpu-baseline --em-scale 0 > gpurun_out/${TAG}_benchprof_cfg5.json 2> gpurun_out/${TAG}_benchprof_cfg5.err
 echo "prof exit $?"
