@@ -144,6 +144,20 @@ __device__ __attribute__((always_inline)) inline void append(const FiltArgs &A, 
     }
 }
 
+// A per-column constant held in a scalar register.  The level a lane takes is a select among a column's constants
+// (`nul ? null_level : same ? lv_same : lv_diff`); written on the kernel-argument fields directly, the compiler
+// turned that into a select of their ADDRESSES and one per-lane vector load of the chosen field, followed by
+// s_waitcnt vmcnt(0) -- a wait on every load in flight, the next pairs' rows included -- once per column, pair
+// group and iteration (12 of ~38 vector-memory instructions per 192 pairs, round-6 ISA).  readfirstlane makes the
+// operands values, not loads, so the select is a v_cndmask between scalar registers.
+__device__ __attribute__((always_inline)) inline uint32_t sconst(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+// (level + 1) * stride: the amount a level adds to the pair's code
+__device__ __attribute__((always_inline)) inline uint32_t sadd(int32_t level, uint32_t stride) {
+    return sconst((uint32_t)(level + 1) * stride);
+}
+
 __device__ __attribute__((always_inline)) inline bool implied(const FCommon &c, int64_t base, int64_t span) {
     return base >= c.imp_lo && base + span <= c.imp_hi;  // wave-uniform
 }
@@ -216,15 +230,17 @@ __device__ __attribute__((always_inline)) inline void ev_jw(const FJw &J, const 
             hi[u] = (j >= 0.7f - 1e-4f ? j + pw * (1.0f - j) : j) + 1e-5f;
         }
     }
+    const uint32_t a_one = sadd(J.lv_one, J.c.stride), a_zero = sadd(J.lv_zero, J.c.stride);
+    const uint32_t a_bound = sadd(J.lv_bound, J.c.stride), a_null = sadd(J.c.null_level, J.c.stride);
+    const bool und_same = sconst((uint32_t)J.c.und_same) != 0;
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
         const bool sat = lf[u] >= LEN_SAT || ls[u] >= LEN_SAT;
         const bool exact = same[u] || zero[u];
-        const int lv = same[u] ? (lf[u] > 0 ? J.lv_one : J.lv_zero) : (zero[u] ? J.lv_zero : J.lv_bound);
-        const bool u0 = (same[u] && J.c.und_same) || sat || (!exact && hi[u] >= J.cf);
+        const uint32_t add = same[u] ? (lf[u] > 0 ? a_one : a_zero) : (zero[u] ? a_zero : a_bound);
+        const bool u0 = (same[u] && und_same) || sat || (!exact && hi[u] >= J.cf);
         und[u] = act[u] && !nul[u] && u0;
-        const int level = nul[u] ? J.c.null_level : lv;
-        acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * J.c.stride;
+        acc[u] += und[u] ? 0u : (nul[u] ? a_null : add);
     }
 }
 template <int FP>
@@ -338,12 +354,15 @@ __device__ __attribute__((always_inline)) inline void ev_lev(const FLev &L, cons
             }
         }
     }
+    const uint32_t stride = sconst(L.c.stride);
+    const int lv_same = (int)sconst((uint32_t)L.lv_same), lv_same_empty = (int)sconst((uint32_t)L.lv_same_empty);
+    const int null_level = (int)sconst((uint32_t)L.c.null_level);
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
-        const int lv = same[u] ? (lens_u16(a[u].y) > 0 ? L.lv_same : L.lv_same_empty) : ch[u].lvl;
+        const int lv = same[u] ? (lens_u16(a[u].y) > 0 ? lv_same : lv_same_empty) : ch[u].lvl;
         und[u] = act[u] && !nul[u] && (u0[u] || (!same[u] && ch[u].und));
-        const int level = nul[u] ? L.c.null_level : lv;
-        acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * L.c.stride;
+        const int level = nul[u] ? null_level : lv;
+        acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * stride;
     }
 }
 template <int FP>
@@ -366,13 +385,15 @@ __device__ __attribute__((always_inline)) inline void ev_eq(const FEq &E, const 
                                                             uint32_t (&acc)[FP], bool (&und)[FP]) {
     const uint2(&a)[FP] = d.a;
     const uint2(&b)[FP] = d.b;
+    const uint32_t a_same = sadd(E.lv_same, E.c.stride), a_diff = sadd(E.lv_diff, E.c.stride);
+    const uint32_t a_null = sadd(E.c.null_level, E.c.stride);
+    const bool und_same = sconst((uint32_t)E.c.und_same) != 0;
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
         const bool same = a[u].x == b[u].x && a[u].y == b[u].y;
         const bool nul = a[u].y == LENS_NULL || b[u].y == LENS_NULL;
-        und[u] = act[u] && !nul && same && E.c.und_same;
-        const int level = nul ? E.c.null_level : (same ? E.lv_same : E.lv_diff);
-        acc[u] += und[u] ? 0u : (uint32_t)(level + 1) * E.c.stride;
+        und[u] = act[u] && !nul && same && und_same;
+        acc[u] += und[u] ? 0u : (nul ? a_null : (same ? a_same : a_diff));
     }
 }
 // A gap equality column from the high half (z, w) of the head chunks: the 8-byte field, or the 4-byte id at
@@ -383,13 +404,14 @@ __device__ __attribute__((always_inline)) inline void ev_gap_eq(const FEq &E, co
                                                                 bool (&und)[FP]) {
     if (E.eq4) {  // kernel-argument (wave-uniform) branch
         const bool hi = E.c.in == 12;
+        const uint32_t a_same = sadd(E.lv_same, E.c.stride), a_diff = sadd(E.lv_diff, E.c.stride);
+        const uint32_t a_null = sadd(E.c.null_level, E.c.stride);
 #pragma unroll
         for (int u = 0; u < FP; ++u) {
             const uint32_t a = hi ? ha[u].y : ha[u].x, b = hi ? hb[u].y : hb[u].x;
             const bool nul = a == 0xFFFFFFFFu || b == 0xFFFFFFFFu;
             und[u] = false;  // ids: equal ids are equal strings
-            const int level = nul ? E.c.null_level : (a == b ? E.lv_same : E.lv_diff);
-            acc[u] += (uint32_t)(level + 1) * E.c.stride;
+            acc[u] += nul ? a_null : (a == b ? a_same : a_diff);
         }
         (void)act;
         return;
