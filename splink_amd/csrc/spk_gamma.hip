@@ -842,11 +842,16 @@ __device__ int jw_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1
 // both rows' bit-planes are loaded in the same round trip as the records and the distance comes
 // from them alone (lev_rows_planes).  Rows without planes (> 64 units or a unit >= 256) go to the
 // global-memory pass.  A kernel of its own, so its register budget is not the JW path's.
+// The column descriptors come from LDS, so their pointers are generic: the records and planes are read through
+// global-address-space views (global_load, not flat -- a flat load also counts against lgkmcnt, so every wait on
+// it waits for the LDS reads too).
+typedef const __attribute__((address_space(1))) uint4 GU4;
+typedef const __attribute__((address_space(1))) RecMeta GMeta;
 __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level) {
     uint64_t pa[N_PLANES], pb[N_PLANES];
     {
-        const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
-        const uint4 *qb = reinterpret_cast<const uint4 *>(c1.planes + (int64_t)y * N_PLANES);
+        GU4 *qa = (GU4 *)(c0.planes + (int64_t)x * N_PLANES);
+        GU4 *qb = (GU4 *)(c1.planes + (int64_t)y * N_PLANES);
 #pragma unroll
         for (int i = 0; i < N_PLANES / 2; ++i) {
             const uint4 u = qa[i], v = qb[i];
@@ -856,7 +861,7 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
             pb[2 * i + 1] = ((uint64_t)v.w << 32) | v.z;
         }
     }
-    const RecMeta ma = c0.meta[x], mb = c1.meta[y];
+    const RecMeta ma = ((GMeta *)c0.meta)[x], mb = ((GMeta *)c1.meta)[y];
     if (ma.len16 < 0 || mb.len16 < 0) {
         level = sc.null_level;
         return ST_DONE;
@@ -1011,7 +1016,9 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
     const int32_t *items = xlist + xinfo[k];
     const int64_t stride = (int64_t)C.g * X_THREADS;
     // software pipeline: the next item's pair rows (and, for Levenshtein, the rows' lengths) are in
-    // flight while this one is evaluated
+    // flight while this one is evaluated, and the list entry after that one is read a round earlier still, so
+    // the pair-row loads of the next item never wait on its list entry (one memory round trip per cell, shared
+    // with the current cell's records and planes)
     int64_t i = bid * X_THREADS + threadIdx.x;
     int32_t p = -1, x = 0, y = 0, key = LEV_BINS - 1;  // p = -1: no cell (past the list, or a k_compact_lev slot)
     if (i < n) {
@@ -1019,6 +1026,7 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         x = A.pl[p < 0 ? 0 : p];
         y = A.pr[p < 0 ? 0 : p];
     }
+    int32_t pn = i + stride < n ? items[i + stride] : -1;  // the next item's list entry
     __syncthreads();
 #ifdef SPK_X_STAMPS
     x_t1 = wall_clock64();
@@ -1033,13 +1041,16 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
     for (int64_t base = bid * X_THREADS; base < n; base += stride) {  // block-uniform
         bool have = p >= 0;
         const int64_t i2 = i + stride;
-        int32_t p2 = -1, x2 = 0, y2 = 0, key2 = LEV_BINS - 1;
-        if (i2 < n) {
-            p2 = items[i2];
-            x2 = A.pl[p2 < 0 ? 0 : p2];
-            y2 = A.pr[p2 < 0 ? 0 : p2];
-            if (regroup && p2 >= 0) key2 = lev_work_bin(s_c0.meta[x2].len16, s_c1.meta[y2].len16);
-        }
+        // unconditional loads (clamped indices: pair 0 and the list's last entry are read harmlessly), so no
+        // divergent branch makes the compiler wait on the loads in flight
+        const int32_t p2 = i2 < n ? pn : -1;
+        const int32_t q2 = p2 < 0 ? 0 : p2;
+        const int32_t x2 = A.pl[q2], y2 = A.pr[q2];
+        int32_t key2 = LEV_BINS - 1;
+        if (regroup && p2 >= 0) key2 = lev_work_bin(s_c0.meta[x2].len16, s_c1.meta[y2].len16);
+        const int64_t i3 = i2 + stride;
+        const int32_t pn3 = items[i3 < n ? i3 : n - 1];
+        pn = i3 < n ? pn3 : -1;
         if (regroup) lev_sort_items(key, have, p, x, y);
         bool to_slow = false;
         if (have && regroup && key >= 128) {
