@@ -845,23 +845,29 @@ __device__ int jw_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1
 // The column descriptors come from LDS, so their pointers are generic: the records and planes are read through
 // global-address-space views (global_load, not flat -- a flat load also counts against lgkmcnt, so every wait on
 // it waits for the LDS reads too).
-typedef const __attribute__((address_space(1))) uint4 GU4;
-typedef const __attribute__((address_space(1))) RecMeta GMeta;
+typedef const __attribute__((address_space(1))) uint64_t GU64;
+__device__ __attribute__((always_inline)) inline RecMeta load_meta_global(const RecMeta *m, int64_t row) {
+    static_assert(sizeof(RecMeta) == 32, "RecMeta: four 8-byte words");
+    GU64 *q = (GU64 *)(m + row);
+    uint64_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = q[i];
+    RecMeta out;
+    __builtin_memcpy(&out, w, sizeof(out));
+    return out;
+}
 __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level) {
     uint64_t pa[N_PLANES], pb[N_PLANES];
     {
-        GU4 *qa = (GU4 *)(c0.planes + (int64_t)x * N_PLANES);
-        GU4 *qb = (GU4 *)(c1.planes + (int64_t)y * N_PLANES);
+        GU64 *qa = (GU64 *)(c0.planes + (int64_t)x * N_PLANES);
+        GU64 *qb = (GU64 *)(c1.planes + (int64_t)y * N_PLANES);
 #pragma unroll
-        for (int i = 0; i < N_PLANES / 2; ++i) {
-            const uint4 u = qa[i], v = qb[i];
-            pa[2 * i] = ((uint64_t)u.y << 32) | u.x;
-            pa[2 * i + 1] = ((uint64_t)u.w << 32) | u.z;
-            pb[2 * i] = ((uint64_t)v.y << 32) | v.x;
-            pb[2 * i + 1] = ((uint64_t)v.w << 32) | v.z;
+        for (int i = 0; i < N_PLANES; ++i) {
+            pa[i] = qa[i];
+            pb[i] = qb[i];
         }
     }
-    const RecMeta ma = ((GMeta *)c0.meta)[x], mb = ((GMeta *)c1.meta)[y];
+    const RecMeta ma = load_meta_global(c0.meta, x), mb = load_meta_global(c1.meta, y);
     if (ma.len16 < 0 || mb.len16 < 0) {
         level = sc.null_level;
         return ST_DONE;
