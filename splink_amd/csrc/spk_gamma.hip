@@ -1680,7 +1680,24 @@ __global__ __launch_bounds__(64) void k_gamma_huge(GammaArgs A, int k, const int
 // (non-Latin-1 or longer rows) runs the global-memory evaluation of k_gamma_slow.
 __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y,
                            int &level) {
-    const RecMeta ma = c0.meta[x], mb = c1.meta[y];
+    // One memory round trip: both rows' records, planes and upper planes are requested together (the upper
+    // planes unconditionally -- from the lower planes' own row when the column has none -- and masked by the
+    // records' flags afterwards), through global-address-space views.  Loading the upper planes only after the
+    // records said a row has them took two round trips more per cell (item, pair rows, records, planes).
+    const RecMeta ma = load_meta_global(c0.meta, x), mb = load_meta_global(c1.meta, y);
+    uint64_t la[N_PLANES], lb[N_PLANES], ua[N_PLANES], ub[N_PLANES];
+    {
+        GU64 *qa = (GU64 *)(c0.planes + (int64_t)x * N_PLANES), *qb = (GU64 *)(c1.planes + (int64_t)y * N_PLANES);
+        GU64 *ra = (GU64 *)((c0.planes_hi ? c0.planes_hi : c0.planes) + (int64_t)x * N_PLANES);
+        GU64 *rb = (GU64 *)((c1.planes_hi ? c1.planes_hi : c1.planes) + (int64_t)y * N_PLANES);
+#pragma unroll
+        for (int i = 0; i < N_PLANES; ++i) {
+            la[i] = qa[i];
+            lb[i] = qb[i];
+            ua[i] = ra[i];
+            ub[i] = rb[i];
+        }
+    }
     if (ma.len16 < 0 || mb.len16 < 0) {
         level = sc.null_level;
         return ST_DONE;
@@ -1688,31 +1705,12 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
     constexpr uint32_t ANY = CPF_PLANES | CPF_PLANES2;
     if (!(ma.cpf & ANY) || !(mb.cpf & ANY)) return ST_NEEDS_SLOW;
     if (((ma.cpf & CPF_PLANES2) && !c0.planes_hi) || ((mb.cpf & CPF_PLANES2) && !c1.planes_hi)) return ST_NEEDS_SLOW;
+    const uint64_t ka = (ma.cpf & CPF_PLANES2) ? ~0ull : 0ull, kb = (mb.cpf & CPF_PLANES2) ? ~0ull : 0ull;
     u128 pa[N_PLANES], pb[N_PLANES];
-    {
-        const uint4 *qa = reinterpret_cast<const uint4 *>(c0.planes + (int64_t)x * N_PLANES);
-        const uint4 *qb = reinterpret_cast<const uint4 *>(c1.planes + (int64_t)y * N_PLANES);
-        uint4 ha[N_PLANES / 2], hb[N_PLANES / 2];
 #pragma unroll
-        for (int i = 0; i < N_PLANES / 2; ++i) ha[i] = hb[i] = make_uint4(0, 0, 0, 0);
-        if (ma.cpf & CPF_PLANES2) {
-            const uint4 *ra = reinterpret_cast<const uint4 *>(c0.planes_hi + (int64_t)x * N_PLANES);
-#pragma unroll
-            for (int i = 0; i < N_PLANES / 2; ++i) ha[i] = ra[i];
-        }
-        if (mb.cpf & CPF_PLANES2) {
-            const uint4 *rb = reinterpret_cast<const uint4 *>(c1.planes_hi + (int64_t)y * N_PLANES);
-#pragma unroll
-            for (int i = 0; i < N_PLANES / 2; ++i) hb[i] = rb[i];
-        }
-#pragma unroll
-        for (int i = 0; i < N_PLANES / 2; ++i) {
-            const uint4 u = qa[i], v = qb[i];
-            pa[2 * i] = ((u128)(((uint64_t)ha[i].y << 32) | ha[i].x) << 64) | (((uint64_t)u.y << 32) | u.x);
-            pa[2 * i + 1] = ((u128)(((uint64_t)ha[i].w << 32) | ha[i].z) << 64) | (((uint64_t)u.w << 32) | u.z);
-            pb[2 * i] = ((u128)(((uint64_t)hb[i].y << 32) | hb[i].x) << 64) | (((uint64_t)v.y << 32) | v.x);
-            pb[2 * i + 1] = ((u128)(((uint64_t)hb[i].w << 32) | hb[i].z) << 64) | (((uint64_t)v.w << 32) | v.z);
-        }
+    for (int i = 0; i < N_PLANES; ++i) {
+        pa[i] = ((u128)(ua[i] & ka) << 64) | la[i];
+        pb[i] = ((u128)(ub[i] & kb) << 64) | lb[i];
     }
     int eq = meta_equal(ma, mb);
     if (eq < 0) {  // equal keys without dictionary ids: the planes are the units
@@ -1766,12 +1764,26 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int s
     int32_t *rest = xlist + xinfo[k];
     // (regrouping these cells by work bin, as k_gamma_exact_simple does for free-text columns,
     // measured no faster here: 2.43-2.47 ms per cfg5 call either way)
-    for (int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * X_THREADS) {
-        const int32_t p = items[i];
+    // Software pipeline as the exact pass: the next cell's pair rows are in flight during this cell's scan, and
+    // the list entry after that one a round earlier still (unconditional loads at clamped indices).
+    const int64_t stride = (int64_t)gridDim.x * X_THREADS;
+    int64_t i = (int64_t)blockIdx.x * X_THREADS + threadIdx.x;
+    if (n <= 0) return;
+    int32_t p = items[i < n ? i : n - 1];
+    int32_t x = A.pl[p], y = A.pr[p];
+    int32_t pn = items[i + stride < n ? i + stride : n - 1];
+    for (; i < n; i += stride) {
+        const int32_t x2 = A.pl[pn], y2 = A.pr[pn];
+        const int64_t i3 = i + 2 * stride;
+        const int32_t pn3 = items[i3 < n ? i3 : n - 1];
         int level = 0;
-        const bool done = lev_cell128(s_sc, s_c0, s_c1, A.pl[p], A.pr[p], level) == ST_DONE;
+        const bool done = lev_cell128(s_sc, s_c0, s_c1, x, y, level) == ST_DONE;
         if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
         wave_append(rest, A.slow_count + A.K + k, !done, p);
+        p = pn;
+        x = x2;
+        y = y2;
+        pn = pn3;
     }
 }
 
