@@ -468,11 +468,14 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
     const uint32_t end = (uint32_t)r1;
     uint32_t base = (uint32_t)r0 + (uint32_t)(threadIdx.x >> 6) * SPAN;
     int32_t nx[FP], ny[FP];
+    // pair rows of the lane's next pairs: unconditional loads at clamped ordinals (inactive lanes re-read the
+    // region's last pair harmlessly), so no divergent branch sits between them and the field gathers
+    const uint32_t last = end > (uint32_t)r0 ? end - 1 : (uint32_t)r0;
 #pragma unroll
     for (int u = 0; u < FP; ++u) {
         const uint32_t q = base + u * 64 + lane;
-        nx[u] = q < end ? A.pl[q] : 0;  // inactive lanes read row 0 harmlessly
-        ny[u] = q < end ? A.pr[q] : 0;
+        nx[u] = A.pl[q < end ? q : last];
+        ny[u] = A.pr[q < end ? q : last];
     }
     for (; base < end; base += STEP) {  // wave-uniform
         uint32_t p[FP], ox[FP], oy[FP], acc[FP];
@@ -484,9 +487,17 @@ __global__ __launch_bounds__(F_THREADS, MINW) void k_filter(const FiltArgs A) {
             ox[u] = (uint32_t)nx[u] << 4;
             oy[u] = (uint32_t)ny[u] << 4;
             acc[u] = 0;
+        }
+        // The next pairs' rows are requested only after this iteration's row offsets are taken from the last
+        // ones: hoisted above the shifts, the loads made the compiler wait for them right there (s_waitcnt
+        // vmcnt(0) at the loop head), so every iteration paid the pair-row and the field-gather round trips one
+        // after the other instead of together.
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < FP; ++u) {
             const uint32_t q = p[u] + STEP;
-            nx[u] = q < end ? A.pl[q] : 0;
-            ny[u] = q < end ? A.pr[q] : 0;
+            nx[u] = A.pl[q < end ? q : last];
+            ny[u] = A.pr[q < end ? q : last];
         }
 #pragma unroll 1
         for (int j = 0; j < A.nj; ++j) {
