@@ -2278,9 +2278,26 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         jw.col[jw.n] = sc.col;
         jw.si[jw.n++] = G.simple_of[k];
     }
-    if (jk.n)
-        k_compact<<<dim3((unsigned)G.n_regions, (unsigned)jk.n), 256, 0, ctx->stream>>>(A, jk, ctx->xpref.p,
-                                                                                       ctx->xlist.p, ctx->xinfo.p);
+    // One compaction launch for the JW lists and the other plain-compacted lists (up to four columns): the
+    // launch is one workgroup per region and column, and a short list's workgroups cost dispatch rounds alone
+    // (cfg2: the JW lists' launch took as long as the email list's, 15 us each)
+    ColSet pre = jk;
+    for (int k = 0; k < K && pre.n < 4; ++k) {
+        if (!G.may_exact[k]) continue;
+        const int si = G.simple_of[k];
+        bool in_jw = false;
+        for (int c = 0; c < jw.n; ++c) in_jw = in_jw || jw.si[c] == si;
+        if (in_jw || (si >= 0 && simple[si].cls == SC_LEV && G.bag[k])) continue;
+        pre.k[pre.n++] = k;
+    }
+    auto precompacted = [&](int k) {
+        for (int c = 0; c < pre.n; ++c)
+            if (pre.k[c] == k) return true;
+        return false;
+    };
+    if (pre.n)
+        k_compact<<<dim3((unsigned)G.n_regions, (unsigned)pre.n), 256, 0, ctx->stream>>>(A, pre, ctx->xpref.p,
+                                                                                        ctx->xlist.p, ctx->xinfo.p);
     // (running this launch on a second stream beside the Levenshtein pass measured no faster:
     // 1.198-1.205 ms per cfg2 pass either way)
     for (int c = 0; c < K; ++c)
@@ -2310,7 +2327,7 @@ static int enqueue_phase(spk_ctx *ctx, GammaPlan &G, int64_t cap, bool skip = fa
         if (lev && G.bag[k])
             k_compact_lev<<<(unsigned)G.n_regions, CL_THREADS, 0, ctx->stream>>>(A, k, si, ctx->xpref.p, ctx->xlist.p,
                                                                                 ctx->xinfo.p);
-        else
+        else if (!precompacted(k))
             k_compact<<<(unsigned)G.n_regions, 256, 0, ctx->stream>>>(A, one_k, ctx->xpref.p, ctx->xlist.p, ctx->xinfo.p);
         if (refill) {
             // one resident round (LEVQ_WAVES per SIMD, 3 for NP = 8): every wave owns a contiguous range of the list
