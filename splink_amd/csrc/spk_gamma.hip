@@ -556,7 +556,16 @@ __global__ void k_compact(GammaArgs A, ColSet cs, const int64_t *__restrict__ xp
     const int32_t *src = region_list(A, k, R);
     const int64_t n = A.region_count[(int64_t)k * A.n_regions + blockIdx.x];
     int32_t *dst = xlist + xinfo[k] + pref[blockIdx.x];
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    // four entries per thread in flight before their stores (a long region's copy is latency-bound otherwise)
+    const int64_t bd = blockDim.x;
+    for (int64_t i = threadIdx.x; i < n; i += 4 * bd) {
+        int32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = i + u * bd < n ? src[i + u * bd] : 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u * bd < n) dst[i + u * bd] = v[u];
+    }
 }
 
 __device__ inline int64_t exact_count(const GammaArgs &A, const int64_t *xinfo, int k) {
