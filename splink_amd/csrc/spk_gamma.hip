@@ -1666,7 +1666,9 @@ __global__ __launch_bounds__(64) void k_gamma_slow(GammaArgs A, ColSet cs, int32
         const int32_t p = items[i];
         int level = 0;
         const bool done = eval_column<M_SLOW>(A, k, A.pl[p], A.pr[p], nullptr, nullptr, level) == ST_DONE;
-        if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        // several columns in one launch (the fused JW lists) can hold the same pair: their adds to its code race
+        if (done && cs.n > 1) code_add_atomic(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
+        else if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
         wave_append(huge, A.slow_count + 2 * A.K + k, !done, p);
     }
 }
