@@ -295,6 +295,42 @@ def test_levenshtein_cut_around_thresholds(amd):
     _lev_variants_agree(gf.job, gf.settings, got)
 
 
+def test_fused_jw_slow_lists_of_one_pair(amd):
+    """Two Jaro-Winkler columns share one exact launch and one slow-list launch (k_gamma_slow over both lists).
+    When BOTH of a pair's cells are past the exact pass's 64 units they are on both slow lists, and the two
+    columns' adds to the pair's one packed code must not race (round 6: they were plain read-modify-writes).
+    Every pair here has long, similar first names and surnames, so most cells of both columns take the slow
+    lists; the codes must match the oracle's comparison vectors exactly."""
+    from splink_amd.engine import Job
+    from splink_amd.settings import complete_settings_dict
+    rng = np.random.Generator(np.random.PCG64(91))
+    n = 360
+    base_f, base_s = "Maximiliana-Theodora-" * 3, "Vanderbilt-Oosterhuizen-" * 3
+
+    def noisy(base):
+        s = list(base + "".join(rng.choice(list("abcdefgh"), 6)))
+        for _ in range(int(rng.integers(0, 6))):
+            s[int(rng.integers(len(s)))] = str(rng.choice(list("xyzqw")))
+        return "".join(s)
+
+    df = pd.DataFrame({"unique_id": np.arange(n), "first_name": [noisy(base_f) for _ in range(n)],
+                       "surname": [noisy(base_s) for _ in range(n)]})
+    st = complete_settings_dict({"link_type": "dedupe_only", "blocking_rules": [],
+                                 "comparison_columns": [{"col_name": "first_name", "num_levels": 3},
+                                                        {"col_name": "surname", "num_levels": 3}]}, amd)
+    job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block([])
+    job.gammas(st)
+    got = job.gammas_host()
+    l, r = job.pair_rows()
+    t = job.tables[0]
+    cols = [orc.StrCol(t[c].tolist()) for c in ("first_name", "surname")]
+    want = orc.template_gammas([("jw", 3, [0.94, 0.88]), ("jw", 3, [0.94, 0.88])], cols, cols, l, r)
+    assert len(got) == n * (n - 1) // 2
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert len(bad) == 0, (len(bad), got[bad[:5]], want[bad[:5]])
+
+
 def test_jw_filter_field_edges(amd):
     """The filter bounds a Jaro-Winkler column from the row image's fields: the sketch (matches) and the
     four head units (the Winkler prefix, which this jar does not cap at four).  Pairs at those edges --
