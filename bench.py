@@ -34,10 +34,10 @@ warnings.filterwarnings("ignore")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 # HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same command
 # (scripts_gpu_round.sh -> tools/traffic.py); the counters cannot be read inside a timed run.
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r5_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r6_traffic.json")
 # per-kernel issue counters of the same command (rocprofv3 --pmc passes, tools/pmc_summary.py)
-PMC_FILE = os.path.join(ROOT, "profiles", "r5_pmc_kernels.json")
-PMC_FILE_CFG5 = os.path.join(ROOT, "profiles", "r5_cfg5_lev_pmc.json")  # tools/gpu/pmc_cfg5_lev.sh
+PMC_FILE = os.path.join(ROOT, "profiles", "r6_pmc_kernels.json")
+PMC_FILE_CFG5 = os.path.join(ROOT, "profiles", "r6_cfg5_lev_pmc.json")  # tools/gpu/pmc_cfg5_lev.sh
 COLS = ["first_name", "surname", "dob", "city", "email"]
 WORKLOADS = {2: "cfg2: synthetic person-record dedupe, 1M x sqrt(N) records, blocking surname|dob, "
                 "5 comparison columns (JW-3 x2, exact-2 x2, Levenshtein-3)",

@@ -765,6 +765,39 @@ __device__ inline int simple_lev_cut(const SimpleCol &sc, int ncp_a, int ncp_b) 
     return cut;
 }
 
+// Per len_l + len_r (S < S_MAX): the scan's cut and each test's largest passing distance for unequal strings
+// (the filter's integer forms: lev_a, the host's ratio tables), and *tab = 1 when every test is a `<=` / `<` on
+// the distance or a string (in)equality, so a cell's level is a table lookup.  Callers barrier after it.
+template <int S_MAX, int CUT_MAX>
+__device__ inline void lev_tables(const GammaArgs &A, const SimpleCol &sc, uint8_t *s_cut, int16_t (*s_bp)[MAX_TESTS],
+                                  int *tab) {
+    for (int S = threadIdx.x; S < S_MAX; S += X_THREADS) {  // blocks of X_THREADS
+        const int c = simple_lev_cut(sc, S, 0);
+        s_cut[S] = (uint8_t)(c < CUT_MAX ? c : CUT_MAX);
+        for (int i = 0; i < sc.n_tests; ++i) {
+            int bp = -1;
+            if (sc.op[i] == SPK_OP_STR_CMP) bp = sc.cmp[i] == SPK_CMP_EQ ? -1 : CUT_MAX + 1;
+            else if (sc.op[i] == SPK_OP_LEV) bp = sc.lev_a[i];
+            else if (sc.thr_off[i] >= 0 && S < THR_S) bp = A.thr[sc.thr_off[i] + S];
+            else if (sc.thr_off[i] >= 0) {  // len_l + len_r past the host tables (WW = 2: S = 256): the same scan
+                const double den = (double)S / 2.0;
+                for (int v = 0; v <= CUT_MAX + 1 && cmpd((double)v / den, sc.t[i], sc.cmp[i]) == KT; ++v) bp = v;
+            }
+            s_bp[S][i] = (int16_t)(bp < -1 ? -1 : (bp > CUT_MAX + 1 ? CUT_MAX + 1 : bp));
+        }
+    }
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        for (int i = 0; i < sc.n_tests; ++i) {
+            const int op = sc.op[i];
+            if (op == SPK_OP_LEV) ok &= (sc.tflag[i] & (TF_GE | TF_EXACT)) ? 0 : 1;
+            else if (op == SPK_OP_LEVRATIO) ok &= sc.thr_off[i] >= 0 ? 1 : 0;
+            else ok &= op == SPK_OP_STR_CMP ? 1 : 0;
+        }
+        *tab = ok;
+    }
+}
+
 __device__ int simple_exact(const GammaArgs &A, const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x,
                             int32_t y, int &level) {
     uint64_t pa[N_PLANES], pb[N_PLANES];
@@ -865,7 +898,9 @@ __device__ __attribute__((always_inline)) inline RecMeta load_meta_global(const 
     __builtin_memcpy(&out, w, sizeof(out));
     return out;
 }
-__device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level) {
+// cutt / bpt: lev_tables' per len_l + len_r cut and thresholds for a 64-bit scan (nullptr: the tests one by one)
+__device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y, int &level,
+                        const uint8_t *cutt = nullptr, const int16_t (*bpt)[MAX_TESTS] = nullptr) {
     uint64_t pa[N_PLANES], pb[N_PLANES];
     {
         GU64 *qa = (GU64 *)(c0.planes + (int64_t)x * N_PLANES);
@@ -900,7 +935,17 @@ __device__ int lev_cell(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c
                 if (lev < 0) {
                     if (eq == 1) lev = 0;
                     else if (!planes) return ST_NEEDS_SLOW;
-                    else lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
+                    else {
+                        const int S = na + nb;  // <= 128: rows of <= 64 units
+                        lev = lev_rows_planes(pa, ma.len16, pb, mb.len16, bpt != nullptr ? (int)cutt[S] : simple_lev_cut(sc, na, nb),
+                                              sc.np);
+                        if (bpt != nullptr) {  // levels by table: the tests before this one failed for eq = 0 too
+                            int lv = sc.else_level;
+                            for (int j = sc.n_tests - 1; j >= 0; --j) lv = lev <= bpt[S][j] ? sc.level[j] : lv;
+                            level = lv;
+                            return ST_DONE;
+                        }
+                    }
                 }
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
@@ -1007,6 +1052,10 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
                                                                    const int32_t *xlist, const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
     __shared__ ColDesc s_c0, s_c1;
+    constexpr int XS_MAX = MODE == X_LEV ? 129 : 1;  // len_l + len_r of 64-bit rows, plus one
+    __shared__ uint8_t s_cut[XS_MAX];
+    __shared__ int16_t s_bp[XS_MAX][MAX_TESTS];
+    __shared__ int s_tab;
 #ifdef SPK_X_STAMPS
     unsigned long long x_t0 = wall_clock64(), x_cells = 0, x_t1 = 0, x_t2 = 0;
 #endif
@@ -1047,10 +1096,15 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
     x_t1 = wall_clock64();
 #endif
     const SimpleCol &sc = s_sc;
+    constexpr bool LEV = MODE == X_LEV;
+    if constexpr (LEV) {
+        lev_tables<XS_MAX, XS_MAX - 2>(A, sc, s_cut, s_bp, &s_tab);
+        __syncthreads();
+    }
+    const bool tab = LEV && s_tab != 0;  // block-uniform
     // Regroup by work bin only in free-text columns (rows past 64 units, so planes_hi exists): there the
     // trip counts spread widely (cfg5 addresses: 2.98 -> 2.67 ms per call).  In short-string columns
     // the sort's barriers cost more than it saves (cfg2 email: 475 -> 505 us), so they keep the old order.
-    constexpr bool LEV = MODE == X_LEV;
     const bool regroup = LEV && s_c0.planes_hi != nullptr && s_c1.planes_hi != nullptr;  // block-uniform
     if (regroup && p >= 0) key = lev_work_bin(s_c0.meta[x].len16, s_c1.meta[y].len16);
     for (int64_t base = bid * X_THREADS; base < n; base += stride) {  // block-uniform
@@ -1075,7 +1129,8 @@ __global__ __launch_bounds__(X_THREADS, XW) void k_gamma_exact_simple(GammaArgs 
         } else if (have) {
             int level = 0;
             int st;
-            if constexpr (MODE == X_LEV) st = lev_cell(sc, s_c0, s_c1, x, y, level);
+            if constexpr (MODE == X_LEV)
+                st = lev_cell(sc, s_c0, s_c1, x, y, level, s_cut, tab ? s_bp : nullptr);
             else if constexpr (MODE == X_JW) st = jw_cell(sc, s_c0, s_c1, x, y, level);
             else st = simple_exact(A, sc, s_c0, s_c1, x, y, level);
 #ifdef SPK_X_STAMPS
@@ -1214,32 +1269,7 @@ __global__ __launch_bounds__(X_THREADS, WW == 2 ? 2 : (NP == 8 ? 3 : LEVQ_WAVES)
     }
     __syncthreads();
     const SimpleCol &sc = s_sc;
-    // per len_l + len_r: the cut and each test's threshold (the filter's integer forms: lev_a, the ratio tables)
-    for (int S = threadIdx.x; S < S_MAX; S += X_THREADS) {
-        const int c = simple_lev_cut(sc, S, 0);
-        s_cut[S] = (uint8_t)(c < CUT_MAX ? c : CUT_MAX);
-        for (int i = 0; i < sc.n_tests; ++i) {
-            int bp = -1;
-            if (sc.op[i] == SPK_OP_STR_CMP) bp = sc.cmp[i] == SPK_CMP_EQ ? -1 : CUT_MAX + 1;
-            else if (sc.op[i] == SPK_OP_LEV) bp = sc.lev_a[i];
-            else if (sc.thr_off[i] >= 0 && S < THR_S) bp = A.thr[sc.thr_off[i] + S];
-            else if (sc.thr_off[i] >= 0) {  // len_l + len_r past the host tables (WW = 2: S = 256): the same scan
-                const double den = (double)S / 2.0;
-                for (int v = 0; v <= CUT_MAX + 1 && cmpd((double)v / den, sc.t[i], sc.cmp[i]) == KT; ++v) bp = v;
-            }
-            s_bp[S][i] = (int16_t)(bp < -1 ? -1 : (bp > CUT_MAX + 1 ? CUT_MAX + 1 : bp));
-        }
-    }
-    if (threadIdx.x == 0) {  // every test a `<=` / `<` on the distance or a string (in)equality: levels by table
-        int ok = 1;
-        for (int i = 0; i < sc.n_tests; ++i) {
-            const int op = sc.op[i];
-            if (op == SPK_OP_LEV) ok &= (sc.tflag[i] & (TF_GE | TF_EXACT)) ? 0 : 1;
-            else if (op == SPK_OP_LEVRATIO) ok &= sc.thr_off[i] >= 0 ? 1 : 0;
-            else ok &= op == SPK_OP_STR_CMP ? 1 : 0;
-        }
-        s_tab = ok;
-    }
+    lev_tables<S_MAX, CUT_MAX>(A, sc, s_cut, s_bp, &s_tab);
     __syncthreads();
     const bool tab = s_tab != 0;
     const int k = sc.k, n_tests = sc.n_tests;
