@@ -604,8 +604,9 @@ __device__ inline int bag_inter_ub(const uint4 &a0, const uint4 &a1, const uint4
 // here (its level is lev_cell's for any distance past the cut), one with a row past 64 units goes straight to
 // the slow list; the others are packed to the front of the
 // region's slice of the list in order, and the slice's tail is -1, which the exact passes skip (whole waves of
-// it, mostly).  0.206 ms per cfg5 call; four cells per thread per round (their loads in flight together) took
-// 0.260, and unordered packing through one LDS counter per workgroup (no barriers) 0.210.
+// it, mostly).  0.206 ms per cfg5 call (round 5); four cells per thread per round (their loads in flight together)
+// took 0.260, and unordered packing through one LDS counter per workgroup (no barriers) 0.210.  Round 6 sorts the
+// slow cells (0.272 ms) and pipelines the loads across rounds (0.242 ms, profiles/r6_ab_compact_lev_pipeline.log).
 constexpr int CL_THREADS = 256;
 constexpr int CL_SLOW = 1024;  // LDS buffer of slow-list cells per workgroup
 __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, int si, const int64_t *__restrict__ xpref,
@@ -665,23 +666,39 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
         if (threadIdx.x == 0) s_ns = 0;
     };
     int64_t kept = 0;  // block-uniform
+    // software pipeline: the next round's pair rows and the list entry after that are in flight with this
+    // round's bag rows, so a round waits on one memory round trip instead of three
+    int32_t pc = 0, xc = 0, yc = 0;
+    if (threadIdx.x < n) {
+        pc = src[threadIdx.x];
+        xc = A.pl[pc];
+        yc = A.pr[pc];
+    }
+    int32_t pn = threadIdx.x + CL_THREADS < n ? src[threadIdx.x + CL_THREADS] : 0;
     for (int64_t i0 = 0; i0 < n; i0 += CL_THREADS) {
         const int64_t i = i0 + threadIdx.x;
+        // unconditional loads at clamped indices (pair 0's rows, the list's last entry), no branch around them:
+        // this round's bag rows, the next round's pair rows, the list entry after that
+        const uint4 a0 = bag0[2 * (int64_t)xc], a1 = bag0[2 * (int64_t)xc + 1];
+        const uint4 b0 = bag1[2 * (int64_t)yc], b1 = bag1[2 * (int64_t)yc + 1];
+        const int64_t i2 = i + CL_THREADS, i3 = i2 + CL_THREADS;
+        const int32_t p2 = i2 < n ? pn : 0;
+        const int32_t x2 = A.pl[p2], y2 = A.pr[p2];
+        pn = src[i3 < n ? i3 : n - 1];
+        __builtin_amdgcn_sched_barrier(0);  // all issued before the first wait
+        // the bound before any branch on the rows' lengths, so no load is sunk into one (two round trips)
+        const int la = (int)(a1.w >> 24), lb = (int)(b1.w >> 24);
+        int inter = bag_inter_ub(a0, a1, b0, b1);
         bool keep = false, slow = false;
-        int32_t p = 0;
+        const int32_t p = pc;
         int skey = 0;
         if (i < n) {
-            p = src[i];
             keep = true;
-            const int64_t x = A.pl[p], y = A.pr[p];
-            const uint4 a0 = bag0[2 * x], a1 = bag0[2 * x + 1], b0 = bag1[2 * y], b1 = bag1[2 * y + 1];
-            const int la = (int)(a1.w >> 24), lb = (int)(b1.w >> 24);
             if (la != 255 && lb != 255) {
                 // a row past 64 units has no 64-bit planes: the exact pass would only pass the cell on to the
                 // 128-bit slow pass, after loading its rows -- it goes to the slow list from here
                 slow = la > 64 || lb > 64;
                 skey = la < lb ? la : lb;  // <= 128: rows with bag rows have at most 128 units
-                int inter = bag_inter_ub(a0, a1, b0, b1);
                 if (inter >= 0) {
                     const int mn = la < lb ? la : lb, mx = la < lb ? lb : la;
                     inter = inter < mn ? inter : mn;
@@ -719,6 +736,9 @@ __global__ __launch_bounds__(CL_THREADS) void k_compact_lev(GammaArgs A, int k, 
         kept += tot;
         if (s_ns > CL_SLOW - CL_THREADS || i0 + CL_THREADS >= n) flush_slow();  // block-uniform (after the barrier)
         __syncthreads();
+        pc = p2;
+        xc = x2;
+        yc = y2;
     }
     for (int64_t i = kept + threadIdx.x; i < n; i += CL_THREADS) dst[i] = -1;
 }
