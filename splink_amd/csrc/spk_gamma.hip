@@ -1739,6 +1739,7 @@ __global__ __launch_bounds__(64) void k_gamma_huge(GammaArgs A, int k, const int
 // PLANES2_MAX units (CPF_PLANES / CPF_PLANES2) are exact from 128-bit planes in registers
 // (lev_rows_planes128) -- free-text columns such as cfg5's addresses land here; any other cell
 // (non-Latin-1 or longer rows) runs the global-memory evaluation of k_gamma_slow.
+template <bool P8>
 __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc &c1, int32_t x, int32_t y,
                            int &level) {
     // One memory round trip: both rows' records, planes and upper planes are requested together (the upper
@@ -1793,7 +1794,7 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
                 r = KN;
             } else {
                 if (lev < 0)
-                    lev = eq == 1 ? 0 : lev_rows_planes128(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
+                    lev = eq == 1 ? 0 : lev_rows_planes128<P8>(pa, ma.len16, pb, mb.len16, simple_lev_cut(sc, na, nb), sc.np);
                 r = op == SPK_OP_LEV ? cmpd((double)lev, t, cmp) : cmpd((double)lev / den, t, cmp);
             }
         }
@@ -1809,6 +1810,7 @@ __device__ int lev_cell128(const SimpleCol &sc, const ColDesc &c0, const ColDesc
 // Cells without planes on both rows are handed on (rest list: column k's exact-list region, free
 // once the exact pass ran, and counter slow_count[K + k]) to k_gamma_rest, so this kernel does not
 // carry the general interpreter's registers (the 128-bit scan alone holds ~100).
+template <bool P8>  // the column's scans read all 8 planes (SimpleCol.np == 8)
 __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int si, int32_t *xlist,
                                                               const int64_t *xinfo) {
     __shared__ SimpleCol s_sc;
@@ -1838,7 +1840,7 @@ __global__ __launch_bounds__(X_THREADS) void k_gamma_slow_lev(GammaArgs A, int s
         const int64_t i3 = i + 2 * stride;
         const int32_t pn3 = items[i3 < n ? i3 : n - 1];
         int level = 0;
-        const bool done = lev_cell128(s_sc, s_c0, s_c1, x, y, level) == ST_DONE;
+        const bool done = lev_cell128<P8>(s_sc, s_c0, s_c1, x, y, level) == ST_DONE;
         if (done) code_add(A, p, (uint32_t)(level + 1) * (uint32_t)A.stride[k]);
         wave_append(rest, A.slow_count + A.K + k, !done, p);
         p = pn;
@@ -2290,7 +2292,10 @@ static int enqueue_slow(spk_ctx *ctx, GammaPlan &G, int k, const ColSet *jk) {
             // round 6)
             constexpr int SLOWLEV_WG_PER_CU = 8;  // the 128-bit scan holds 3 waves per SIMD: 3 workgroups per CU at once
             const int64_t g_sl = std::max<int64_t>(1, std::min<int64_t>(G.g_exact, (int64_t)SLOWLEV_WG_PER_CU * ctx->n_cu));
-            k_gamma_slow_lev<<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
+            if (G.simple[si].np >= N_PLANES)
+                k_gamma_slow_lev<true><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
+            else
+                k_gamma_slow_lev<false><<<(unsigned)g_sl, X_THREADS, 0, ctx->stream>>>(A, si, ctx->xlist.p, ctx->xinfo.p);
             k_gamma_rest<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, k, ctx->xlist.p, ctx->xinfo.p);
         } else {
             k_gamma_slow<<<(unsigned)(4 * ctx->n_cu), 64, 0, ctx->stream>>>(A, one_k, ctx->xlist.p, ctx->xinfo.p);

@@ -786,9 +786,131 @@ __device__ inline int myers_plane_text128_lazy(const u128 (&P)[N_PLANES], int m,
     return dist > cut ? cut + 1 : dist;
 }
 
+// Patterns of 65..128 units in Ukkonen's diagonal band, held in one BW-bit word (Hyyro's banded
+// bit-vector form).  With d = i - j (pattern row minus text column) and dm = m - n, a path of cost
+// <= cut through a cell needs |d| + |d - dm| <= cut, so only diagonals [dlo, dhi] = [-((cut - dm) >> 1),
+// (cut + dm) >> 1] matter: at most cut + 1 of them (cfg5's 65..128-unit addresses: cut <= 52).  At column
+// c the word holds the vertical deltas of rows s + 1 .. s + BW with s = max(0, c + dlo - 1), the row above
+// it tracked as a score.  Moving to the next column drops the top row into the score (its value becomes
+// D[s][c - 1] + 1, the rows entering below take D[row - 1] + 1: both >= the true values, and a cell of an
+// optimal path of cost <= cut never reads one of them), and the text unit's match mask is the pattern's
+// window [s, s + BW) (a funnel shift of a per-32-column window of the planes).  Every distance <= cut
+// comes out exact, every larger one > cut.  The early exit reads the end cell's diagonal as the other
+// scans do: from that row the score plus the diagonal gap |d - dm| never decreases along the column (one
+// row changes the score by at most 1 and the gap by exactly 1), so a score > cut there bounds every
+// cell of the column.  Columns with s = 0 (j <= -dlo) run the plain scan over rows 1..BW first.
+// Host emulation against a full DP (180 k random cells, BW = 32 and 64) before building.
+template <int NP, int BW>
+__device__ inline int myers_plane_text128_band(const u128 (&P)[N_PLANES], int m, const u128 (&T)[N_PLANES], int n,
+                                               int cut, int dlo) {
+    typedef typename std::conditional<BW == 64, uint64_t, uint32_t>::type W;
+    constexpr int NQ = BW / 32 + 1;  // window dwords per plane
+    const int dm = m - n;
+    const int mine = 1 - dlo;  // columns j < mine have s = 0
+    int lo = 0, hi = 128;      // wave minimum by bisection over ballots
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (__ballot(mine <= mid)) hi = mid;
+        else lo = mid + 1;
+    }
+    const int J1 = lo;
+    W vp = ~(W)0, vn = 0;
+    {
+        W pl[N_PLANES];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) pl[b] = (W)P[b];
+        const int j1 = n < J1 ? n : J1;
+        for (int h = 0; h < 4 && 32 * h < j1; ++h) {
+            uint32_t tw[N_PLANES];
+#pragma unroll
+            for (int b = 0; b < N_PLANES; ++b) tw[b] = (uint32_t)(T[b] >> (32 * h));
+            const int jn = j1 - 32 * h < 32 ? j1 - 32 * h : 32;
+            for (int jj = 0; jj < jn; ++jj) {
+                W eq = ~(W)0;
+#pragma unroll
+                for (int b = 0; b < NP; ++b)
+                    eq = eq_plane(eq, (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1), pl[b]);
+                const W x = eq | vn;
+                const W d0 = (((x & vp) + vp) ^ vp) | x;
+                const W hp = (vn | ~(d0 | vp)) << 1 | (W)1;
+                const W hn = (d0 & vp) << 1;
+                vp = hn | ~(d0 | hp);
+                vn = hp & d0;
+                // row i* = j + 1 + dm <= 1 - dlo + dm <= the band's width: inside the word
+                if ((jj & 3) == 3 && diag_score<W>(vp, vn, 32 * h + jj, m, n) > cut) return cut + 1;
+            }
+        }
+    }
+    if (n <= J1) {  // s = 0 at the end, so m <= the band's width <= BW
+        const W M = low_mask<W>(m);
+        const int dist = n + popc_w(vp & M) - popc_w(vn & M);
+        return dist > cut ? cut + 1 : dist;
+    }
+    int s = 0, D = 0;  // band offset; deltas of the rows dropped above it (the score of row s is c + D)
+    for (int h = J1 >> 5; h < 4 && 32 * h < n; ++h) {
+        const int jb = 32 * h < J1 ? J1 - 32 * h : 0;
+        const int jn = n - 32 * h < 32 ? n - 32 * h : 32;
+        const int sb = 32 * h + jb + dlo > 0 ? 32 * h + jb + dlo : 0;  // s at the chunk's first column
+        uint32_t tw[N_PLANES], wq[N_PLANES][NQ];
+#pragma unroll
+        for (int b = 0; b < N_PLANES; ++b) {
+            tw[b] = (uint32_t)(T[b] >> (32 * h));
+            const u128 v = P[b] >> sb;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) wq[b][q] = (uint32_t)(v >> (32 * q));
+        }
+        for (int jj = jb; jj < jn; ++jj) {
+            const int j = 32 * h + jj;
+            const uint32_t sh = j + dlo > 0 ? 1u : 0u;
+            // the top row leaves the word (its delta into D), a +1 row enters below
+            if constexpr (BW == 64) {
+                const uint32_t pl0 = (uint32_t)vp, ph0 = (uint32_t)(vp >> 32);
+                const uint32_t nl0 = (uint32_t)vn, nh0 = (uint32_t)(vn >> 32);
+                D += (int)__builtin_amdgcn_ubfe(pl0, 0, sh) - (int)__builtin_amdgcn_ubfe(nl0, 0, sh);
+                vp = ((uint64_t)__builtin_amdgcn_alignbit(~0u, ph0, sh) << 32) | __builtin_amdgcn_alignbit(ph0, pl0, sh);
+                vn = ((uint64_t)__builtin_amdgcn_alignbit(0u, nh0, sh) << 32) | __builtin_amdgcn_alignbit(nh0, nl0, sh);
+            } else {
+                D += (int)__builtin_amdgcn_ubfe((uint32_t)vp, 0, sh) - (int)__builtin_amdgcn_ubfe((uint32_t)vn, 0, sh);
+                vp = __builtin_amdgcn_alignbit(~0u, (uint32_t)vp, sh);
+                vn = __builtin_amdgcn_alignbit(0u, (uint32_t)vn, sh);
+            }
+            s += (int)sh;
+            const uint32_t k = (uint32_t)(s - sb);  // 0..31
+            uint32_t e[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) e[q] = ~0u;
+#pragma unroll
+            for (int b = 0; b < NP; ++b) {
+                const uint32_t tb = (uint32_t)__builtin_amdgcn_sbfe((int)tw[b], jj, 1);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) e[q] = eq_plane(e[q], tb, wq[b][q]);
+            }
+            W eq;
+            if constexpr (BW == 64)
+                eq = ((uint64_t)__builtin_amdgcn_alignbit(e[2], e[1], k) << 32) | __builtin_amdgcn_alignbit(e[1], e[0], k);
+            else
+                eq = __builtin_amdgcn_alignbit(e[1], e[0], k);
+            const W x = eq | vn;
+            const W d0 = (((x & vp) + vp) ^ vp) | x;
+            const W hp = (vn | ~(d0 | vp)) << 1 | (W)1;
+            const W hn = (d0 & vp) << 1;
+            vp = hn | ~(d0 | hp);
+            vn = hp & d0;
+            if ((jj & 3) == 3) {  // the end cell's diagonal, row j + 1 + dm: bit j + dm - s of the word
+                const W M = low_mask<W>(j + 1 + dm - s);
+                if (j + 1 + D + popc_w(vp & M) - popc_w(vn & M) > cut) return cut + 1;
+            }
+        }
+    }
+    const W M = low_mask<W>(m - s);
+    const int dist = n + D + popc_w(vp & M) - popc_w(vn & M);
+    return dist > cut ? cut + 1 : dist;
+}
+
 // lev_rows_planes for rows of up to 128 units held as 128-bit planes (bits past a row's length are
 // zero).  After the common prefix and suffix are stripped, a pattern of <= 64 units runs the
-// one-word scan (the same word width for the whole wave), else the 128-bit one.
+// one-word scan (the same word width for the whole wave), else the banded scan in 32- or 64-bit words
+// when every lane's band fits one (the same width for the whole wave), else the 128-bit one.
 template <int NP>
 __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
                                             int cut) {
@@ -827,16 +949,25 @@ __device__ inline int lev_rows_planes128_np(const u128 (&pa)[N_PLANES], int la, 
         if (!__any(m > 32)) return myers_plane_text<uint32_t, NP>(P64, m, T64, n, cut);
         return myers_plane_text_lazy<NP>(P64, m, T64, n, cut);
     }
+#ifndef SPK_NO_LEV_BAND
+    const int dlo = -((cut - (m - n)) >> 1), width = ((cut + (m - n)) >> 1) - dlo + 1;
+    if (!__any(width > 32)) return myers_plane_text128_band<NP, 32>(P, m, T, n, cut, dlo);
+    if (!__any(width > 64)) return myers_plane_text128_band<NP, 64>(P, m, T, n, cut, dlo);
+#endif
     return myers_plane_text128_lazy<NP>(P, m, T, n, cut);
 }
 
+// P8: the caller's column uses all 8 planes (Latin-1 beyond ASCII); a kernel instantiated for the columns that
+// drop the top plane (np <= 7) holds 162 VGPRs instead of 174 (3 waves per SIMD instead of 2).
+template <bool P8>
 __device__ inline int lev_rows_planes128(const u128 (&pa)[N_PLANES], int la, const u128 (&pb)[N_PLANES], int lb,
                                          int cut, int np = N_PLANES) {
+    if (P8) return lev_rows_planes128_np<N_PLANES>(pa, la, pb, lb, cut);
     switch (np) {
         case 5: return lev_rows_planes128_np<5>(pa, la, pb, lb, cut);
         case 6: return lev_rows_planes128_np<6>(pa, la, pb, lb, cut);
         case 7: return lev_rows_planes128_np<7>(pa, la, pb, lb, cut);
-        default: return lev_rows_planes128_np<N_PLANES>(pa, la, pb, lb, cut);
+        default: return lev_rows_planes128_np<7>(pa, la, pb, lb, cut);
     }
 }
 

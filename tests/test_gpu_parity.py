@@ -295,6 +295,58 @@ def test_levenshtein_cut_around_thresholds(amd):
     _lev_variants_agree(gf.job, gf.settings, got)
 
 
+def test_levenshtein_band_widths(amd):
+    """Rows of 65-128 units run the slow pass's banded scan (diagonals [-(cut - dm) / 2, (cut + dm) / 2] in one
+    word) when every lane's band fits: a ratio cut at 0.2 (bands of <= 32 diagonals), at 0.45 (33-64), and an
+    absolute cut of 75 (bands past 64: the 128-bit scan).  Distances straddle each cut, the lengths differ by
+    up to the cut, and some pairs share long prefixes / suffixes (the band then covers a stripped remainder of
+    <= 64 units).  Levels against the oracle's Levenshtein, in every kernel mode."""
+    from splink_amd.gammas import add_gammas
+    rng = np.random.Generator(np.random.PCG64(65))
+    alphas = [list("ab"), list("abcdefghijklmnopqrstuvwxyz0123456789 ,.")]
+    left, right = [], []
+    for n in (65, 70, 81, 96, 110, 127, 128):
+        for alpha in alphas:
+            for frac in (0.05, 0.15, 0.2, 0.25, 0.4, 0.45, 0.5, 0.6, 0.75, 0.9):
+                for rep in range(4):
+                    a = "".join(rng.choice(alpha, size=n))
+                    b = list(a)
+                    lo, hi = (0, len(b)) if rep < 3 else (n // 3, 2 * n // 3)  # rep 3: edits in the middle third
+                    for _e in range(int(round(frac * n))):
+                        op = int(rng.integers(3 if rep != 1 else 2))  # rep 1: no deletions (length gaps)
+                        i = int(rng.integers(lo, min(hi, len(b)) + 1))
+                        if op == 0 and len(b) < 128:
+                            b.insert(i, alpha[int(rng.integers(len(alpha)))])
+                        elif op == 2 and len(b) > 1:
+                            del b[min(i, len(b) - 1)]
+                        elif b:
+                            b[min(i, len(b) - 1)] = alpha[int(rng.integers(len(alpha)))]
+                    left.append(a)
+                    right.append("".join(b))
+    ratio = "levenshtein(a_l, a_r)/((length(a_l) + length(a_r))/2)"
+    r2 = ("case when a_l is null or a_r is null then -1 when a_l = a_r then 2 "
+          f"when {ratio} <= 0.2 then 1 else 0 end")
+    r45 = ("case when a_l is null or a_r is null then -1 when a_l = a_r then 3 "
+           f"when {ratio} <= 0.3 then 2 when {ratio} <= 0.45 then 1 else 0 end")
+    a75 = ("case when a_l is null or a_r is null then -1 when levenshtein(a_l, a_r) <= 10 then 3 "
+           "when levenshtein(a_l, a_r) <= 40 then 2 when levenshtein(a_l, a_r) <= 75 then 1 else 0 end")
+    df = pd.DataFrame({"a_l": left, "a_r": right})
+    st = {"link_type": "dedupe_only", "comparison_columns": [
+        {"custom_name": "r2", "custom_columns_used": ["a"], "num_levels": 3, "case_expression": r2},
+        {"custom_name": "r45", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": r45},
+        {"custom_name": "a75", "custom_columns_used": ["a"], "num_levels": 4, "case_expression": a75}]}
+    gf = add_gammas(df, st, amd)
+    got = gf.gamma_matrix()
+    for i, (a, b) in enumerate(zip(left, right)):
+        d = orc.levenshtein(a, b)
+        r = d / ((len(a) + len(b)) / 2)
+        want = [2 if a == b else 1 if r <= 0.2 else 0,
+                3 if a == b else 2 if r <= 0.3 else 1 if r <= 0.45 else 0,
+                3 if d <= 10 else 2 if d <= 40 else 1 if d <= 75 else 0]
+        assert list(got[i]) == want, (len(a), len(b), d, r, list(got[i]))
+    _lev_variants_agree(gf.job, gf.settings, got)
+
+
 def test_fused_jw_slow_lists_of_one_pair(amd):
     """Two Jaro-Winkler columns share one exact launch and one slow-list launch (k_gamma_slow over both lists).
     When BOTH of a pair's cells are past the exact pass's 64 units they are on both slow lists, and the two
