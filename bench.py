@@ -110,6 +110,9 @@ def launch_ranks(n: int, argv) -> int:
     return code
 
 
+GAMMA_STREAMS = 2  # --gamma-streams
+
+
 def timed_run(config, records, shard, world, rank, local, steps, warmup):
     """Build one workload's job (records, blocking, first comparison pass) and time `steps` steps after
     `warmup` untimed ones, bracketed by a barrier + device synchronisation; the wall time is the maximum
@@ -140,6 +143,7 @@ def timed_run(config, records, shard, world, rank, local, steps, warmup):
 
     job = Job("dedupe_only", [df], "unique_id", local, shard=shard)
     job.ctx.enable_timing(True)
+    job.ctx.gammas_set_streams(GAMMA_STREAMS)
     t0 = time.time()
     job.block(st["blocking_rules"])
     block_s = time.time() - t0
@@ -242,9 +246,13 @@ def main():
     ap.add_argument("--cfg5-steps", type=int, default=10,
                     help="the cfg5_columns sub-record of a one-GPU cfg2 run: steps timed (0 = off)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--gamma-streams", type=int, default=2, choices=[1, 2],
+                    help="comparison pass as two concurrent half windows on two streams (2, default) or one (1)")
     ap.add_argument("--em-scale", type=int, default=8,
                     help="separate E/M streaming row: the run's comparison vectors tiled this many times (0 = off)")
     args = ap.parse_args()
+    global GAMMA_STREAMS
+    GAMMA_STREAMS = args.gamma_streams
 
     if "WORLD_SIZE" not in os.environ:
         n = 1 if args.gpus is None else args.gpus
@@ -589,7 +597,7 @@ def string_rates(job, st, pairs, g_ms):
             tot = cnt = 0
             for i in sample:
                 a, b = vals.iat[int(l[items[i]])], vals.iat[int(r[items[i]])]
-                if a is None or b is None or max(len(a), len(b)) > 64:
+                if not isinstance(a, str) or not isinstance(b, str) or max(len(a), len(b)) > 64:
                     continue
                 # simple_lev_cut: one unit over the largest passing distance (ratio tests: t x mean length)
                 ratio = "length(" in expr

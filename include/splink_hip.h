@@ -269,6 +269,12 @@ int spk_gammas_simple_count(spk_ctx *ctx, int *out);
  * spk_gammas ran. */
 int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs);
 int spk_gammas_windows(spk_ctx *ctx, int64_t *out);
+/* Two-stream split (an implementation choice, not a reference interface): with streams = 2 (default), a pair
+ * set that fits one window and holds at least min_pairs pairs (default 2^22) runs as two windows of half the
+ * pairs at once, the second on a stream of its own joined back before spk_gammas returns, so one window's
+ * filter and the other's exact passes share the device.  streams = 1: one window on the context stream.
+ * Identical codes either way (spk_gammas_windows reports 2 for a split call). */
+int spk_gammas_set_streams(spk_ctx *ctx, int streams, int64_t min_pairs);
 /* Levenshtein pass kernels (same codes in every mode; for A/B tests): 2 = lane refill (a lane that finishes its
  * cell takes the next one from its wave's queue) in the exact pass of free-text columns -- rows past 64 units on
  * both sides -- and one cell per lane elsewhere (default), 1 = lane refill in every exact pass (the 128-bit slow

@@ -52,7 +52,7 @@ EXPORTS = [
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
     "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_raw_utf8_arrow_chunks", "spk_table_digest", "spk_raw_release",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
-    "spk_em_finalize_start", "spk_gammas_exact_ms", "spk_gammas_set_window", "spk_gammas_windows",
+    "spk_em_finalize_start", "spk_gammas_exact_ms", "spk_gammas_set_window", "spk_gammas_windows", "spk_gammas_set_streams",
     "spk_gammas_set_lev_kernel",
 ]
 TF_LIMBS = 14  # SPK_TF_LIMBS
@@ -382,6 +382,11 @@ class Context:
     def gammas_set_window(self, pairs: int):
         """Cap spk_gammas' ordinal windows at `pairs` (0 = default, just under 2^31; for testing)."""
         check(self._lib.spk_gammas_set_window(self._h, ctypes.c_int64(int(pairs))), "spk_gammas_set_window")
+
+    def gammas_set_streams(self, streams: int, min_pairs: int = 1 << 22):
+        """spk_gammas' two-stream split: 2 streams (default) for pair sets of at least min_pairs, or 1."""
+        check(self._lib.spk_gammas_set_streams(self._h, ctypes.c_int(int(streams)), ctypes.c_int64(int(min_pairs))),
+              "spk_gammas_set_streams")
 
     def gammas_windows(self) -> int:
         n = ctypes.c_int64(0)

@@ -425,6 +425,18 @@ void spk_ctx_destroy(spk_ctx *ctx) {
         (void)hipEventDestroy(ctx->xev0[k]);
         (void)hipEventDestroy(ctx->xev1[k]);
     }
+    if (ctx->split_ready) {
+        (void)hipStreamSynchronize(ctx->alt.stream);
+        for (size_t k = 0; k < ctx->alt.xev0.size(); ++k) {
+            (void)hipEventDestroy(ctx->alt.xev0[k]);
+            (void)hipEventDestroy(ctx->alt.xev1[k]);
+        }
+        (void)hipEventDestroy(ctx->alt.ev_info);
+        (void)hipEventDestroy(ctx->ev_fork);
+        (void)hipEventDestroy(ctx->ev_join);
+        if (ctx->alt.h_info) (void)hipHostFree(ctx->alt.h_info);
+        (void)hipStreamDestroy(ctx->alt.stream);
+    }
     if (ctx->ev_info) (void)hipEventDestroy(ctx->ev_info);
     if (ctx->ev_stats) (void)hipEventDestroy(ctx->ev_stats);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);

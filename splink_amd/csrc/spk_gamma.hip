@@ -2274,6 +2274,30 @@ struct GammaPlan {
 };
 }  // namespace spk
 
+template <class T>
+static void swap_buf(spk::DevBuf<T> &a, spk::DevBuf<T> &b) {
+    std::swap(a.p, b.p);
+    std::swap(a.n, b.n);
+}
+
+void spk_ctx::swap_slot() {
+    swap_buf(work, alt.work);
+    swap_buf(xlist, alt.xlist);
+    swap_buf(xpref, alt.xpref);
+    swap_buf(xinfo, alt.xinfo);
+    swap_buf(region_count, alt.region_count);
+    std::swap(xcap, alt.xcap);
+    std::swap(h_info, alt.h_info);
+    std::swap(h_info_n, alt.h_info_n);
+    std::swap(ev_info, alt.ev_info);
+    std::swap(gplan, alt.gplan);
+    std::swap(gamma_pending, alt.gamma_pending);
+    std::swap(stream, alt.stream);
+    std::swap(xev0, alt.xev0);
+    std::swap(xev1, alt.xev1);
+    std::swap(xev_used, alt.xev_used);
+}
+
 // The exact and slow passes over the lists the filter wrote (list capacity `cap`).  k_prefix sizes the
 // lists on the device; if they exceed `cap` every exact kernel is a no-op and settle_gammas re-runs
 // this phase with the right capacity.
@@ -2465,7 +2489,37 @@ int settle_gammas(spk_ctx *ctx, bool *fixed) {
     return SPK_OK;
 }
 
+static int settle_slot(spk_ctx *ctx, bool *fixed);
+// Both windows of a two-stream split: the own slot, then the alternate one (its counts added to the first's
+// through the window carry, its slow-list flags or-ed in).
 static int settle_info(spk_ctx *ctx, bool *fixed) {
+    if (fixed) *fixed = false;
+    const bool two = ctx->gamma_pending && ctx->alt.gamma_pending;
+    bool f0 = false, f1 = false;
+    SPK_TRY(settle_slot(ctx, &f0));
+    if (two) {
+        ctx->exact_carry = ctx->last_exact;
+        ctx->deferred_carry = ctx->last_deferred;
+        ctx->split_first = ctx->last_exact;
+        const std::vector<int64_t> xbase0 = ctx->last_xbase;
+        const std::vector<uint8_t> seen = ctx->slow_seen;
+        ctx->swap_slot();
+        const int rc = settle_slot(ctx, &f1);
+        ctx->swap_slot();
+        ctx->alt_xbase = ctx->last_xbase;
+        ctx->last_xbase = xbase0;
+        ctx->exact_carry.clear();
+        ctx->deferred_carry = 0;
+        SPK_TRY(rc);
+        for (size_t k = 0; k < seen.size() && k < ctx->slow_seen.size(); ++k) ctx->slow_seen[k] |= seen[k];
+    } else if (ctx->alt.gamma_pending) {
+        ctx->alt.gamma_pending = false;  // its call's codes were replaced before the own slot was settled
+    }
+    if (fixed) *fixed = f0 || f1;
+    return SPK_OK;
+}
+
+static int settle_slot(spk_ctx *ctx, bool *fixed) {
     if (fixed) *fixed = false;
     if (!ctx->gamma_pending) return SPK_OK;
     // the info block is on the host once the readback behind it completed (later work -- an EM
@@ -2727,10 +2781,21 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     const int64_t WMAX = ((int64_t)1 << 31) - ((int64_t)1 << 22);
     const int64_t wcap = ctx->gamma_window > 0 ? std::min<int64_t>(ctx->gamma_window, WMAX) : WMAX;
     const int64_t n_win0 = std::max<int64_t>(1, (P + wcap - 1) / wcap);
-    const int64_t W = n_win0 == 1 ? P : ((P + n_win0 - 1) / n_win0 + 63) / 64 * 64;  // pairs per window (the last: rest)
+    // the two-stream split (spk_ctx::alt): two windows of half the pairs at once, one per stream
+    const bool split = ctx->gamma_streams >= 2 && ctx->gamma_window == 0 && n_win0 == 1 &&
+                       P >= std::max<int64_t>(ctx->split_min, 256);
+    const int64_t W = split ? ((P + 1) / 2 + 63) / 64 * 64
+                            : (n_win0 == 1 ? P : ((P + n_win0 - 1) / n_win0 + 63) / 64 * 64);  // pairs per window
     // rounding W up to a multiple of 64 can leave trailing windows empty (small test windows): count the
     // windows from W itself
-    const int64_t n_win = n_win0 == 1 ? 1 : (P + W - 1) / W;
+    const int64_t n_win = split ? 2 : (n_win0 == 1 ? 1 : (P + W - 1) / W);
+    if (split && !ctx->split_ready) {
+        SPK_HIP(hipStreamCreateWithFlags(&ctx->alt.stream, hipStreamNonBlocking));
+        SPK_HIP(hipEventCreateWithFlags(&ctx->alt.ev_info, hipEventDisableTiming));
+        SPK_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        SPK_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+        ctx->split_ready = true;
+    }
     // work lists only for the columns whose filter can leave cells undecided (a dictionary-id equality
     // or numeric column never does): one slot of W pair indices each
     std::vector<int32_t> wslot(K, 0);
@@ -2741,7 +2806,6 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
             if (sc.k == k && (sc.kind == SK_NUM || sc.cls == SC_NUM || (sc.cls == SC_EQ && sc.has_ids))) may = false;
         wslot[k] = may ? n_wslots++ : 0;
     }
-    SPK_TRY(ctx->work.alloc((size_t)std::max(n_wslots, 1) * (size_t)W + 1));
     SPK_TRY(ctx->codes.alloc((size_t)(P + 1) * ctx->code_bytes));
     // one filter workgroup per region of consecutive pair ordinals (a multiple of the wave size)
     // 20 regions (256-thread workgroups) per CU: four rounds of the 5 resident workgroups a CU holds
@@ -2752,15 +2816,28 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         return (int)std::max<int64_t>(1, std::min<int64_t>(max_regions, (pw + F_THREADS - 1) / F_THREADS));
     };
     const int n_regions_max = regions_of(W);
-    // every (column, region) count is written by the filter launch that covers the region: no memset
-    SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions_max));
     // One device info block, read back with one copy: xinfo (k_prefix: list bases and counts, overflow,
     // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed per window.
     const int n_info = 2 * K + 2;
     const int n_cnt = (3 * K + 1) / 2;  // int64 slots of the 3K uint32 list lengths
     const int n_all = n_info + n_cnt + 2;  // + the error word and k_prefix's completion counter
-    SPK_TRY(ctx->xinfo.alloc((size_t)n_all));
-    SPK_TRY(ctx->pinned_info((size_t)n_all));
+    // the per-window buffers (of the alternate slot too when split): every (column, region) count is written
+    // by the filter launch that covers the region, so region_count needs no memset
+    auto alloc_slot = [&]() -> int {
+        SPK_TRY(ctx->work.alloc((size_t)std::max(n_wslots, 1) * (size_t)W + 1));
+        SPK_TRY(ctx->region_count.alloc((size_t)K * n_regions_max));
+        SPK_TRY(ctx->xinfo.alloc((size_t)n_all));
+        SPK_TRY(ctx->pinned_info((size_t)n_all));
+        SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions_max + 1)));
+        return SPK_OK;
+    };
+    SPK_TRY(alloc_slot());
+    if (split) {
+        ctx->swap_slot();
+        const int rc = alloc_slot();
+        ctx->swap_slot();
+        SPK_TRY(rc);
+    }
 
     GammaArgs A{};
     A.cols0 = t0.d_desc.p;
@@ -2784,13 +2861,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     at(A.complex_k, o_complex);
     at(A.thr, o_thr);
     A.n_thr = (int)thr_tab.size();
-    A.err = reinterpret_cast<int *>(ctx->xinfo.p + n_info + n_cnt);
     A.codes = ctx->codes.p;
     A.code16 = ctx->code_bytes == 2;
-    A.work = ctx->work.p;
     for (int k = 0; k < K; ++k) A.wslot[k] = wslot[k];
-    A.region_count = ctx->region_count.p;
-    A.slow_count = reinterpret_cast<unsigned int *>(ctx->xinfo.p + n_info);
     A.n_simple = (int)simple.size();
     A.n_complex = (int)complex_k.size();
     ctx->last_simple = (int)simple.size();
@@ -2830,11 +2903,16 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         for (const Column *c : t->cols)
             if (c && c->kind == COL_STR) G.max_units = std::max<int64_t>(G.max_units, c->max_bytes);
     for (int i = 0; i < n_lits; ++i) G.max_units = std::max<int64_t>(G.max_units, llen[i]);
-    SPK_TRY(ctx->xpref.alloc((size_t)K * (n_regions_max + 1)));
+    if (split) {  // window 1's plan: the same program, its own window arguments
+        if (!ctx->alt.gplan) ctx->alt.gplan = new GammaPlan();
+        *ctx->alt.gplan = G;
+    }
 
     ctx->exact_carry.clear();
     ctx->deferred_carry = 0;
     ctx->last_windows = n_win;
+    ctx->last_split = split;
+    ctx->split_w = split ? W : 0;
     SPK_TRY(ctx->begin(K_GAMMA));
     // row images and rule-view images: kernels only when a table, the column layout or the pairs changed
     ViewLaunch V{};
@@ -2850,11 +2928,25 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
         if ((ctx->use_views == 1 && big) || ctx->use_views == 2) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
     }
+    if (split) {
+        // window 1's stream starts after everything queued so far (images, program blob, earlier reads of the
+        // codes), together with window 0.  Starting it after window 0's filter instead (so that its filter runs
+        // beside window 0's exact passes) measured slower: the short JW launch then waited behind the second
+        // filter's workgroups (cfg2 0.99 -> 1.02 ms per step, profiles/r6_ab_gamma_streams.log).
+        SPK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+        SPK_HIP(hipStreamWaitEvent(ctx->alt.stream, ctx->ev_fork, 0));
+    }
     for (int64_t w = 0; w < n_win; ++w) {
+        if (split && w == 1) ctx->swap_slot();  // window 1: the alternate buffers, plan and stream
+        GammaPlan &G = *ctx->gplan;
         const int64_t b = w * W, Pw = std::min<int64_t>(W, P - b);
         const int n_regions = regions_of(Pw);
         const int64_t region_len = ((Pw + n_regions - 1) / n_regions + 63) / 64 * 64;
         GammaArgs AW = A;  // the window [b, b + Pw) as a pair set of its own
+        AW.err = reinterpret_cast<int *>(ctx->xinfo.p + n_info + n_cnt);
+        AW.work = ctx->work.p;
+        AW.region_count = ctx->region_count.p;
+        AW.slow_count = reinterpret_cast<unsigned int *>(ctx->xinfo.p + n_info);
         AW.pl = ctx->pl.p + b;
         AW.pr = ctx->pr.p + b;
         AW.P = Pw;
@@ -2903,6 +2995,17 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         G.A = AW;
         const int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(Pw, 1 << 16));
         SPK_TRY(enqueue_phase(ctx, G, cap, /*skip=*/true));
+        if (split) {
+            if (w == 0) continue;  // window 0's info block is read back below, behind the join
+            // window 1: its info block, then the join (the context stream waits for window 1) and the own slot back
+            SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+            SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+            ctx->gamma_pending = true;
+            SPK_HIP(hipEventRecord(ctx->ev_join, ctx->stream));
+            ctx->swap_slot();
+            SPK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+            break;
+        }
         if (w + 1 == n_win) break;
         // settle this window before the next one reuses the lists
         SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -2949,6 +3052,7 @@ extern "C" int spk_gammas_load(spk_ctx *ctx, int n_cols, const int32_t *n_levels
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     ctx->n_pairs = n;
     ctx->gamma_pending = false;
+    ctx->alt.gamma_pending = false;
     ++ctx->gamma_seq;
     ctx->codes_valid = true;
     return SPK_OK;
@@ -3117,12 +3221,19 @@ extern "C" int spk_gammas_exact_ms(spk_ctx *ctx, double *out, int n) {
     SPK_HIP(hipSetDevice(ctx->device));
     SPK_TRY(settle_gammas(ctx, nullptr));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
+    // a two-stream split timed each window's launch on its own stream: the sum of both
+    const bool two = ctx->last_windows == 2 && ctx->split_ready && ctx->alt.xev_used.size();
     for (int k = 0; k < n; ++k) {
         out[k] = -1.0;
         if (k < (int)ctx->xev_used.size() && ctx->xev_used[k]) {
             float ms = 0.f;
             SPK_HIP(hipEventElapsedTime(&ms, ctx->xev0[k], ctx->xev1[k]));
             out[k] = (double)ms;
+        }
+        if (two && k < (int)ctx->alt.xev_used.size() && ctx->alt.xev_used[k]) {
+            float ms = 0.f;
+            SPK_HIP(hipEventElapsedTime(&ms, ctx->alt.xev0[k], ctx->alt.xev1[k]));
+            out[k] = (out[k] < 0 ? 0.0 : out[k]) + (double)ms;
         }
     }
     return SPK_OK;
@@ -3141,8 +3252,20 @@ extern "C" int spk_gammas_exact_list(spk_ctx *ctx, int k, int32_t *out, int64_t 
     SPK_REQUIRE(out && k >= 0 && k < (int)ctx->last_exact.size() && n >= 0, SPK_E_INVALID,
                 "spk_gammas_exact_list: bad args");
     const int64_t m = std::min<int64_t>(n, ctx->last_exact[k]);
-    if (m > 0)
-        SPK_HIP(hipMemcpy(out, ctx->xlist.p + ctx->last_xbase[k], (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (!ctx->last_split) {
+        if (m > 0)
+            SPK_HIP(hipMemcpy(out, ctx->xlist.p + ctx->last_xbase[k], (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost));
+        return SPK_OK;
+    }
+    // a split call: window 0's list, then window 1's with its window-relative ordinals made global
+    const int64_t m0 = std::min<int64_t>(m, ctx->split_first[k]), m1 = m - m0;
+    if (m0 > 0)
+        SPK_HIP(hipMemcpy(out, ctx->xlist.p + ctx->last_xbase[k], (size_t)m0 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (m1 > 0) {
+        SPK_HIP(hipMemcpy(out + m0, ctx->alt.xlist.p + ctx->alt_xbase[k], (size_t)m1 * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int64_t i = m0; i < m; ++i)
+            if (out[i] >= 0) out[i] += (int32_t)ctx->split_w;
+    }
     return SPK_OK;
 }
 
@@ -3220,6 +3343,15 @@ extern "C" int spk_gammas_simple_count(spk_ctx *ctx, int *out) {
 extern "C" int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs) {
     SPK_REQUIRE(ctx && pairs >= 0, SPK_E_INVALID, "spk_gammas_set_window: bad args");
     ctx->gamma_window = pairs;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_set_streams(spk_ctx *ctx, int streams, int64_t min_pairs) {
+    SPK_REQUIRE(ctx && (streams == 1 || streams == 2) && min_pairs >= 0, SPK_E_INVALID,
+                "spk_gammas_set_streams: 1 or 2 streams, min_pairs >= 0");
+    SPK_TRY(settle_gammas(ctx, nullptr));
+    ctx->gamma_streams = streams;
+    ctx->split_min = min_pairs;
     return SPK_OK;
 }
 

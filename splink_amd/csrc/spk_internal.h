@@ -310,6 +310,34 @@ struct spk_ctx {
     uint64_t slow_key_pairs = 0, slow_key_tables = 0;
     spk::DevBuf<unsigned int> region_count;  // [K][regions] filter work-list lengths
 
+    // Two-stream split (spk_gammas_set_streams): a pair set that fits one ordinal window but holds at least
+    // split_min pairs runs as two windows at once, window 0 on `stream`, window 1 on alt.stream, so one
+    // window's filter (texture-address bound) shares the CUs with the other's exact passes (VALU bound).  `alt`
+    // is a second set of the per-window state; swap_slot() exchanges it with the members above, so the phase,
+    // slow-list and settle functions run unchanged on either window.
+    struct Slot {
+        spk::DevBuf<int32_t> work, xlist;
+        spk::DevBuf<int64_t> xpref, xinfo;
+        spk::DevBuf<unsigned int> region_count;
+        int64_t xcap = 0;
+        int64_t *h_info = nullptr;
+        size_t h_info_n = 0;
+        hipEvent_t ev_info = nullptr;
+        spk::GammaPlan *gplan = nullptr;
+        bool gamma_pending = false;
+        hipStream_t stream = nullptr;
+        std::vector<hipEvent_t> xev0, xev1;
+        std::vector<char> xev_used;
+    } alt;
+    int gamma_streams = 2;
+    int64_t split_min = (int64_t)1 << 22;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool split_ready = false;  // alt.stream and the events exist
+    bool last_split = false;   // the last spk_gammas ran split: window 1 = pairs [split_w, P)
+    int64_t split_w = 0;
+    std::vector<int64_t> split_first, alt_xbase;  // per column: window 0's exact cells; window 1's list base
+    void swap_slot();
+
     // EM state
     spk::DevBuf<uint64_t> hist;
     spk::DevBuf<double> mpat, llpat, cpat, stats, mu;  // per pattern: mp, ln(...), count; statistics; m / u
@@ -342,6 +370,7 @@ struct spk_ctx {
     ~spk_ctx() {
         for (spk::RawCol *r : raw) delete r;
         if (gplan && gplan_free) gplan_free(gplan);
+        if (alt.gplan && gplan_free) gplan_free(alt.gplan);
     }
     bool mpat_valid = false;  // mpat_score holds the mp per pattern of the current codes' last spk_score
     uint64_t score_seq = 0;   // spk_score calls so far (the tf runs depend on their mp per pattern)

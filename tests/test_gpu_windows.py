@@ -90,6 +90,75 @@ def test_windows_give_identical_codes(dedupe_job, size, mode):
     assert np.array_equal(stats_w, stats_1)
 
 
+def _em_args(job):
+    lam, m, u = 0.2, [], []
+    for L in job.code_meta[1]:
+        pm = np.linspace(1.0, 3.0, L)
+        m += list(pm / pm.sum())
+        u += list(pm[::-1] / pm.sum())
+    return lam, m, u, 5 + 4 * sum(L + 1 for L in job.code_meta[1])
+
+
+@pytest.mark.parametrize("mode,lev", [(1, 2), (21, 2), (0, 2), (101, 2), (1, 0), (1, 1), (1, 3), (101, 1)])
+def test_two_stream_split_gives_identical_codes(dedupe_job, mode, lev):
+    """spk_gammas_set_streams: the pair set as two windows at once, the second on a stream of its own (forced
+    here at any size).  Codes, exact-pass cell counts and the E+M statistics equal the one-stream pass: the
+    filter, the interpreter, forced view launches, every slow-list launch left to the settlement of both windows
+    (+100), and every Levenshtein kernel mode."""
+    job, st, ref = dedupe_job
+    lam, m, u, n_stats = _em_args(job)
+    job.ctx.gammas_set_simple(mode)
+    job.ctx.gammas_set_lev_kernel(lev)
+    try:
+        job.ctx.gammas_set_streams(1)
+        job.gammas(st)
+        one = job.gammas_host()
+        exact_one = job.ctx.gammas_exact_counts(len(COLS))
+        list_one = np.sort(job.ctx.gammas_exact_list(4, exact_one[4]))
+        stats_1 = job.ctx.em_iteration(lam, 1 - lam, m, u, n_stats)
+        job.ctx.gammas_set_streams(2, 0)
+        job.gammas(st)
+        assert job.ctx.gammas_windows() == 2
+        # the E+M launch queued right behind the split pass (its codes settled through both windows first)
+        stats_2 = job.ctx.em_iteration(lam, 1 - lam, m, u, n_stats)
+        got = job.gammas_host()
+        exact = job.ctx.gammas_exact_counts(len(COLS))
+        list_two = np.sort(job.ctx.gammas_exact_list(4, exact[4]))  # both windows' lists, global ordinals
+        # two split passes back to back (the first left pending) and a read after the second
+        job.gammas(st)
+        job.gammas(st)
+        again = job.gammas_host()
+    finally:
+        job.ctx.gammas_set_streams(2)
+        job.ctx.gammas_set_simple(1)
+        job.ctx.gammas_set_lev_kernel(2)
+    assert (one == ref).all()
+    assert (got == ref).all(), np.nonzero((got != ref).any(axis=1))[0][:10]
+    assert (again == ref).all()
+    assert exact == exact_one
+    assert np.array_equal(list_two, list_one)
+    assert np.array_equal(stats_2, stats_1)
+
+
+def test_two_stream_split_exact_ms(dedupe_job):
+    """The split pass reports an exact launch's time as the sum of its two windows' launches (spk_gammas_exact_ms),
+    the one-stream pass as its one launch."""
+    job, st, ref = dedupe_job
+    job.ctx.enable_timing(True)
+    try:
+        job.ctx.gammas_set_streams(2, 0)
+        job.gammas(st)
+        ms2 = job.ctx.gammas_exact_ms(len(COLS))
+        job.ctx.gammas_set_streams(1)
+        job.gammas(st)
+        ms1 = job.ctx.gammas_exact_ms(len(COLS))
+    finally:
+        job.ctx.gammas_set_streams(2)
+        job.ctx.enable_timing(False)
+    for k in (0, 4):  # the fused JW launch (timed under its first column, first_name), email
+        assert ms1[k] > 0 and ms2[k] > 0, (k, ms1, ms2)
+
+
 def test_windows_link_only(amd):
     """link_only (two tables, asymmetric sides) with three rules, windows of 3000 pairs."""
     from splink_amd.engine import Job
