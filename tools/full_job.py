@@ -147,6 +147,7 @@ def main():
     exact_cells = dict(zip(names, job.ctx.gammas_exact_counts(len(names))))
     job.gammas(st)  # a second pass (row images built, lists sized): the per-pass device time
     gamma_warm = job.ctx.kernel_ms()["gamma"]
+    windows = job.ctx.gammas_windows()
     lam0, lp0 = params.params["λ"], params._level_probabilities()
     t = time.perf_counter()
     em_dev = []
@@ -182,6 +183,11 @@ def main():
         tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
         wall["tf_adjust"] = time.perf_counter() - t
     total = time.perf_counter() - t_job
+    # outside the job's wall: the same pass on one stream (spk_gammas_set_streams), against the default split
+    job.ctx.gammas_set_streams(1)
+    job.gammas(st)
+    gamma_one_stream = job.ctx.kernel_ms()["gamma"]
+    job.ctx.gammas_set_streams(2)
     P = job.n_pairs
     row = {
         "row": "full job, one GPU (separately labelled; never the headline)",
@@ -192,7 +198,8 @@ def main():
                      f"pair-ordinal shard {shard}/{n_shards}"),
         "records": a.records, "candidates_total": int(job.n_candidates), "pairs_this_gpu": int(P),
         "iterations": a.iters, "wall_s": wall, "job_wall_s": total, "job_timings_s": dict(job.timings),
-        "device_ms": {"block": block_dev, "gamma_pass_first": gamma_dev, "gamma_pass": gamma_warm,
+        "device_ms": {"block": block_dev, "gamma_pass_first": gamma_dev, "gamma_pass": gamma_warm, "gamma_pass_one_stream": gamma_one_stream,
+                      "gamma_windows": windows,
                       "em_per_iter_mean": float(np.mean(em_dev)), "score": score_dev,
                       "em_per_iter": [round(x, 4) for x in em_dev]},
         "exact_cells_per_column": exact_cells,
