@@ -764,7 +764,13 @@ int launch_template_filter(hipStream_t stream, const GammaArgs &A, const std::ve
     const size_t shm = (size_t)A.n_thr * sizeof(int16_t);
     // 3 pairs per lane per step at a register budget for 5 waves per SIMD (94 VGPRs): the best point of the
     // round-4 sweep (<2,6> / <4,4> slower, <3,6> / <2,8> spill: profiles/r4_ab_filter_occupancy.log)
-    constexpr int FP = 3, MINW = 5;
+#ifndef SPK_FILTER_FP
+#define SPK_FILTER_FP 3
+#endif
+#ifndef SPK_FILTER_MINW
+#define SPK_FILTER_MINW 5
+#endif
+    constexpr int FP = SPK_FILTER_FP, MINW = SPK_FILTER_MINW;
     if (A.code16) k_filter<FP, MINW, false><<<g, F_THREADS, shm, stream>>>(F);
     else k_filter<FP, MINW, true><<<g, F_THREADS, shm, stream>>>(F);
     SPK_HIP(hipGetLastError());

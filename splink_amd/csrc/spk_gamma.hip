@@ -22,6 +22,8 @@
 // The filter pass writes each pair's code = Σ_k (γ_k + 1) · Π_{j<k}(L_j + 1) over the columns it
 // decided (uint16 when the pattern space fits, else uint32); passes 2 and 3 add the rest in place.
 // Bounds are exact decisions (never approximations), so the result is the exact evaluation.
+#include <chrono>
+#include <cstdio>
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
@@ -2608,7 +2610,13 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     SPK_REQUIRE(ctx->pairs_valid, SPK_E_STATE, "spk_gammas: no pairs");
     SPK_REQUIRE(n_operands < 4096 && n_instr >= 0 && n_when >= 0, SPK_E_LIMIT, "spk_gammas: program too large");
     SPK_HIP(hipSetDevice(ctx->device));
+#ifdef SPK_HOST_TIMING
+    const auto ht0 = std::chrono::steady_clock::now();
+#endif
     SPK_TRY(settle_gammas(ctx, nullptr));  // the previous call's capacity feedback (its codes are replaced)
+#ifdef SPK_HOST_TIMING
+    const auto ht1 = std::chrono::steady_clock::now();
+#endif
     // ---- host-side validation of the program against the loaded tables
     Table &t0 = ctx->table[0];
     Table &t1 = ctx->side_table(1);
@@ -2771,6 +2779,9 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         SPK_HIP(hipMemcpyAsync(ctx->prog_blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, ctx->stream));
         ctx->last_blob = blob;
     }
+#ifdef SPK_HOST_TIMING
+    const auto ht2 = std::chrono::steady_clock::now();
+#endif
     uint8_t *base = ctx->prog_blob.p;
     auto at = [&](auto *&dst, size_t off) { dst = reinterpret_cast<std::remove_reference_t<decltype(dst)>>(base + off); };
     const int64_t P = ctx->n_pairs;
@@ -3025,6 +3036,21 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     ctx->mpat_valid = false;
     ctx->last_implied.assign((size_t)K, 0);
     for (const SimpleCol &sc : simple) ctx->last_implied[sc.k] = sc.imp_hi - sc.imp_lo;
+#ifdef SPK_HOST_TIMING
+    {  // diagnostic build only: host time per spk_gammas phase (settle wait, program preparation, enqueue)
+        static double acc[3] = {0, 0, 0};
+        static int calls = 0;
+        const auto ht3 = std::chrono::steady_clock::now();
+        acc[0] += std::chrono::duration<double, std::micro>(ht1 - ht0).count();
+        acc[1] += std::chrono::duration<double, std::micro>(ht2 - ht1).count();
+        acc[2] += std::chrono::duration<double, std::micro>(ht3 - ht2).count();
+        if (++calls % 20 == 0) {
+            std::fprintf(stderr, "[spk host] per call: settle %.1f us, prepare %.1f us, enqueue %.1f us\n", acc[0] / 20,
+                         acc[1] / 20, acc[2] / 20);
+            acc[0] = acc[1] = acc[2] = 0;
+        }
+    }
+#endif
     return SPK_OK;
 }
 
