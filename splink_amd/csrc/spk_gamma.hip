@@ -3339,7 +3339,8 @@ extern "C" int spk_ctx_memory(spk_ctx *ctx, int64_t *out8) {
     m[3] = b(ctx->pl) + b(ctx->pr) + b(ctx->pvl) + b(ctx->pvr);
     for (int v = 0; v < MAX_VIEWS; ++v) m[3] += b(ctx->views[v].rowsL) + b(ctx->views[v].rowsR);
     m[4] = b(ctx->codes);
-    m[5] = b(ctx->work) + b(ctx->xlist) + b(ctx->xpref) + b(ctx->xinfo) + b(ctx->region_count) + b(ctx->prog_blob);
+    m[5] = b(ctx->work) + b(ctx->xlist) + b(ctx->xpref) + b(ctx->xinfo) + b(ctx->region_count) + b(ctx->prog_blob) +
+           b(ctx->alt.work) + b(ctx->alt.xlist) + b(ctx->alt.xpref) + b(ctx->alt.xinfo) + b(ctx->alt.region_count);
     m[6] = b(ctx->hist) + b(ctx->mpat) + b(ctx->llpat) + b(ctx->cpat) + b(ctx->stats) + b(ctx->mu) + b(ctx->em_ticket) +
            b(ctx->em_row) + b(ctx->em_hot) + b(ctx->mp) + b(ctx->mpat_score) + b(ctx->tf_uniq) + b(ctx->tf_runs) +
            b(ctx->tf_nruns);
