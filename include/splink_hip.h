@@ -58,6 +58,8 @@ int spk_ctx_kernel_ms(spk_ctx *ctx, double *out5);
 /* The same without synchronising: per family the newest launch that has completed (-1 = none), so a
  * caller can read the timings of iteration i while iteration i + 1 is still queued. */
 int spk_ctx_kernel_ms_done(spk_ctx *ctx, double *out5);
+/* on = 1: HIP events around each kernel family (spk_ctx_kernel_ms); on = 2: also around each column's exact-pass
+ * launch (spk_gammas_exact_ms); 0: off. */
 int spk_ctx_enable_timing(spk_ctx *ctx, int on);
 /* LDS bytes one workgroup may allocate on the context's device (sizes the E/M histogram copies). */
 int spk_ctx_lds_per_block(spk_ctx *ctx, int *out);
@@ -237,7 +239,7 @@ int spk_gammas_deferred(spk_ctx *ctx, int64_t *out);
 /* Per comparison column: pairs the last spk_gammas could not decide from bounds in the filter pass
  * and evaluated with the exact similarity (out[n], n >= number of columns). */
 int spk_gammas_exact_counts(spk_ctx *ctx, int64_t *out, int n);
-/* With timing on (spk_ctx_enable_timing): milliseconds of each column's exact-pass launch in the last
+/* With timing on at level 2 (spk_ctx_enable_timing): milliseconds of each column's exact-pass launch in the last
  * spk_gammas (HIP events; -1 = none; the Jaro-Winkler columns share one launch, reported at the first
  * of them).  Synchronises. */
 int spk_gammas_exact_ms(spk_ctx *ctx, double *out, int n);

@@ -150,8 +150,10 @@ class Context:
     def set_link_type(self, link_type: int):
         check(self._lib.spk_ctx_set_link_type(self._h, ctypes.c_int(link_type)), "spk_ctx_set_link_type")
 
-    def enable_timing(self, on: bool = True):
-        check(self._lib.spk_ctx_enable_timing(self._h, ctypes.c_int(1 if on else 0)), "spk_ctx_enable_timing")
+    def enable_timing(self, on: bool = True, exact: bool = False):
+        """HIP-event timing of the kernel families; exact=True also times each column's exact-pass launch."""
+        check(self._lib.spk_ctx_enable_timing(self._h, ctypes.c_int((2 if exact else 1) if on else 0)),
+              "spk_ctx_enable_timing")
 
     def kernel_ms(self):
         out = np.zeros(5, dtype=np.float64)

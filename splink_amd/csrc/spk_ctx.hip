@@ -342,7 +342,7 @@ int spk_ctx::end(Kern k) {
 }
 
 int spk_ctx::xbegin(int k) {
-    if (!timing) return SPK_OK;
+    if (!timing || !timing_exact) return SPK_OK;
     while ((int)xev0.size() <= k) {
         hipEvent_t a = nullptr, b = nullptr;
         SPK_HIP(hipEventCreate(&a));
@@ -356,7 +356,7 @@ int spk_ctx::xbegin(int k) {
     return SPK_OK;
 }
 int spk_ctx::xend(int k) {
-    if (!timing) return SPK_OK;
+    if (!timing || !timing_exact) return SPK_OK;
     SPK_HIP(hipEventRecord(xev1[k], stream));
     xev_used[k] = 1;
     return SPK_OK;
@@ -462,6 +462,7 @@ int spk_ctx_sync(spk_ctx *ctx) {
 int spk_ctx_enable_timing(spk_ctx *ctx, int on) {
     SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
     ctx->timing = on != 0;
+    ctx->timing_exact = on >= 2;
     return SPK_OK;
 }
 

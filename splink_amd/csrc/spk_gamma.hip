@@ -3007,12 +3007,17 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         const int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(Pw, 1 << 16));
         SPK_TRY(enqueue_phase(ctx, G, cap, /*skip=*/true));
         if (split) {
-            if (w == 0) continue;  // window 0's info block is read back below, behind the join
-            // window 1: its info block, then the join (the context stream waits for window 1) and the own slot back
+            if (w == 0) {  // window 0's info block, on its own stream (not behind the join)
+                SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+                SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+                continue;
+            }
+            // window 1: the join right after its last kernel (the context stream waits for nothing else of it), then
+            // its info block, and the own slot back
+            SPK_HIP(hipEventRecord(ctx->ev_join, ctx->stream));
             SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
             SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
             ctx->gamma_pending = true;
-            SPK_HIP(hipEventRecord(ctx->ev_join, ctx->stream));
             ctx->swap_slot();
             SPK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
             break;
@@ -3028,8 +3033,10 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         ctx->deferred_carry = ctx->last_deferred;
     }
     SPK_TRY(ctx->end(K_GAMMA));
-    SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
-    SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+    if (!split) {  // (a split call read window 0's info block back in the loop)
+        SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+        SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+    }
     ++ctx->gamma_seq;
     ctx->gamma_pending = true;
     ctx->codes_valid = true;

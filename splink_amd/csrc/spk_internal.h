@@ -398,6 +398,7 @@ struct spk_ctx {
     // timing: two event pairs per kind, alternating, so the last completed launch of a kind can be read
     // while a newer one is still in flight (spk_ctx_kernel_ms_done)
     bool timing = false;
+    bool timing_exact = false;  // also each column's exact-pass launch (spk_ctx_enable_timing 2): events cost host time per launch
     hipEvent_t ev0[2][spk::K_COUNT] = {}, ev1[2][spk::K_COUNT] = {};
     bool ev_used[2][spk::K_COUNT] = {};
     int ev_slot[spk::K_COUNT] = {};

@@ -18,6 +18,12 @@ class _StubCtx:
     def gammas_exact_ms(self, n):
         return [-1.0, 0.5][:n]
 
+    def enable_timing(self, on=True, exact=False):
+        self.exact_timing = on and exact
+
+    def gammas_set_streams(self, streams, min_pairs=1 << 22):
+        self.streams = streams
+
     def gammas_exact_list(self, k, n):
         assert k == 1 and n == 2
         return np.array([1, 3], dtype=np.int32)  # pair ordinals the Levenshtein exact pass evaluated
@@ -31,6 +37,9 @@ class _StubJob:
 
     def pair_rows(self):
         return self._lr
+
+    def gammas(self, st):  # bench.exact_pass_ms: one pass on one stream with per-launch events
+        assert self.ctx.exact_timing and self.ctx.streams == 1
 
 
 def test_string_rates_counts_dp_cells_and_rates():

@@ -150,7 +150,7 @@ def test_async_em_iteration_matches_sync(amd):
     from splink_amd.engine import m_step_rows
     from splink_amd.params import Params
     job, st = _anagram_job(amd)
-    job.ctx.enable_timing(True)
+    job.ctx.enable_timing(True, exact=True)
     p_sync, p_async = Params(copy.deepcopy(st), amd), Params(copy.deepcopy(st), amd)
     assert p_sync._level_probabilities() == p_async._level_probabilities()
     job.gammas(st)  # first call: the work lists overflow, the correction happens at the EM's wait

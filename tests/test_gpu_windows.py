@@ -144,7 +144,7 @@ def test_two_stream_split_exact_ms(dedupe_job):
     """The split pass reports an exact launch's time as the sum of its two windows' launches (spk_gammas_exact_ms),
     the one-stream pass as its one launch."""
     job, st, ref = dedupe_job
-    job.ctx.enable_timing(True)
+    job.ctx.enable_timing(True, exact=True)
     try:
         job.ctx.gammas_set_streams(2, 0)
         job.gammas(st)

@@ -28,7 +28,7 @@ df = make_records(1_000_000, surname_vocab=15000, with_address=cfg == 5, arrow=T
 params = Params(cfg_settings(cfg), AmdSession(0))
 st = params.settings
 job = Job("dedupe_only", [df], "unique_id", 0)
-job.ctx.enable_timing(True)
+job.ctx.enable_timing(True, exact=True)
 job.block(st["blocking_rules"])
 job.gammas(st)
 names, nlev = job.code_meta
