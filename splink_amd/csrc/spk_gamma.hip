@@ -2795,7 +2795,15 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     // the two-stream split (spk_ctx::alt): two windows of half the pairs at once, one per stream
     const bool split = ctx->gamma_streams >= 2 && ctx->gamma_window == 0 && n_win0 == 1 &&
                        P >= std::max<int64_t>(ctx->split_min, 256);
-    const int64_t W = split ? ((P + 1) / 2 + 63) / 64 * 64
+    // Window 0 (the context stream, which starts first and continues after the join) takes 60 % of the pairs, or half
+    // when a free-text Levenshtein column's long exact and slow passes dominate the pass: measured best shares, cfg2
+    // 0.966 -> 0.943 ms per step at 60 %, cfg5 best at 50 % (profiles/r6_ab_split_share.log)
+    bool long_exact = false;
+    for (const SimpleCol &sc : simple) {
+        const Column *a = t0.cols[sc.col], *b = t1.cols[sc.col];
+        long_exact = long_exact || (sc.cls == SC_LEV && a && b && a->planes_hi.n && b->planes_hi.n);
+    }
+    const int64_t W = split ? (P * (long_exact ? 500 : 600) / 1000 + 63) / 64 * 64
                             : (n_win0 == 1 ? P : ((P + n_win0 - 1) / n_win0 + 63) / 64 * 64);  // pairs per window
     // rounding W up to a multiple of 64 can leave trailing windows empty (small test windows): count the
     // windows from W itself
@@ -2826,7 +2834,7 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
     auto regions_of = [&](int64_t pw) {
         return (int)std::max<int64_t>(1, std::min<int64_t>(max_regions, (pw + F_THREADS - 1) / F_THREADS));
     };
-    const int n_regions_max = regions_of(W);
+    const int n_regions_max = regions_of(W);  // (window 0 is the larger one)
     // One device info block, read back with one copy: xinfo (k_prefix: list bases and counts, overflow,
     // total), then the slow / rest / huge list lengths (3K uint32) and the error word, both zeroed per window.
     const int n_info = 2 * K + 2;
