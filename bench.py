@@ -111,6 +111,7 @@ def launch_ranks(n: int, argv) -> int:
 
 
 GAMMA_STREAMS = 2  # --gamma-streams
+GAMMA_GRAPH = False  # --gamma-graph
 
 
 def timed_run(config, records, shard, world, rank, local, steps, warmup):
@@ -144,6 +145,7 @@ def timed_run(config, records, shard, world, rank, local, steps, warmup):
     job = Job("dedupe_only", [df], "unique_id", local, shard=shard)
     job.ctx.enable_timing(True)
     job.ctx.gammas_set_streams(GAMMA_STREAMS)
+    job.ctx.gammas_set_graph(GAMMA_GRAPH)
     t0 = time.time()
     job.block(st["blocking_rules"])
     block_s = time.time() - t0
@@ -246,6 +248,8 @@ def main():
     ap.add_argument("--cfg5-steps", type=int, default=10,
                     help="the cfg5_columns sub-record of a one-GPU cfg2 run: steps timed (0 = off)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--gamma-graph", action="store_true",
+                    help="replay unchanged comparison passes from a captured HIP graph (measured slower; A/B only)")
     ap.add_argument("--gamma-streams", type=int, default=2, choices=[1, 2],
                     help="comparison pass as two concurrent half windows on two streams (2, default) or one (1)")
     ap.add_argument("--em-scale", type=int, default=8,
@@ -253,6 +257,8 @@ def main():
     args = ap.parse_args()
     global GAMMA_STREAMS
     GAMMA_STREAMS = args.gamma_streams
+    global GAMMA_GRAPH
+    GAMMA_GRAPH = args.gamma_graph
 
     if "WORLD_SIZE" not in os.environ:
         n = 1 if args.gpus is None else args.gpus

@@ -277,6 +277,13 @@ int spk_gammas_windows(spk_ctx *ctx, int64_t *out);
  * filter and the other's exact passes share the device.  streams = 1: one window on the context stream.
  * Identical codes either way (spk_gammas_windows reports 2 for a split call). */
 int spk_gammas_set_streams(spk_ctx *ctx, int streams, int64_t min_pairs);
+/* Graph replay (an implementation choice): a call whose program, pairs, tables, buffers, window layout and
+ * slow-list decisions equal the previous call's records the pass's launches as a HIP graph; later such calls
+ * (an EM run's iterations) replay it with one launch.  Off by default (on MI355X the replay measured slower than
+ * direct launches); on = 0 enqueues every call directly.  Identical codes.
+ * spk_gammas_graph_launches: replays so far on this context (diagnostics). */
+int spk_gammas_set_graph(spk_ctx *ctx, int on);
+int spk_gammas_graph_launches(spk_ctx *ctx, int64_t *out);
 /* Levenshtein pass kernels (same codes in every mode; for A/B tests): 2 = lane refill (a lane that finishes its
  * cell takes the next one from its wave's queue) in the exact pass of free-text columns -- rows past 64 units on
  * both sides -- and one cell per lane elsewhere (default), 1 = lane refill in every exact pass (the 128-bit slow

@@ -52,7 +52,8 @@ EXPORTS = [
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
     "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_raw_utf8_arrow_chunks", "spk_table_digest", "spk_raw_release",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
-    "spk_em_finalize_start", "spk_gammas_exact_ms", "spk_gammas_set_window", "spk_gammas_windows", "spk_gammas_set_streams",
+    "spk_em_finalize_start", "spk_gammas_exact_ms", "spk_gammas_set_window", "spk_gammas_windows", "spk_gammas_set_streams", "spk_gammas_set_graph",
+    "spk_gammas_graph_launches",
     "spk_gammas_set_lev_kernel",
 ]
 TF_LIMBS = 14  # SPK_TF_LIMBS
@@ -389,6 +390,15 @@ class Context:
         """spk_gammas' two-stream split: 2 streams (default) for pair sets of at least min_pairs, or 1."""
         check(self._lib.spk_gammas_set_streams(self._h, ctypes.c_int(int(streams)), ctypes.c_int64(int(min_pairs))),
               "spk_gammas_set_streams")
+
+    def gammas_set_graph(self, on: bool):
+        """Replay unchanged comparison passes from a captured HIP graph (default off: slower than direct launches)."""
+        check(self._lib.spk_gammas_set_graph(self._h, ctypes.c_int(1 if on else 0)), "spk_gammas_set_graph")
+
+    def gammas_graph_launches(self) -> int:
+        n = ctypes.c_int64(0)
+        check(self._lib.spk_gammas_graph_launches(self._h, ctypes.byref(n)), "spk_gammas_graph_launches")
+        return n.value
 
     def gammas_windows(self) -> int:
         n = ctypes.c_int64(0)

@@ -437,6 +437,8 @@ void spk_ctx_destroy(spk_ctx *ctx) {
         if (ctx->alt.h_info) (void)hipHostFree(ctx->alt.h_info);
         (void)hipStreamDestroy(ctx->alt.stream);
     }
+    if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+    if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
     if (ctx->ev_info) (void)hipEventDestroy(ctx->ev_info);
     if (ctx->ev_stats) (void)hipEventDestroy(ctx->ev_stats);
     if (ctx->h_stats) (void)hipHostFree(ctx->h_stats);

@@ -2922,10 +2922,6 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         for (const Column *c : t->cols)
             if (c && c->kind == COL_STR) G.max_units = std::max<int64_t>(G.max_units, c->max_bytes);
     for (int i = 0; i < n_lits; ++i) G.max_units = std::max<int64_t>(G.max_units, llen[i]);
-    if (split) {  // window 1's plan: the same program, its own window arguments
-        if (!ctx->alt.gplan) ctx->alt.gplan = new GammaPlan();
-        *ctx->alt.gplan = G;
-    }
 
     ctx->exact_carry.clear();
     ctx->deferred_carry = 0;
@@ -2947,6 +2943,39 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         const bool big = (A.img_rows0 + A.img_rows1) * img_stride > VIEW_MIN_IMAGE_BYTES;
         if ((ctx->use_views == 1 && big) || ctx->use_views == 2) SPK_TRY(build_view_images(ctx, A, img_stride, &V, &have_view));
     }
+    // ---- graph replay: everything the launches' arguments and decisions depend on
+    std::vector<int64_t> gkey;
+    {
+        auto ptr = [](const void *q) { return (int64_t)(uintptr_t)q; };
+        gkey = {P, n_win, split ? 1 : 0, W, K, ctx->code_bytes, (int64_t)ctx->pairs_epoch, (int64_t)ctx->table_epoch,
+                (int64_t)std::hash<std::string>()(std::string(blob.begin(), blob.end())), ctx->lev_kernel,
+                ctx->lev_bag ? 1 : 0, ctx->filter_mode, ctx->use_views, ctx->slow_force_skip ? 1 : 0,
+                have_view ? 1 : 0, ptr(ctx->stream), ptr(ctx->codes.p), ptr(ctx->pl.p), ptr(ctx->pr.p), ptr(ctx->pvl.p),
+                ptr(ctx->prog_blob.p), ptr(ctx->img[0].p), ptr(ctx->img[1].p), ptr(ctx->work.p), ptr(ctx->xlist.p),
+                ptr(ctx->xinfo.p), ptr(ctx->xpref.p), ptr(ctx->region_count.p), ctx->xcap, ptr(ctx->alt.work.p),
+                ptr(ctx->alt.xlist.p), ptr(ctx->alt.xinfo.p), ptr(ctx->alt.xpref.p), ptr(ctx->alt.region_count.p),
+                ctx->alt.xcap, ptr(ctx->alt.stream), ctx->slow_seen_valid ? 1 : 0, (int64_t)ctx->timing};
+        for (uint8_t f : ctx->slow_seen) gkey.push_back(f);
+        for (int v = 0; v < MAX_VIEWS; ++v) gkey.push_back(ptr(ctx->vimg[v][0].p));
+    }
+    const bool graphable = ctx->use_graph && !ctx->timing_exact && P > 0 && fresh_blob && (split || n_win == 1);
+    const bool replay = graphable && ctx->gexec && gkey == ctx->gkey;
+    const bool capture = graphable && !replay && gkey == ctx->gkey_prev;  // the second call with this key
+    ctx->gkey_prev = gkey;
+    if (split && !replay) {  // window 1's plan: the same program, its own window arguments
+        if (!ctx->alt.gplan) ctx->alt.gplan = new GammaPlan();
+        *ctx->alt.gplan = G;
+    }
+    bool via_graph = replay;
+    if (replay) {
+        // the plans as the captured call left them; the slow-list launches it skipped
+        ctx->gplan->slow_skipped = ctx->gskip0;
+        if (split) ctx->alt.gplan->slow_skipped = ctx->gskip1;
+        ctx->last_view_regions = ctx->gview_regions;
+        SPK_HIP(hipGraphLaunch(ctx->gexec, ctx->stream));
+        ++ctx->graph_launches;
+    } else {
+    auto run_windows = [&](bool in_graph) -> int {
     if (split) {
         // window 1's stream starts after everything queued so far (images, program blob, earlier reads of the
         // codes), together with window 0.  Starting it after window 0's filter instead (so that its filter runs
@@ -3015,16 +3044,20 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         const int64_t cap = std::max<int64_t>(ctx->xcap, std::max<int64_t>(Pw, 1 << 16));
         SPK_TRY(enqueue_phase(ctx, G, cap, /*skip=*/true));
         if (split) {
-            if (w == 0) {  // window 0's info block, on its own stream (not behind the join)
-                SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
-                SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+            if (w == 0) {  // window 0's info block, on its own stream (not behind the join; a graph reads it after)
+                if (!in_graph) {
+                    SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+                    SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+                }
                 continue;
             }
             // window 1: the join right after its last kernel (the context stream waits for nothing else of it), then
             // its info block, and the own slot back
             SPK_HIP(hipEventRecord(ctx->ev_join, ctx->stream));
-            SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
-            SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+            if (!in_graph) {
+                SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+                SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+            }
             ctx->gamma_pending = true;
             ctx->swap_slot();
             SPK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
@@ -3040,10 +3073,57 @@ extern "C" int spk_gammas(spk_ctx *ctx, int n_cols, const spk_column_program *co
         ctx->exact_carry = ctx->last_exact;
         ctx->deferred_carry = ctx->last_deferred;
     }
+        return SPK_OK;
+    };
+    bool cap = capture;
+    if (cap) {
+        if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+        if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
+        ctx->gexec = nullptr;
+        ctx->graph = nullptr;
+        ctx->gkey.clear();
+        if (hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            (void)hipGetLastError();
+            cap = false;
+            ctx->use_graph = false;
+        }
+    }
+    int rc = run_windows(cap);
+    if (cap) {
+        hipGraph_t g = nullptr;
+        hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (rc == SPK_OK && e == hipSuccess) e = hipGraphInstantiate(&ctx->gexec, g, nullptr, nullptr, 0);
+        if (rc == SPK_OK && e == hipSuccess) {
+            ctx->graph = g;
+            ctx->gkey = gkey;
+            ctx->gskip0 = ctx->gplan->slow_skipped;
+            if (split) ctx->gskip1 = ctx->alt.gplan->slow_skipped;
+            ctx->gview_regions = ctx->last_view_regions;
+            rc = hipGraphLaunch(ctx->gexec, ctx->stream) == hipSuccess ? SPK_OK : SPK_E_HIP;
+        } else {
+            // nothing of the captured pass ran: no graphs on this context from now on, the pass enqueued directly
+            if (g) (void)hipGraphDestroy(g);
+            ctx->gexec = nullptr;
+            (void)hipGetLastError();
+            ctx->use_graph = false;
+            cap = false;
+            if (rc == SPK_OK) rc = run_windows(false);
+        }
+    }
+    SPK_TRY(rc);
+    via_graph = cap;
+    }  // (not a replay)
     SPK_TRY(ctx->end(K_GAMMA));
-    if (!split) {  // (a split call read window 0's info block back in the loop)
+    if (!split || via_graph) {
+        // the info blocks on the context stream behind the pass (a split call without a graph read window 0's back
+        // in the loop, window 1's on its own stream)
         SPK_HIP(hipMemcpyAsync(ctx->h_info, ctx->xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
         SPK_HIP(hipEventRecord(ctx->ev_info, ctx->stream));
+        if (split) {
+            SPK_HIP(hipMemcpyAsync(ctx->alt.h_info, ctx->alt.xinfo.p, (size_t)n_all * 8, hipMemcpyDeviceToHost, ctx->stream));
+            SPK_HIP(hipEventRecord(ctx->alt.ev_info, ctx->stream));
+            ctx->alt.gamma_pending = true;
+        }
     }
     ++ctx->gamma_seq;
     ctx->gamma_pending = true;
@@ -3385,6 +3465,19 @@ extern "C" int spk_gammas_simple_count(spk_ctx *ctx, int *out) {
 extern "C" int spk_gammas_set_window(spk_ctx *ctx, int64_t pairs) {
     SPK_REQUIRE(ctx && pairs >= 0, SPK_E_INVALID, "spk_gammas_set_window: bad args");
     ctx->gamma_window = pairs;
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_set_graph(spk_ctx *ctx, int on) {
+    SPK_REQUIRE(ctx, SPK_E_INVALID, "null ctx");
+    ctx->use_graph = on != 0;
+    ctx->gkey_prev.clear();
+    return SPK_OK;
+}
+
+extern "C" int spk_gammas_graph_launches(spk_ctx *ctx, int64_t *out) {
+    SPK_REQUIRE(ctx && out, SPK_E_INVALID, "null arg");
+    *out = ctx->graph_launches;
     return SPK_OK;
 }
 

@@ -333,6 +333,17 @@ struct spk_ctx {
     int64_t split_min = (int64_t)1 << 22;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool split_ready = false;  // alt.stream and the events exist
+    // The pass's launches as a captured HIP graph (spk_gammas_set_graph, off by default): a call whose key -- program,
+    // pairs, tables, buffers, window layout, slow-list decisions -- equals the previous call's is captured, later
+    // calls with that key replay it (one launch instead of ~25 API calls).  Measured slower than direct launches
+    // on MI355X (cfg2 0.939 -> 0.954 ms per step, profiles/r6_ab_gamma_graph.log), so it is opt-in.
+    bool use_graph = false;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    std::vector<int64_t> gkey, gkey_prev;
+    std::vector<char> gskip0, gskip1;  // the slots' slow_skipped at capture
+    int64_t gview_regions = 0;
+    int64_t graph_launches = 0;        // replays so far (diagnostics)
     bool last_split = false;   // the last spk_gammas ran split: window 1 = pairs [split_w, P)
     int64_t split_w = 0;
     std::vector<int64_t> split_first, alt_xbase;  // per column: window 0's exact cells; window 1's list base

@@ -140,6 +140,43 @@ def test_two_stream_split_gives_identical_codes(dedupe_job, mode, lev):
     assert np.array_equal(stats_2, stats_1)
 
 
+@pytest.mark.parametrize("streams,mode", [(2, 1), (1, 1), (2, 101), (2, 21)])
+def test_graph_replay_gives_identical_codes(dedupe_job, streams, mode):
+    """spk_gammas_set_graph: repeated passes with the same program replay a captured HIP graph (the second call
+    captures, later ones replay).  Every pass's codes, exact-pass cells and the E+M statistics equal the directly
+    enqueued pass -- split or one stream, with every slow-list launch left to the settlement (+100, restored on
+    replay), with the forced rule-1 view launch (+20)."""
+    job, st, ref = dedupe_job
+    lam, m, u, n_stats = _em_args(job)
+    job.ctx.gammas_set_simple(mode)
+    try:
+        job.ctx.gammas_set_streams(streams, 0)
+        job.ctx.gammas_set_graph(False)
+        job.gammas(st)
+        stats_direct = job.ctx.em_iteration(lam, 1 - lam, m, u, n_stats)
+        exact_direct = job.ctx.gammas_exact_counts(len(COLS))
+        job.ctx.gammas_set_graph(True)
+        before = job.ctx.gammas_graph_launches()
+        for _ in range(4):
+            job.gammas(st)
+            stats = job.ctx.em_iteration(lam, 1 - lam, m, u, n_stats)
+            assert np.array_equal(stats, stats_direct)
+            assert job.ctx.gammas_exact_counts(len(COLS)) == exact_direct
+            assert (job.gammas_host() == ref).all()
+        assert job.ctx.gammas_graph_launches() - before >= 2  # calls 3 and 4 (call 2 captured)
+        # a different program (one column fewer) is enqueued directly, and the first program again is exact
+        st2 = dict(st)
+        st2["comparison_columns"] = st["comparison_columns"][:4]
+        job.gammas(st2)
+        assert (job.gammas_host() == ref[:, :4]).all()
+        job.gammas(st)
+        assert (job.gammas_host() == ref).all()
+    finally:
+        job.ctx.gammas_set_graph(False)
+        job.ctx.gammas_set_streams(2)
+        job.ctx.gammas_set_simple(1)
+
+
 def test_two_stream_split_exact_ms(dedupe_job):
     """The split pass reports an exact launch's time as the sum of its two windows' launches (spk_gammas_exact_ms),
     the one-stream pass as its one launch."""
