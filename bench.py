@@ -352,7 +352,7 @@ def main():
     rec_bytes = int(sum(arrow_utf8(df[c])[0][-1] for c in cols))
     gamma_bytes = local_pairs * (8 + K) + rec_bytes
     gamma_bytes_packed = local_pairs * (8 + code_bytes) + rec_bytes
-    roofline = {"bound": "hbm", "kernel": "spk_gammas pass (k_gamma_simple + k_gamma_exact per undecided column)",
+    roofline = {"bound": "hbm", "kernel": "spk_gammas pass (k_filter + list compaction + the exact passes of the undecided cells)",
                 "achieved": gamma_bytes / (g_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gamma_bytes / (g_ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                 "algorithmic_bytes_per_launch": gamma_bytes,
