@@ -383,10 +383,20 @@ int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *cols, const
                          const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
                          double *out_adj /* [count x n_tf_cols] or NULL */);
 /* tf_adjusted_match_prob = bayes(mp, adj_1, ..., adj_n) (:98-117) with adj_c = table_c[id] for pairs
- * with equal non-null values and 0.5 otherwise.  out (host) [start, start+count). */
+ * with equal non-null values and 0.5 otherwise.  out (host) [start, start+count); out_tf_mp = NULL keeps
+ * the results on the device (as spk_score with out = NULL), read back by range with spk_tf_copy. */
 int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0, const int64_t *const *ids_side1,
                  const double *const *adj_tables, const int64_t *table_sizes, int64_t start, int64_t count,
                  double *out_tf_mp, double *out_adj /* [count x n_tf_cols] or NULL */);
+/* Pairs [start, start + count) of the tf_adjusted_match_prob the last spk_tf_apply* call with out_tf_mp = NULL
+ * kept on the device (SPK_E_STATE when there is none for the current pair set; the range must lie inside the
+ * applied one).  Replaces collecting the reference's tf_adjusted_match_prob column (term_frequencies.py:159-168). */
+int spk_tf_copy(spk_ctx *ctx, int64_t start, int64_t count, double *out_tf_mp);
+/* How the per-value sums find the (value, pattern) counts: 0 (default) a direct histogram when n_values x
+ * n_patterns <= 2^28, else keys (value x n_patterns + pattern, 32-bit when they fit) + radix sort + run-length
+ * encode; 1 always the sort; 2 the sort with 64-bit keys (tests hold the three identical).  No reference
+ * counterpart (an implementation choice below term_frequencies.py:49-65). */
+int spk_tf_set_mode(spk_ctx *ctx, int mode);
 
 #ifdef __cplusplus
 }

@@ -48,7 +48,7 @@ EXPORTS = [
     "spk_tf_accumulate", "spk_tf_apply", "spk_jaro_winkler_sim", "spk_levenshtein", "spk_gammas_exact_counts",
     "spk_gammas_set_simple", "spk_gammas_exact_list", "spk_gammas_simple_count", "spk_em_set_lane_histogram", "spk_table_set_rank_null",
     "spk_gammas_view_regions", "spk_ctx_lds_per_block", "spk_ctx_memory", "spk_raw_utf8", "spk_raw_i64", "spk_key_build", "spk_rank_from_raw", "spk_cluster", "spk_table_add_raw_utf8",
-    "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns",
+    "spk_gammas_implied_pairs", "spk_tf_column_values", "spk_tf_accumulate_column", "spk_tf_apply_columns", "spk_tf_copy", "spk_tf_set_mode",
     "spk_tf_accumulate_exact", "spk_tf_accumulate_column_exact", "spk_tf_limbs_to_sum", "spk_tf_scales",
     "spk_tf_scales_column", "spk_raw_utf8_arrow", "spk_raw_utf8_arrow_chunks", "spk_table_digest", "spk_raw_release",
     "spk_em_iteration_start", "spk_em_iteration_wait", "spk_ctx_kernel_ms_done", "spk_em_histogram_async",
@@ -574,18 +574,27 @@ class Context:
               "spk_tf_accumulate_column")
         return s[:n_values], c[:n_values]
 
-    def tf_apply_columns(self, cols, tables, start, count, want_adj=True):
+    def tf_apply_columns(self, cols, tables, start, count, want_adj=True, want_host=True):
+        """want_host=False: tf_adjusted_match_prob stays on the device (tf_copy reads ranges of it)."""
         n = len(tables)
         keep = [np.ascontiguousarray(t, dtype=np.float64) if len(t) else np.zeros(1) for t in tables]
         tabs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in keep])
         sizes = np.array([len(t) for t in tables], dtype=np.int64)
         cols = np.ascontiguousarray(cols, dtype=np.int32)
-        out = np.empty(count, dtype=np.float64)
+        out = np.empty(count, dtype=np.float64) if want_host else None
         adj = np.empty((count, n), dtype=np.float64) if want_adj else None
         check(self._lib.spk_tf_apply_columns(self._h, ctypes.c_int(n), _ptr(cols), tabs, _ptr(sizes),
                                              ctypes.c_int64(start), ctypes.c_int64(count), _ptr(out), _ptr(adj)),
               "spk_tf_apply_columns")
         return out, adj
+
+    def tf_set_mode(self, mode: int):
+        check(self._lib.spk_tf_set_mode(self._h, ctypes.c_int(mode)), "spk_tf_set_mode")
+
+    def tf_copy(self, start, count):
+        out = np.empty(count, dtype=np.float64)
+        check(self._lib.spk_tf_copy(self._h, ctypes.c_int64(start), ctypes.c_int64(count), _ptr(out)), "spk_tf_copy")
+        return out
 
     def tf_apply(self, ids0_list, ids1_list, tables, start, count, want_adj=True):
         n = len(tables)

@@ -3438,7 +3438,8 @@ extern "C" int spk_ctx_memory(spk_ctx *ctx, int64_t *out8) {
            b(ctx->alt.work) + b(ctx->alt.xlist) + b(ctx->alt.xpref) + b(ctx->alt.xinfo) + b(ctx->alt.region_count);
     m[6] = b(ctx->hist) + b(ctx->mpat) + b(ctx->llpat) + b(ctx->cpat) + b(ctx->stats) + b(ctx->mu) + b(ctx->em_ticket) +
            b(ctx->em_row) + b(ctx->em_hot) + b(ctx->mp) + b(ctx->mpat_score) + b(ctx->tf_uniq) + b(ctx->tf_runs) +
-           b(ctx->tf_nruns);
+           b(ctx->tf_nruns) + b(ctx->tf_mp) + b(ctx->tf_hist) +
+           b(ctx->tf_sort);
     for (int i = 0; i < 7; ++i) m[7] += m[i];
     for (int i = 0; i < 8; ++i) out8[i] = m[i];
     return SPK_OK;

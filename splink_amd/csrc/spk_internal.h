@@ -374,6 +374,11 @@ struct spk_ctx {
         return SPK_OK;
     }
     spk::DevBuf<double> mp;  // per-pair scores (final E-step)
+    // tf_adjusted_match_prob kept on the device (spk_tf_apply* with out_tf_mp = NULL): pairs [tf_start, tf_start +
+    // tf_count) of the pair set tf_epoch (pairs_epoch then); read back by range with spk_tf_copy
+    spk::DevBuf<double> tf_mp;
+    int64_t tf_start = 0, tf_count = -1;
+    uint64_t tf_epoch = 0;
     // mp per pattern of the last spk_score (the tf sums read it): a table of its own, since every EM
     // launch rewrites mpat with its iteration's parameters
     spk::DevBuf<double> mpat_score;
@@ -388,7 +393,11 @@ struct spk_ctx {
     // the (value, pattern) runs of the last tf scale pass over a device-id column, reused by its sum pass
     spk::DevBuf<unsigned long long> tf_uniq;
     spk::DevBuf<unsigned int> tf_runs, tf_nruns;
+    // or, when n_values x n_patterns is small enough, the (value, pattern) pair counts themselves (tf_pass)
+    spk::DevBuf<unsigned long long> tf_hist;
+    spk::DevBuf<uint8_t> tf_sort;  // the sort form's keys, sorted keys and sort scratch (scale pass to sum pass)
     std::vector<int64_t> tf_key;
+    int tf_mode = 0;  // spk_tf_set_mode: 0 auto (histogram when it fits), 1 always the sort, 2 the sort with 64-bit keys
     bool hist_lanes = true;  // k_hist_lanes (lane-private LDS counters) when the pattern space fits
     bool em_fence = true;    // k_em_iter: release fence before each ticket (spk_em_set_lane_histogram 2: none)
 

@@ -28,17 +28,20 @@ constexpr int TF_LIMBS = SPK_TF_LIMBS;
 constexpr int TF_BITS = 20;
 constexpr unsigned long long TF_NONE = ~0ull;  // key of a pair that does not qualify
 
-// key = value << 32 | code for pairs with equal, non-NULL values and a non-NULL mp, else TF_NONE
-template <typename CodeT>
+// key = value * n_patterns + code for pairs with equal, non-NULL values and a non-NULL mp, else `none` (all ones in
+// the key's bits: the keys are sorted over bit_length(n_values * n_patterns) bits only, in 32-bit words when that
+// fits -- cfg3 on one GPU: 31 bits instead of 64, half the bytes and half the radix passes)
+template <typename KeyT, typename CodeT>
 __global__ void k_tf_keys(int64_t P, const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
                           const int64_t *__restrict__ ids0, const int64_t *__restrict__ ids1, const CodeT *__restrict__ codes,
-                          const double *__restrict__ mpat, int64_t n_values, unsigned long long *__restrict__ keys) {
+                          const double *__restrict__ mpat, int64_t n_values, int64_t npat, KeyT none,
+                          KeyT *__restrict__ keys) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
     const int64_t a = ids0[pl[p]], b = ids1[pr[p]];
     const uint32_t c = (uint32_t)codes[p];
     const bool ok = a >= 0 && a == b && a < n_values && !isnan(mpat[c]);
-    keys[p] = ok ? (((unsigned long long)a << 32) | c) : TF_NONE;
+    keys[p] = ok ? (KeyT)(a * npat + (int64_t)c) : none;
 }
 
 // The fixed-point limbs of y = x 2^-E (x > 0, y < 1 for E >= ilogb(x) + 1): y = Σ_j limb_j 2^(-20 j),
@@ -75,31 +78,33 @@ __device__ inline int tf_exponent(double x) {
 constexpr int TF_NO_SCALE = INT32_MIN;  // a value with no (positive) term
 
 // One run of equal keys: the value's scale (max of its terms' exponents).
-__global__ void k_tf_scale(const unsigned long long *__restrict__ keys, const unsigned int *__restrict__ n_runs,
-                           const double *__restrict__ mpat, int *__restrict__ scale) {
+template <typename KeyT>
+__global__ void k_tf_scale(const KeyT *__restrict__ keys, const unsigned int *__restrict__ n_runs,
+                           const double *__restrict__ mpat, int64_t npat, KeyT none, int *__restrict__ scale) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)*n_runs) return;
-    const unsigned long long k = keys[i];
-    if (k == TF_NONE) return;
-    const double x = mpat[(uint32_t)(k & 0xFFFFFFFFu)];
-    if (x > 0.0) atomicMax(&scale[(int64_t)(k >> 32)], tf_exponent(x));
+    const KeyT k = keys[i];
+    if (k == none) return;
+    const int64_t v = (int64_t)k / npat;
+    const double x = mpat[(int64_t)k - v * npat];
+    if (x > 0.0) atomicMax(&scale[v], tf_exponent(x));
 }
 
 // One run of equal keys: its count times the pattern's mp, scaled by the value's 2^-E, limb by limb, into
 // the value's accumulator.
-__global__ void k_tf_runs(const unsigned long long *__restrict__ keys, const unsigned int *__restrict__ counts,
-                          const unsigned int *__restrict__ n_runs, const double *__restrict__ mpat,
+template <typename KeyT>
+__global__ void k_tf_runs(const KeyT *__restrict__ keys, const unsigned int *__restrict__ counts,
+                          const unsigned int *__restrict__ n_runs, const double *__restrict__ mpat, int64_t npat, KeyT none,
                           const int *__restrict__ scale, unsigned long long *__restrict__ acc,
                           unsigned long long *__restrict__ cnt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)*n_runs) return;
-    const unsigned long long k = keys[i];
-    if (k == TF_NONE) return;
-    const int64_t v = (int64_t)(k >> 32);
-    const uint32_t c = (uint32_t)(k & 0xFFFFFFFFu);
+    const KeyT k = keys[i];
+    if (k == none) return;
+    const int64_t v = (int64_t)k / npat;
+    const double x = mpat[(int64_t)k - v * npat];
     const unsigned long long n = counts[i];
     atomicAdd(&cnt[v], n);
-    const double x = mpat[c];
     const int E = scale[v];
     if (!(x > 0.0) || E == TF_NO_SCALE) return;
     uint32_t limb[TF_LIMBS];
@@ -107,6 +112,136 @@ __global__ void k_tf_runs(const unsigned long long *__restrict__ keys, const uns
 #pragma unroll
     for (int j = 0; j < TF_LIMBS; ++j)
         if (limb[j]) atomicAdd(&acc[v * TF_LIMBS + j], n * (unsigned long long)limb[j]);
+}
+
+// The (value, pattern) counts directly: one counter per value x pattern (64-bit), lanes of a wave with equal
+// keys add once (the pairs of a block share a value and mostly a pattern, so a wave adds a few times, not 64).
+// Replaces the keys + radix sort + run-length encode of tf_pass when n_values x n_patterns <= TF_HIST_MAX: the
+// whole cfg3 job on one GPU (3.08e9 pairs, 300k values x 576 patterns) sorted 6 x 2^30 keys, ~0.35 s of device
+// time (profiles/r6_tf_sort_kernel_stats.csv).  The counts are the runs' counts, so the sums are identical.
+constexpr int64_t TF_HIST_MAX = (int64_t)1 << 28;
+template <typename CodeT>
+__global__ void k_tf_hist(int64_t P, const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
+                          const int64_t *__restrict__ ids0, const int64_t *__restrict__ ids1,
+                          const CodeT *__restrict__ codes, const double *__restrict__ mpat, int64_t n_values,
+                          int64_t npat, unsigned long long *__restrict__ hist) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < P; base += stride) {  // wave-uniform
+        const int64_t p = base + threadIdx.x;
+        int64_t key = -1;
+        if (p < P) {
+            const int64_t a = ids0[pl[p]], b = ids1[pr[p]];
+            const uint32_t c = (uint32_t)codes[p];
+            if (a >= 0 && a == b && a < n_values && !isnan(mpat[c])) key = a * npat + (int64_t)c;
+        }
+        bool todo = key >= 0;
+        while (__any(todo)) {  // one add per distinct key of the wave
+            const unsigned long long m = __ballot(todo);
+            const int lead = __ffsll((unsigned long long)m) - 1;
+            const int64_t k = __shfl(key, lead);
+            const unsigned long long same = __ballot(todo && key == k);
+            if ((int)(threadIdx.x & 63) == lead) atomicAdd(&hist[k], (unsigned long long)__popcll(same));
+            todo = todo && key != k;
+        }
+    }
+}
+
+// The scale / sum passes over the histogram's non-zero counters (as k_tf_scale / k_tf_runs over the runs).
+__global__ void k_tf_hist_apply(int64_t M, int64_t npat, const unsigned long long *__restrict__ hist,
+                                const double *__restrict__ mpat, int *__restrict__ scale, unsigned long long *__restrict__ acc,
+                                unsigned long long *__restrict__ cnt) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += stride) {
+        const unsigned long long n = hist[i];
+        if (!n) continue;
+        const int64_t v = i / npat;
+        const double x = mpat[i - v * npat];
+        if (!acc) {
+            if (x > 0.0) atomicMax(&scale[v], tf_exponent(x));
+            continue;
+        }
+        atomicAdd(&cnt[v], n);
+        const int E = scale[v];
+        if (!(x > 0.0) || E == TF_NO_SCALE) continue;
+        uint32_t limb[TF_LIMBS];
+        tf_limbs(x, E, limb);
+#pragma unroll
+        for (int j = 0; j < TF_LIMBS; ++j)
+            if (limb[j]) atomicAdd(&acc[v * TF_LIMBS + j], n * (unsigned long long)limb[j]);
+    }
+}
+
+// The sort form of tf_pass: (value, pattern) keys of `bits` bits, radix-sorted and run-length encoded, chunk by
+// chunk.  The keys, the sorted keys and the sort's scratch live in one context buffer (tf_sort) from the scale
+// pass to the sum pass, instead of five hipMalloc / hipFree pairs per pass: at cfg3's 3.08e9 pairs those were
+// ~36 GB per pass, and the same kernels' tf stage took 0.49 s on one box and 1.8 s on another
+// (profiles/r6_fulljob_cfg3_1gpu_tfsort*.json).
+template <typename KeyT>
+static int tf_pass_sort(spk_ctx *ctx, int64_t n_values, int64_t npat, int bits, const int64_t *d0, const int64_t *d1,
+                        int *d_scale, unsigned long long *acc, unsigned long long *cnt, const std::vector<int64_t> *key) {
+    const int64_t P = ctx->n_pairs;
+    const KeyT none = (KeyT)(bits >= 64 ? ~0ull : ((1ull << bits) - 1));
+    // the sort and the run counts work on uint32 lengths: chunks of at most 2^30 pairs
+    const int64_t CH = (int64_t)1 << 30;
+    const bool cache = key != nullptr && P <= CH;
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(P, 1), CH);
+    const size_t kb = ((size_t)cap * sizeof(KeyT) + 255) & ~(size_t)255;
+    auto finish = [&]() {  // the sum pass ends the column's use of the sort buffers
+        if (acc) {
+            ctx->tf_sort.release();
+            ctx->tf_uniq.release();
+            ctx->tf_runs.release();
+            ctx->tf_key.clear();
+        }
+    };
+    if (cache && ctx->tf_key == *key && ctx->tf_uniq.p) {  // the runs of the scale pass
+        const unsigned g = (unsigned)((cap + 255) / 256);
+        const KeyT *uk = reinterpret_cast<const KeyT *>(ctx->tf_uniq.p);
+        if (acc) k_tf_runs<KeyT><<<g, 256, 0, ctx->stream>>>(uk, ctx->tf_runs.p, ctx->tf_nruns.p, ctx->mpat_score.p, npat, none,
+                                                             d_scale, acc, cnt);
+        else k_tf_scale<KeyT><<<g, 256, 0, ctx->stream>>>(uk, ctx->tf_nruns.p, ctx->mpat_score.p, npat, none, d_scale);
+        SPK_HIP(hipGetLastError());
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        finish();
+        return SPK_OK;
+    }
+    ctx->tf_key.clear();
+    SPK_TRY(ctx->tf_uniq.alloc((size_t)cap));  // 8-byte slots: room for either key width
+    SPK_TRY(ctx->tf_runs.alloc((size_t)cap));
+    SPK_TRY(ctx->tf_nruns.alloc(1));
+    KeyT *uniq = reinterpret_cast<KeyT *>(ctx->tf_uniq.p);
+    size_t bytes = 0, b2 = 0;
+    SPK_HIP(rocprim::radix_sort_keys(nullptr, bytes, (KeyT *)nullptr, (KeyT *)nullptr, (size_t)cap, 0, bits, ctx->stream));
+    SPK_HIP(rocprim::run_length_encode(nullptr, b2, (KeyT *)nullptr, (size_t)cap, uniq, ctx->tf_runs.p, ctx->tf_nruns.p,
+                                       ctx->stream));
+    const size_t tb = std::max(bytes, b2) + 256;
+    SPK_TRY(ctx->tf_sort.alloc(2 * kb + tb));
+    KeyT *k_in = reinterpret_cast<KeyT *>(ctx->tf_sort.p), *k_out = reinterpret_cast<KeyT *>(ctx->tf_sort.p + kb);
+    uint8_t *tmp = ctx->tf_sort.p + 2 * kb;
+    for (int64_t c0 = 0; c0 < P; c0 += CH) {
+        const int64_t n = std::min<int64_t>(CH, P - c0);
+        const unsigned g = (unsigned)((n + 255) / 256);
+        if (ctx->code_bytes == 2)
+            k_tf_keys<KeyT, uint16_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
+                                                                 reinterpret_cast<const uint16_t *>(ctx->codes.p) + c0,
+                                                                 ctx->mpat_score.p, n_values, npat, none, k_in);
+        else
+            k_tf_keys<KeyT, uint32_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
+                                                                 reinterpret_cast<const uint32_t *>(ctx->codes.p) + c0,
+                                                                 ctx->mpat_score.p, n_values, npat, none, k_in);
+        SPK_HIP(hipGetLastError());
+        size_t tb1 = tb, tb2 = tb;
+        SPK_HIP(rocprim::radix_sort_keys(tmp, tb1, k_in, k_out, (size_t)n, 0, bits, ctx->stream));
+        SPK_HIP(rocprim::run_length_encode(tmp, tb2, k_out, (size_t)n, uniq, ctx->tf_runs.p, ctx->tf_nruns.p, ctx->stream));
+        if (acc) k_tf_runs<KeyT><<<g, 256, 0, ctx->stream>>>(uniq, ctx->tf_runs.p, ctx->tf_nruns.p, ctx->mpat_score.p, npat,
+                                                             none, d_scale, acc, cnt);
+        else k_tf_scale<KeyT><<<g, 256, 0, ctx->stream>>>(uniq, ctx->tf_nruns.p, ctx->mpat_score.p, npat, none, d_scale);
+        SPK_HIP(hipGetLastError());
+    }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    if (cache && !acc) ctx->tf_key = *key;  // the sum pass reuses these runs
+    finish();
+    return SPK_OK;
 }
 
 // The runs of (value, pattern) keys of the current pairs, value ids per row on the device (d0 side 0, d1
@@ -121,68 +256,44 @@ static int tf_pass(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int6
     SPK_REQUIRE(ctx->mpat_valid && ctx->mpat_score.p, SPK_E_STATE, "tf: run spk_score first (mp per pattern)");
     SPK_REQUIRE(n_values < ((int64_t)1 << 31), SPK_E_LIMIT, "tf: more than 2^31 distinct values");
     const int64_t P = ctx->n_pairs;
-    // the sort and the run counts work on uint32 lengths: chunks of at most 2^30 pairs
-    const int64_t CH = (int64_t)1 << 30;
-    const bool cache = key != nullptr && P <= CH;
-    const int64_t cap = std::min<int64_t>(std::max<int64_t>(P, 1), CH);
-    if (cache && ctx->tf_key == *key && ctx->tf_uniq.p) {  // the runs of the scale pass
-        const unsigned g = (unsigned)((cap + 255) / 256);
-        if (acc) k_tf_runs<<<g, 256, 0, ctx->stream>>>(ctx->tf_uniq.p, ctx->tf_runs.p, ctx->tf_nruns.p, ctx->mpat_score.p,
-                                                       d_scale, acc, cnt);
-        else k_tf_scale<<<g, 256, 0, ctx->stream>>>(ctx->tf_uniq.p, ctx->tf_nruns.p, ctx->mpat_score.p, d_scale);
-        SPK_HIP(hipGetLastError());
-        if (acc) {
-            SPK_HIP(hipStreamSynchronize(ctx->stream));
+    const int64_t npat = std::max<int64_t>(ctx->n_patterns, 1);
+    if (ctx->tf_mode == 0 && n_values <= TF_HIST_MAX / npat) {  // the counts directly, no sort
+        const int64_t M = std::max<int64_t>(n_values * npat, 1);
+        const bool hit = key != nullptr && ctx->tf_key == *key && ctx->tf_hist.p && ctx->tf_hist.n >= (size_t)M;
+        if (!hit) {
+            ctx->tf_key.clear();
             ctx->tf_uniq.release();
             ctx->tf_runs.release();
+            SPK_TRY(ctx->tf_hist.alloc((size_t)M));
+            SPK_HIP(hipMemsetAsync(ctx->tf_hist.p, 0, (size_t)M * 8, ctx->stream));
+            const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((P + 255) / 256, 64 * (int64_t)ctx->n_cu));
+            if (P > 0) {
+                if (ctx->code_bytes == 2)
+                    k_tf_hist<uint16_t><<<g, 256, 0, ctx->stream>>>(P, ctx->pl.p, ctx->pr.p, d0, d1,
+                                                                   reinterpret_cast<const uint16_t *>(ctx->codes.p),
+                                                                   ctx->mpat_score.p, n_values, npat, ctx->tf_hist.p);
+                else
+                    k_tf_hist<uint32_t><<<g, 256, 0, ctx->stream>>>(P, ctx->pl.p, ctx->pr.p, d0, d1,
+                                                                   reinterpret_cast<const uint32_t *>(ctx->codes.p),
+                                                                   ctx->mpat_score.p, n_values, npat, ctx->tf_hist.p);
+                SPK_HIP(hipGetLastError());
+            }
+        }
+        const unsigned g2 = (unsigned)std::max<int64_t>(1, std::min<int64_t>((M + 255) / 256, 16 * (int64_t)ctx->n_cu));
+        k_tf_hist_apply<<<g2, 256, 0, ctx->stream>>>(M, npat, ctx->tf_hist.p, ctx->mpat_score.p, d_scale, acc, cnt);
+        SPK_HIP(hipGetLastError());
+        SPK_HIP(hipStreamSynchronize(ctx->stream));
+        if (key != nullptr && !acc) {
+            ctx->tf_key = *key;  // the sum pass with the same key reuses the counts
+        } else {
             ctx->tf_key.clear();
+            ctx->tf_hist.release();
         }
         return SPK_OK;
     }
-    DevBuf<unsigned long long> k_in, k_out, uniq_l;
-    DevBuf<unsigned int> runs_l, n_runs_l;
-    DevBuf<uint8_t> tmp;
-    DevBuf<unsigned long long> &uniq = cache ? ctx->tf_uniq : uniq_l;
-    DevBuf<unsigned int> &runs = cache ? ctx->tf_runs : runs_l;
-    DevBuf<unsigned int> &n_runs = cache ? ctx->tf_nruns : n_runs_l;
-    if (cache) ctx->tf_key.clear();
-    SPK_TRY(k_in.alloc((size_t)cap));
-    SPK_TRY(k_out.alloc((size_t)cap));
-    SPK_TRY(uniq.alloc((size_t)cap));
-    SPK_TRY(runs.alloc((size_t)cap));
-    SPK_TRY(n_runs.alloc(1));
-    for (int64_t c0 = 0; c0 < P; c0 += CH) {
-        const int64_t n = std::min<int64_t>(CH, P - c0);
-        const unsigned g = (unsigned)((n + 255) / 256);
-        if (ctx->code_bytes == 2)
-            k_tf_keys<uint16_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
-                                                           reinterpret_cast<const uint16_t *>(ctx->codes.p) + c0,
-                                                           ctx->mpat_score.p, n_values, k_in.p);
-        else
-            k_tf_keys<uint32_t><<<g, 256, 0, ctx->stream>>>(n, ctx->pl.p + c0, ctx->pr.p + c0, d0, d1,
-                                                           reinterpret_cast<const uint32_t *>(ctx->codes.p) + c0,
-                                                           ctx->mpat_score.p, n_values, k_in.p);
-        SPK_HIP(hipGetLastError());
-        size_t bytes = 0, b2 = 0;
-        SPK_HIP(rocprim::radix_sort_keys(nullptr, bytes, k_in.p, k_out.p, (size_t)n, 0, 64, ctx->stream));
-        SPK_HIP(rocprim::run_length_encode(nullptr, b2, k_out.p, (size_t)n, uniq.p, runs.p, n_runs.p, ctx->stream));
-        SPK_TRY(tmp.alloc(std::max(bytes, b2) + 1));
-        SPK_HIP(rocprim::radix_sort_keys(tmp.p, bytes, k_in.p, k_out.p, (size_t)n, 0, 64, ctx->stream));
-        SPK_HIP(rocprim::run_length_encode(tmp.p, b2, k_out.p, (size_t)n, uniq.p, runs.p, n_runs.p, ctx->stream));
-        if (acc) k_tf_runs<<<g, 256, 0, ctx->stream>>>(uniq.p, runs.p, n_runs.p, ctx->mpat_score.p, d_scale, acc, cnt);
-        else k_tf_scale<<<g, 256, 0, ctx->stream>>>(uniq.p, n_runs.p, ctx->mpat_score.p, d_scale);
-        SPK_HIP(hipGetLastError());
-    }
-    if (cache) {
-        SPK_HIP(hipStreamSynchronize(ctx->stream));  // the locals (keys, sort scratch) are freed on return
-        if (acc) {
-            ctx->tf_uniq.release();
-            ctx->tf_runs.release();
-        } else {
-            ctx->tf_key = *key;
-        }
-    }
-    return SPK_OK;
+    const int bits = 64 - __builtin_clzll((unsigned long long)std::max<int64_t>(n_values * npat, 1));
+    if (bits <= 32 && ctx->tf_mode != 2) return tf_pass_sort<uint32_t>(ctx, n_values, npat, bits, d0, d1, d_scale, acc, cnt, key);
+    return tf_pass_sort<unsigned long long>(ctx, n_values, npat, bits, d0, d1, d_scale, acc, cnt, key);
 }
 
 __global__ void k_fill_i32(int64_t n, int v, int *__restrict__ out) {
@@ -419,18 +530,58 @@ static int tf_apply_dev(spk_ctx *ctx, TfApply &T, const double *const *adj_table
         T.tab[c] = dt[c].p;
         T.tab_n[c] = table_sizes[c];
     }
-    SPK_TRY(dout.alloc((size_t)count + 1));
+    // out_tf_mp = NULL: the results stay on the device (ctx->tf_mp, read by range with spk_tf_copy), as spk_score
+    // keeps mp there -- at cfg3's 3.08e9 pairs the host copy alone (24.6 GB into pageable memory) took ~5.8 s of
+    // the 6.1 s tf stage (profiles/r6_fulljob_cfg3_10Mx10M_1gpu.json)
+    const bool dev_out = out_tf_mp == nullptr;
+    ctx->tf_count = -1;
+    double *res = nullptr;
+    if (dev_out) {
+        SPK_TRY(ctx->tf_mp.alloc((size_t)count + 1));
+        res = ctx->tf_mp.p;
+    } else {
+        SPK_TRY(dout.alloc((size_t)count + 1));
+        res = dout.p;
+    }
     if (out_adj) SPK_TRY(dadj.alloc((size_t)count * T.n + 1));
     if (count)
         k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
-                                                                         ctx->mp.p, dout.p,
-                                                                         out_adj ? dadj.p : nullptr);
+                                                                         ctx->mp.p, res, out_adj ? dadj.p : nullptr);
     SPK_HIP(hipGetLastError());
     if (count) {
-        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (!dev_out) SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
         if (out_adj)
             SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * T.n * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
+    SPK_HIP(hipStreamSynchronize(ctx->stream));
+    if (dev_out) {
+        ctx->tf_start = start;
+        ctx->tf_count = count;
+        ctx->tf_epoch = ctx->pairs_epoch;
+    }
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_set_mode(spk_ctx *ctx, int mode) {
+    SPK_REQUIRE(ctx && mode >= 0 && mode <= 2, SPK_E_INVALID, "spk_tf_set_mode: mode 0 (auto), 1 (sort) or 2 (sort, 64-bit keys)");
+    ctx->tf_mode = mode;
+    ctx->tf_key.clear();
+    ctx->tf_hist.release();
+    ctx->tf_uniq.release();
+    ctx->tf_runs.release();
+    return SPK_OK;
+}
+
+extern "C" int spk_tf_copy(spk_ctx *ctx, int64_t start, int64_t count, double *out_tf_mp) {
+    SPK_REQUIRE(ctx && count >= 0 && (count == 0 || out_tf_mp), SPK_E_INVALID, "spk_tf_copy: bad args");
+    SPK_REQUIRE(ctx->tf_count >= 0 && ctx->tf_epoch == ctx->pairs_epoch, SPK_E_STATE,
+                "spk_tf_copy: no device-resident tf results for this pair set (spk_tf_apply* with out_tf_mp = NULL)");
+    SPK_REQUIRE(start >= ctx->tf_start && start + count <= ctx->tf_start + ctx->tf_count, SPK_E_INVALID,
+                "spk_tf_copy: range outside the applied pairs");
+    SPK_HIP(hipSetDevice(ctx->device));
+    if (count)
+        SPK_HIP(hipMemcpyAsync(out_tf_mp, ctx->tf_mp.p + (start - ctx->tf_start), (size_t)count * 8,
+                               hipMemcpyDeviceToHost, ctx->stream));
     SPK_HIP(hipStreamSynchronize(ctx->stream));
     return SPK_OK;
 }
@@ -438,8 +589,7 @@ static int tf_apply_dev(spk_ctx *ctx, TfApply &T, const double *const *adj_table
 extern "C" int spk_tf_apply_columns(spk_ctx *ctx, int n_tf_cols, const int32_t *cols, const double *const *adj_tables,
                                     const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
                                     double *out_adj) {
-    SPK_REQUIRE(ctx && cols && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID,
-                "spk_tf_apply_columns: 1..8 columns");
+    SPK_REQUIRE(ctx && cols && n_tf_cols >= 1 && n_tf_cols <= 8, SPK_E_INVALID, "spk_tf_apply_columns: 1..8 columns");
     SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply_columns: run spk_score first");
     SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply_columns: range");
     SPK_HIP(hipSetDevice(ctx->device));
@@ -462,42 +612,22 @@ extern "C" int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *i
                             const int64_t *const *ids_side1, const double *const *adj_tables,
                             const int64_t *table_sizes, int64_t start, int64_t count, double *out_tf_mp,
                             double *out_adj) {
-    SPK_REQUIRE(ctx && n_tf_cols >= 1 && n_tf_cols <= 8 && out_tf_mp, SPK_E_INVALID, "spk_tf_apply: 1..8 columns");
+    SPK_REQUIRE(ctx && n_tf_cols >= 1 && n_tf_cols <= 8, SPK_E_INVALID, "spk_tf_apply: 1..8 columns");
     SPK_REQUIRE(ctx->pairs_valid && ctx->mp.p, SPK_E_STATE, "spk_tf_apply: run spk_score first");
     SPK_REQUIRE(start >= 0 && count >= 0 && start + count <= ctx->n_pairs, SPK_E_INVALID, "spk_tf_apply: range");
     SPK_HIP(hipSetDevice(ctx->device));
     SPK_TRY(settle_gammas(ctx, nullptr));
     Table &t0 = ctx->table[0], &t1 = ctx->side_table(1);
     DevBuf<int64_t> d0[8], d1[8];
-    DevBuf<double> dt[8], dout, dadj;
     TfApply T{};
     T.n = n_tf_cols;
     for (int c = 0; c < n_tf_cols; ++c) {
         SPK_TRY(d0[c].alloc((size_t)t0.n + 1));
         SPK_TRY(d1[c].alloc((size_t)t1.n + 1));
-        SPK_TRY(dt[c].alloc((size_t)table_sizes[c] + 1));
         SPK_HIP(hipMemcpyAsync(d0[c].p, ids_side0[c], (size_t)t0.n * 8, hipMemcpyHostToDevice, ctx->stream));
         SPK_HIP(hipMemcpyAsync(d1[c].p, ids_side1[c], (size_t)t1.n * 8, hipMemcpyHostToDevice, ctx->stream));
-        if (table_sizes[c])
-            SPK_HIP(hipMemcpyAsync(dt[c].p, adj_tables[c], (size_t)table_sizes[c] * 8, hipMemcpyHostToDevice,
-                                   ctx->stream));
         T.ids0[c] = d0[c].p;
         T.ids1[c] = d1[c].p;
-        T.tab[c] = dt[c].p;
-        T.tab_n[c] = table_sizes[c];
     }
-    SPK_TRY(dout.alloc((size_t)count + 1));
-    if (out_adj) SPK_TRY(dadj.alloc((size_t)count * n_tf_cols + 1));
-    if (count)
-        k_tf_apply<<<(unsigned)((count + 255) / 256), 256, 0, ctx->stream>>>(T, start, count, ctx->pl.p, ctx->pr.p,
-                                                                         ctx->mp.p, dout.p,
-                                                                         out_adj ? dadj.p : nullptr);
-    SPK_HIP(hipGetLastError());
-    if (count) {
-        SPK_HIP(hipMemcpyAsync(out_tf_mp, dout.p, (size_t)count * 8, hipMemcpyDeviceToHost, ctx->stream));
-        if (out_adj)
-            SPK_HIP(hipMemcpyAsync(out_adj, dadj.p, (size_t)count * n_tf_cols * 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    SPK_HIP(hipStreamSynchronize(ctx->stream));
-    return SPK_OK;
+    return tf_apply_dev(ctx, T, adj_tables, table_sizes, start, count, out_tf_mp, out_adj);
 }

@@ -328,3 +328,100 @@ def test_tf_adjusted_tiny_mp_link_only_matches_oracle(amd):
     codes, _ = pd.factorize(pd.concat([vl, vr], ignore_index=True), use_na_sentinel=True)
     want, _ = orc.tf_adjust_codes(codes[:len(vl)][l], codes[len(vl):][r], mp, lam)
     assert np.allclose(tf_mp, want, rtol=1e-9, atol=0, equal_nan=True)
+
+
+def test_tf_results_kept_on_device(amd):
+    """spk_tf_apply_columns with out_tf_mp = NULL keeps tf_adjusted_match_prob on the device (as spk_score keeps mp);
+    spk_tf_copy reads ranges of it back, bit-identical to the host-copy form; ranges outside the applied pairs and a
+    replaced pair set are refused (term_frequencies.py:159-168)."""
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    from splink_amd.term_frequencies import _bayes_pair
+    df = make_records(30_000, seed=46, surname_vocab=600)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
+    a, b = df.iloc[:15_000].reset_index(drop=True), df.iloc[15_000:].reset_index(drop=True)
+    settings = cfg_settings(2)
+    settings["link_type"] = "link_only"
+    params = Params(settings, amd)
+    st = params.settings
+    job = Job("link_only", [a, b], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    lam = 0.3
+    job.score(lam, params._level_probabilities(), want_host=False)
+    col = job._col_index[("surname", "str")]
+    n_values = job.ctx.tf_column_values(col)
+    sums, counts = job.ctx.tf_accumulate_column(col, n_values)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
+    table = _bayes_pair(adj_lambda, float(1 - lam))
+    P = job.n_pairs
+    assert P > 10_000
+    host, _ = job.ctx.tf_apply_columns([col], [table], 0, P, want_adj=False)
+    with pytest.raises(RuntimeError):  # the host form keeps nothing on the device
+        job.ctx.tf_copy(0, 1)
+    assert job.ctx.tf_apply_columns([col], [table], 0, P, want_adj=False, want_host=False)[0] is None
+    assert np.array_equal(job.ctx.tf_copy(0, P), host, equal_nan=True)
+    s0, n = P // 3, P // 4
+    assert np.array_equal(job.ctx.tf_copy(s0, n), host[s0:s0 + n], equal_nan=True)
+    job.ctx.tf_apply_columns([col], [table], s0, n, want_adj=False, want_host=False)  # a range of the pairs
+    assert np.array_equal(job.ctx.tf_copy(s0 + 5, 100), host[s0 + 5:s0 + 105], equal_nan=True)
+    with pytest.raises(ValueError):
+        job.ctx.tf_copy(0, 10)
+    with pytest.raises(ValueError):
+        job.ctx.tf_copy(s0 + n - 5, 10)
+    assert job.ctx.memory()["em_score_tf"] >= n * 8
+    job.block(st["blocking_rules"])  # a new pair set: the kept results no longer describe it
+    with pytest.raises(RuntimeError):
+        job.ctx.tf_copy(0, 1)
+
+
+@pytest.mark.parametrize("link_type", ["dedupe_only", "link_only"])
+def test_tf_histogram_matches_sort(amd, link_type):
+    """The tf sums from the direct (value, pattern) histogram (spk_tf_set_mode 0, the default when n_values x
+    n_patterns fits) equal the keys + radix sort + run-length encode form (mode 1: 32-bit keys; mode 2: 64-bit) exactly: scales, fixed-point limbs,
+    counts, and tf_adjusted_match_prob (term_frequencies.py:49-65, :122-168); through the device-id and the host-id
+    entry points, and with the scale pass's counts reused by the sum pass."""
+    from splink_amd.engine import Job
+    from splink_amd.params import Params
+    from splink_amd.synthetic import cfg_settings, make_records
+    from splink_amd import table as T
+    from splink_amd.term_frequencies import _bayes_pair
+    df = make_records(30_000, seed=47, surname_vocab=500)[["unique_id", "first_name", "surname", "dob", "city", "email"]]
+    settings = cfg_settings(2)
+    settings["link_type"] = link_type
+    params = Params(settings, amd)
+    st = params.settings
+    if link_type == "link_only":
+        job = Job("link_only", [df.iloc[:15_000].reset_index(drop=True), df.iloc[15_000:].reset_index(drop=True)],
+                  "unique_id", 0)
+    else:
+        job = Job("dedupe_only", [df], "unique_id", 0)
+    job.block(st["blocking_rules"])
+    job.gammas(st)
+    lam = 0.2
+    job.score(lam, params._level_probabilities(), want_host=False)
+    col = job._col_index[("surname", "str")]
+    n_values = job.ctx.tf_column_values(col)
+    got = {}
+    for mode in (0, 1, 2):
+        job.ctx.tf_set_mode(mode)
+        scale = job.ctx.tf_scales_column(col, n_values)
+        limbs, counts = job.ctx.tf_accumulate_column_exact(col, n_values, scale)
+        sums, counts2 = job.ctx.tf_accumulate_column(col, n_values)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            table = _bayes_pair(np.where(counts2 > 0, sums / np.maximum(counts2, 1), np.nan), float(1 - lam))
+        tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
+        sides = (0, 1) if link_type == "link_only" else (0,)  # host value ids (the non-device-id entry points)
+        vals = [pd.Series([None if T.is_null_scalar(v) else v for v in job.host_values(s, "surname").tolist()],
+                          dtype=object) for s in sides]
+        codes, nv = T.factorize_joint(vals)
+        ids0, ids1 = codes[0], (codes[1] if len(codes) > 1 else codes[0])
+        scale_h = job.ctx.tf_scales(nv, ids0, ids1)
+        limbs_h, counts_h = job.ctx.tf_accumulate_exact(nv, ids0, ids1, scale_h)
+        got[mode] = (scale, limbs, counts, sums, counts2, tf_mp, scale_h, limbs_h, counts_h)
+    job.ctx.tf_set_mode(0)
+    assert (got[0][2] > 0).sum() > 50
+    for mode in (1, 2):
+        for a, b in zip(got[0], got[mode]):
+            assert np.array_equal(a, b, equal_nan=True)

@@ -170,18 +170,21 @@ def main():
     wall["score"] = time.perf_counter() - t
     score_dev = job.ctx.kernel_ms()["score"]
     mem_mark("score")
-    tf_mp = None
     if link:  # term-frequency adjustment on surname (term_frequencies.py:122-168), device value ids
         from splink_amd.term_frequencies import _bayes_pair
         t = time.perf_counter()
         col = job._col_index[("surname", "str")]
         n_values = job.ctx.tf_column_values(col)
         sums, counts = job.ctx.tf_accumulate_column(col, n_values)
+        wall["tf_sums"] = time.perf_counter() - t
         with np.errstate(invalid="ignore", divide="ignore"):
             adj_lambda = np.where(counts > 0, sums / np.maximum(counts, 1), np.nan)
         table = _bayes_pair(adj_lambda, float(1 - params.params["λ"]))
-        tf_mp, _ = job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False)
+        # tf_adjusted_match_prob stays on the device, as the scores do (want_host=False above); the parity pass
+        # reads it back (spk_tf_copy)
+        job.ctx.tf_apply_columns([col], [table], 0, job.n_pairs, want_adj=False, want_host=False)
         wall["tf_adjust"] = time.perf_counter() - t
+        mem_mark("tf")
     total = time.perf_counter() - t_job
     # outside the job's wall: the same pass on one stream (spk_gammas_set_streams), against the default split
     job.ctx.gammas_set_streams(1)
@@ -250,6 +253,7 @@ def main():
         row["parity_em"] = {"iterations": len(hist_o), "lambda_m_u_1e-9": bool(ok), "match_probability_1e-9": mp_ok,
                             "pairs": int(P)}
         if link:
+            tf_mp = job.ctx.tf_copy(0, job.n_pairs)
             row["parity_tf"] = tf_parity(job, l, r, mp_dev, params.params["λ"], tf_mp)
         row["parity_check_s"] = time.perf_counter() - t
     out = json.dumps(row)
