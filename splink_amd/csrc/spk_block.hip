@@ -569,6 +569,8 @@ extern "C" int spk_block(spk_ctx *ctx, int link_type, int n_rules, const int32_t
     ctx->n_pairs = n_out;
     ctx->pairs_valid = true;
     ctx->pairs_epoch++;
+    ctx->tf_mp.release();  // a kept tf result describes the old pair set (spk_tf_copy refuses it)
+    ctx->tf_count = -1;
     ctx->codes_valid = false;
     if (out_n_pairs) *out_n_pairs = n_out;
     if (out_n_candidates_total) *out_n_candidates_total = total;

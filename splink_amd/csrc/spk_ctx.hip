@@ -694,6 +694,8 @@ int spk_pairs_load(spk_ctx *ctx, int64_t n, const int32_t *rows_l, const int32_t
     ctx->n_pairs = n;
     ctx->pairs_valid = true;
     ctx->pairs_epoch++;
+    ctx->tf_mp.release();  // a kept tf result describes the old pair set (spk_tf_copy refuses it)
+    ctx->tf_count = -1;
     ctx->n_views = 0;
     ctx->pv_base = n;
     ctx->pair_terms.clear();
