@@ -393,7 +393,7 @@ int spk_tf_apply(spk_ctx *ctx, int n_tf_cols, const int64_t *const *ids_side0, c
  * applied one).  Replaces collecting the reference's tf_adjusted_match_prob column (term_frequencies.py:159-168). */
 int spk_tf_copy(spk_ctx *ctx, int64_t start, int64_t count, double *out_tf_mp);
 /* How the per-value sums find the (value, pattern) counts: 0 (default) a direct histogram when n_values x
- * n_patterns <= 2^28, else keys (value x n_patterns + pattern, 32-bit when they fit) + radix sort + run-length
+ * n_patterns <= min(2^30, max(4 x pairs, 2^24)), else keys (value x n_patterns + pattern, 32-bit when they fit) + radix sort + run-length
  * encode; 1 always the sort; 2 the sort with 64-bit keys (tests hold the three identical).  No reference
  * counterpart (an implementation choice below term_frequencies.py:49-65). */
 int spk_tf_set_mode(spk_ctx *ctx, int mode);

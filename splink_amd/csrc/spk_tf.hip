@@ -119,7 +119,8 @@ __global__ void k_tf_runs(const KeyT *__restrict__ keys, const unsigned int *__r
 // Replaces the keys + radix sort + run-length encode of tf_pass when n_values x n_patterns <= TF_HIST_MAX: the
 // whole cfg3 job on one GPU (3.08e9 pairs, 300k values x 576 patterns) sorted 6 x 2^30 keys, ~0.35 s of device
 // time (profiles/r6_tf_sort_kernel_stats.csv).  The counts are the runs' counts, so the sums are identical.
-constexpr int64_t TF_HIST_MAX = (int64_t)1 << 28;
+// Up to 2^30 counters (8 GB) and no more than ~4 per pair: beyond that the sort's keys (4-8 B per pair) are smaller.
+constexpr int64_t TF_HIST_MAX = (int64_t)1 << 30;
 template <typename CodeT>
 __global__ void k_tf_hist(int64_t P, const int32_t *__restrict__ pl, const int32_t *__restrict__ pr,
                           const int64_t *__restrict__ ids0, const int64_t *__restrict__ ids1,
@@ -257,7 +258,8 @@ static int tf_pass(spk_ctx *ctx, int64_t n_values, const int64_t *d0, const int6
     SPK_REQUIRE(n_values < ((int64_t)1 << 31), SPK_E_LIMIT, "tf: more than 2^31 distinct values");
     const int64_t P = ctx->n_pairs;
     const int64_t npat = std::max<int64_t>(ctx->n_patterns, 1);
-    if (ctx->tf_mode == 0 && n_values <= TF_HIST_MAX / npat) {  // the counts directly, no sort
+    if (ctx->tf_mode == 0 && n_values <= TF_HIST_MAX / npat &&
+        n_values * npat <= std::max<int64_t>(4 * P, (int64_t)1 << 24)) {  // the counts directly, no sort
         const int64_t M = std::max<int64_t>(n_values * npat, 1);
         const bool hit = key != nullptr && ctx->tf_key == *key && ctx->tf_hist.p && ctx->tf_hist.n >= (size_t)M;
         if (!hit) {

@@ -67,6 +67,7 @@ def main():
                     help="generate the records as this many independent chunks over one vocabulary, in parallel "
                          "(synthetic.make_records_parallel; 0 = the serial make_records)")
     ap.add_argument("--workers", type=int, default=16)
+    ap.add_argument("--tf-mode", type=int, default=0, help="spk_tf_set_mode: 0 histogram when it fits, 1 / 2 the sort")
     ap.add_argument("--no-prefetch", dest="prefetch", action="store_false",
                     help="upload the comparison-only columns in the first comparison call (no background prefetch)")
     a = ap.parse_args()
@@ -174,7 +175,9 @@ def main():
         from splink_amd.term_frequencies import _bayes_pair
         t = time.perf_counter()
         col = job._col_index[("surname", "str")]
+        job.ctx.tf_set_mode(a.tf_mode)
         n_values = job.ctx.tf_column_values(col)
+        tf_values = int(n_values)
         sums, counts = job.ctx.tf_accumulate_column(col, n_values)
         wall["tf_sums"] = time.perf_counter() - t
         with np.errstate(invalid="ignore", divide="ignore"):
@@ -218,6 +221,9 @@ def main():
                                                              if k.startswith("after_") and k.endswith("_bytes"))},
         "lambda_final": params.params["λ"],
     }
+    if link:
+        row["tf_n_values"] = tf_values  # distinct surnames: n_values x patterns decides histogram vs sort
+        row["tf_mode"] = a.tf_mode
     if not a.no_parity:
         import oracle as orc
         t = time.perf_counter()
